@@ -1,0 +1,156 @@
+/*
+ * hipgle.h -- C-ABI of the MI355X-native generalized-Langevin (GLE) stepper.
+ *
+ * This is the drop-in boundary for sclmd's per-step hot path: md.vv + md.force + the bath forces
+ * (ebath.bforce / phbath.bforce) + the coloured-noise generator (noise.phnoise / noise.enoise).
+ * Plain C types only (no torch, no HIP types).  The Python shim sclmd_amd/ binds it with ctypes;
+ * INTEGRATION.md shows the binding a sclmd maintainer would add.
+ *
+ * Units and array meaning follow the reference exactly (mass-weighted p, q; eV; time unit
+ * 0.658211814201041 fs; sclmd/units.py:5-10).
+ *
+ * Layout conventions of HOST buffers (all row-major, float64, caller-owned, copied in/out):
+ *   per-trajectory state  [ntraj][nph]
+ *   bath kernel           [ml][nc][nc]          (phbath.kernel / ebath.kernel, baths.py:119,426)
+ *   bath noise            [ntraj][nmd][nc]      (bath.noise, baths.py:191,408)
+ *   heat current          [nbath][ntraj][nmd]   (bath.cur, md.py:397)
+ *   kinetic energy        [ntraj][nmd]          (md.etot, md.py:383)
+ *
+ * Every entry returns 0 on success and a negative GLE_ERR_* code on failure; gle_last_error()
+ * returns a description.  (Deviation from the reference, which prints and calls sys.exit(0) on
+ * bad shapes, e.g. baths.py:115-116, md.py:171-176: here errors are reported, never exit.)
+ *
+ * Threading: a handle is bound to one HIP device and one stream and is not thread-safe.
+ * Multi-GPU = one handle per process/device (torch.distributed + RCCL reduce in the shim).
+ */
+#ifndef HIPGLE_H
+#define HIPGLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GLE_ABI_VERSION 1
+
+#define GLE_OK 0
+#define GLE_ERR_ARG (-1)     /* bad argument / shape                      */
+#define GLE_ERR_HIP (-2)     /* HIP runtime error (no device, fault, ...) */
+#define GLE_ERR_STATE (-3)   /* call out of order (e.g. no noise set)     */
+#define GLE_ERR_NOMEM (-4)   /* device allocation failed                  */
+#define GLE_ERR_UNSUP (-5)   /* unsupported configuration                 */
+
+#define GLE_BATH_PHONON 0    /* phbath: memory kernel, ml >= 1 (baths.py:258)     */
+#define GLE_BATH_ELECTRON 1  /* ebath: time-local, ml == 1, bias terms (baths.py:55) */
+
+typedef struct gle_handle gle_handle;
+
+typedef struct gle_config {
+    int64_t nph;        /* system degrees of freedom, md.nph (md.py:86)                      */
+    int64_t ntraj;      /* independent trajectories batched on this device (ensemble size)   */
+    int64_t nmd;        /* MD steps per run = noise period, md.nmd (md.py:59); even          */
+    double dt;          /* MD time step, md.dt (md.py:59)                                    */
+    int32_t device;     /* HIP device ordinal                                                */
+    int32_t block_len;  /* far-field time block L for the memory-kernel contraction; 0=auto  */
+} gle_config;
+
+/* ---- lifetime ------------------------------------------------------------------------- */
+int gle_abi_version(void);
+/* replaces md.__init__ (md.py:56-130) for the state the hot path needs */
+int gle_create(const gle_config* cfg, gle_handle** out);
+int gle_destroy(gle_handle* h);
+/* last error of h, or of the last failed gle_create when h == NULL */
+const char* gle_last_error(const gle_handle* h);
+int gle_device_count(int32_t* count);
+
+/* ---- system / baths ------------------------------------------------------------------- */
+/* md.AddBath (md.py:167-183) + the bath's bforce parameters (baths.py:224-255, 448-458).
+ * kind     GLE_BATH_PHONON or GLE_BATH_ELECTRON
+ * cids     [nc] DOF indices the bath couples to (bath.cids = cats, baths.py:80,303)
+ * kernel   [ml][nc][nc] friction kernel (bath.kernel); the dt factor is applied iff ml > 1
+ *          (baths.py:454-457)
+ * bias, exim, zeta1, zeta2: electron bath only; exim/zeta2 antisymmetrised, zeta1 symmetrised by
+ *          the caller (ebath.CheckEmat, baths.py:100-174).  The bias terms are active only when
+ *          all three matrices are non-NULL and nonzero (baths.py:233).  Pass NULL otherwise.
+ * bath_id  out: index of this bath (AddBath order) */
+int gle_add_bath(gle_handle* h, int32_t kind, const int64_t* cids, int64_t nc, int64_t ml,
+                 const double* kernel, double bias, const double* exim, const double* zeta1,
+                 const double* zeta2, int32_t* bath_id);
+/* md.setDyn (md.py:250-292): harmonic potential force -dyn.q used when no host force is given
+ * (md.potforce, md.py:466-467).  dyn [nph][nph] as already processed by setDyn. */
+int gle_set_dyn(gle_handle* h, const double* dyn);
+/* md.AddConstr (md.py:189) flattened: the DOF indices ApplyConstraint zeroes (md.py:782-794) */
+int gle_set_constraint(gle_handle* h, const int64_t* dofs, int64_t n);
+
+/* ---- state ---------------------------------------------------------------------------- */
+/* md.p, md.q, md.t (md.py:372, 411).  p, q: [ntraj][nph].  Resets the potential-force cache
+ * (md.q0 = [], md.py:105) and re-derives the memory sums from the current history. */
+int gle_set_state(gle_handle* h, const double* p, const double* q, int64_t t);
+int gle_get_state(gle_handle* h, double* p, double* q, int64_t* t);
+/* md.phis restricted to the bath's cids, newest first (md.py:345-346, 386-387).
+ * phis: [ntraj][ml][nc] (ml of that bath).  NULL in set = zeros (md.ResetHis, md.py:340-349). */
+int gle_set_history(gle_handle* h, int32_t bath, const double* phis);
+int gle_get_history(gle_handle* h, int32_t bath, double* phis);
+/* last total force md.f (md.py:411): [ntraj][nph] */
+int gle_get_force(gle_handle* h, double* f);
+
+/* ---- noise (bath.gnoi, baths.py:176-192, 397-409; noise.py:50-100, 149-206) ----------- */
+/* Inject a noise realisation: noise [ntraj][nmd][nc] (bath.noise after gnoi). */
+int gle_set_noise(gle_handle* h, int32_t bath, const double* noise);
+int gle_get_noise(gle_handle* h, int32_t bath, double* noise);
+/* Spectral factors of the noise covariance for the nfreq = nmd/2+1 positive frequencies:
+ * m_re/m_im [nfreq][nc][nc] (m_im NULL for a real factor).  The generator computes
+ *   a_w = M_w . x_w   for every trajectory, mirrors a into a length-nmd spectrum exactly as
+ *   noise.py:87-94 does (Nyquist row -> conj(a_hlen)), applies numpy's forward-FFT convention
+ *   times dw/2pi (functions.py:36-53) and keeps the real part (baths.py:191,408).
+ * With M = U (eigenvectors) and host draws x = vargau's r (noise.py:297-303) this reproduces the
+ * reference draw for draw; with M = U.diag(sqrt(max(lambda,0))) and device Gaussians it is the
+ * ensemble generator. */
+int gle_noise_factors(gle_handle* h, int32_t bath, int64_t nfreq, const double* m_re,
+                      const double* m_im);
+/* Generate bath noise on the device.  x_host [ntraj][nfreq][nc] host draws, or NULL to draw
+ * N(0,1) on the device with a counter-based Philox stream keyed by (seed, traj_offset + b). */
+int gle_noise_generate(gle_handle* h, int32_t bath, const double* x_host, uint64_t seed,
+                       uint64_t traj_offset);
+
+/* ---- stepping (md.vv, md.py:367-411) -------------------------------------------------- */
+/* Phase A of one step: F0 = Fpot(q_t) + sum_b bforce_b(t, id=0), current, half kick, drift.
+ * fpot  [ntraj][nph] host force at q_t (driver.force(q), md.py:463-464) or NULL to use the
+ *       harmonic -dyn.q with md.potforce's cache rule (sameq, md.py:449-450, 767-779).
+ * q_tilde_out [ntraj][nph] receives q_t + p dt + F0 dt^2/2 (the position the host driver must
+ *       be evaluated at next), or NULL. */
+int gle_step_begin(gle_handle* h, const double* fpot, double* q_tilde_out);
+/* Phase B: the two velocity iterations at q~ (md.py:401-404) and the constraints (:407-408).
+ * fpot_qt [ntraj][nph] host force at q~ or NULL for the harmonic force. */
+int gle_step_end(gle_handle* h, const double* fpot_qt);
+/* nsteps full steps with the harmonic force, entirely on the device (no host round trips). */
+int gle_run(gle_handle* h, int64_t nsteps);
+int gle_sync(gle_handle* h);
+
+/* ---- outputs -------------------------------------------------------------------------- */
+/* bath.cur for every bath: [nbath][ntraj][nmd] (md.py:397) */
+int gle_get_current(gle_handle* h, double* cur);
+/* md.etot: [ntraj][nmd] (md.py:383) */
+int gle_get_energy(gle_handle* h, double* etot);
+/* Per bath: [sum over trajectories of mean_t cur, sum of (mean_t cur)^2, ntraj] -- the
+ * per-run heat-current statistics the ensemble reduce sums (md.py:663, tools.py:193).
+ * out: [nbath][3] */
+int gle_current_sums(gle_handle* h, double* out);
+
+/* ---- measurement ---------------------------------------------------------------------- */
+/* Record HIP events around every launch of the memory-kernel contraction (the dominant kernel)
+ * on the handle's stream. */
+int gle_profile(gle_handle* h, int32_t enable);
+/* launches, total milliseconds, algorithmic flops and bytes of the profiled contraction
+ * launches since profiling was enabled (flops/bytes per SURVEY.md section 8d). */
+int gle_profile_read(gle_handle* h, int64_t* nlaunch, double* total_ms, double* flops,
+                     double* bytes);
+/* Planner summary of the current configuration: block length L, far-field work items, bytes of
+ * device memory in use. */
+int gle_plan_info(gle_handle* h, int64_t* block_len, int64_t* far_items, int64_t* device_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HIPGLE_H */

@@ -1,0 +1,274 @@
+"""ctypes binding of the hipgle C-ABI (include/hipgle.h).
+
+The library is built in-tree (``make`` or ``__graft_entry__.build()``) into sclmd_amd/_lib/.
+There is no CPU fallback: every compute call goes through this library and raises when it is
+missing or when no HIP device is present.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("SCLMD_AMD_LIB", os.path.join(_HERE, "_lib", "libhipgle.so"))
+
+GLE_BATH_PHONON = 0
+GLE_BATH_ELECTRON = 1
+
+_ERRNAMES = {-1: "GLE_ERR_ARG", -2: "GLE_ERR_HIP", -3: "GLE_ERR_STATE", -4: "GLE_ERR_NOMEM",
+             -5: "GLE_ERR_UNSUP"}
+
+# every symbol include/hipgle.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "gle_abi_version", "gle_create", "gle_destroy", "gle_last_error", "gle_device_count",
+    "gle_add_bath", "gle_set_dyn", "gle_set_constraint", "gle_set_state", "gle_get_state",
+    "gle_set_history", "gle_get_history", "gle_get_force", "gle_set_noise", "gle_get_noise",
+    "gle_noise_factors", "gle_noise_generate", "gle_step_begin", "gle_step_end", "gle_run",
+    "gle_sync", "gle_get_current", "gle_get_energy", "gle_current_sums", "gle_profile",
+    "gle_profile_read", "gle_plan_info",
+]
+
+
+class GLEError(RuntimeError):
+    pass
+
+
+class gle_config(ctypes.Structure):
+    _fields_ = [("nph", ctypes.c_int64), ("ntraj", ctypes.c_int64), ("nmd", ctypes.c_int64),
+                ("dt", ctypes.c_double), ("device", ctypes.c_int32), ("block_len", ctypes.c_int32)]
+
+
+_P = ctypes.c_void_p
+_D = ctypes.POINTER(ctypes.c_double)
+_I64 = ctypes.POINTER(ctypes.c_int64)
+
+_SIGS = {
+    "gle_abi_version": (ctypes.c_int, []),
+    "gle_create": (ctypes.c_int, [ctypes.POINTER(gle_config), ctypes.POINTER(_P)]),
+    "gle_destroy": (ctypes.c_int, [_P]),
+    "gle_last_error": (ctypes.c_char_p, [_P]),
+    "gle_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int32)]),
+    "gle_add_bath": (ctypes.c_int, [_P, ctypes.c_int32, _I64, ctypes.c_int64, ctypes.c_int64, _D,
+                                    ctypes.c_double, _D, _D, _D, ctypes.POINTER(ctypes.c_int32)]),
+    "gle_set_dyn": (ctypes.c_int, [_P, _D]),
+    "gle_set_constraint": (ctypes.c_int, [_P, _I64, ctypes.c_int64]),
+    "gle_set_state": (ctypes.c_int, [_P, _D, _D, ctypes.c_int64]),
+    "gle_get_state": (ctypes.c_int, [_P, _D, _D, _I64]),
+    "gle_set_history": (ctypes.c_int, [_P, ctypes.c_int32, _D]),
+    "gle_get_history": (ctypes.c_int, [_P, ctypes.c_int32, _D]),
+    "gle_get_force": (ctypes.c_int, [_P, _D]),
+    "gle_set_noise": (ctypes.c_int, [_P, ctypes.c_int32, _D]),
+    "gle_get_noise": (ctypes.c_int, [_P, ctypes.c_int32, _D]),
+    "gle_noise_factors": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int64, _D, _D]),
+    "gle_noise_generate": (ctypes.c_int, [_P, ctypes.c_int32, _D, ctypes.c_uint64, ctypes.c_uint64]),
+    "gle_step_begin": (ctypes.c_int, [_P, _D, _D]),
+    "gle_step_end": (ctypes.c_int, [_P, _D]),
+    "gle_run": (ctypes.c_int, [_P, ctypes.c_int64]),
+    "gle_sync": (ctypes.c_int, [_P]),
+    "gle_get_current": (ctypes.c_int, [_P, _D]),
+    "gle_get_energy": (ctypes.c_int, [_P, _D]),
+    "gle_current_sums": (ctypes.c_int, [_P, _D]),
+    "gle_profile": (ctypes.c_int, [_P, ctypes.c_int32]),
+    "gle_profile_read": (ctypes.c_int, [_P, _I64, _D, _D, _D]),
+    "gle_plan_info": (ctypes.c_int, [_P, _I64, _I64, _I64]),
+}
+
+_lib = None
+
+
+def load():
+    """Load libhipgle.so (raises GLEError with the build hint when it is missing)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise GLEError("hipgle library not found at %s -- build it with `make` or "
+                       "`python -c 'import __graft_entry__ as g; g.build()'`" % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    return a.ctypes.data_as(_D)
+
+
+def _f64(a, shape=None):
+    a = np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+    if shape is not None and a.shape != tuple(shape):
+        a = a.reshape(shape)
+    return a
+
+
+def device_count():
+    lib = load()
+    n = ctypes.c_int32(0)
+    rc = lib.gle_device_count(ctypes.byref(n))
+    return int(n.value) if rc == 0 else 0
+
+
+class Stepper:
+    """Owner of one gle_handle: a batch of ntraj trajectories of one system on one device."""
+
+    def __init__(self, nph, ntraj, nmd, dt, device=0, block_len=0):
+        self.lib = load()
+        self.nph, self.ntraj, self.nmd, self.dt = int(nph), int(ntraj), int(nmd), float(dt)
+        cfg = gle_config(self.nph, self.ntraj, self.nmd, self.dt, int(device), int(block_len))
+        h = _P()
+        rc = self.lib.gle_create(ctypes.byref(cfg), ctypes.byref(h))
+        if rc != 0:
+            raise GLEError("gle_create failed (%s): %s" % (_ERRNAMES.get(rc, rc),
+                                                           self.lib.gle_last_error(None).decode()))
+        self.h = h
+        self.nbath = 0
+        self.bath_nc = []
+        self.bath_ml = []
+
+    # --------------------------------------------------------------------------- helpers
+    def _chk(self, rc, what):
+        if rc != 0:
+            msg = self.lib.gle_last_error(self.h).decode() if self.h else ""
+            raise GLEError("%s failed (%s): %s" % (what, _ERRNAMES.get(rc, rc), msg))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.gle_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # --------------------------------------------------------------------------- setup
+    def add_bath(self, kind, cids, kernel, bias=0.0, exim=None, zeta1=None, zeta2=None):
+        cids = np.ascontiguousarray(np.asarray(cids, dtype=np.int64))
+        nc = len(cids)
+        kernel = _f64(kernel)
+        ml = kernel.shape[0]
+        kernel = _f64(kernel, (ml, nc, nc))
+        mats = [None if m is None else _f64(m, (nc, nc)) for m in (exim, zeta1, zeta2)]
+        bid = ctypes.c_int32(-1)
+        self._chk(self.lib.gle_add_bath(self.h, int(kind), cids.ctypes.data_as(_I64), nc, ml,
+                                        _ptr(kernel), float(bias), _ptr(mats[0]), _ptr(mats[1]),
+                                        _ptr(mats[2]), ctypes.byref(bid)), "gle_add_bath")
+        self.nbath += 1
+        self.bath_nc.append(nc)
+        self.bath_ml.append(ml)
+        return int(bid.value)
+
+    def set_dyn(self, dyn):
+        d = _f64(dyn, (self.nph, self.nph))
+        self._chk(self.lib.gle_set_dyn(self.h, _ptr(d)), "gle_set_dyn")
+
+    def set_constraint(self, dofs):
+        d = np.ascontiguousarray(np.asarray(sorted(set(int(x) for x in dofs)), dtype=np.int64))
+        self._chk(self.lib.gle_set_constraint(self.h, d.ctypes.data_as(_I64), len(d)),
+                  "gle_set_constraint")
+
+    def set_state(self, p, q, t):
+        p = _f64(p, (self.ntraj, self.nph))
+        q = _f64(q, (self.ntraj, self.nph))
+        self._chk(self.lib.gle_set_state(self.h, _ptr(p), _ptr(q), int(t)), "gle_set_state")
+
+    def get_state(self):
+        p = np.empty((self.ntraj, self.nph))
+        q = np.empty((self.ntraj, self.nph))
+        t = ctypes.c_int64(0)
+        self._chk(self.lib.gle_get_state(self.h, _ptr(p), _ptr(q), ctypes.byref(t)), "gle_get_state")
+        return p, q, int(t.value)
+
+    def set_history(self, bath, phis=None):
+        if phis is not None:
+            phis = _f64(phis, (self.ntraj, self.bath_ml[bath], self.bath_nc[bath]))
+        self._chk(self.lib.gle_set_history(self.h, int(bath), _ptr(phis)), "gle_set_history")
+
+    def get_history(self, bath):
+        out = np.empty((self.ntraj, self.bath_ml[bath], self.bath_nc[bath]))
+        self._chk(self.lib.gle_get_history(self.h, int(bath), _ptr(out)), "gle_get_history")
+        return out
+
+    def get_force(self):
+        out = np.empty((self.ntraj, self.nph))
+        self._chk(self.lib.gle_get_force(self.h, _ptr(out)), "gle_get_force")
+        return out
+
+    def set_noise(self, bath, noise):
+        n = _f64(noise, (self.ntraj, self.nmd, self.bath_nc[bath]))
+        self._chk(self.lib.gle_set_noise(self.h, int(bath), _ptr(n)), "gle_set_noise")
+
+    def get_noise(self, bath):
+        out = np.empty((self.ntraj, self.nmd, self.bath_nc[bath]))
+        self._chk(self.lib.gle_get_noise(self.h, int(bath), _ptr(out)), "gle_get_noise")
+        return out
+
+    def noise_factors(self, bath, m):
+        """m: (nfreq, nc, nc) real or complex spectral factors."""
+        m = np.asarray(m)
+        nf = m.shape[0]
+        mre = _f64(np.real(m))
+        mim = _f64(np.imag(m)) if np.iscomplexobj(m) else None
+        self._chk(self.lib.gle_noise_factors(self.h, int(bath), nf, _ptr(mre), _ptr(mim)),
+                  "gle_noise_factors")
+
+    def noise_generate(self, bath, x=None, seed=0, traj_offset=0):
+        if x is not None:
+            x = _f64(x)
+        self._chk(self.lib.gle_noise_generate(self.h, int(bath), _ptr(x), int(seed) & (2**64 - 1),
+                                              int(traj_offset)), "gle_noise_generate")
+
+    # --------------------------------------------------------------------------- stepping
+    def step_begin(self, fpot=None, want_qt=True):
+        f = None if fpot is None else _f64(fpot, (self.ntraj, self.nph))
+        qt = np.empty((self.ntraj, self.nph)) if want_qt else None
+        self._chk(self.lib.gle_step_begin(self.h, _ptr(f), _ptr(qt)), "gle_step_begin")
+        return qt
+
+    def step_end(self, fpot_qt=None):
+        f = None if fpot_qt is None else _f64(fpot_qt, (self.ntraj, self.nph))
+        self._chk(self.lib.gle_step_end(self.h, _ptr(f)), "gle_step_end")
+
+    def run(self, nsteps):
+        self._chk(self.lib.gle_run(self.h, int(nsteps)), "gle_run")
+
+    def sync(self):
+        self._chk(self.lib.gle_sync(self.h), "gle_sync")
+
+    # --------------------------------------------------------------------------- outputs
+    def get_current(self):
+        out = np.empty((self.nbath, self.ntraj, self.nmd))
+        self._chk(self.lib.gle_get_current(self.h, _ptr(out)), "gle_get_current")
+        return out
+
+    def get_energy(self):
+        out = np.empty((self.ntraj, self.nmd))
+        self._chk(self.lib.gle_get_energy(self.h, _ptr(out)), "gle_get_energy")
+        return out
+
+    def current_sums(self):
+        out = np.empty((self.nbath, 3))
+        self._chk(self.lib.gle_current_sums(self.h, _ptr(out)), "gle_current_sums")
+        return out
+
+    def profile(self, enable=True):
+        self._chk(self.lib.gle_profile(self.h, 1 if enable else 0), "gle_profile")
+
+    def profile_read(self):
+        n = ctypes.c_int64(0)
+        ms, fl, by = ctypes.c_double(0), ctypes.c_double(0), ctypes.c_double(0)
+        self._chk(self.lib.gle_profile_read(self.h, ctypes.byref(n), ctypes.byref(ms),
+                                            ctypes.byref(fl), ctypes.byref(by)), "gle_profile_read")
+        return {"launches": int(n.value), "ms": ms.value, "flops": fl.value, "bytes": by.value}
+
+    def plan_info(self):
+        a, b, c = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int64(0)
+        self._chk(self.lib.gle_plan_info(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
+                  "gle_plan_info")
+        return {"block_len": int(a.value), "far_items": int(b.value), "device_bytes": int(c.value)}

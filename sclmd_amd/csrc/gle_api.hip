@@ -1,0 +1,1309 @@
+// Host side of the hipgle C-ABI: handle, device buffers, work planner, step orchestration.
+//
+// Step schedule (one md.vv, md.py:367-411), all on the handle's stream:
+//   [every L steps] FAR  : far(t+j) = sum_{i>=L} K_i p_{t+j-i}, j = 1..L      (one contraction)
+//   OP0  : Y0 = K0 p_t, near S(t+1) = sum_{1<=i<L} K_i p_{t+1-i}, Yq = Kq q_t, [dyn q_t]
+//   RED0 : S(t+1) = far(t+1) + near;  split-K sums
+//   [POTSEL(q_t)]  PHASE A : F0, heat current, p_half, q~, gathers
+//   OP1a : [dyn q~], Y = K0 p_half, Yq = Kq q~ ; RED1a ; [POTSEL(q~)] ; PHASE B : p1
+//   OP1b : Y = K0 p1 ; RED1b ; PHASE C : p2, constraints, history push, t+1
+// The memory sum S is computed once per step (the reference recomputes the whole history sum in
+// each of its three md.force calls, baths.py:453-457; the i>=1 tail is identical in all three).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/hipgle.h"
+#include "gle_internal.h"
+
+using namespace gle;
+
+namespace {
+
+thread_local std::string g_create_error;
+
+struct Op {
+  int rn = 1;
+  std::vector<CItem> items;
+  std::vector<RItem> ritems;
+  CItem* d_items = nullptr;
+  RItem* d_ritems = nullptr;
+  double* partial = nullptr;
+  size_t partial_doubles = 0;
+  double flops = 0, bytes = 0;  // algorithmic, per launch
+  bool empty() const { return items.empty() && ritems.empty(); }
+};
+
+struct Bath {
+  int kind = 0;
+  int nc = 0, ncp = 0, nrt = 0, nks = 0, ml = 1;
+  double c = 1.0;
+  bool has_q = false;
+  std::vector<int64_t> cids;
+  std::vector<double> K;  // host copy [ml][nc][nc] of the p-channel kernel (bias folded)
+  std::vector<double> Kq; // [nc][nc] q-channel
+  double* d_K = nullptr;
+  double* d_Kq = nullptr;
+  int32_t* d_inv = nullptr;
+  double *d_noise = nullptr, *d_Y = nullptr, *d_S = nullptr, *d_Yq = nullptr;
+  double *d_Xcur = nullptr, *d_Xq = nullptr, *d_H = nullptr, *d_cur = nullptr, *d_far = nullptr;
+  int64_t ldh = 0;
+  int R = 1;
+  bool noise_set = false;
+  // noise generator
+  int64_t nfreq = 0;
+  bool fac_complex = false;
+  int fac_rows = 0, fac_nrt = 0;
+  double* d_fac = nullptr;
+};
+
+}  // namespace
+
+struct gle_handle {
+  gle_config cfg{};
+  std::string err;
+  hipStream_t stream = nullptr;
+  int64_t nph = 0, B = 0, nmd = 0, nphp = 0;
+  double dt = 0;
+  int L = 1;
+  std::vector<Bath> baths;
+  bool has_dyn = false;
+  int dyn_nrt = 0, dyn_nks = 0;
+  double* d_dyn = nullptr;
+  std::vector<int64_t> constr;
+  uint8_t* d_cmask = nullptr;
+  double *d_P = nullptr, *d_Q = nullptr, *d_Ph = nullptr, *d_Qt = nullptr, *d_Fc = nullptr;
+  double *d_Flast = nullptr, *d_etot = nullptr, *d_Q0 = nullptr, *d_part = nullptr, *d_Ypot = nullptr;
+  int32_t* d_qvalid = nullptr;
+  Clock* d_clk = nullptr;
+  StepDev* d_sd = nullptr;
+  double* d_tw = nullptr;
+  int ndblk = 1, dchunk = 1;
+  int64_t t = 0;
+  bool frozen = false, state_set = false;
+  bool need_prime = true;
+  int steps_since_far = 0;
+  bool far_due = true;
+  bool pot_cache_exact = false;  // q_t == q~_{t-1} bitwise (no constraints): id0 cache hit
+  Op op_far, op_prime, op0, op0p, op1a, op1a_np, op1b;
+  Op op_near[2];  // S(t+1) into S[(t+1)&1]: one plan per destination parity
+  std::vector<void*> allocs;
+  size_t dev_bytes = 0;
+  // profiling of the dominant contraction
+  bool prof = false;
+  std::vector<hipEvent_t> ev;
+  size_t ev_used = 0;
+  int64_t prof_n = 0;
+  double prof_ms = 0, prof_flops = 0, prof_bytes = 0;
+};
+
+namespace {
+
+#define HIPCHK(h, x)                                                                       \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess) return fail(h, GLE_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+int fail(gle_handle* h, int code, const std::string& msg) {
+  if (h) h->err = msg;
+  else g_create_error = msg;
+  return code;
+}
+
+int dalloc(gle_handle* h, void** p, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess) {
+    *p = nullptr;
+    return fail(h, GLE_ERR_NOMEM, "hipMalloc(" + std::to_string(bytes) + "): " + hipGetErrorString(e));
+  }
+  e = hipMemsetAsync(*p, 0, bytes, h->stream);
+  if (e != hipSuccess) return fail(h, GLE_ERR_HIP, std::string("hipMemset: ") + hipGetErrorString(e));
+  h->allocs.push_back(*p);
+  h->dev_bytes += bytes;
+  return GLE_OK;
+}
+
+template <class T>
+int dalloc_n(gle_handle* h, T** p, size_t n) {
+  return dalloc(h, (void**)p, n * sizeof(T));
+}
+
+inline int64_t rup(int64_t a, int64_t m) { return (a + m - 1) / m * m; }
+
+// Pack A slices [nsl][M][Kd] (row-major, optionally two real blocks stacked for complex) into
+// the fragment-native layout [rt][ks][i][64] with zero padding; rows padded to 16*nrt, k to 4*nks.
+std::vector<double> pack_frags(const double* a, int64_t nsl, int64_t M, int64_t Kd, int nrt, int nks,
+                               const double* a2 = nullptr) {
+  // a2: optional second block stacked below a (rows M..2M-1), used for complex factors
+  const int64_t Mtot = a2 ? 2 * M : M;
+  std::vector<double> f((size_t)nrt * nks * nsl * 64, 0.0);
+  for (int rt = 0; rt < nrt; ++rt)
+    for (int ks = 0; ks < nks; ++ks)
+      for (int64_t i = 0; i < nsl; ++i) {
+        double* dst = &f[(((size_t)rt * nks + ks) * nsl + i) * 64];
+        for (int l = 0; l < 64; ++l) {
+          const int64_t r = 16 * rt + (l & 15);
+          const int64_t k = 4 * ks + (l >> 4);
+          if (r >= Mtot || k >= Kd) continue;
+          const double* src = (r < M) ? a : a2;
+          const int64_t rr = (r < M) ? r : r - M;
+          dst[l] = src[(i * M + rr) * Kd + k];
+        }
+      }
+  return f;
+}
+
+int upload(gle_handle* h, void* d, const void* s, size_t bytes) {
+  HIPCHK(h, hipMemcpyAsync(d, s, bytes, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return GLE_OK;
+}
+
+int rn_for(int64_t ncols) {
+  int need = (int)((ncols + 15) / 16);
+  int rn = 1;
+  while (rn < need && rn < 16) rn *= 2;
+  return rn;
+}
+
+// One dense product  dst[M][N] (+)= sum_{i in [i0,i1)} A_i . X_i  planned as work items.
+struct Gemm {
+  const double* A;
+  int64_t a_rt, a_ks;
+  int nrt_total, nks_total;
+  int i0, i1;
+  const double* X;
+  int64_t ldx;
+  int ring, cs, tshift;
+  int M, N;
+  double* dst;
+  int64_t ldd;
+  const double* add = nullptr;  // far addend
+  int64_t lda = 0;
+  int add_cs = 0;
+  bool force_reduce = false;
+};
+
+// Split policy: target ~target_items work items in total for this product, each with at least
+// min_work (slice x k-step) units; split slices first (history windows share LDS staging across
+// slices only within an item, so long slice runs per item are kept), then k.
+void plan_gemm(Op& op, const Gemm& g, int target_items, int min_work) {
+  const int NT = 16 * op.rn;
+  const int ngroups = (g.nrt_total + 3) / 4;
+  const int ncol = (int)((g.N + NT - 1) / NT);
+  const int ni = g.i1 - g.i0;
+  const int nkp = g.nks_total / 2;  // k-step pairs
+  const int base = ngroups * ncol;
+  int split = std::max(1, target_items / std::max(1, base));
+  const int64_t work = (int64_t)std::max(ni, 0) * g.nks_total;
+  split = (int)std::min<int64_t>(split, std::max<int64_t>(1, work / std::max(1, min_work)));
+  int si = 1, sk = 1;
+  if (ni > 0) {
+    if (g.ring) {
+      si = std::min(split, ni);
+      sk = std::max(1, std::min(nkp, split / si));
+    } else {
+      sk = std::min(split, nkp);
+      si = std::max(1, std::min(ni, split / sk));
+    }
+  }
+  const int nsplit = (ni > 0) ? si * sk : 0;
+  const bool use_partial = g.force_reduce || g.add != nullptr || nsplit > 1;
+  for (int gi = 0; gi < ngroups; ++gi)
+    for (int ct = 0; ct < ncol; ++ct) {
+      const int col0 = ct * NT;
+      const int ncols = std::min<int>(NT, g.N - col0);
+      const int nrows = std::min(64, g.M - 64 * gi);
+      if (nrows <= 0) continue;
+      const size_t slot0 = op.partial_doubles;
+      if (use_partial) op.partial_doubles += (size_t)nsplit * 64 * NT;
+      int slot = 0;
+      for (int a = 0; a < si && ni > 0; ++a) {
+        const int ia = g.i0 + (int)((int64_t)ni * a / si);
+        const int ib = g.i0 + (int)((int64_t)ni * (a + 1) / si);
+        if (ib <= ia) continue;
+        for (int b = 0; b < sk; ++b) {
+          const int kp0 = (int)((int64_t)nkp * b / sk), kp1 = (int)((int64_t)nkp * (b + 1) / sk);
+          if (kp1 <= kp0) continue;
+          CItem it{};
+          it.A = g.A + (int64_t)(4 * gi) * g.a_rt + (int64_t)(2 * kp0) * g.a_ks + (int64_t)ia * 64;
+          it.X = g.X + (int64_t)(8 * kp0) * g.ldx;
+          it.a_rt = g.a_rt;
+          it.a_ks = g.a_ks;
+          it.nks = 2 * (kp1 - kp0);
+          it.ia = ia;
+          it.ni = ib - ia;
+          it.nrt = std::min(4, g.nrt_total - 4 * gi);
+          it.ldx = (int32_t)g.ldx;
+          it.ring = g.ring;
+          it.cs = g.cs;
+          it.tshift = g.tshift;
+          it.col0 = col0;
+          it.ncols = ncols;
+          it.nrows = nrows;
+          if (use_partial) {
+            it.out = (double*)(uintptr_t)((slot0 + (size_t)slot * 64 * NT) * sizeof(double));  // offset, fixed up later
+            it.ldo = NT;
+          } else {
+            it.out = g.dst + (int64_t)(64 * gi) * g.ldd + col0;
+            it.ldo = (int32_t)g.ldd;
+          }
+          op.items.push_back(it);
+          ++slot;
+        }
+      }
+      if (use_partial) {
+        RItem r{};
+        r.dst = g.dst + (int64_t)(64 * gi) * g.ldd + col0;
+        r.src = (const double*)(uintptr_t)(slot0 * sizeof(double));  // offset, fixed up later
+        r.add = g.add ? g.add + (int64_t)(64 * gi) * g.lda + col0 : nullptr;
+        r.ldd = (int32_t)g.ldd;
+        r.lds = NT;
+        r.lda = (int32_t)g.lda;
+        r.nslots = slot;
+        r.slot_stride = (int64_t)64 * NT;
+        r.rows = nrows;
+        r.cols = ncols;
+        r.add_cs = g.add_cs;
+        op.ritems.push_back(r);
+      }
+    }
+  // algorithmic work of this product: each kernel entry read once, X read
+  // once, output written once.
+  if (ni > 0) {
+    const double kd = 4.0 * g.nks_total;
+    op.flops += 2.0 * g.M * kd * g.N * ni;
+    op.bytes += 8.0 * ((double)ni * g.M * kd + kd * (g.ring ? (double)(ni + (g.N + g.cs - 1) / std::max(1, g.cs) - 1) * g.cs : g.N) + (double)g.M * g.N);
+  }
+}
+
+// Fix up partial-slot offsets once the partial buffer exists.  Items that write partials were
+// tagged with ldo == NT and an offset pointer smaller than the partial size.
+int materialize(gle_handle* h, Op& op, const std::vector<bool>& is_partial) {
+  if (op.partial_doubles) {
+    int rc = dalloc_n(h, &op.partial, op.partial_doubles);
+    if (rc) return rc;
+  }
+  for (size_t i = 0; i < op.items.size(); ++i)
+    if (is_partial[i]) op.items[i].out = op.partial + (uintptr_t)op.items[i].out / sizeof(double);
+  for (auto& r : op.ritems) r.src = op.partial + (uintptr_t)r.src / sizeof(double);
+  if (!op.items.empty()) {
+    int rc = dalloc_n(h, &op.d_items, op.items.size());
+    if (rc) return rc;
+    rc = upload(h, op.d_items, op.items.data(), op.items.size() * sizeof(CItem));
+    if (rc) return rc;
+  }
+  if (!op.ritems.empty()) {
+    int rc = dalloc_n(h, &op.d_ritems, op.ritems.size());
+    if (rc) return rc;
+    rc = upload(h, op.d_ritems, op.ritems.data(), op.ritems.size() * sizeof(RItem));
+    if (rc) return rc;
+  }
+  return GLE_OK;
+}
+
+// Wrapper that records which items are partial writers while planning.
+struct Planner {
+  gle_handle* h;
+  Op& op;
+  std::vector<bool> partial;
+  Planner(gle_handle* hh, Op& o, int rn) : h(hh), op(o) { op.rn = rn; }
+  void add(const Gemm& g, int target, int min_work) {
+    const size_t n0 = op.items.size();
+    const size_t r0 = op.ritems.size();
+    plan_gemm(op, g, target, min_work);
+    const bool use_partial = op.ritems.size() > r0;
+    for (size_t i = n0; i < op.items.size(); ++i) partial.push_back(use_partial);
+  }
+  int done() { return materialize(h, op, partial); }
+};
+
+void run_op(gle_handle* h, Op& op, int set_tfar, bool profile) {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (profile && h->prof && !op.items.empty()) {
+    if (h->ev_used + 2 > h->ev.size()) {
+      // drain the pool into the running sum
+      hipStreamSynchronize(h->stream);
+      for (size_t i = 0; i + 1 < h->ev_used; i += 2) {
+        float ms = 0;
+        hipEventElapsedTime(&ms, h->ev[i], h->ev[i + 1]);
+        h->prof_ms += ms;
+      }
+      h->ev_used = 0;
+    }
+    e0 = h->ev[h->ev_used];
+    e1 = h->ev[h->ev_used + 1];
+    h->ev_used += 2;
+    hipEventRecord(e0, h->stream);
+  }
+  launch_contract(op.rn, op.d_items, (int)op.items.size(), h->d_clk, h->stream);
+  if (e1) {
+    hipEventRecord(e1, h->stream);
+    h->prof_n += 1;
+    h->prof_flops += op.flops;
+    h->prof_bytes += op.bytes;
+  }
+  launch_reduce(op.d_ritems, (int)op.ritems.size(), h->d_clk, set_tfar, h->stream);
+}
+
+int check_bath(gle_handle* h, int32_t b) {
+  if (!h) return GLE_ERR_ARG;
+  if (b < 0 || b >= (int)h->baths.size()) return fail(h, GLE_ERR_ARG, "bad bath id");
+  return GLE_OK;
+}
+
+int build_near(gle_handle* h);
+
+// Build every work plan once the system is fixed (first state / step call).
+int freeze(gle_handle* h) {
+  if (h->frozen) return GLE_OK;
+  const int64_t B = h->B;
+  // block length L of the far-field contraction: enough columns (L*B) for MFMA reuse of each
+  // streamed kernel slice, bounded so the per-step near-field stays small
+  int mlmax = 1;
+  for (auto& b : h->baths) mlmax = std::max(mlmax, b.ml);
+  if (h->cfg.block_len > 0) {
+    h->L = h->cfg.block_len;
+  } else {
+    int L = 1;
+    while (L * B < 256 && L < 32) L *= 2;
+    h->L = L;
+  }
+  const int L = h->L;
+  const int rn_step = rn_for(B);
+  // ring sizes and buffers that depend on L
+  for (auto& b : h->baths) {
+    b.R = b.ml + 2 * L + 2;
+    b.ldh = 2 * (int64_t)b.R * B + 512 + 16 * rn_for(L * B);
+    int rc = dalloc_n(h, &b.d_H, (size_t)b.ncp * b.ldh + 4096);
+    if (rc) return rc;
+    if (b.ml > L) {
+      rc = dalloc_n(h, &b.d_far, (size_t)b.ncp * L * B + 4096);
+      if (rc) return rc;
+    }
+  }
+  // StepDev
+  StepDev sd{};
+  sd.nph = (int32_t)h->nph;
+  sd.B = (int32_t)B;
+  sd.nmd = (int32_t)h->nmd;
+  sd.nbath = (int32_t)h->baths.size();
+  sd.dt = h->dt;
+  sd.P = h->d_P;
+  sd.Q = h->d_Q;
+  sd.Ph = h->d_Ph;
+  sd.Qt = h->d_Qt;
+  sd.G = nullptr;
+  sd.Fc = h->d_Fc;
+  sd.Flast = h->d_Flast;
+  sd.etot = h->d_etot;
+  sd.Q0 = h->d_Q0;
+  sd.qvalid = h->d_qvalid;
+  // DOF chunking of the phase kernels: ~ one 256-thread block per 64x(256/BT) elements
+  const int BT = (int)std::min<int64_t>(B, 64);
+  const int DL = 256 / BT;
+  h->dchunk = std::max(DL, (int)rup(std::max<int64_t>(1, h->nph / 64), DL));
+  h->dchunk = std::max(h->dchunk, DL * 4);
+  h->ndblk = (int)((h->nph + h->dchunk - 1) / h->dchunk);
+  sd.ndblk = h->ndblk;
+  sd.dchunk = h->dchunk;
+  int rc = dalloc_n(h, &h->d_part, (size_t)h->ndblk * (h->baths.size() + 1) * B);
+  if (rc) return rc;
+  sd.part = h->d_part;
+  // constraint mask
+  std::vector<uint8_t> mask(h->nph, 0);
+  for (auto d : h->constr) mask[d] = 1;
+  rc = dalloc_n(h, &h->d_cmask, h->nph);
+  if (rc) return rc;
+  rc = upload(h, h->d_cmask, mask.data(), h->nph);
+  if (rc) return rc;
+  sd.cmask = h->d_cmask;
+  for (size_t j = 0; j < h->baths.size(); ++j) {
+    Bath& b = h->baths[j];
+    BathDev& bd = sd.bath[j];
+    bd.inv = b.d_inv;
+    bd.noise = b.d_noise;
+    bd.Y = b.d_Y;
+    bd.S = b.d_S;
+    bd.Yq = b.d_Yq;
+    bd.Xcur = b.d_Xcur;
+    bd.Xq = b.d_Xq;
+    bd.H = b.d_H;
+    bd.cur = b.d_cur;
+    bd.c = b.c;
+    bd.nc = b.nc;
+    bd.ncp = b.ncp;
+    bd.ldh = (int32_t)b.ldh;
+    bd.R = b.R;
+    bd.has_q = b.has_q ? 1 : 0;
+  }
+  rc = dalloc_n(h, &h->d_sd, 1);
+  if (rc) return rc;
+  rc = upload(h, h->d_sd, &sd, sizeof(sd));
+  if (rc) return rc;
+
+  // ---- plans
+  const int TGT_STEP = 128, TGT_BIG = 512;
+  auto kgemm = [&](Bath& b, const double* A, int i0, int i1, const double* X, int64_t ldx, int ring,
+                   int tshift, int N, double* dst, int64_t ldd) {
+    Gemm g{};
+    g.A = A;
+    g.a_ks = (int64_t)(A == b.d_K ? b.ml : 1) * 64;
+    g.a_rt = (int64_t)b.nks * g.a_ks;
+    g.nrt_total = b.nrt;
+    g.nks_total = b.nks;
+    g.i0 = i0;
+    g.i1 = i1;
+    g.X = X;
+    g.ldx = ldx;
+    g.ring = ring;
+    g.cs = (int)B;
+    g.tshift = tshift;
+    g.M = b.nc;
+    g.N = N;
+    g.dst = dst;
+    g.ldd = ldd;
+    return g;
+  };
+  // FAR: slices [L, ml), windows ending at t+1..t+L
+  {
+    const int rnf = rn_for((int64_t)L * B);
+    Planner p(h, h->op_far, rnf);
+    for (auto& b : h->baths)
+      if (b.ml > L) {
+        Gemm g = kgemm(b, b.d_K, L, b.ml, b.d_H, b.ldh, b.R, 1, (int)(L * B), b.d_far, (int64_t)L * B);
+        g.force_reduce = true;
+        p.add(g, TGT_BIG, 16);
+      }
+    rc = p.done();
+    if (rc) return rc;
+  }
+  // PRIME: S(t) = sum_{i>=1} K_i p_{t-i} from the current history (after set_state/history)
+  {
+    Planner p(h, h->op_prime, rn_step);
+    for (auto& b : h->baths)
+      if (b.ml > 1) {
+        Gemm g = kgemm(b, b.d_K, 1, b.ml, b.d_H, b.ldh, b.R, 0, (int)B, b.d_S, B);  // S[0]; parity fixed at run time
+        g.force_reduce = true;
+        p.add(g, TGT_BIG, 16);
+      }
+    rc = p.done();
+    if (rc) return rc;
+  }
+  // OP0 (+ pot variant): K0 p_t, near S(t+1) (+ far addend), Kq q_t, [dyn q_t]
+  for (int variant = 0; variant < 2; ++variant) {
+    Op& op = variant ? h->op0p : h->op0;
+    Planner p(h, op, rn_step);
+    for (auto& b : h->baths) {
+      p.add(kgemm(b, b.d_K, 0, 1, b.d_H, b.ldh, b.R, 0, (int)B, b.d_Y, B), TGT_STEP, 16);
+      if (b.has_q) {
+        Gemm g = kgemm(b, b.d_Kq, 0, 1, b.d_Xq, B, 0, 0, (int)B, b.d_Yq, B);
+        g.a_ks = 64;
+        g.a_rt = (int64_t)b.nks * 64;
+        p.add(g, TGT_STEP, 16);
+      }
+    }
+    if (variant && h->has_dyn) {
+      Gemm g{};
+      g.A = h->d_dyn;
+      g.a_ks = 64;
+      g.a_rt = (int64_t)h->dyn_nks * 64;
+      g.nrt_total = h->dyn_nrt;
+      g.nks_total = h->dyn_nks;
+      g.i0 = 0;
+      g.i1 = 1;
+      g.X = h->d_Q;
+      g.ldx = B;
+      g.M = (int)h->nph;
+      g.N = (int)B;
+      g.dst = h->d_Ypot;
+      g.ldd = B;
+      p.add(g, TGT_STEP, 16);
+    }
+    rc = p.done();
+    if (rc) return rc;
+  }
+  // OP1a (+/- pot), OP1b
+  for (int variant = 0; variant < 3; ++variant) {
+    Op& op = variant == 0 ? h->op1a : (variant == 1 ? h->op1a_np : h->op1b);
+    Planner p(h, op, rn_step);
+    for (auto& b : h->baths) {
+      Gemm g = kgemm(b, b.d_K, 0, 1, b.d_Xcur, B, 0, 0, (int)B, b.d_Y, B);
+      g.a_ks = (int64_t)b.ml * 64;
+      g.a_rt = (int64_t)b.nks * g.a_ks;
+      p.add(g, TGT_STEP, 16);
+      if (b.has_q && variant < 2) {
+        Gemm gq = kgemm(b, b.d_Kq, 0, 1, b.d_Xq, B, 0, 0, (int)B, b.d_Yq, B);
+        gq.a_ks = 64;
+        gq.a_rt = (int64_t)b.nks * 64;
+        p.add(gq, TGT_STEP, 16);
+      }
+    }
+    if (variant == 0 && h->has_dyn) {
+      Gemm g{};
+      g.A = h->d_dyn;
+      g.a_ks = 64;
+      g.a_rt = (int64_t)h->dyn_nks * 64;
+      g.nrt_total = h->dyn_nrt;
+      g.nks_total = h->dyn_nks;
+      g.i0 = 0;
+      g.i1 = 1;
+      g.X = h->d_Qt;
+      g.ldx = B;
+      g.M = (int)h->nph;
+      g.N = (int)B;
+      g.dst = h->d_Ypot;
+      g.ldd = B;
+      p.add(g, TGT_STEP, 16);
+    }
+    rc = p.done();
+    if (rc) return rc;
+  }
+  rc = build_near(h);
+  if (rc) return rc;
+  h->frozen = true;
+  return GLE_OK;
+}
+
+// The near-field S(t+1) product writes S[(t+1)&1]; its destination alternates every step, so it
+// is planned once per destination parity.
+int build_near(gle_handle* h) {
+  const int64_t B = h->B;
+  const int L = h->L;
+  for (int par = 0; par < 2; ++par) {
+    Planner p(h, h->op_near[par], rn_for(B));
+    for (auto& b : h->baths) {
+      if (b.ml <= 1) continue;
+      Gemm g{};
+      g.A = b.d_K;
+      g.a_ks = (int64_t)b.ml * 64;
+      g.a_rt = (int64_t)b.nks * g.a_ks;
+      g.nrt_total = b.nrt;
+      g.nks_total = b.nks;
+      g.i0 = 1;
+      g.i1 = std::min(b.ml, L);
+      g.X = b.d_H;
+      g.ldx = b.ldh;
+      g.ring = b.R;
+      g.cs = (int)B;
+      g.tshift = 1;
+      g.M = b.nc;
+      g.N = (int)B;
+      g.dst = b.d_S + (int64_t)par * b.ncp * B;
+      g.ldd = B;
+      if (b.ml > L) {
+        g.add = b.d_far;
+        g.lda = (int64_t)L * B;
+        g.add_cs = (int)B;
+      }
+      g.force_reduce = true;
+      if (g.i1 <= g.i0) g.i1 = g.i0;  // no near slices: the reduce copies far(t+1)
+      p.add(g, 128, 16);
+    }
+    int rc = p.done();
+    if (rc) return rc;
+  }
+  return GLE_OK;
+}
+
+int prime(gle_handle* h) {
+  // S(t) into S[t&1]: the prime op writes S[0]; copy when t is odd
+  if (!h->op_prime.empty()) {
+    run_op(h, h->op_prime, 0, false);
+    if (h->t & 1)
+      for (auto& b : h->baths)
+        if (b.ml > 1)
+          HIPCHK(h, hipMemcpyAsync(b.d_S + (int64_t)b.ncp * h->B, b.d_S, (size_t)b.ncp * h->B * 8,
+                                   hipMemcpyDeviceToDevice, h->stream));
+  }
+  h->need_prime = false;
+  h->far_due = true;
+  return GLE_OK;
+}
+
+int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
+  if (!h->state_set) return fail(h, GLE_ERR_STATE, "gle_set_state has not been called");
+  for (size_t j = 0; j < h->baths.size(); ++j)
+    if (!h->baths[j].noise_set) return fail(h, GLE_ERR_STATE, "bath " + std::to_string(j) + " has no noise");
+  int rc = 0;
+  if (h->need_prime) {
+    rc = prime(h);
+    if (rc) return rc;
+  }
+  if (h->far_due) {
+    if (!h->op_far.items.empty()) run_op(h, h->op_far, 1, true);
+    h->far_due = false;
+    h->steps_since_far = 0;
+  }
+  const bool need_pot = (fpot_host_T == nullptr) && !h->pot_cache_exact;
+  if (fpot_host_T == nullptr && !h->has_dyn)
+    return fail(h, GLE_ERR_STATE, "no potential force: pass fpot or call gle_set_dyn (md.py:468-470)");
+  Op& op0 = need_pot ? h->op0p : h->op0;
+  run_op(h, op0, 0, h->op_far.items.empty());
+  run_op(h, h->op_near[(h->t + 1) & 1], 0, false);
+  if (fpot_host_T) {
+    HIPCHK(h, hipMemcpyAsync(h->d_Fc, fpot_host_T, (size_t)h->nph * h->B * 8, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipMemsetAsync(h->d_qvalid, 0, (size_t)h->B * 4, h->stream));
+  } else if (need_pot) {
+    launch_potsel(h->d_sd, h->d_Ypot, h->d_Q, (int)h->B, h->stream);
+  }
+  launch_phaseA(h->d_sd, h->d_clk, (int)h->B, (int)h->nph, h->ndblk, h->stream);
+  return GLE_OK;
+}
+
+int step_end_impl(gle_handle* h, const double* fpot_host_T) {
+  if (fpot_host_T) {
+    run_op(h, h->op1a_np, 0, false);
+    HIPCHK(h, hipMemcpyAsync(h->d_Fc, fpot_host_T, (size_t)h->nph * h->B * 8, hipMemcpyHostToDevice, h->stream));
+  } else {
+    if (!h->has_dyn) return fail(h, GLE_ERR_STATE, "no potential force at q~");
+    run_op(h, h->op1a, 0, false);
+    launch_potsel(h->d_sd, h->d_Ypot, h->d_Qt, (int)h->B, h->stream);
+  }
+  launch_phaseB(h->d_sd, h->d_clk, (int)h->B, (int)h->nph, h->ndblk, h->stream);
+  run_op(h, h->op1b, 0, false);
+  launch_phaseC(h->d_sd, h->d_clk, (int)h->B, (int)h->nph, h->ndblk, h->stream);
+  h->t += 1;
+  h->pot_cache_exact = (fpot_host_T == nullptr) && h->constr.empty();
+  if (++h->steps_since_far >= h->L) h->far_due = true;
+  HIPCHK(h, hipGetLastError());
+  return GLE_OK;
+}
+
+// transpose host [B][n] <-> device layout [n][B] (row stride ld >= B)
+void to_dev_layout(const double* src, std::vector<double>& dst, int64_t B, int64_t n, int64_t rows_alloc) {
+  dst.assign((size_t)rows_alloc * B, 0.0);
+  for (int64_t b = 0; b < B; ++b)
+    for (int64_t i = 0; i < n; ++i) dst[(size_t)i * B + b] = src[(size_t)b * n + i];
+}
+
+void from_dev_layout(const std::vector<double>& src, double* dst, int64_t B, int64_t n) {
+  for (int64_t b = 0; b < B; ++b)
+    for (int64_t i = 0; i < n; ++i) dst[(size_t)b * n + i] = src[(size_t)i * B + b];
+}
+
+int download(gle_handle* h, void* dst, const void* src, size_t bytes) {
+  HIPCHK(h, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return GLE_OK;
+}
+
+}  // namespace
+
+// =========================================================================================
+extern "C" {
+
+int gle_abi_version(void) { return GLE_ABI_VERSION; }
+
+const char* gle_last_error(const gle_handle* h) {
+  return h ? h->err.c_str() : g_create_error.c_str();
+}
+
+int gle_device_count(int32_t* count) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    g_create_error = std::string("hipGetDeviceCount: ") + hipGetErrorString(e);
+    if (count) *count = 0;
+    return GLE_ERR_HIP;
+  }
+  if (count) *count = n;
+  return GLE_OK;
+}
+
+int gle_create(const gle_config* cfg, gle_handle** out) {
+  if (!cfg || !out) return fail(nullptr, GLE_ERR_ARG, "null argument");
+  *out = nullptr;
+  if (cfg->nph <= 0 || cfg->ntraj <= 0 || cfg->nmd <= 0 || !(cfg->dt > 0))
+    return fail(nullptr, GLE_ERR_ARG, "nph, ntraj, nmd must be > 0 and dt > 0");
+  if (cfg->nmd % 2) return fail(nullptr, GLE_ERR_ARG, "nmd must be even (functions.py:47-50 length check)");
+  if (cfg->nph > (1 << 24) || cfg->ntraj > (1 << 20)) return fail(nullptr, GLE_ERR_UNSUP, "size too large");
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev == 0)
+    return fail(nullptr, GLE_ERR_HIP, std::string("no HIP device: ") + (e != hipSuccess ? hipGetErrorString(e) : "count 0"));
+  if (cfg->device < 0 || cfg->device >= ndev) return fail(nullptr, GLE_ERR_ARG, "bad device ordinal");
+  e = hipSetDevice(cfg->device);
+  if (e != hipSuccess) return fail(nullptr, GLE_ERR_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
+  gle_handle* h = new gle_handle();
+  h->cfg = *cfg;
+  h->nph = cfg->nph;
+  h->B = cfg->ntraj;
+  h->nmd = cfg->nmd;
+  h->dt = cfg->dt;
+  h->nphp = rup(h->nph, 8);
+  e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete h;
+    return fail(nullptr, GLE_ERR_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+  }
+  const size_t nst = (size_t)(h->nphp + 64) * h->B + 1024;  // row slack for static windows
+  int rc = 0;
+  rc |= dalloc_n(h, &h->d_P, nst);
+  rc |= dalloc_n(h, &h->d_Q, nst);
+  rc |= dalloc_n(h, &h->d_Ph, nst);
+  rc |= dalloc_n(h, &h->d_Qt, nst);
+  rc |= dalloc_n(h, &h->d_Fc, nst);
+  rc |= dalloc_n(h, &h->d_Flast, nst);
+  rc |= dalloc_n(h, &h->d_Q0, nst);
+  rc |= dalloc_n(h, &h->d_Ypot, nst);
+  rc |= dalloc_n(h, &h->d_etot, (size_t)h->nmd * h->B);
+  rc |= dalloc_n(h, &h->d_qvalid, (size_t)h->B);
+  rc |= dalloc_n(h, &h->d_clk, 1);
+  if (rc) {
+    g_create_error = h->err;
+    gle_destroy(h);
+    return GLE_ERR_NOMEM;
+  }
+  // twiddles exp(-2 pi i k / nmd), k < nmd/2 (long double for accuracy)
+  {
+    std::vector<double> tw((size_t)h->nmd);
+    for (int64_t k = 0; k < h->nmd / 2; ++k) {
+      const long double ang = -2.0L * 3.14159265358979323846264338327950288L * (long double)k / (long double)h->nmd;
+      tw[2 * k] = (double)cosl(ang);
+      tw[2 * k + 1] = (double)sinl(ang);
+    }
+    rc = dalloc_n(h, &h->d_tw, (size_t)h->nmd);
+    if (!rc) rc = upload(h, h->d_tw, tw.data(), tw.size() * 8);
+    if (rc) {
+      g_create_error = h->err;
+      gle_destroy(h);
+      return rc;
+    }
+  }
+  *out = h;
+  return GLE_OK;
+}
+
+int gle_destroy(gle_handle* h) {
+  if (!h) return GLE_OK;
+  hipSetDevice(h->cfg.device);
+  if (h->stream) hipStreamSynchronize(h->stream);
+  for (void* p : h->allocs) hipFree(p);
+  for (auto e : h->ev) hipEventDestroy(e);
+  if (h->stream) hipStreamDestroy(h->stream);
+  delete h;
+  return GLE_OK;
+}
+
+int gle_add_bath(gle_handle* h, int32_t kind, const int64_t* cids, int64_t nc, int64_t ml,
+                 const double* kernel, double bias, const double* exim, const double* zeta1,
+                 const double* zeta2, int32_t* bath_id) {
+  if (!h) return GLE_ERR_ARG;
+  if (h->frozen) return fail(h, GLE_ERR_STATE, "baths must be added before the first state/step call");
+  if ((int)h->baths.size() >= MAXBATH) return fail(h, GLE_ERR_UNSUP, "too many baths");
+  if (kind != GLE_BATH_PHONON && kind != GLE_BATH_ELECTRON) return fail(h, GLE_ERR_ARG, "bad bath kind");
+  if (!cids || nc <= 0 || nc > h->nph || ml <= 0 || !kernel) return fail(h, GLE_ERR_ARG, "bad bath shape");
+  if (kind == GLE_BATH_ELECTRON && ml != 1) return fail(h, GLE_ERR_ARG, "electron bath is time-local (ml == 1, baths.py:97)");
+  std::vector<int> seen(h->nph, 0);
+  for (int64_t k = 0; k < nc; ++k) {
+    if (cids[k] < 0 || cids[k] >= h->nph) return fail(h, GLE_ERR_ARG, "cids out of range");
+    if (seen[cids[k]]++) return fail(h, GLE_ERR_ARG, "duplicate DOF in cids");
+  }
+  hipSetDevice(h->cfg.device);
+  Bath b;
+  b.kind = kind;
+  b.nc = (int)nc;
+  b.ncp = (int)rup(nc, 8);
+  b.nrt = (int)((nc + 15) / 16);
+  b.nks = b.ncp / 4;
+  b.ml = (int)ml;
+  b.c = ml > 1 ? h->dt : 1.0;  // baths.py:454-457 (and :235-241)
+  b.cids.assign(cids, cids + nc);
+  b.K.assign(kernel, kernel + ml * nc * nc);
+  // electron-bath bias terms, active only if exim, zeta1, zeta2 are all nonzero (baths.py:233)
+  auto anynz = [&](const double* m) {
+    if (!m) return false;
+    for (int64_t i = 0; i < nc * nc; ++i)
+      if (m[i] != 0.0) return true;
+    return false;
+  };
+  if (kind == GLE_BATH_ELECTRON && anynz(exim) && anynz(zeta1) && anynz(zeta2)) {
+    b.has_q = true;
+    b.Kq.assign((size_t)nc * nc, 0.0);
+    for (int64_t i = 0; i < nc * nc; ++i) {
+      b.K[i] += bias * zeta2[i];                     //  - V zeta2 . p   (baths.py:248-249)
+      b.Kq[i] = -(bias * exim[i] - bias * zeta1[i]);  // + V exim . q - V zeta1 . q (:246-247)
+    }
+  }
+  int rc = 0;
+  {
+    std::vector<double> f = pack_frags(b.K.data(), ml, nc, nc, b.nrt, b.nks);
+    rc = dalloc_n(h, &b.d_K, f.size());
+    if (!rc) rc = upload(h, b.d_K, f.data(), f.size() * 8);
+    if (rc) return rc;
+    if (b.has_q) {
+      std::vector<double> fq = pack_frags(b.Kq.data(), 1, nc, nc, b.nrt, b.nks);
+      rc = dalloc_n(h, &b.d_Kq, fq.size());
+      if (!rc) rc = upload(h, b.d_Kq, fq.data(), fq.size() * 8);
+      if (rc) return rc;
+    }
+  }
+  std::vector<int32_t> inv(h->nph, -1);
+  for (int64_t k = 0; k < nc; ++k) inv[cids[k]] = (int32_t)k;
+  const int64_t B = h->B;
+  const size_t nbuf = (size_t)(b.ncp + 64) * B + 1024;
+  rc |= dalloc_n(h, &b.d_inv, (size_t)h->nph);
+  if (!rc) rc = upload(h, b.d_inv, inv.data(), inv.size() * 4);
+  rc |= dalloc_n(h, &b.d_noise, (size_t)h->nmd * nc * B);
+  rc |= dalloc_n(h, &b.d_Y, nbuf);
+  rc |= dalloc_n(h, &b.d_S, 2 * nbuf);
+  rc |= dalloc_n(h, &b.d_Xcur, nbuf);
+  rc |= dalloc_n(h, &b.d_Xq, nbuf);
+  rc |= dalloc_n(h, &b.d_cur, (size_t)h->nmd * B);
+  if (b.has_q) rc |= dalloc_n(h, &b.d_Yq, nbuf);
+  if (rc) return GLE_ERR_NOMEM;
+  b.K.clear();
+  b.K.shrink_to_fit();
+  h->baths.push_back(std::move(b));
+  if (bath_id) *bath_id = (int32_t)h->baths.size() - 1;
+  return GLE_OK;
+}
+
+int gle_set_dyn(gle_handle* h, const double* dyn) {
+  if (!h || !dyn) return GLE_ERR_ARG;
+  if (h->frozen) return fail(h, GLE_ERR_STATE, "dyn must be set before the first state/step call");
+  hipSetDevice(h->cfg.device);
+  h->dyn_nrt = (int)((h->nph + 15) / 16);
+  h->dyn_nks = (int)(h->nphp / 4);
+  std::vector<double> f = pack_frags(dyn, 1, h->nph, h->nph, h->dyn_nrt, h->dyn_nks);
+  int rc = dalloc_n(h, &h->d_dyn, f.size());
+  if (!rc) rc = upload(h, h->d_dyn, f.data(), f.size() * 8);
+  if (rc) return rc;
+  h->has_dyn = true;
+  return GLE_OK;
+}
+
+int gle_set_constraint(gle_handle* h, const int64_t* dofs, int64_t n) {
+  if (!h || (n > 0 && !dofs) || n < 0) return GLE_ERR_ARG;
+  if (h->frozen) return fail(h, GLE_ERR_STATE, "constraints must be set before the first state/step call");
+  h->constr.clear();
+  for (int64_t i = 0; i < n; ++i) {
+    if (dofs[i] < 0 || dofs[i] >= h->nph) return fail(h, GLE_ERR_ARG, "constraint DOF out of range");
+    h->constr.push_back(dofs[i]);
+  }
+  return GLE_OK;
+}
+
+int gle_set_state(gle_handle* h, const double* p, const double* q, int64_t t) {
+  if (!h || !p || !q) return GLE_ERR_ARG;
+  if (t < 0) return fail(h, GLE_ERR_ARG, "t must be >= 0");
+  hipSetDevice(h->cfg.device);
+  int rc = freeze(h);
+  if (rc) return rc;
+  const int64_t B = h->B, n = h->nph;
+  std::vector<double> tp, tq;
+  to_dev_layout(p, tp, B, n, n);
+  to_dev_layout(q, tq, B, n, n);
+  rc = upload(h, h->d_P, tp.data(), tp.size() * 8);
+  if (!rc) rc = upload(h, h->d_Q, tq.data(), tq.size() * 8);
+  if (rc) return rc;
+  h->t = t;
+  Clock c{};
+  c.t = t;
+  c.t_far = t;
+  rc = upload(h, h->d_clk, &c, sizeof(c));
+  if (rc) return rc;
+  HIPCHK(h, hipMemsetAsync(h->d_qvalid, 0, (size_t)B * 4, h->stream));
+  // p_t into the history ring slot of t; q_t into the q gather
+  for (auto& b : h->baths) {
+    std::vector<double> col((size_t)b.nc * B), colq((size_t)b.ncp * B, 0.0);
+    for (int64_t k = 0; k < b.nc; ++k)
+      for (int64_t j = 0; j < B; ++j) {
+        col[(size_t)k * B + j] = p[(size_t)j * n + b.cids[k]];
+        colq[(size_t)k * B + j] = q[(size_t)j * n + b.cids[k]];
+      }
+    double* d_tmp = nullptr;
+    HIPCHK(h, hipMalloc((void**)&d_tmp, col.size() * 8));
+    hipMemcpyAsync(d_tmp, col.data(), col.size() * 8, hipMemcpyHostToDevice, h->stream);
+    launch_ring_copy(b.d_H, b.ldh, b.R, (int)B, b.nc, t, 1, d_tmp, 0, h->stream);
+    hipMemcpyAsync(b.d_Xq, colq.data(), colq.size() * 8, hipMemcpyHostToDevice, h->stream);
+    hipError_t e = hipStreamSynchronize(h->stream);
+    hipFree(d_tmp);
+    if (e != hipSuccess) return fail(h, GLE_ERR_HIP, std::string("set_state: ") + hipGetErrorString(e));
+  }
+  h->state_set = true;
+  h->need_prime = true;
+  h->pot_cache_exact = false;
+  return GLE_OK;
+}
+
+int gle_get_state(gle_handle* h, double* p, double* q, int64_t* t) {
+  if (!h) return GLE_ERR_ARG;
+  hipSetDevice(h->cfg.device);
+  const int64_t B = h->B, n = h->nph;
+  std::vector<double> buf((size_t)n * B);
+  if (p) {
+    int rc = download(h, buf.data(), h->d_P, buf.size() * 8);
+    if (rc) return rc;
+    from_dev_layout(buf, p, B, n);
+  }
+  if (q) {
+    int rc = download(h, buf.data(), h->d_Q, buf.size() * 8);
+    if (rc) return rc;
+    from_dev_layout(buf, q, B, n);
+  }
+  if (t) *t = h->t;
+  return GLE_OK;
+}
+
+int gle_set_history(gle_handle* h, int32_t bath, const double* phis) {
+  int rc = check_bath(h, bath);
+  if (rc) return rc;
+  if (!h->state_set) return fail(h, GLE_ERR_STATE, "call gle_set_state first (history slots are relative to t)");
+  hipSetDevice(h->cfg.device);
+  Bath& b = h->baths[bath];
+  const int64_t B = h->B;
+  // phis[i] (newest first) is p at time t-1-i (md.phis between steps, md.py:386-387)
+  double* d_tmp = nullptr;
+  if (phis) {
+    std::vector<double> buf((size_t)b.ml * b.nc * B);
+    for (int64_t j = 0; j < B; ++j)
+      for (int64_t i = 0; i < b.ml; ++i)
+        for (int64_t k = 0; k < b.nc; ++k)
+          buf[((size_t)i * b.nc + k) * B + j] = phis[((size_t)j * b.ml + i) * b.nc + k];
+    HIPCHK(h, hipMalloc((void**)&d_tmp, buf.size() * 8));
+    hipMemcpyAsync(d_tmp, buf.data(), buf.size() * 8, hipMemcpyHostToDevice, h->stream);
+    launch_ring_copy(b.d_H, b.ldh, b.R, (int)B, b.nc, h->t - 1, b.ml, d_tmp, 0, h->stream);
+    hipError_t e = hipStreamSynchronize(h->stream);
+    hipFree(d_tmp);
+    if (e != hipSuccess) return fail(h, GLE_ERR_HIP, std::string("set_history: ") + hipGetErrorString(e));
+  } else {
+    launch_ring_copy(b.d_H, b.ldh, b.R, (int)B, b.nc, h->t - 1, b.ml, nullptr, 0, h->stream);
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+  }
+  h->need_prime = true;
+  return GLE_OK;
+}
+
+int gle_get_history(gle_handle* h, int32_t bath, double* phis) {
+  int rc = check_bath(h, bath);
+  if (rc) return rc;
+  if (!phis) return fail(h, GLE_ERR_ARG, "null output");
+  if (!h->frozen) return fail(h, GLE_ERR_STATE, "no state yet");
+  hipSetDevice(h->cfg.device);
+  Bath& b = h->baths[bath];
+  const int64_t B = h->B;
+  std::vector<double> buf((size_t)b.ml * b.nc * B);
+  double* d_tmp = nullptr;
+  HIPCHK(h, hipMalloc((void**)&d_tmp, buf.size() * 8));
+  launch_ring_copy(b.d_H, b.ldh, b.R, (int)B, b.nc, h->t - 1, b.ml, d_tmp, 1, h->stream);
+  hipMemcpyAsync(buf.data(), d_tmp, buf.size() * 8, hipMemcpyDeviceToHost, h->stream);
+  hipError_t e = hipStreamSynchronize(h->stream);
+  hipFree(d_tmp);
+  if (e != hipSuccess) return fail(h, GLE_ERR_HIP, std::string("get_history: ") + hipGetErrorString(e));
+  for (int64_t j = 0; j < B; ++j)
+    for (int64_t i = 0; i < b.ml; ++i)
+      for (int64_t k = 0; k < b.nc; ++k)
+        phis[((size_t)j * b.ml + i) * b.nc + k] = buf[((size_t)i * b.nc + k) * B + j];
+  return GLE_OK;
+}
+
+int gle_get_force(gle_handle* h, double* f) {
+  if (!h || !f) return GLE_ERR_ARG;
+  hipSetDevice(h->cfg.device);
+  std::vector<double> buf((size_t)h->nph * h->B);
+  int rc = download(h, buf.data(), h->d_Flast, buf.size() * 8);
+  if (rc) return rc;
+  from_dev_layout(buf, f, h->B, h->nph);
+  return GLE_OK;
+}
+
+int gle_set_noise(gle_handle* h, int32_t bath, const double* noise) {
+  int rc = check_bath(h, bath);
+  if (rc) return rc;
+  if (!noise) return fail(h, GLE_ERR_ARG, "null noise");
+  hipSetDevice(h->cfg.device);
+  Bath& b = h->baths[bath];
+  const int64_t B = h->B, nmd = h->nmd, nc = b.nc;
+  std::vector<double> buf((size_t)nmd * nc * B);
+  for (int64_t j = 0; j < B; ++j)
+    for (int64_t t = 0; t < nmd; ++t)
+      for (int64_t k = 0; k < nc; ++k) buf[((size_t)t * nc + k) * B + j] = noise[((size_t)j * nmd + t) * nc + k];
+  rc = upload(h, b.d_noise, buf.data(), buf.size() * 8);
+  if (rc) return rc;
+  b.noise_set = true;
+  return GLE_OK;
+}
+
+int gle_get_noise(gle_handle* h, int32_t bath, double* noise) {
+  int rc = check_bath(h, bath);
+  if (rc) return rc;
+  if (!noise) return fail(h, GLE_ERR_ARG, "null output");
+  hipSetDevice(h->cfg.device);
+  Bath& b = h->baths[bath];
+  const int64_t B = h->B, nmd = h->nmd, nc = b.nc;
+  std::vector<double> buf((size_t)nmd * nc * B);
+  rc = download(h, buf.data(), b.d_noise, buf.size() * 8);
+  if (rc) return rc;
+  for (int64_t j = 0; j < B; ++j)
+    for (int64_t t = 0; t < nmd; ++t)
+      for (int64_t k = 0; k < nc; ++k) noise[((size_t)j * nmd + t) * nc + k] = buf[((size_t)t * nc + k) * B + j];
+  return GLE_OK;
+}
+
+int gle_noise_factors(gle_handle* h, int32_t bath, int64_t nfreq, const double* m_re, const double* m_im) {
+  int rc = check_bath(h, bath);
+  if (rc) return rc;
+  if (!m_re || nfreq != h->nmd / 2 + 1) return fail(h, GLE_ERR_ARG, "factors must cover nmd/2+1 frequencies");
+  hipSetDevice(h->cfg.device);
+  Bath& b = h->baths[bath];
+  b.fac_complex = m_im != nullptr;
+  b.fac_rows = b.fac_complex ? 2 * b.nc : b.nc;
+  b.fac_nrt = (b.fac_rows + 15) / 16;
+  b.nfreq = nfreq;
+  std::vector<double> f = pack_frags(m_re, nfreq, b.nc, b.nc, b.fac_nrt, b.nks, m_im);
+  if (b.d_fac) {
+    hipFree(b.d_fac);
+    auto it = std::find(h->allocs.begin(), h->allocs.end(), (void*)b.d_fac);
+    if (it != h->allocs.end()) h->allocs.erase(it);
+    b.d_fac = nullptr;
+  }
+  rc = dalloc_n(h, &b.d_fac, f.size());
+  if (!rc) rc = upload(h, b.d_fac, f.data(), f.size() * 8);
+  return rc;
+}
+
+int gle_noise_generate(gle_handle* h, int32_t bath, const double* x_host, uint64_t seed, uint64_t traj_offset) {
+  int rc = check_bath(h, bath);
+  if (rc) return rc;
+  Bath& b = h->baths[bath];
+  if (!b.d_fac) return fail(h, GLE_ERR_STATE, "gle_noise_factors not set for this bath");
+  hipSetDevice(h->cfg.device);
+  const int64_t B = h->B, nf = b.nfreq, ncp = b.ncp, nc = b.nc;
+  // x [nfreq][ncp][B]
+  double* d_x = nullptr;
+  double* d_a = nullptr;
+  const size_t nx = (size_t)nf * ncp * B + (size_t)(64 + 16) * B + 4096;
+  const size_t na = (size_t)nf * b.fac_rows * B + 4096;
+  HIPCHK(h, hipMalloc((void**)&d_x, nx * 8));
+  if (hipMalloc((void**)&d_a, na * 8) != hipSuccess) {
+    hipFree(d_x);
+    return fail(h, GLE_ERR_NOMEM, "noise work buffers");
+  }
+  auto cleanup = [&]() {
+    hipStreamSynchronize(h->stream);
+    hipFree(d_x);
+    hipFree(d_a);
+  };
+  if (hipMemsetAsync(d_x, 0, nx * 8, h->stream) != hipSuccess) {
+    cleanup();
+    return fail(h, GLE_ERR_HIP, "memset");
+  }
+  if (x_host) {
+    std::vector<double> buf((size_t)nf * ncp * B, 0.0);
+    for (int64_t j = 0; j < B; ++j)
+      for (int64_t w = 0; w < nf; ++w)
+        for (int64_t k = 0; k < nc; ++k) buf[((size_t)w * ncp + k) * B + j] = x_host[((size_t)j * nf + w) * nc + k];
+    hipError_t e = hipMemcpyAsync(d_x, buf.data(), buf.size() * 8, hipMemcpyHostToDevice, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) {
+      cleanup();
+      return fail(h, GLE_ERR_HIP, std::string("upload draws: ") + hipGetErrorString(e));
+    }
+  } else {
+    launch_philox_normal(d_x, nf, ncp, nc, B, seed, traj_offset, h->stream);
+  }
+  // a_w = M_w . x_w  : batched over frequencies (one slice per item)
+  Op op;
+  {
+    Planner p(h, op, rn_for(B));
+    for (int64_t w = 0; w < nf; ++w) {
+      Gemm g{};
+      g.A = b.d_fac + w * 64;
+      g.a_ks = nf * 64;
+      g.a_rt = (int64_t)b.nks * g.a_ks;
+      g.nrt_total = b.fac_nrt;
+      g.nks_total = b.nks;
+      g.i0 = 0;
+      g.i1 = 1;
+      g.X = d_x + (size_t)w * ncp * B;
+      g.ldx = B;
+      g.M = b.fac_rows;
+      g.N = (int)B;
+      g.dst = d_a + (size_t)w * b.fac_rows * B;
+      g.ldd = B;
+      plan_gemm(op, g, 1, 1 << 30);
+    }
+    op.rn = rn_for(B);
+    std::vector<bool> part(op.items.size(), false);
+    // direct-write items only: allocate descriptors temporarily
+    CItem* d_items = nullptr;
+    hipError_t e = hipMalloc((void**)&d_items, op.items.size() * sizeof(CItem));
+    if (e != hipSuccess) {
+      cleanup();
+      return fail(h, GLE_ERR_NOMEM, "noise items");
+    }
+    e = hipMemcpyAsync(d_items, op.items.data(), op.items.size() * sizeof(CItem), hipMemcpyHostToDevice, h->stream);
+    // chunk the grid to stay well inside launch limits
+    const int CH = 1 << 20;
+    for (size_t s = 0; s < op.items.size(); s += CH)
+      launch_contract(op.rn, d_items + s, (int)std::min<size_t>(CH, op.items.size() - s), h->d_clk, h->stream);
+    const double scale = 1.0 / (h->dt * (double)h->nmd);  // dw/2pi (functions.py:51)
+    int frc = launch_fft_noise(d_a, b.d_noise, h->d_tw, h->nmd, nc, b.fac_rows, B, b.fac_complex ? 1 : 0, scale, h->stream);
+    e = hipStreamSynchronize(h->stream);
+    hipFree(d_items);
+    if (frc) {
+      cleanup();
+      return fail(h, GLE_ERR_UNSUP, "device noise FFT needs nmd a power of two <= 8192 (got " + std::to_string(h->nmd) + ")");
+    }
+    if (e != hipSuccess) {
+      cleanup();
+      return fail(h, GLE_ERR_HIP, std::string("noise generation: ") + hipGetErrorString(e));
+    }
+  }
+  cleanup();
+  b.noise_set = true;
+  return GLE_OK;
+}
+
+int gle_step_begin(gle_handle* h, const double* fpot, double* q_tilde_out) {
+  if (!h) return GLE_ERR_ARG;
+  hipSetDevice(h->cfg.device);
+  int rc = 0;
+  if (fpot) {
+    std::vector<double> tf;
+    to_dev_layout(fpot, tf, h->B, h->nph, h->nph);
+    rc = step_begin_impl(h, tf.data());
+    if (!rc) HIPCHK(h, hipStreamSynchronize(h->stream));  // tf goes out of scope
+  } else {
+    rc = step_begin_impl(h, nullptr);
+  }
+  if (rc) return rc;
+  if (q_tilde_out) {
+    std::vector<double> buf((size_t)h->nph * h->B);
+    rc = download(h, buf.data(), h->d_Qt, buf.size() * 8);
+    if (rc) return rc;
+    from_dev_layout(buf, q_tilde_out, h->B, h->nph);
+  }
+  return GLE_OK;
+}
+
+int gle_step_end(gle_handle* h, const double* fpot_qt) {
+  if (!h) return GLE_ERR_ARG;
+  hipSetDevice(h->cfg.device);
+  if (fpot_qt) {
+    std::vector<double> tf;
+    to_dev_layout(fpot_qt, tf, h->B, h->nph, h->nph);
+    int rc = step_end_impl(h, tf.data());
+    if (!rc) HIPCHK(h, hipStreamSynchronize(h->stream));
+    return rc;
+  }
+  return step_end_impl(h, nullptr);
+}
+
+int gle_run(gle_handle* h, int64_t nsteps) {
+  if (!h || nsteps < 0) return GLE_ERR_ARG;
+  hipSetDevice(h->cfg.device);
+  for (int64_t s = 0; s < nsteps; ++s) {
+    int rc = step_begin_impl(h, nullptr);
+    if (rc) return rc;
+    rc = step_end_impl(h, nullptr);
+    if (rc) return rc;
+  }
+  return GLE_OK;
+}
+
+int gle_sync(gle_handle* h) {
+  if (!h) return GLE_ERR_ARG;
+  hipSetDevice(h->cfg.device);
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipGetLastError());
+  return GLE_OK;
+}
+
+int gle_get_current(gle_handle* h, double* cur) {
+  if (!h || !cur) return GLE_ERR_ARG;
+  hipSetDevice(h->cfg.device);
+  const int64_t B = h->B, nmd = h->nmd;
+  std::vector<double> buf((size_t)nmd * B);
+  for (size_t j = 0; j < h->baths.size(); ++j) {
+    int rc = download(h, buf.data(), h->baths[j].d_cur, buf.size() * 8);
+    if (rc) return rc;
+    for (int64_t b = 0; b < B; ++b)
+      for (int64_t t = 0; t < nmd; ++t) cur[((size_t)j * B + b) * nmd + t] = buf[(size_t)t * B + b];
+  }
+  return GLE_OK;
+}
+
+int gle_get_energy(gle_handle* h, double* etot) {
+  if (!h || !etot) return GLE_ERR_ARG;
+  hipSetDevice(h->cfg.device);
+  const int64_t B = h->B, nmd = h->nmd;
+  std::vector<double> buf((size_t)nmd * B);
+  int rc = download(h, buf.data(), h->d_etot, buf.size() * 8);
+  if (rc) return rc;
+  for (int64_t b = 0; b < B; ++b)
+    for (int64_t t = 0; t < nmd; ++t) etot[(size_t)b * nmd + t] = buf[(size_t)t * B + b];
+  return GLE_OK;
+}
+
+int gle_current_sums(gle_handle* h, double* out) {
+  if (!h || !out) return GLE_ERR_ARG;
+  const int64_t B = h->B, nmd = h->nmd;
+  std::vector<double> cur(h->baths.size() * B * nmd);
+  int rc = gle_get_current(h, cur.data());
+  if (rc) return rc;
+  for (size_t j = 0; j < h->baths.size(); ++j) {
+    double s = 0, s2 = 0;
+    for (int64_t b = 0; b < B; ++b) {
+      double m = 0;
+      for (int64_t t = 0; t < nmd; ++t) m += cur[((size_t)j * B + b) * nmd + t];
+      m /= (double)nmd;
+      s += m;
+      s2 += m * m;
+    }
+    out[3 * j] = s;
+    out[3 * j + 1] = s2;
+    out[3 * j + 2] = (double)B;
+  }
+  return GLE_OK;
+}
+
+int gle_profile(gle_handle* h, int32_t enable) {
+  if (!h) return GLE_ERR_ARG;
+  hipSetDevice(h->cfg.device);
+  if (enable && h->ev.empty()) {
+    h->ev.resize(4096);
+    for (auto& e : h->ev) HIPCHK(h, hipEventCreate(&e));
+  }
+  h->prof = enable != 0;
+  h->ev_used = 0;
+  h->prof_n = 0;
+  h->prof_ms = h->prof_flops = h->prof_bytes = 0;
+  return GLE_OK;
+}
+
+int gle_profile_read(gle_handle* h, int64_t* nlaunch, double* total_ms, double* flops, double* bytes) {
+  if (!h) return GLE_ERR_ARG;
+  hipSetDevice(h->cfg.device);
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  for (size_t i = 0; i + 1 < h->ev_used; i += 2) {
+    float ms = 0;
+    HIPCHK(h, hipEventElapsedTime(&ms, h->ev[i], h->ev[i + 1]));
+    h->prof_ms += ms;
+  }
+  h->ev_used = 0;
+  if (nlaunch) *nlaunch = h->prof_n;
+  if (total_ms) *total_ms = h->prof_ms;
+  if (flops) *flops = h->prof_flops;
+  if (bytes) *bytes = h->prof_bytes;
+  return GLE_OK;
+}
+
+int gle_plan_info(gle_handle* h, int64_t* block_len, int64_t* far_items, int64_t* device_bytes) {
+  if (!h) return GLE_ERR_ARG;
+  if (block_len) *block_len = h->frozen ? h->L : 0;
+  if (far_items) *far_items = (int64_t)h->op_far.items.size();
+  if (device_bytes) *device_bytes = (int64_t)h->dev_bytes;
+  return GLE_OK;
+}
+
+}  // extern "C"
