@@ -1,0 +1,207 @@
+#!/usr/bin/env python3
+"""Benchmark of the GLE hot path: trajectory-steps per second on the BASELINE.json workload.
+
+Workload (BASELINE.json metric, configs[2] = SURVEY.md C3): 300-atom chain junction, 2 phonon
+baths with nc = 300 coupled DOF each, 1024-step memory kernel, nmd = 4096, fp64, 64 independent
+trajectories per GPU (weak scaling: C4 = 8 x 64).  A "step" is one md.vv of every trajectory on
+this GPU.  Setup (memory-kernel construction, noise factorisation and generation, H2D) is outside
+the timed region.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU, RCCL reduce)
+
+Prints one JSON line (rank 0).  roofline: the dominant kernel (far-field memory-kernel
+contraction) timed with HIP events on its own stream inside the library over the timed region;
+cpu_baseline: the oracle's reference-equivalent numpy step timed on this host for one trajectory.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense FP64 matrix (AMD spec; == FP64 vector peak)
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_info():
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return model
+
+
+def cpu_baseline(baths_host, dyn, nph, dt, nmd, budget_s=15.0, max_steps=200):
+    """Time the oracle's reference-shaped step (3 memory passes/step, per-slice matvecs,
+    shift-copied history) for ONE trajectory -- the reference runs trajectories one after another
+    (md.py:506), so its ensemble throughput equals this single-trajectory rate."""
+    from oracle import sclmd_oracle as O
+
+    bs = [O.Bath("ph", c, k, n, dt, nmd) for (c, k, n) in baths_host]
+    sim = O.GLE(nph, dt, nmd, bs, dyn=dyn)
+    rng = np.random.default_rng(0)
+    sim.p = rng.normal(size=nph) * 1e-3
+    sim.q = rng.normal(size=nph) * 1e-3
+    sim.step()  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while n < max_steps:
+        sim.step()
+        n += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    el = time.perf_counter() - t0
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.environ.get("OPENBLAS_NUM_THREADS", os.cpu_count() or 1)))
+    return {"value": n / el, "unit": "traj-steps/s", "cores": min(threads, os.cpu_count() or 1),
+            "kind": "port",
+            "sample": "%d md.vv steps of 1 trajectory of the same C3 junction (oracle restatement of "
+                      "sclmd md.vv/phbath.bforce, numpy+OpenBLAS, %s)" % (n, cpu_info())}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--ntraj", type=int, default=64, help="trajectories per GPU")
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--block-len", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
+                    help="PMC-derived HBM bytes per dominant-kernel launch (from a rocprofv3 --pmc pass)")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+
+    from sclmd_amd import md as MD
+    from sclmd_amd import synthetic
+
+    t_setup = time.perf_counter()
+    dyn, axyz, baths, meta = synthetic.junction(args.config, seed=1234)
+    m = MD.md(meta["dt"], meta["nmd"], meta["T"], axyz=axyz, dyn=dyn, ntraj=args.ntraj,
+              seed=1000 + rank * args.ntraj, traj_offset=rank * args.ntraj, device=local_rank,
+              noise_mode="device", block_len=args.block_len, verbose=False)
+    for b in baths:
+        m.AddBath(b)
+    m.initialise()
+    m.ResetHis()
+    for i in range(len(baths)):
+        m.gen_noise(i, 0)
+    st = m._st
+    st.sync()
+    setup_s = time.perf_counter() - t_setup
+    log("[bench] rank %d setup %.1fs plan %s" % (rank, setup_s, st.plan_info()))
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    m.steps(args.warmup)
+    st.sync()
+    st.profile(True)
+    barrier()
+    st.sync()
+    t0 = time.perf_counter()
+    m.steps(args.steps)
+    st.sync()
+    barrier()
+    el = time.perf_counter() - t0
+    prof = st.profile_read()
+    st.profile(False)
+    # one reduce of the time-averaged current statistics (the ensemble output)
+    sums = m._reduce(st.current_sums())
+    if dist is not None:
+        import torch
+
+        tt = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+
+    value = world * args.ntraj * args.steps / el
+    res = {
+        "metric": "GLE steps/sec/GPU, 300-atom junction, 1024-step kernel, 64-traj ensemble",
+        "value": value,
+        "unit": "traj-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded chain junction, gmem kernels, device Philox coloured noise)",
+        "config": {"workload": "%s: %d-atom chain junction, %d phonon baths nc=%s, ml=%d, nmd=%d, "
+                               "%d traj/GPU" % (args.config, meta["natom"], len(baths), meta["nc"],
+                                                meta["ml"], meta["nmd"], args.ntraj),
+                   "ntraj_per_gpu": args.ntraj, "ntraj_total": world * args.ntraj,
+                   "block_len": st.plan_info()["block_len"], "parallelism": "ensemble-dp%d" % world},
+        "value_per_gpu": value / world,
+        "setup_s": setup_s,
+    }
+    if prof["launches"] > 0:
+        avg_ms = prof["ms"] / prof["launches"]
+        fl = prof["flops"] / prof["launches"]
+        by = prof["bytes"] / prof["launches"]
+        ai = fl / max(by, 1.0)
+        ridge = FP64_MFMA_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)
+        if ai >= ridge:
+            roof = {"bound": "mfma", "achieved": fl / (avg_ms * 1e-3) / 1e12, "peak": FP64_MFMA_PEAK_TFLOPS,
+                    "unit": "TFLOP/s"}
+        else:
+            roof = {"bound": "hbm", "achieved": by / (avg_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+        roof["frac"] = roof["achieved"] / roof["peak"]
+        roof["traffic"] = None
+        try:
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+            if tj.get("config") == args.config and tj.get("ntraj") == args.ntraj:
+                roof["traffic"] = tj.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
+        roof.update({"kernel": "contract_kernel (far-field memory-kernel contraction)",
+                     "launches": prof["launches"], "avg_launch_ms": avg_ms,
+                     "algorithmic_flops_per_launch": fl, "algorithmic_bytes_per_launch": by})
+        res["roofline"] = roof
+    kap = sums[:, 0] / sums[:, 2] * 243414.0
+    res["heat_current_nW"] = [float(x) for x in kap]
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        noise = [st.get_noise(i)[0] for i in range(len(baths))]
+        bh = [(b.cids, b.kernel, noise[i]) for i, b in enumerate(baths)]
+        res["cpu_baseline"] = cpu_baseline(bh, m.dyn, meta["nph"], meta["dt"], meta["nmd"], args.cpu_budget)
+        res["speedup_vs_cpu_baseline"] = value / res["cpu_baseline"]["value"]
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    m.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,254 @@
+"""Bath models with sclmd's API (sclmd/baths.py): ebath (time-local electron bath with bias terms)
+and phbath (phonon bath with a memory kernel).
+
+The bath objects hold parameters, the friction kernel and the noise factorisation.  Their forces
+(bforce, baths.py:224-255 / 448-458) are evaluated inside the HIP stepper, not here.
+Deviation: invalid shapes raise ValueError instead of print + sys.exit (baths.py:115-116, ...).
+"""
+import os
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+from . import noise as _noise
+from .functions import antisymmetrize, chkShape, flinterp_many, symmetrize
+
+
+def gamt(tl, wl, gwl, gam, eta_ad=0):
+    """Friction kernel in time, K(t) = (2 wl[-1]/pi) mean_w Gamma(w) cos(w t) (baths.py:19-52),
+    evaluated as one matrix product cos(w t) . Gamma(w) over all times and frequencies."""
+    tl = np.asarray(tl, dtype=float)
+    wl = np.asarray(wl, dtype=float)
+    g = flinterp_many(wl, gwl, gam)            # (nw, nc, nc)
+    shape = g.shape[1:]
+    g2 = g.reshape(len(wl), -1)
+    nw = len(wl)
+    if eta_ad == 0:
+        c = np.cos(np.outer(tl, wl))
+        k = (c @ g2) * (2.0 * wl[-1] / np.pi / nw)
+    else:
+        w = wl[None, :]
+        tt = tl[:, None]
+        c = (w / (w - 1j * eta_ad) * np.exp(-1j * w * tt - eta_ad * tt)
+             + w / (w + 1j * eta_ad) * np.exp(1j * w * tt - eta_ad * tt))
+        k = (np.real(c) @ g2) * (wl[-1] / np.pi / nw)
+    return np.real(k).reshape((len(tl),) + shape)
+
+
+def _eigh_stack(spec):
+    """eigh of a stack of matrices; large stacks are split over threads (numpy releases the GIL)."""
+    n = spec.shape[0]
+    if spec.shape[-1] < 64 or n < 64:
+        return _noise.NoiseFactor(spec)
+    nthr = min(16, os.cpu_count() or 1)
+    parts = np.array_split(np.arange(n), 4 * nthr)
+    try:
+        from threadpoolctl import threadpool_limits
+        lim = threadpool_limits(1)   # one BLAS thread per worker: no oversubscription
+    except Exception:  # pragma: no cover
+        lim = None
+    try:
+        with ThreadPoolExecutor(nthr) as ex:
+            res = list(ex.map(lambda ix: np.linalg.eigh(spec[ix]), parts))
+    finally:
+        if lim is not None:
+            lim.restore_original_limits()
+    f = _noise.NoiseFactor.__new__(_noise.NoiseFactor)
+    f.nfreq, f.nc = n, spec.shape[1]
+    f.evals = np.concatenate([r[0] for r in res])
+    f.evecs = np.concatenate([r[1] for r in res])
+    f.pos = f.evals > 0
+    f.sigma = np.sqrt(np.where(f.pos, f.evals, 0.0))
+    f.complex = np.iscomplexobj(f.evecs)
+    return f
+
+
+class _BathBase:
+    kind = None
+
+    def _noise_key(self):
+        raise NotImplementedError
+
+    def noise_factor(self):
+        """Eigendecomposition of the noise spectrum, cached until a parameter changes."""
+        key = self._noise_key()
+        if getattr(self, "_fac_key", None) != key:
+            self._fac = _eigh_stack(self._spectrum())
+            self._fac_key = key
+        return self._fac
+
+    @property
+    def noise(self):
+        src = getattr(self, "_noise_src", None)
+        if src is not None:  # realisation lives on the device of an md object
+            stepper, bid = src
+            n = stepper.get_noise(bid)
+            return n[0] if n.shape[0] == 1 else n
+        return self._noise_host
+
+    @noise.setter
+    def noise(self, value):
+        self._noise_host = None if value is None else np.asarray(value, dtype=float)
+        self._noise_src = None
+        self._noise_version = getattr(self, "_noise_version", 0) + 1
+
+    def gnoi(self):
+        """Generate one realisation with the global numpy RNG (reference draw order) on the device."""
+        if self.nmd is None or self.dt is None:
+            raise ValueError("%s.gnoi: dt and nmd must be set" % type(self).__name__)
+        self.noise = _noise.generate(self.noise_factor(), self.dt, self.nmd)[0]
+
+    def SetMDsteps(self, dt, nmd):
+        self.dt, self.nmd = dt, nmd
+        self.cur = np.zeros(nmd)
+
+
+class ebath(_BathBase):
+    """Electron bath (baths.py:55-255).  cats are DOF indices (baths.py:80)."""
+
+    kind = "ebath"
+
+    def __init__(self, cats, T, dt, nmd, wmax=None, nw=None, bias=0., efric=None, exim=None,
+                 exip=None, zeta1=None, zeta2=None, classical=False, zpmotion=True):
+        self.cats = np.array(cats, dtype=int)
+        self.cids = np.array(cats, dtype=int)
+        self.nc = len(self.cids)
+        self.T, self.wmax = T, wmax
+        self.nw, self.bias = nw, bias
+        self.dt, self.nmd = dt, nmd
+        self.cur = np.zeros(nmd)
+        self.classical = classical
+        self.zpmotion = zpmotion
+        self.wl = None if (nw is None or wmax is None) else [self.wmax * i / nw for i in range(nw)]
+        self.CheckEmat(efric, exim, exip, zeta1, zeta2)
+        self.ml = 1
+        self.noise = None
+
+    def CheckEmat(self, efric=None, exim=None, exip=None, zeta1=None, zeta2=None):
+        """Symmetrise efric/exip/zeta1, antisymmetrise exim/zeta2 (baths.py:100-174)."""
+        if efric is None:
+            self.efric = self.kernel = self.exim = self.exip = self.zeta1 = self.zeta2 = None
+            self.ebath = False
+            return
+        n = chkShape(efric)
+        if n != self.nc:
+            raise ValueError("ebath.CheckEmat: efric shape error")
+        self.efric = symmetrize(efric)
+        self.kernel = np.array([self.efric])
+        z = np.zeros((n, n))
+        self.exip, self.exim, self.zeta1, self.zeta2 = z.copy(), z.copy(), z.copy(), z.copy()
+        self.ebath = True
+        for name, m, op in (("exim", exim, antisymmetrize), ("exip", exip, symmetrize),
+                            ("zeta1", zeta1, symmetrize), ("zeta2", zeta2, antisymmetrize)):
+            if m is not None:
+                if chkShape(m) != self.nc:
+                    raise ValueError("ebath.CheckEmat: the dimension of %s is wrong" % name)
+                setattr(self, name, op(m))
+
+    def setbias(self, bias=0.0):
+        self.bias = bias
+
+    def biased(self):
+        """Bias friction terms are active only if exim, zeta1, zeta2 are all nonzero (baths.py:233)."""
+        return bool(self.exim.any() and self.zeta1.any() and self.zeta2.any())
+
+    def _noise_key(self):
+        return ("e", self.T, self.bias, self.wmax, self.dt, self.nmd, self.classical, self.zpmotion,
+                id(self.efric), id(self.exim), id(self.exip))
+
+    def _spectrum(self):
+        if not self.ebath:
+            raise ValueError("ebath.gnoi: ebath is False (no efric)")
+        return _noise.electron_spectrum(self.efric, self.exim, self.exip, self.bias, self.T, self.wmax,
+                                        self.dt, self.nmd, self.classical, self.zpmotion)
+
+
+class phbath(_BathBase):
+    """Phonon bath (baths.py:258-458)."""
+
+    kind = "phbath"
+
+    def __init__(self, T, cats, debye, nw, dt, nmd, ml=None, mcof=2.0, sig=None, gamma=None, gwl=None,
+                 K00=None, K01=None, V01=None, eta_ad=0, classical=False, zpmotion=True):
+        self.classical = classical
+        self.zpmotion = zpmotion
+        self.T, self.debye, self.cats = T, debye, np.array(cats, dtype=int)
+        self.K00, self.K01, self.V01 = K00, K01, V01
+        self.dt, self.nmd, self.ml = dt, nmd, ml
+        self.kernel = None
+        self.cids = np.array(cats, dtype=int)
+        self.nc = len(self.cids)
+        self.wmax = mcof * debye
+        self.local = False
+        self.nw = nw
+        self.wl = [self.wmax * i / nw for i in range(nw)]
+        self.gamma = gamma
+        self.sig = sig
+        self.gwl = gwl
+        self.cur = np.zeros(nmd)
+        self.eta_ad = eta_ad
+        self.noise = None
+        if self.UseK():
+            raise NotImplementedError("phbath: self-energy from K00/K01/V01 is not implemented "
+                                      "(the reference exits here too, baths.py:316-320)")
+        elif self.UseG() or self.UsePi():
+            if self.UsePi():
+                if len(self.sig[0]) != self.nc:
+                    raise ValueError("phbath: inconsistent cids and sig")
+                self.ggamma()
+            if len(self.gamma[0]) != self.nc:
+                raise ValueError("phbath: inconsistent cids and gamma")
+        else:
+            # Debye model, time-local friction (baths.py:333-340)
+            self.gamma = np.array([np.diag(debye * np.pi / 6.0 + np.zeros(int(self.nc)))])
+            self.gwl = np.array([0])
+            self.local = True
+            self.ml = 1
+
+    def SetMemlen(self, len):
+        self.ml = len
+
+    def SetT(self, T):
+        self.T = T
+
+    def UseG(self):
+        return self.gamma is not None and self.gwl is not None
+
+    def UsePi(self):
+        return self.sig is not None and self.gwl is not None
+
+    def UseK(self):
+        return self.K00 is not None and self.K01 is not None and self.V01 is not None
+
+    def ggamma(self):
+        """Gamma(w) = -Im Sigma(w) / w, w = 0 taking the next point's value (baths.py:375-395)."""
+        sig, wl = np.asarray(self.sig), self.gwl
+        a = []
+        for i in range(len(wl)):
+            j = i + 1 if wl[i] == 0 else i
+            a.append(-np.imag(sig[j]) / wl[j])
+        self.gamma = np.array(a)
+
+    def gmem(self):
+        """Memory kernel K_i = gamt(dt*i) for i < ml (baths.py:412-445)."""
+        if self.ml is None or self.dt is None:
+            raise ValueError("phbath.gmem: length of memory kernel not set")
+        if self.local:
+            self.ml = 1
+            self.kernel = self.gamma
+            return
+        tl = [self.dt * i for i in range(self.ml)]
+        self.kernel = gamt(tl, self.wl, self.gwl, self.gamma, self.eta_ad)
+        if self.eta_ad != 0:
+            c = np.cos(np.outer(np.asarray(self.gwl, dtype=float), np.asarray(tl))) * self.dt
+            g = c @ self.kernel.reshape(len(tl), -1)
+            self.gammaOld = self.gamma
+            self.gamma = np.real(g).reshape(np.shape(self.gammaOld))
+
+    def _noise_key(self):
+        return ("ph", self.T, self.wmax, self.dt, self.nmd, self.classical, self.zpmotion,
+                id(self.gamma), id(self.gwl))
+
+    def _spectrum(self):
+        return _noise.phonon_spectrum(self.gamma, self.gwl, self.T, self.wmax, self.dt, self.nmd,
+                                      self.classical, self.zpmotion)

@@ -29,6 +29,8 @@ thread_local std::string g_create_error;
 
 struct Op {
   int rn = 1;
+  int cu = 1;          // staged X columns per thread per row (contract_kernel template)
+  int max_elems = 0;   // largest reduce tile
   std::vector<CItem> items;
   std::vector<RItem> ritems;
   CItem* d_items = nullptr;
@@ -79,6 +81,7 @@ struct gle_handle {
   uint8_t* d_cmask = nullptr;
   double *d_P = nullptr, *d_Q = nullptr, *d_Ph = nullptr, *d_Qt = nullptr, *d_Fc = nullptr;
   double *d_Flast = nullptr, *d_etot = nullptr, *d_Q0 = nullptr, *d_part = nullptr, *d_Ypot = nullptr;
+  double* d_pdiff = nullptr;
   int32_t* d_qvalid = nullptr;
   Clock* d_clk = nullptr;
   StepDev* d_sd = nullptr;
@@ -90,6 +93,7 @@ struct gle_handle {
   int steps_since_far = 0;
   bool far_due = true;
   bool pot_cache_exact = false;  // q_t == q~_{t-1} bitwise (no constraints): id0 cache hit
+  bool host_force_step = false;
   Op op_far, op_prime, op0, op0p, op1a, op1a_np, op1b;
   Op op_near[2];  // S(t+1) into S[(t+1)&1]: one plan per destination parity
   std::vector<void*> allocs;
@@ -287,6 +291,15 @@ void plan_gemm(Op& op, const Gemm& g, int target_items, int min_work) {
 // Fix up partial-slot offsets once the partial buffer exists.  Items that write partials were
 // tagged with ldo == NT and an offset pointer smaller than the partial size.
 int materialize(gle_handle* h, Op& op, const std::vector<bool>& is_partial) {
+  // staged window width -> registers per thread for the next-stage prefetch
+  int maxww = 16 * op.rn;
+  for (const auto& it : op.items) {
+    const int ww = it.ring ? (it.ni - 1) * it.cs + 16 * op.rn : 16 * op.rn;
+    maxww = std::max(maxww, std::min(ww, LDS_WW_MAX));
+  }
+  const int cap = op.rn >= 16 ? 3 : 4;
+  op.cu = std::max(1, std::min(cap, (maxww + 255) / 256));
+  for (const auto& r : op.ritems) op.max_elems = std::max(op.max_elems, r.rows * r.cols);
   if (op.partial_doubles) {
     int rc = dalloc_n(h, &op.partial, op.partial_doubles);
     if (rc) return rc;
@@ -343,14 +356,14 @@ void run_op(gle_handle* h, Op& op, int set_tfar, bool profile) {
     h->ev_used += 2;
     hipEventRecord(e0, h->stream);
   }
-  launch_contract(op.rn, op.d_items, (int)op.items.size(), h->d_clk, h->stream);
+  launch_contract(op.rn, op.cu, op.d_items, (int)op.items.size(), h->d_clk, h->stream);
   if (e1) {
     hipEventRecord(e1, h->stream);
     h->prof_n += 1;
     h->prof_flops += op.flops;
     h->prof_bytes += op.bytes;
   }
-  launch_reduce(op.d_ritems, (int)op.ritems.size(), h->d_clk, set_tfar, h->stream);
+  launch_reduce(op.d_ritems, (int)op.ritems.size(), op.max_elems, h->d_clk, set_tfar, h->stream);
 }
 
 int check_bath(gle_handle* h, int32_t b) {
@@ -406,6 +419,7 @@ int freeze(gle_handle* h) {
   sd.etot = h->d_etot;
   sd.Q0 = h->d_Q0;
   sd.qvalid = h->d_qvalid;
+  sd.Ypot = h->d_Ypot;
   // DOF chunking of the phase kernels: ~ one 256-thread block per 64x(256/BT) elements
   const int BT = (int)std::min<int64_t>(B, 64);
   const int DL = 256 / BT;
@@ -417,6 +431,9 @@ int freeze(gle_handle* h) {
   int rc = dalloc_n(h, &h->d_part, (size_t)h->ndblk * (h->baths.size() + 1) * B);
   if (rc) return rc;
   sd.part = h->d_part;
+  rc = dalloc_n(h, &h->d_pdiff, (size_t)2 * h->ndblk * B);
+  if (rc) return rc;
+  sd.pdiff = h->d_pdiff;
   // constraint mask
   std::vector<uint8_t> mask(h->nph, 0);
   for (auto d : h->constr) mask[d] = 1;
@@ -450,7 +467,7 @@ int freeze(gle_handle* h) {
   if (rc) return rc;
 
   // ---- plans
-  const int TGT_STEP = 128, TGT_BIG = 512;
+  const int TGT_STEP = 256, TGT_BIG = 512;
   auto kgemm = [&](Bath& b, const double* A, int i0, int i1, const double* X, int64_t ldx, int ring,
                    int tshift, int N, double* dst, int64_t ldd) {
     Gemm g{};
@@ -502,12 +519,12 @@ int freeze(gle_handle* h) {
     Op& op = variant ? h->op0p : h->op0;
     Planner p(h, op, rn_step);
     for (auto& b : h->baths) {
-      p.add(kgemm(b, b.d_K, 0, 1, b.d_H, b.ldh, b.R, 0, (int)B, b.d_Y, B), TGT_STEP, 16);
+      p.add(kgemm(b, b.d_K, 0, 1, b.d_H, b.ldh, b.R, 0, (int)B, b.d_Y, B), TGT_STEP, 4);
       if (b.has_q) {
         Gemm g = kgemm(b, b.d_Kq, 0, 1, b.d_Xq, B, 0, 0, (int)B, b.d_Yq, B);
         g.a_ks = 64;
         g.a_rt = (int64_t)b.nks * 64;
-        p.add(g, TGT_STEP, 16);
+        p.add(g, TGT_STEP, 4);
       }
     }
     if (variant && h->has_dyn) {
@@ -525,7 +542,7 @@ int freeze(gle_handle* h) {
       g.N = (int)B;
       g.dst = h->d_Ypot;
       g.ldd = B;
-      p.add(g, TGT_STEP, 16);
+      p.add(g, TGT_STEP, 4);
     }
     rc = p.done();
     if (rc) return rc;
@@ -538,12 +555,12 @@ int freeze(gle_handle* h) {
       Gemm g = kgemm(b, b.d_K, 0, 1, b.d_Xcur, B, 0, 0, (int)B, b.d_Y, B);
       g.a_ks = (int64_t)b.ml * 64;
       g.a_rt = (int64_t)b.nks * g.a_ks;
-      p.add(g, TGT_STEP, 16);
+      p.add(g, TGT_STEP, 4);
       if (b.has_q && variant < 2) {
         Gemm gq = kgemm(b, b.d_Kq, 0, 1, b.d_Xq, B, 0, 0, (int)B, b.d_Yq, B);
         gq.a_ks = 64;
         gq.a_rt = (int64_t)b.nks * 64;
-        p.add(gq, TGT_STEP, 16);
+        p.add(gq, TGT_STEP, 4);
       }
     }
     if (variant == 0 && h->has_dyn) {
@@ -561,7 +578,7 @@ int freeze(gle_handle* h) {
       g.N = (int)B;
       g.dst = h->d_Ypot;
       g.ldd = B;
-      p.add(g, TGT_STEP, 16);
+      p.add(g, TGT_STEP, 4);
     }
     rc = p.done();
     if (rc) return rc;
@@ -605,7 +622,7 @@ int build_near(gle_handle* h) {
       }
       g.force_reduce = true;
       if (g.i1 <= g.i0) g.i1 = g.i0;  // no near slices: the reduce copies far(t+1)
-      p.add(g, 128, 16);
+      p.add(g, 256, 4);
     }
     int rc = p.done();
     if (rc) return rc;
@@ -648,28 +665,27 @@ int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
   Op& op0 = need_pot ? h->op0p : h->op0;
   run_op(h, op0, 0, h->op_far.items.empty());
   run_op(h, h->op_near[(h->t + 1) & 1], 0, false);
-  if (fpot_host_T) {
+  if (fpot_host_T)
     HIPCHK(h, hipMemcpyAsync(h->d_Fc, fpot_host_T, (size_t)h->nph * h->B * 8, hipMemcpyHostToDevice, h->stream));
-    HIPCHK(h, hipMemsetAsync(h->d_qvalid, 0, (size_t)h->B * 4, h->stream));
-  } else if (need_pot) {
-    launch_potsel(h->d_sd, h->d_Ypot, h->d_Q, (int)h->B, h->stream);
-  }
-  launch_phaseA(h->d_sd, h->d_clk, (int)h->B, (int)h->nph, h->ndblk, h->stream);
+  launch_phaseA(h->d_sd, h->d_clk, (int)h->B, h->ndblk, need_pot ? 1 : 0, fpot_host_T ? 0 : 1, h->stream);
+  h->host_force_step = fpot_host_T != nullptr;
   return GLE_OK;
 }
 
 int step_end_impl(gle_handle* h, const double* fpot_host_T) {
+  int mode1 = 1;
   if (fpot_host_T) {
     run_op(h, h->op1a_np, 0, false);
     HIPCHK(h, hipMemcpyAsync(h->d_Fc, fpot_host_T, (size_t)h->nph * h->B * 8, hipMemcpyHostToDevice, h->stream));
+    mode1 = 0;
   } else {
     if (!h->has_dyn) return fail(h, GLE_ERR_STATE, "no potential force at q~");
+    if (h->host_force_step) return fail(h, GLE_ERR_STATE, "step begun with a host force must end with one");
     run_op(h, h->op1a, 0, false);
-    launch_potsel(h->d_sd, h->d_Ypot, h->d_Qt, (int)h->B, h->stream);
   }
-  launch_phaseB(h->d_sd, h->d_clk, (int)h->B, (int)h->nph, h->ndblk, h->stream);
+  launch_phaseB(h->d_sd, h->d_clk, (int)h->B, h->ndblk, mode1, h->stream);
   run_op(h, h->op1b, 0, false);
-  launch_phaseC(h->d_sd, h->d_clk, (int)h->B, (int)h->nph, h->ndblk, h->stream);
+  launch_phaseC(h->d_sd, h->d_clk, (int)h->B, h->ndblk, mode1, mode1, h->stream);
   h->t += 1;
   h->pot_cache_exact = (fpot_host_T == nullptr) && h->constr.empty();
   if (++h->steps_since_far >= h->L) h->far_due = true;
@@ -1145,7 +1161,7 @@ int gle_noise_generate(gle_handle* h, int32_t bath, const double* x_host, uint64
     // chunk the grid to stay well inside launch limits
     const int CH = 1 << 20;
     for (size_t s = 0; s < op.items.size(); s += CH)
-      launch_contract(op.rn, d_items + s, (int)std::min<size_t>(CH, op.items.size() - s), h->d_clk, h->stream);
+      launch_contract(op.rn, 1, d_items + s, (int)std::min<size_t>(CH, op.items.size() - s), h->d_clk, h->stream);
     const double scale = 1.0 / (h->dt * (double)h->nmd);  // dw/2pi (functions.py:51)
     int frc = launch_fft_noise(d_a, b.d_noise, h->d_tw, h->nmd, nc, b.fac_rows, B, b.fac_complex ? 1 : 0, scale, h->stream);
     e = hipStreamSynchronize(h->stream);

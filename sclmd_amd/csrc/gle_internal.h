@@ -91,6 +91,8 @@ struct StepDev {
   double *P, *Q, *Ph, *Qt, *G, *Fc, *Flast, *etot;
   double* Q0;             // last q the potential force was evaluated at (md.q0)
   int32_t* qvalid;        // [B] md.q0 != [] flag
+  double* Ypot;           // dyn . x of the latest potential product [nph][B]
+  double* pdiff;          // [2][ndblk][B] partial max |x - q0| (slot 0: id0, slot 1: id1)
   double* part;           // [ndblk][nbath+1][B] current / energy partial sums
   const uint8_t* cmask;   // [nph] constraint mask
   int32_t ndblk;          // DOF chunks of the phase kernels
@@ -99,12 +101,14 @@ struct StepDev {
 };
 
 // launchers (gle_kernels.hip)
-void launch_contract(int rn, const CItem* items, int nitems, const Clock* clk, hipStream_t s);
-void launch_reduce(const RItem* items, int nitems, const Clock* clk, int set_tfar, hipStream_t s);
-void launch_potsel(const StepDev* sd, const double* Y, const double* X, int B, hipStream_t s);
-void launch_phaseA(const StepDev* sd, const Clock* clk, int B, int nph, int ndblk, hipStream_t s);
-void launch_phaseB(const StepDev* sd, const Clock* clk, int B, int nph, int ndblk, hipStream_t s);
-void launch_phaseC(const StepDev* sd, Clock* clk, int B, int nph, int ndblk, hipStream_t s);
+void launch_contract(int rn, int cu, const CItem* items, int nitems, const Clock* clk, hipStream_t s);
+void launch_reduce(const RItem* items, int nitems, int max_elems, const Clock* clk, int set_tfar,
+                   hipStream_t s);
+void launch_phaseA(const StepDev* sd, const Clock* clk, int B, int ndblk, int mode0, int diff1,
+                   hipStream_t s);
+void launch_phaseB(const StepDev* sd, const Clock* clk, int B, int ndblk, int mode1, hipStream_t s);
+void launch_phaseC(const StepDev* sd, Clock* clk, int B, int ndblk, int mode1, int diff0,
+                   hipStream_t s);
 void launch_philox_normal(double* x, int64_t nfreq, int64_t ncp, int64_t nc, int64_t B,
                           uint64_t seed, uint64_t traj_offset, hipStream_t s);
 void launch_ring_copy(double* H, int64_t ldh, int R, int B, int nc, int64_t tau0, int nt, double* buf,

@@ -33,11 +33,17 @@ __device__ __forceinline__ int64_t load_t(const Clock* clk) {
 
 // ------------------------------------------------------------------------------------------
 // contraction
-template <int RN>
+//
+// Per work item: for each k-stage (KC = 2 k-steps = 8 rows of X), the window of X columns that all
+// slices of the current slice-chunk need is staged in LDS; while the MFMAs of stage s run, the
+// next stage's X columns (CU per thread per row) and the first A fragments are already in flight
+// into registers (software pipelining without a second LDS buffer).
+template <int RN, int CU>
 __global__ __launch_bounds__(WG, 2) void contract_kernel(const CItem* __restrict__ items,
                                                          const Clock* __restrict__ clk) {
   __shared__ double lds[KROWS * LDS_COLS];
   constexpr int NT = 16 * RN;
+  constexpr int WWCAP = (256 * CU < LDS_WW_MAX) ? 256 * CU : LDS_WW_MAX;
   const CItem it = items[blockIdx.x];
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
@@ -48,11 +54,12 @@ __global__ __launch_bounds__(WG, 2) void contract_kernel(const CItem* __restrict
 #pragma unroll
   for (int n = 0; n < RN; ++n) acc[n] = d4{0.0, 0.0, 0.0, 0.0};
 
-  const int ns_max = it.ring ? (LDS_WW_MAX - NT) / it.cs + 1 : 1;
+  const int ns_max = it.ring ? (WWCAP - NT) / it.cs + 1 : 1;
   const bool active = wave < it.nrt;
   const double* Aw = it.A + (int64_t)wave * it.a_rt + lane;
   const int brow = lane >> 4;
   const int bcol = lane & 15;
+  const int nst = it.nks / KC;
 
   for (int s0 = 0; s0 < it.ni; s0 += ns_max) {
     const int ns = min(ns_max, it.ni - s0);
@@ -64,25 +71,60 @@ __global__ __launch_bounds__(WG, 2) void contract_kernel(const CItem* __restrict
       const int64_t tau = t + it.tshift - (int64_t)(it.ia + s0 + ns - 1);
       wbase += pmod(tau, it.ring) * it.cs;
     }
-    for (int kc = 0; kc < it.nks; kc += KC) {
-      __syncthreads();
-      const double* xs = it.X + (int64_t)(4 * kc) * it.ldx + wbase;
+    const double* xs0 = it.X + wbase;
+    const double* As0 = Aw + (int64_t)s0 * 64;
+    double xr[KROWS * CU];
+    double na0 = 0.0, na1 = 0.0;
+    // prefetch stage 0
 #pragma unroll
-      for (int r = 0; r < KROWS; ++r) {
-        const double* xr = xs + (int64_t)r * it.ldx;
-        double* lr = lds + r * wwp;
-        for (int c = tid; c < ww; c += WG) lr[c] = xr[c];
+    for (int r = 0; r < KROWS; ++r)
+#pragma unroll
+      for (int u = 0; u < CU; ++u) {
+        const int c = tid + WG * u;
+        xr[r * CU + u] = (c < ww) ? xs0[(int64_t)r * it.ldx + c] : 0.0;
       }
+    if (active) {
+      na0 = As0[0];
+      na1 = As0[it.a_ks];
+    }
+    for (int st = 0; st < nst; ++st) {
+      __syncthreads();  // previous stage's LDS reads are done
+#pragma unroll
+      for (int r = 0; r < KROWS; ++r)
+#pragma unroll
+        for (int u = 0; u < CU; ++u) {
+          const int c = tid + WG * u;
+          if (c < ww) lds[r * wwp + c] = xr[r * CU + u];
+        }
       __syncthreads();
+      double a0 = na0, a1 = na1;
+      const double* Ak = As0 + (int64_t)(st * KC) * it.a_ks;
+      if (st + 1 < nst) {  // next stage in flight during this stage's MFMAs
+        const double* xs = xs0 + (int64_t)(4 * KC * (st + 1)) * it.ldx;
+#pragma unroll
+        for (int r = 0; r < KROWS; ++r)
+#pragma unroll
+          for (int u = 0; u < CU; ++u) {
+            const int c = tid + WG * u;
+            xr[r * CU + u] = (c < ww) ? xs[(int64_t)r * it.ldx + c] : 0.0;
+          }
+        if (active) {
+          na0 = Ak[KC * it.a_ks];
+          na1 = Ak[(KC + 1) * it.a_ks];
+        }
+      }
       if (active) {
-        const double* Ak = Aw + (int64_t)kc * it.a_ks + (int64_t)s0 * 64;
-        double a0 = Ak[0];
-        double a1 = Ak[it.a_ks];
+        // A fragments run two slices ahead of the MFMAs that consume them
+        double m0 = 0.0, m1 = 0.0;
+        if (ns > 1) {
+          m0 = Ak[64];
+          m1 = Ak[it.a_ks + 64];
+        }
         for (int ss = 0; ss < ns; ++ss) {
           double n0 = 0.0, n1 = 0.0;
-          if (ss + 1 < ns) {
-            n0 = Ak[(ss + 1) * 64];
-            n1 = Ak[it.a_ks + (ss + 1) * 64];
+          if (ss + 2 < ns) {
+            n0 = Ak[(ss + 2) * 64];
+            n1 = Ak[it.a_ks + (ss + 2) * 64];
           }
           const int off = (ns - 1 - ss) * it.cs;
           const double* b0 = lds + brow * wwp + off + bcol;
@@ -93,8 +135,10 @@ __global__ __launch_bounds__(WG, 2) void contract_kernel(const CItem* __restrict
 #pragma unroll
           for (int n = 0; n < RN; ++n)
             acc[n] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1[16 * n], acc[n], 0, 0, 0);
-          a0 = n0;
-          a1 = n1;
+          a0 = m0;
+          a1 = m1;
+          m0 = n0;
+          m1 = n1;
         }
       }
     }
@@ -113,45 +157,97 @@ __global__ __launch_bounds__(WG, 2) void contract_kernel(const CItem* __restrict
   }
 }
 
-void launch_contract(int rn, const CItem* items, int nitems, const Clock* clk, hipStream_t s) {
-  if (nitems <= 0) return;
+template <int RN>
+static void launch_rn(int cu, const CItem* items, int nitems, const Clock* clk, hipStream_t s) {
   dim3 g(nitems), b(WG);
+  switch (cu) {
+    case 1: contract_kernel<RN, 1><<<g, b, 0, s>>>(items, clk); break;
+    case 2: contract_kernel<RN, 2><<<g, b, 0, s>>>(items, clk); break;
+    case 3: contract_kernel<RN, 3><<<g, b, 0, s>>>(items, clk); break;
+    default: contract_kernel<RN, 4><<<g, b, 0, s>>>(items, clk); break;
+  }
+}
+
+void launch_contract(int rn, int cu, const CItem* items, int nitems, const Clock* clk, hipStream_t s) {
+  if (nitems <= 0) return;
   switch (rn) {
-    case 1: contract_kernel<1><<<g, b, 0, s>>>(items, clk); break;
-    case 2: contract_kernel<2><<<g, b, 0, s>>>(items, clk); break;
-    case 4: contract_kernel<4><<<g, b, 0, s>>>(items, clk); break;
-    case 8: contract_kernel<8><<<g, b, 0, s>>>(items, clk); break;
-    default: contract_kernel<16><<<g, b, 0, s>>>(items, clk); break;
+    case 1: launch_rn<1>(cu, items, nitems, clk, s); break;
+    case 2: launch_rn<2>(cu, items, nitems, clk, s); break;
+    case 4: launch_rn<4>(cu, items, nitems, clk, s); break;
+    case 8: launch_rn<8>(cu, items, nitems, clk, s); break;
+    default: launch_rn<16>(cu, items, nitems, clk, s); break;
   }
 }
 
 // ------------------------------------------------------------------------------------------
+// grid (item, chunk): each block sums RED_PER_BLOCK consecutive elements of one tile over all of
+// its partial slots in slot order (deterministic).
+constexpr int RED_PER_BLOCK = 256;
+
+// s + p[0] + p[st] + ... + p[(n-1)*st], added in slot order; loads issued 8 at a time so their
+// latencies overlap (same rounding as the plain loop).
+__device__ __forceinline__ double sum_slots(double s, const double* p, int64_t st, int n) {
+  int q = 0;
+  for (; q + 8 <= n; q += 8) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = p[(q + u) * st];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; q < n; ++q) s += p[q * st];
+  return s;
+}
+
+__device__ __forceinline__ double max_slots(const double* p, int64_t st, int n, bool& nan) {
+  double m = 0.0;
+  int q = 0;
+  for (; q + 8 <= n; q += 8) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = p[(q + u) * st];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      nan |= (v[u] != v[u]);
+      m = fmax(m, v[u]);
+    }
+  }
+  for (; q < n; ++q) {
+    const double v = p[q * st];
+    nan |= (v != v);
+    m = fmax(m, v);
+  }
+  return m;
+}
 __global__ __launch_bounds__(256) void reduce_kernel(const RItem* __restrict__ items,
                                                      Clock* __restrict__ clk, int set_tfar) {
   const RItem it = items[blockIdx.x];
+  const int n = it.rows * it.cols;
+  const int e0 = blockIdx.y * RED_PER_BLOCK;
   const int64_t t = load_t(clk);
+  if (set_tfar && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) clk->t_far = t;
+  if (e0 >= n) return;
   const double* add = nullptr;
   if (it.add) add = it.add + (t - clk->t_far) * it.add_cs;
-  const int n = it.rows * it.cols;
-  for (int e = threadIdx.x; e < n; e += blockDim.x) {
+  for (int e = e0 + threadIdx.x; e < min(n, e0 + RED_PER_BLOCK); e += blockDim.x) {
     const int r = e / it.cols;
     const int c = e - r * it.cols;
-    double s = add ? add[(int64_t)r * it.lda + c] : 0.0;
-    const double* p = it.src + (int64_t)r * it.lds + c;
-    for (int q = 0; q < it.nslots; ++q) s += p[q * it.slot_stride];
-    it.dst[(int64_t)r * it.ldd + c] = s;
+    const double s0 = add ? add[(int64_t)r * it.lda + c] : 0.0;
+    it.dst[(int64_t)r * it.ldd + c] = sum_slots(s0, it.src + (int64_t)r * it.lds + c, it.slot_stride, it.nslots);
   }
-  if (set_tfar && blockIdx.x == 0 && threadIdx.x == 0) clk->t_far = t;
 }
 
-void launch_reduce(const RItem* items, int nitems, const Clock* clk, int set_tfar, hipStream_t s) {
+void launch_reduce(const RItem* items, int nitems, int max_elems, const Clock* clk, int set_tfar,
+                   hipStream_t s) {
   if (nitems <= 0) return;
-  reduce_kernel<<<nitems, 256, 0, s>>>(items, const_cast<Clock*>(clk), set_tfar);
+  dim3 g(nitems, (max_elems + RED_PER_BLOCK - 1) / RED_PER_BLOCK);
+  reduce_kernel<<<g, 256, 0, s>>>(items, const_cast<Clock*>(clk), set_tfar);
 }
 
 // ------------------------------------------------------------------------------------------
 // Thread mapping shared by the per-step kernels: a block owns BT = min(B, 64) consecutive
-// trajectories (fastest index, so lanes are coalesced) and DL = 256/BT DOF lanes.
+// trajectories (fastest index, so lanes are coalesced) and DL = 256/BT DOF lanes; blockIdx.y
+// selects a chunk of DOFs.
 struct Lanes {
   int BT, DL, bl, dl, b;
   bool ok;
@@ -165,46 +261,32 @@ struct Lanes {
   }
 };
 
-__global__ __launch_bounds__(256) void potsel_kernel(const StepDev* __restrict__ sd,
-                                                     const double* __restrict__ Y,
-                                                     const double* __restrict__ X) {
-  __shared__ double red[WG];
-  __shared__ int hit[64];
-  const int B = sd->B, nph = sd->nph;
-  Lanes L(B);
-  double m = 0.0;
-  if (L.ok)
-    for (int d = L.dl; d < nph; d += L.DL) {
-      const int64_t i = (int64_t)d * B + L.b;
-      m = fmax(m, fabs(X[i] - sd->Q0[i]));
-    }
-  red[threadIdx.x] = L.ok ? m : 0.0;
-  __syncthreads();
-  if (L.dl == 0 && L.ok) {
-    double mm = 0.0;
-    bool nan = false;
-    for (int x = 0; x < L.DL; ++x) {
-      const double v = red[x * L.BT + L.bl];
-      nan |= (v != v);
-      mm = fmax(mm, v);
-    }
-    // md.py:776: max(abs(dif)) < 10e-10, and md.q0 = [] before the first evaluation
-    hit[L.bl] = (sd->qvalid[L.b] != 0) && !nan && (mm < 10e-10);
-  }
-  __syncthreads();
-  if (L.ok && !hit[L.bl]) {
-    for (int d = L.dl; d < nph; d += L.DL) {
-      const int64_t i = (int64_t)d * B + L.b;
-      sd->Fc[i] = -1.0 * Y[i];  // f = -1.0*mdot(dyn, q)  (md.py:467)
-      sd->Q0[i] = X[i];
-    }
-  }
-  if (L.ok && L.dl == 0) sd->qvalid[L.b] = 1;
+// md.potforce's cache (md.py:449-450, 767-779) for the harmonic force, per trajectory: hit iff the
+// cache is valid and max_d |q - q0| < 1e-9; the max over DOF chunks comes from the partial maxima
+// the previous phase kernel wrote (pdiff[slot][dblk][b]).
+__device__ __forceinline__ bool pot_hit(const StepDev* sd, int slot, int b, bool need_valid) {
+  if (need_valid && sd->qvalid[b] == 0) return false;
+  bool nan = false;
+  const double m = max_slots(sd->pdiff + (int64_t)slot * sd->ndblk * sd->B + b, sd->B, sd->ndblk, nan);
+  return !nan && m < 10e-10;
 }
 
-void launch_potsel(const StepDev* sd, const double* Y, const double* X, int B, hipStream_t s) {
-  const int BT = B < 64 ? B : 64;
-  potsel_kernel<<<(B + BT - 1) / BT, WG, 0, s>>>(sd, Y, X);
+// block max of v over the DOF lanes of each trajectory -> pdiff[slot][blockIdx.y][b]
+__device__ __forceinline__ void block_max_store(const StepDev* sd, const Lanes& L, double v, int slot,
+                                                double* red) {
+  red[threadIdx.x] = L.ok ? v : 0.0;
+  __syncthreads();
+  if (L.dl == 0 && L.ok) {
+    double m = 0.0;
+    bool nan = false;
+    for (int x = 0; x < L.DL; ++x) {
+      const double w = red[x * L.BT + L.bl];
+      nan |= (w != w);
+      m = fmax(m, w);
+    }
+    sd->pdiff[((int64_t)slot * sd->ndblk + blockIdx.y) * sd->B + L.b] = nan ? NAN : m;
+  }
+  __syncthreads();
 }
 
 // bath force of bath j at DOF-local index k (baths.py:232-255, 452-458):
@@ -218,8 +300,12 @@ __device__ __forceinline__ double bath_force(const BathDev& bd, int k, int b, in
   return f;
 }
 
+// mode0: 0 = potential force at q_t already in Fc (exact cache hit or host force)
+//        1 = harmonic: select between the cache and -dyn.q_t (Ypot) per trajectory
+// diff1: write the per-chunk max |q~ - q0| for the id1 cache decision
 __global__ __launch_bounds__(256) void phaseA_kernel(const StepDev* __restrict__ sd,
-                                                     const Clock* __restrict__ clk) {
+                                                     const Clock* __restrict__ clk, int mode0,
+                                                     int diff1) {
   __shared__ double red[WG];
   const int B = sd->B, nph = sd->nph, nb = sd->nbath;
   Lanes L(B);
@@ -229,15 +315,23 @@ __global__ __launch_bounds__(256) void phaseA_kernel(const StepDev* __restrict__
   const double dt = sd->dt, dt2 = dt * dt;
   const int d0 = blockIdx.y * sd->dchunk;
   const int d1 = min(nph, d0 + sd->dchunk);
+  const bool hit = (mode0 == 1 && L.ok) ? pot_hit(sd, 0, L.b, true) : true;
   double cur[MAXBATH];
 #pragma unroll
   for (int j = 0; j < MAXBATH; ++j) cur[j] = 0.0;
-  double e = 0.0;
+  double e = 0.0, dq = 0.0;
   if (L.ok)
     for (int d = d0 + L.dl; d < d1; d += L.DL) {
       const int64_t i = (int64_t)d * B + L.b;
       const double p = sd->P[i], q = sd->Q[i];
-      double f = sd->Fc[i];  // potforce(q_t)
+      double f;  // potforce(q_t)
+      if (!hit) {
+        f = -1.0 * sd->Ypot[i];  // f = -1.0*mdot(dyn, q)  (md.py:467)
+        sd->Fc[i] = f;
+        sd->Q0[i] = q;
+      } else {
+        f = sd->Fc[i];
+      }
 #pragma unroll
       for (int j = 0; j < MAXBATH; ++j) {
         if (j < nb) {
@@ -255,6 +349,7 @@ __global__ __launch_bounds__(256) void phaseA_kernel(const StepDev* __restrict__
       const double qt = q + p * dt + f * dt2 / 2.0;  // md.py:392
       sd->Ph[i] = ph;
       sd->Qt[i] = qt;
+      if (diff1) dq = fmax(dq, fabs(qt - (hit ? sd->Q0[i] : q)));
 #pragma unroll
       for (int j = 0; j < MAXBATH; ++j) {
         if (j < nb) {
@@ -281,11 +376,17 @@ __global__ __launch_bounds__(256) void phaseA_kernel(const StepDev* __restrict__
     }
     __syncthreads();
   }
+  if (diff1) block_max_store(sd, L, dq, 1, red);
+}
+
+// potential force at q~ for DOF d: mode1 0 = in Fc (host force), 1 = harmonic cache select
+__device__ __forceinline__ double pot_qt(const StepDev* sd, int64_t i, bool hit1) {
+  return hit1 ? sd->Fc[i] : -1.0 * sd->Ypot[i];
 }
 
 __device__ __forceinline__ double id1_force(const StepDev* sd, int d, int b, int B, int t1,
-                                            int par1) {
-  double f = sd->Fc[(int64_t)d * B + b];  // potforce(q~)
+                                            int par1, double fpot) {
+  double f = fpot;
 #pragma unroll
   for (int j = 0; j < MAXBATH; ++j) {
     if (j < sd->nbath) {
@@ -298,7 +399,7 @@ __device__ __forceinline__ double id1_force(const StepDev* sd, int d, int b, int
 }
 
 __global__ __launch_bounds__(256) void phaseB_kernel(const StepDev* __restrict__ sd,
-                                                     const Clock* __restrict__ clk) {
+                                                     const Clock* __restrict__ clk, int mode1) {
   const int B = sd->B, nph = sd->nph, nb = sd->nbath;
   Lanes L(B);
   const int64_t t = load_t(clk);
@@ -308,14 +409,16 @@ __global__ __launch_bounds__(256) void phaseB_kernel(const StepDev* __restrict__
   const int d0 = blockIdx.y * sd->dchunk;
   const int d1 = min(nph, d0 + sd->dchunk);
   if (!L.ok) return;
+  const bool hit1 = (mode1 == 1) ? pot_hit(sd, 1, L.b, false) : true;
   for (int d = d0 + L.dl; d < d1; d += L.DL) {
     bool inb = false;
 #pragma unroll
     for (int j = 0; j < MAXBATH; ++j)
       if (j < nb && sd->bath[j].inv[d] >= 0) inb = true;
     if (!inb) continue;  // p1 only feeds the bath friction terms
-    const double f = id1_force(sd, d, L.b, B, t1, par1);
-    const double p1 = sd->Ph[(int64_t)d * B + L.b] + dt * f / 2.0;  // md.py:402
+    const int64_t i = (int64_t)d * B + L.b;
+    const double f = id1_force(sd, d, L.b, B, t1, par1, pot_qt(sd, i, hit1));
+    const double p1 = sd->Ph[i] + dt * f / 2.0;  // md.py:402
 #pragma unroll
     for (int j = 0; j < MAXBATH; ++j) {
       if (j < nb) {
@@ -327,8 +430,10 @@ __global__ __launch_bounds__(256) void phaseB_kernel(const StepDev* __restrict__
   }
 }
 
+// diff0: write the per-chunk max |q_{t+1} - q0| for the next step's id0 cache decision
 __global__ __launch_bounds__(256) void phaseC_kernel(const StepDev* __restrict__ sd,
-                                                     Clock* __restrict__ clk) {
+                                                     Clock* __restrict__ clk, int mode1, int diff0) {
+  __shared__ double red[WG];
   const int B = sd->B, nph = sd->nph, nb = sd->nbath;
   Lanes L(B);
   const int64_t t = load_t(clk);
@@ -338,12 +443,22 @@ __global__ __launch_bounds__(256) void phaseC_kernel(const StepDev* __restrict__
   const double dt = sd->dt;
   const int d0 = blockIdx.y * sd->dchunk;
   const int d1 = min(nph, d0 + sd->dchunk);
+  const bool hit1 = (mode1 == 1 && L.ok) ? pot_hit(sd, 1, L.b, false) : true;
+  double dq = 0.0;
   if (L.ok) {
     for (int d = d0 + L.dl; d < d1; d += L.DL) {
       const int64_t i = (int64_t)d * B + L.b;
-      const double f = id1_force(sd, d, L.b, B, t1, par1);
-      double p2 = sd->Ph[i] + dt * f / 2.0;  // md.py:404
+      double fp;
       double qt = sd->Qt[i];
+      if (!hit1) {  // md.potforce miss at q~: evaluate and cache (md.py:472-473)
+        fp = -1.0 * sd->Ypot[i];
+        sd->Fc[i] = fp;
+        sd->Q0[i] = qt;
+      } else {
+        fp = sd->Fc[i];
+      }
+      const double f = id1_force(sd, d, L.b, B, t1, par1, fp);
+      double p2 = sd->Ph[i] + dt * f / 2.0;  // md.py:404
       if (sd->cmask[d]) {  // ApplyConstraint (md.py:407-408, 782-794)
         p2 = 0.0;
         qt = 0.0;
@@ -351,6 +466,7 @@ __global__ __launch_bounds__(256) void phaseC_kernel(const StepDev* __restrict__
       sd->P[i] = p2;
       sd->Q[i] = qt;
       sd->Flast[i] = f;
+      if (diff0) dq = fmax(dq, fabs(qt - sd->Q0[i]));
 #pragma unroll
       for (int j = 0; j < MAXBATH; ++j) {
         if (j < nb) {
@@ -370,8 +486,7 @@ __global__ __launch_bounds__(256) void phaseC_kernel(const StepDev* __restrict__
     // close step t's heat current and kinetic energy from phase A's partial sums (fixed order)
     if (blockIdx.y == 0) {
       for (int qd = L.dl; qd <= nb; qd += L.DL) {
-        double s = 0.0;
-        for (int y = 0; y < sd->ndblk; ++y) s += sd->part[((int64_t)y * (nb + 1) + qd) * B + L.b];
+        const double s = sum_slots(0.0, sd->part + (int64_t)qd * B + L.b, (int64_t)(nb + 1) * B, sd->ndblk);
         if (qd < nb) {
           sd->bath[qd].cur[(int64_t)tn * B + L.b] = s;
         } else {
@@ -380,6 +495,8 @@ __global__ __launch_bounds__(256) void phaseC_kernel(const StepDev* __restrict__
       }
     }
   }
+  if (diff0) block_max_store(sd, L, dq, 0, red);
+  if (mode1 == 1 && L.ok && blockIdx.y == 0 && L.dl == 0) sd->qvalid[L.b] = 1;
   // the last block to finish advances the step counter (all blocks read t before arriving)
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -399,17 +516,16 @@ static inline dim3 phase_grid(int B, int ndblk) {
   return dim3((B + BT - 1) / BT, ndblk);
 }
 
-void launch_phaseA(const StepDev* sd, const Clock* clk, int B, int nph, int ndblk, hipStream_t s) {
-  (void)nph;
-  phaseA_kernel<<<phase_grid(B, ndblk), WG, 0, s>>>(sd, clk);
+void launch_phaseA(const StepDev* sd, const Clock* clk, int B, int ndblk, int mode0, int diff1,
+                   hipStream_t s) {
+  phaseA_kernel<<<phase_grid(B, ndblk), WG, 0, s>>>(sd, clk, mode0, diff1);
 }
-void launch_phaseB(const StepDev* sd, const Clock* clk, int B, int nph, int ndblk, hipStream_t s) {
-  (void)nph;
-  phaseB_kernel<<<phase_grid(B, ndblk), WG, 0, s>>>(sd, clk);
+void launch_phaseB(const StepDev* sd, const Clock* clk, int B, int ndblk, int mode1, hipStream_t s) {
+  phaseB_kernel<<<phase_grid(B, ndblk), WG, 0, s>>>(sd, clk, mode1);
 }
-void launch_phaseC(const StepDev* sd, Clock* clk, int B, int nph, int ndblk, hipStream_t s) {
-  (void)nph;
-  phaseC_kernel<<<phase_grid(B, ndblk), WG, 0, s>>>(sd, clk);
+void launch_phaseC(const StepDev* sd, Clock* clk, int B, int ndblk, int mode1, int diff0,
+                   hipStream_t s) {
+  phaseC_kernel<<<phase_grid(B, ndblk), WG, 0, s>>>(sd, clk, mode1, diff0);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -1,0 +1,587 @@
+"""Langevin MD engine with sclmd's md API (sclmd/md.py), stepping on the MI355X.
+
+The constructor, setters and Run() follow sclmd/md.py:56-682 so examples/runmd.py only changes its
+import line.  Extensions (keyword-only): ntraj (independent noise realisations batched on the
+device), seed / traj_offset (per-trajectory RNG streams), noise_mode ("numpy": reference-compatible
+legacy-RNG draws; "device": Philox draws on the GPU), device, block_len, comm.
+
+State lives on the device after the first step; md.p / md.q / md.t read it back on access.
+With ntraj == 1 arrays have the reference's shapes ((nph,), (nmd,)); with ntraj > 1 a leading
+trajectory axis is added.
+"""
+import os
+import sys
+
+import numpy as np
+
+from . import _native
+from . import units as U
+from .functions import bose, chkShape, mdot, powerspecp, symmetrize
+
+
+def sameq(q1, q2):
+    """Cached-force test of md.potforce: same length and max|dq| < 1e-9 (md.py:767-779)."""
+    if len(q1) != len(q2):
+        return False
+    return bool(np.max(np.abs(np.asarray(q1) - np.asarray(q2))) < 10e-10)
+
+
+def ApplyConstraint(f, constr=None):
+    """Zero the listed DOF index ranges on a copy (md.py:782-794)."""
+    if constr is None:
+        return f
+    nf = np.array(f) * 1.0
+    for c in constr:
+        nf[..., list(c)] = 0
+    return nf
+
+
+class md:
+    def __init__(self, dt, nmd, T, syslist=None, axyz=None, dyn=None, nstart=0, nstop=1, npie=1,
+                 md2ang=0.06466, *, ntraj=1, seed=None, traj_offset=0, device=None,
+                 noise_mode="numpy", block_len=0, comm=None, verbose=True):
+        self.nstart, self.nstop = nstart, nstop
+        self.dt, self.nmd = dt, nmd
+        self.T = T
+        self.npie = npie
+        self.saveall = self.savep = self.saveq = self.rmnc = False
+        self.nstep = None
+        self.pforce = None
+        self.constraint = None
+        self.atomlist = None
+        self.verbose = verbose
+        self.ntraj = int(ntraj)
+        self.seed = seed
+        self.traj_offset = int(traj_offset)
+        if noise_mode not in ("numpy", "device"):
+            raise ValueError("noise_mode must be 'numpy' or 'device'")
+        self.noise_mode = noise_mode
+        self.device = device
+        self.block_len = int(block_len)
+        self.comm = comm
+        self.SetXyz(axyz)
+        if syslist is not None:
+            if len(syslist) > self.nta or min(syslist) < 0 or max(syslist) > self.nta - 1:
+                raise ValueError("syslist out of range")
+            self.syslist = np.array(syslist, dtype=int)
+            self.na = len(syslist)
+            self.nph = 3 * len(syslist)
+        elif axyz is not None:
+            self.syslist = np.arange(len(axyz))
+            self.na = len(self.syslist)
+            self.nph = 3 * self.na
+        else:
+            self.syslist = self.na = self.nph = None
+        self.ml = 1
+        self.cf = 0
+        self._t = 0
+        self._p = []
+        self._q = []
+        self.pinit, self.qinit = [], []
+        self.q0, self.f0 = [], []
+        self.baths = []
+        self.fhis = []
+        self.fbaths = []
+        self.etot_host = np.zeros(nmd)
+        self.initranvel = True
+        self.setDyn(dyn)
+        self.md2ang = md2ang
+        self.mass = []
+        self.get_atommass()
+        if self.els is not None and len(self.mass) != len(self.els):
+            raise ValueError("Wrong setting in els or mass")
+        self.conv = (self.md2ang * np.array([3 * [1.0 / np.sqrt(m)] for m in self.mass]).flatten()
+                     if self.mass else None)
+        self._st = None            # device stepper
+        self._dev_newer = False    # device holds newer p/q/t than the host mirrors
+        self._host_newer = True
+        self._noise_versions = {}
+        self._rngs = None
+        self.kappa_runs = []
+
+    # ------------------------------------------------------------------------------ logging
+    def _log(self, *a):
+        if self.verbose:
+            print(*a)
+
+    # ------------------------------------------------------------------------------ state access
+    def _pull(self):
+        if self._st is not None and self._dev_newer:
+            p, q, t = self._st.get_state()
+            if self.ntraj == 1:
+                p, q = p[0], q[0]
+            self._p, self._q, self._t = p, q, t
+            self._dev_newer = False
+
+    @property
+    def p(self):
+        self._pull()
+        return self._p
+
+    @p.setter
+    def p(self, v):
+        self._pull()
+        self._p = np.asarray(v, dtype=float)
+        self._host_newer = True
+
+    @property
+    def q(self):
+        self._pull()
+        return self._q
+
+    @q.setter
+    def q(self, v):
+        self._pull()
+        self._q = np.asarray(v, dtype=float)
+        self._host_newer = True
+
+    @property
+    def t(self):
+        self._pull()
+        return self._t
+
+    @t.setter
+    def t(self, v):
+        self._pull()
+        self._t = int(v)
+        self._host_newer = True
+
+    @property
+    def etot(self):
+        if self._st is None:
+            return self.etot_host
+        e = self._st.get_energy()
+        return e[0] if self.ntraj == 1 else e
+
+    # ------------------------------------------------------------------------------ setup API
+    def get_atommass(self):
+        if self.els is None:
+            return
+        for name in self.els:
+            if name in U.AtomicMassTable:
+                self.mass.append(U.AtomicMassTable[name])
+
+    def info(self):
+        self._log("--------------------------------------------")
+        self._log("Basis information of the MD simulation:")
+        self._log("System atom number:" + str(self.na))
+        self._log("MD time step:" + str(self.dt))
+        self._log("MD number of steps:" + str(self.nmd))
+        self._log("MD memory kernel length:" + str(self.ml))
+        self._log("Number of baths attached:" + str(len(self.baths)))
+        self._log("Trajectories on this device:" + str(self.ntraj))
+
+    def ResetSavepq(self):
+        if self.savep and self.nmd is not None and self.nph is not None:
+            self.ps = np.zeros((self.nmd, self.nph))
+        if self.saveq and self.nmd is not None and self.nph is not None:
+            self.qs = np.zeros((self.nmd, self.nph))
+
+    def energy(self):
+        """Kinetic energy 1/2 p.p (md.py:161-165)."""
+        p = np.asarray(self.p)
+        return 0.5 * np.sum(p * p, axis=-1)
+
+    def AddBath(self, bath):
+        if self.dt != bath.dt:
+            raise ValueError("md.AddBath: md time step dt not consistent")
+        if self.nmd != bath.nmd:
+            raise ValueError("md.AddBath: number of md steps nmd not consistent")
+        if self._st is not None:
+            raise RuntimeError("md.AddBath: baths must be added before the first step")
+        self.baths.append(bath)
+        if bath.ml > self.ml:
+            self.ml = bath.ml
+        self.fbaths.append(np.zeros(self.nph))
+
+    def AddPowerSection(self, atomlist):
+        self.atomlist = atomlist
+        self.poweratomlist = np.empty((len(self.atomlist), self.nmd, 2))
+
+    def AddConstr(self, constr):
+        self.constraint = constr
+
+    def CalPowerSpec(self, cal=True):
+        self.savep = cal
+        self.power = np.empty((self.nmd, 2))
+
+    def CalAveStruct(self, cal=True):
+        self.saveq = cal
+
+    def SaveAll(self, save=True):
+        self.saveall = save
+
+    def Savep(self, save=True):
+        self.savep = save
+
+    def Saveq(self, save=True):
+        self.saveq = save
+
+    def SaveTraj(self, nstep=100):
+        self.nstep = nstep
+
+    def RemoveNC(self, rmnc=True):
+        self.rmnc = rmnc
+
+    def SetT(self, T):
+        self.T = T
+
+    def SetMD(self, dt, nmd):
+        self.dt, self.nmd = dt, nmd
+        self.etot_host = np.zeros(nmd)
+
+    def noranvel(self, rf=False):
+        self.initranvel = rf
+
+    def SetXyz(self, axyz):
+        if axyz is not None:
+            self.xyz = np.array([a[1:] for a in axyz], dtype="d").flatten()
+            self.els = [a[0] for a in axyz]
+            self.nta = len(axyz)
+        else:
+            self.xyz = self.els = self.nta = None
+
+    def SetSyslist(self, syslist):
+        self.syslist = np.array(syslist)
+        self.na = len(syslist)
+        self.nph = 3 * len(syslist)
+
+    def setDyn(self, dyn=None):
+        """Symmetrise, clip negative eigenvalues, keep U diag(w^2) U^T (md.py:250-292)."""
+        if dyn is None:
+            self.dyn, self.hw, self.U = None, [1.0], None
+            return
+        ndyn = np.array(dyn)
+        n = chkShape(ndyn)
+        if self.nph is not None and self.nph != n:
+            raise ValueError("md.setDyn: the dimension of dynamical matrix is wrong")
+        self.nph = n
+        self.dyn = symmetrize(ndyn)
+        av, au = np.linalg.eigh(self.dyn)
+        if min(av) < 0:
+            av = np.where(av < 0, 0.0, av)
+        self.hw = np.array(list(map(np.real, list(map(np.sqrt, av)))))
+        self.U = np.array(au)
+        self.dyn = mdot(self.U, np.diag(np.array(av)), np.transpose(self.U))
+
+    def AddPotential(self, pint):
+        self.pforce = pint
+
+    def CompareForce(self, forcedriver):
+        self.cf = 1
+        self.forcedriver = forcedriver
+        self.cflist = []
+
+    # ------------------------------------------------------------------------------ RNG streams
+    def _rng(self, b):
+        """Trajectory b's random stream: the global numpy RNG (reference behaviour) when no seed is
+        given, else RandomState(seed + traj_offset + b)."""
+        if self.seed is None:
+            return np.random
+        if self._rngs is None:
+            self._rngs = [np.random.RandomState(int(self.seed) + self.traj_offset + i)
+                          for i in range(self.ntraj)]
+        return self._rngs[b]
+
+    def initialise(self):
+        """Initial displacement and velocity from the modes of dyn (md.py:294-338)."""
+        self._t = 0
+        n = self.nph
+        if self.dyn is None:
+            p = np.zeros((self.ntraj, n))
+            q = np.zeros((self.ntraj, n))
+        else:
+            av, au = self.hw, self.U
+            p = np.zeros((self.ntraj, n))
+            q = np.zeros((self.ntraj, n))
+            for b in range(self.ntraj):
+                rng = self._rng(b)
+                dis = np.zeros(len(av))
+                vel = np.zeros(len(av))
+                for i in range(len(av)):
+                    am = 0.0 if av[i] < 0.01 else ((bose(av[i], self.T) + 0.5) * 2.0 / av[i]) ** 0.5
+                    r = rng.rand()
+                    dis = dis + au[:, i] * am * np.cos(2.0 * np.pi * r)
+                    vel = vel - av[i] * au[:, i] * am * np.sin(2.0 * np.pi * r)
+                dis = ApplyConstraint(dis, self.constraint)
+                vel = ApplyConstraint(vel, self.constraint)
+                if self.initranvel:
+                    p[b], q[b] = vel, dis
+        if self.ntraj == 1:
+            p, q = p[0], q[0]
+        self._p, self._q = p, q
+        self.pinit, self.qinit = p, q
+        self._host_newer = True
+        self._dev_newer = False
+
+    def ResetHis(self):
+        """Zero the friction-kernel history (md.py:340-349)."""
+        if self.nph is None or self.ml is None:
+            raise ValueError("self.nph and self.ml are not set")
+        self._reset_his = True
+        if self._st is not None:
+            self._push_state()
+            for i in range(len(self.baths)):
+                self._st.set_history(i, None)
+            self._reset_his = False
+
+    # ------------------------------------------------------------------------------ device
+    def _constr_dofs(self):
+        if self.constraint is None:
+            return []
+        return sorted(set(int(d) for c in self.constraint for d in c))
+
+    def _ensure_device(self):
+        if self._st is not None:
+            return self._st
+        if self.nph is None:
+            raise ValueError("md: the number of degrees of freedom is not set (axyz/dyn)")
+        dev = self.device
+        if dev is None:
+            dev = int(os.environ.get("LOCAL_RANK", "0")) if _native.device_count() > 1 else 0
+        st = _native.Stepper(self.nph, self.ntraj, self.nmd, self.dt, dev, self.block_len)
+        for b in self.baths:
+            if b.kernel is None:
+                raise ValueError("md: bath %s has no kernel (call phbath.gmem())" % b)
+            if b.kind == "ebath":
+                if b.biased():
+                    st.add_bath(_native.GLE_BATH_ELECTRON, b.cids, b.kernel, b.bias, b.exim, b.zeta1, b.zeta2)
+                else:
+                    st.add_bath(_native.GLE_BATH_ELECTRON, b.cids, b.kernel)
+            else:
+                st.add_bath(_native.GLE_BATH_PHONON, b.cids, b.kernel)
+        if self.dyn is not None:
+            st.set_dyn(self.dyn)
+        c = self._constr_dofs()
+        if c:
+            st.set_constraint(c)
+        self._st = st
+        self._push_state()
+        for i in range(len(self.baths)):
+            st.set_history(i, None)
+        self._reset_his = False
+        return st
+
+    def _push_state(self):
+        if not self._host_newer:
+            return
+        p = np.asarray(self._p, dtype=float).reshape(self.ntraj, self.nph)
+        q = np.asarray(self._q, dtype=float).reshape(self.ntraj, self.nph)
+        self._st.set_state(p, q, self._t)
+        self.q0, self.f0 = [], []
+        self._host_newer = False
+
+    def _sync_injected_noise(self):
+        """Upload host-assigned bath.noise arrays that the device has not seen yet."""
+        for i, b in enumerate(self.baths):
+            if getattr(b, "_noise_src", None) is not None:
+                continue
+            v = getattr(b, "_noise_version", 0)
+            if self._noise_versions.get(i) != v:
+                n = b._noise_host
+                if n is None:
+                    raise RuntimeError("md: bath %d has no noise (call gnoi() or Run())" % i)
+                n = np.asarray(n, dtype=float)
+                if n.ndim == 2:
+                    n = np.broadcast_to(n, (self.ntraj,) + n.shape)
+                self._st.set_noise(i, n)
+                self._noise_versions[i] = v
+
+    def gen_noise(self, i, run=0):
+        """New noise realisation for bath i on the device (bath.gnoi, md.py:569-570)."""
+        st = self._ensure_device()
+        b = self.baths[i]
+        fac = b.noise_factor()
+        key = (self.noise_mode, b._fac_key)
+        if getattr(self, "_fac_loaded", {}).get(i) != key:
+            st.noise_factors(i, fac.evecs if self.noise_mode == "numpy" else fac.scaled())
+            self._fac_loaded = getattr(self, "_fac_loaded", {})
+            self._fac_loaded[i] = key
+        if self.noise_mode == "numpy":
+            x = np.stack([fac.draws(self._rng(bb)) for bb in range(self.ntraj)])
+            st.noise_generate(i, x)
+        else:
+            base = 0 if self.seed is None else int(self.seed)
+            key64 = (base * 0x9E3779B97F4A7C15 + (run + 1) * 0xBF58476D1CE4E5B9 + (i + 1) * 0x94D049BB133111EB) % 2**64
+            st.noise_generate(i, None, seed=key64, traj_offset=self.traj_offset)
+        b._noise_src = (st, i)
+        b._noise_version = getattr(b, "_noise_version", 0) + 1
+        self._noise_versions[i] = b._noise_version
+
+    # ------------------------------------------------------------------------------ forces
+    def potforce(self, q):
+        """Host potential force with md.potforce's cache (md.py:437-474); one trajectory."""
+        if sameq(q, self.q0):
+            return self.f0
+        if self.pforce is not None:
+            f = self.pforce.force(q)
+        elif self.dyn is not None:
+            f = -1.0 * mdot(self.dyn, q)
+        else:
+            raise RuntimeError("no driver, no md")
+        self.q0, self.f0 = q, f
+        return f
+
+    def _host_forces(self, qs, cache):
+        out = np.empty_like(qs)
+        for b in range(self.ntraj):
+            q0, f0 = cache[b]
+            if len(q0) == len(qs[b]) and np.max(np.abs(qs[b] - q0)) < 10e-10:
+                out[b] = f0
+            else:
+                f = np.asarray(self.pforce.force(qs[b].copy()), dtype=float)
+                cache[b] = (qs[b].copy(), f)
+                out[b] = f
+        return out
+
+    # ------------------------------------------------------------------------------ stepping
+    def vv(self, id=0):
+        """One modified velocity-Verlet step (md.py:367-411) on the device."""
+        st = self._ensure_device()
+        self._push_state()
+        if getattr(self, "_reset_his", False):
+            for i in range(len(self.baths)):
+                st.set_history(i, None)
+            self._reset_his = False
+        self._sync_injected_noise()
+        need_host = self.savep or self.saveq or self.cf
+        if need_host:
+            t = self.t
+            p, q = np.asarray(self.p), np.asarray(self.q)
+            if self.savep:
+                self.ps[t % self.nmd] = p if self.ntraj == 1 else p[0]
+            if self.saveq:
+                self.qs[t % self.nmd] = q if self.ntraj == 1 else q[0]
+            if self.cf:
+                qq = q if self.ntraj == 1 else q[0]
+                self.cflist.append(self.forcedriver.force(qq) + mdot(self.dyn, qq))
+        if self.pforce is not None:
+            if not hasattr(self, "_fcache") or len(self._fcache) != self.ntraj:
+                self._fcache = [([], None)] * self.ntraj
+            q = np.asarray(self._q_dev_host()).reshape(self.ntraj, self.nph)
+            f = self._host_forces(q, self._fcache)
+            qt = st.step_begin(f, want_qt=True)
+            f2 = self._host_forces(qt, self._fcache)
+            st.step_end(f2)
+        else:
+            st.step_begin(None, want_qt=False)
+            st.step_end(None)
+        self._dev_newer = True
+
+    def _q_dev_host(self):
+        return self.q
+
+    @property
+    def f(self):
+        if self._st is None:
+            return None
+        f = self._st.get_force()
+        return f[0] if self.ntraj == 1 else f
+
+    def steps(self, n):
+        """n steps; fully on the device when no host work is needed per step."""
+        if self.pforce is None and not (self.savep or self.saveq or self.cf or self.nstep):
+            st = self._ensure_device()
+            self._push_state()
+            self._sync_injected_noise()
+            st.run(n)
+            self._dev_newer = True
+        else:
+            for _ in range(n):
+                self.vv()
+
+    # ------------------------------------------------------------------------------ Run
+    def _reduce(self, sums):
+        from . import ensemble
+
+        return ensemble.allreduce_sums(sums, self.comm)
+
+    def _is_root(self):
+        from . import ensemble
+
+        return ensemble.rank(self.comm) == 0
+
+    def Run(self):
+        """Independent runs nstart..nstop-1 (md.py:493-682): fresh noise per run, state and history
+        carried over, per-run time-averaged heat current written to kappa.{T}.bath{i}.run{j}.dat.
+        NetCDF checkpoint/resume (md.dump, md.py:684-764) is not implemented: runs always start
+        fresh."""
+        self.initialise()
+        self.ResetHis()
+        self.info()
+        self._ensure_device()
+        for j in range(self.nstart, self.nstop):
+            self._log("\nMD run: " + str(j))
+            for i in range(len(self.baths)):
+                self.gen_noise(i, j)
+            self.ResetSavepq()
+            traj = None
+            if self.nstep is not None and self._is_root():
+                traj = open("trajectories." + str(self.T) + ".run" + str(j) + ".ani", "w")
+            for _ in range(self.npie):
+                nsteps = int(self.nmd / self.npie)
+                if self.nstep is None:
+                    self.steps(nsteps)
+                else:
+                    for _s in range(nsteps):
+                        self.vv(j)
+                        tt = self.t - 1
+                        if traj is not None and (tt == 0 or tt % self.nstep == 0):
+                            self._write_frame(traj, tt)
+            if traj is not None:
+                traj.close()
+            if self.cf:
+                np.save("deltaforce.run" + str(j), np.array(self.cflist) / self.forcedriver.conv)
+                self.cflist = []
+            if self.savep:
+                self._power(j)
+            cur = self._st.get_current()                      # (nbath, ntraj, nmd)
+            sums = self._reduce(self._st.current_sums())      # (nbath, 3) over all ranks
+            kap = sums[:, 0] / sums[:, 2] * U.curcof
+            self.kappa_runs.append(kap)
+            for ii, b in enumerate(self.baths):
+                b.cur = cur[ii, 0] if self.ntraj == 1 else cur[ii]
+            if self._is_root():
+                for ii in range(len(self.baths)):
+                    with open("kappa." + str(self.T) + ".bath" + str(ii) + ".run" + str(j) + ".dat", "w") as fk:
+                        fk.write("%i %f    %f \n" % (j, self.T, kap[ii]))
+                if self.saveq:
+                    self._avestructure(j)
+
+    def _write_frame(self, fh, tt):
+        q = self.q if self.ntraj == 1 else self.q[0]
+        f = self.f if self.ntraj == 1 else self.f[0]
+        s = self.xyz + self.conv * q
+        fh.write(str(len(self.els)) + "\n" + str(tt) + "\n")
+        for ip in range(len(self.els)):
+            fh.write(str(self.els[ip]) + "    " + str(s[ip * 3]) + "   " + str(s[ip * 3 + 1]) + "   " +
+                     str(s[ip * 3 + 2]) + "   " + str(f[ip * 3]) + "   " + str(f[ip * 3 + 1]) + "   " +
+                     str(f[ip * 3 + 2]) + "\n")
+
+    def _power(self, j):
+        """Running average of the velocity power spectrum over runs (md.py:604-653)."""
+        prev = np.copy(self.power)
+        self.power = powerspecp(self.ps, self.dt, self.nmd)
+        k = j - self.nstart
+        if k > 0:
+            self.power = (prev * k + self.power) / float(k + 1)
+        if self._is_root():
+            with open("power." + str(self.T) + ".run" + str(j) + ".dat", "w") as f:
+                for ni in range(len(self.power)):
+                    if self.hw is not None and self.power[ni, 0] >= 1.5 * max(self.hw):
+                        break
+                    f.write("%f     %f \n" % (self.power[ni, 0], self.power[ni, 1]))
+
+    def _avestructure(self, j):
+        ave = self.conv * (self.qs.mean(axis=0)) + self.xyz
+        with open("avestructure." + str(self.T) + ".run" + str(j) + ".dat", "w") as f:
+            f.write(str(len(self.els)) + "\n" + "average structure" + "\n")
+            for ip in range(len(self.els)):
+                f.write(str(self.els[ip]) + "    " + str(ave[ip * 3]) + "   " + str(ave[ip * 3 + 1]) +
+                        "   " + str(ave[ip * 3 + 2]) + "\n")
+
+    def close(self):
+        if self._st is not None:
+            self._pull()
+            self._st.close()
+            self._st = None

@@ -1,0 +1,132 @@
+"""Quantum coloured noise (sclmd/noise.py) -- host spectral factorisation + device generation.
+
+The reference draws, for each of the nmd/2+1 positive frequencies w_i, a Gaussian vector with
+covariance A(w_i) (eigh + vargau, noise.py:73-84 / 171-191), mirrors the amplitudes into a
+length-nmd spectrum (noise.py:87-94) and transforms w -> t with numpy's forward FFT times dw/2pi
+(functions.py:36-53).  Here:
+
+  * the covariance matrices A(w_i) and their eigendecompositions are built on the host once per
+    bath (they do not change between runs; numpy's eigh on the stacked matrices is the same
+    LAPACK call the reference makes one frequency at a time);
+  * the Gaussian draws are either numpy-compatible (same legacy RandomState calls in the same
+    order as vargau, so seeded runs reproduce the reference draw for draw) or counter-based Philox
+    on the device (ensemble mode);
+  * the matrix products a_w = U_w r_w, the mirroring and the FFT run in HIP (gle_noise_generate).
+"""
+import numpy as np
+
+from . import _native
+from . import units as U
+from .functions import flinterp, hermitianize
+
+
+def mf(f, cats, lens):
+    """Scatter a bath-local vector into the full DOF space (noise.py:15-22)."""
+    t = np.zeros(lens)
+    t[np.asarray(cats, dtype=int)] = f
+    return t
+
+
+def equ(w, cut, T, classical=False, zpmotion=True):
+    """2*hw*(zp + bose(hw,T)) below the cutoff, 2kT classically or at w = 0 (noise.py:249-270)."""
+    from .functions import bose
+
+    hw = U.hbar * w
+    zp = 0.5 if zpmotion is True else 0.0
+    if hw < cut:
+        if classical or hw == 0:
+            return 2.0 * U.kb * T
+        return 2.0 * hw * (zp + bose(hw, T))
+    return 0.0
+
+
+def frequencies(dt, nmd):
+    hlen = int(nmd / 2)
+    dw = 2.0 * np.pi / dt / nmd
+    return dw * np.arange(hlen + 1), dt * nmd
+
+
+def phonon_spectrum(gamma, wl, T, phcut, dt, nmd, classical=False, zpmotion=True):
+    """A(w_i) = Delta*equ(w_i)*Gamma(w_i), hermitianised (noise.py:73-79).  (nfreq, nc, nc)."""
+    ws, delta = frequencies(dt, nmd)
+    gamma = np.asarray(gamma)
+    out = np.empty((len(ws),) + gamma.shape[1:], dtype=np.result_type(gamma, np.float64))
+    for n, w in enumerate(ws):
+        out[n] = hermitianize(delta * equ(w, phcut, T, classical, zpmotion) * flinterp(w, wl, gamma))
+    return out
+
+
+def electron_spectrum(efric, exim, exip, bias, T, ecut, dt, nmd, classical=False, zpmotion=True):
+    """Complex Hermitian A(w_i) of the (biased) electron bath (noise.py:171-186)."""
+    ws, delta = frequencies(dt, nmd)
+    efric, exim, exip = (np.asarray(m, dtype=float) for m in (efric, exim, exip))
+    out = np.empty((len(ws),) + efric.shape, dtype=complex)
+    for n, w in enumerate(ws):
+        aw = delta * equ(w, ecut, T, classical, zpmotion)
+        awm = delta * equ(U.hbar * w - bias, ecut, T, classical, zpmotion)
+        awp = delta * equ(U.hbar * w + bias, ecut, T, classical, zpmotion)
+        m = aw * efric
+        m = m + (-0.5 * aw * exip + 0.5 * awm * (exip + 1j * exim))
+        m = m + (-0.5 * aw * exip + 0.5 * awp * (exip - 1j * exim))
+        out[n] = hermitianize(m)
+    return out
+
+
+class NoiseFactor:
+    """Eigendecomposition of a bath's noise spectrum, shared by every run and trajectory."""
+
+    def __init__(self, spectrum):
+        spectrum = np.asarray(spectrum)
+        self.nfreq, self.nc = spectrum.shape[0], spectrum.shape[1]
+        ev, vec = np.linalg.eigh(spectrum)
+        self.evals = ev                     # (nfreq, nc) ascending
+        self.evecs = vec                    # (nfreq, nc, nc) columns
+        self.pos = ev > 0                   # vargau draws only for positive eigenvalues
+        self.sigma = np.sqrt(np.where(self.pos, ev, 0.0))
+        self.complex = np.iscomplexobj(vec)
+
+    def scaled(self):
+        """U.diag(sqrt(max(lambda, 0))) -- the factor for device N(0,1) draws."""
+        return self.evecs * self.sigma[:, None, :]
+
+    def draws(self, rng=None):
+        """vargau's r vectors for every frequency (noise.py:297-303): N(0, sqrt(lambda_k)) for
+        lambda_k > 0 in (frequency, ascending-eigenvalue) order, 0 otherwise.  One vectorised call
+        of the legacy RandomState.normal yields the same sequence as the reference's scalar calls."""
+        rng = np.random if rng is None else rng
+        r = np.zeros((self.nfreq, self.nc))
+        s = self.sigma[self.pos]
+        if s.size:
+            r[self.pos] = rng.normal(0.0, s)
+        return r
+
+
+def generate(factor, dt, nmd, ntraj=1, rngs=None, seed=None, device=0):
+    """Standalone device generation of ntraj realisations (ntraj, nmd, nc) for one factor."""
+    st = _native.Stepper(factor.nc, ntraj, nmd, dt, device)
+    try:
+        st.add_bath(_native.GLE_BATH_PHONON, np.arange(factor.nc), np.zeros((1, factor.nc, factor.nc)))
+        if seed is None:
+            st.noise_factors(0, factor.evecs)
+            rngs = rngs if rngs is not None else [np.random] * ntraj
+            x = np.stack([factor.draws(r) for r in rngs])
+            st.noise_generate(0, x)
+        else:
+            st.noise_factors(0, factor.scaled())
+            st.noise_generate(0, None, seed=seed)
+        return st.get_noise(0)
+    finally:
+        st.close()
+
+
+def phnoise(gamma, wl, T, phcut, dt, nmd, classical=False, zpmotion=True):
+    """Phonon-bath noise, same signature and RNG use as noise.py:50-100; returns (nmd, nc) real
+    (the reference returns the complex FFT whose real part baths.py:408 keeps)."""
+    f = NoiseFactor(phonon_spectrum(gamma, wl, T, phcut, dt, nmd, classical, zpmotion))
+    return generate(f, dt, nmd)[0]
+
+
+def enoise(efric, exim, exip, bias, T, ecut, dt, nmd, classical=False, zpmotion=True):
+    """Electron-bath noise, same signature and RNG use as noise.py:149-206; returns (nmd, nc)."""
+    f = NoiseFactor(electron_spectrum(efric, exim, exip, bias, T, ecut, dt, nmd, classical, zpmotion))
+    return generate(f, dt, nmd)[0]
