@@ -1,0 +1,140 @@
+"""Host-side logic of the product (setup code that runs on the CPU): noise factorisation and
+reference-compatible draws, memory-kernel construction, bath matrix conventions, initial state,
+post-processing, ensemble sharding -- each against the reference-generated golden fixtures."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+
+
+def rel(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
+
+
+@pytest.mark.parametrize("tag", ["ph_q", "ph_c", "ph_nozp"])
+def test_phonon_factor_and_draws(tag):
+    from sclmd_amd import noise as N
+
+    g = load_golden("noise")
+    T, phcut, cl, zp = g["params_" + tag]
+    f = N.NoiseFactor(N.phonon_spectrum(g["gam"], g["gwl"], T, phcut, float(g["dt"]), int(g["nmd"]),
+                                        bool(cl), bool(zp)))
+    assert np.array_equal(f.evals, g["eval_" + tag])
+    np.random.seed(11)
+    r = f.draws()
+    assert rel(np.einsum("wij,wj->wi", f.evecs, r), g["amp_" + tag]) < 1e-14
+    # device-mode factor U sqrt(lambda+) reproduces the PSD part of the spectrum
+    m = f.scaled()
+    spec = N.phonon_spectrum(g["gam"], g["gwl"], T, phcut, float(g["dt"]), int(g["nmd"]), bool(cl), bool(zp))
+    psd = np.einsum("wik,wjk->wij", m, m)
+    assert rel(psd, spec) < 1e-10
+
+
+@pytest.mark.parametrize("tag", ["e_eq", "e_bias", "e_cold"])
+def test_electron_factor_and_draws(tag):
+    from sclmd_amd import noise as N
+    from sclmd_amd.functions import antisymmetrize, symmetrize
+
+    g = load_golden("noise")
+    bias, T, ecut, cl, zp = g["params_" + tag]
+    f = N.NoiseFactor(N.electron_spectrum(symmetrize(g["efric"]), antisymmetrize(g["exim"]),
+                                          symmetrize(g["exip"]), bias, T, ecut, float(g["dt"]),
+                                          int(g["nmd"]), bool(cl), bool(zp)))
+    assert np.array_equal(f.evals, g["eval_" + tag])
+    np.random.seed(12)
+    r = f.draws()
+    assert rel(np.einsum("wij,wj->wi", f.evecs, r), g["amp_" + tag]) < 1e-14
+
+
+def test_gamt_and_gmem():
+    from sclmd_amd import baths as B
+
+    g = load_golden("gamt")
+    for tag, eta in (("eta0", 0.0), ("eta1", 0.02)):
+        b = B.phbath(300.0, list(range(4)), debye=0.2, nw=int(g["nw"]), dt=float(g["dt"]), nmd=64,
+                     ml=int(g["ml"]), gamma=g["gam"].copy(), gwl=g["gwl"], eta_ad=eta)
+        b.gmem()
+        assert rel(b.kernel, g["kernel_" + tag]) < 1e-13
+        assert rel(b.gamma, g["gamma_after_" + tag]) < 1e-13
+    assert rel(B.gamt(g["gamt_tl"], g["gamt_wl"], g["gwl"], g["gam"]), g["gamt_direct"]) < 1e-13
+    b = B.phbath(300.0, list(range(4)), debye=0.15, nw=40, dt=0.38, nmd=64, ml=8)
+    b.gmem()
+    assert b.ml == 1 and np.array_equal(b.kernel, g["kernel_debye"])
+
+
+def test_ebath_conventions():
+    from sclmd_amd.baths import ebath
+
+    rng = np.random.default_rng(0)
+    m = rng.normal(size=(4, 4))
+    b = ebath([0, 1, 2, 3], 300.0, 0.38, 16, wmax=1.0, nw=10, bias=0.3, efric=m, exim=m, zeta1=m, zeta2=m)
+    assert np.allclose(b.efric, b.efric.T) and np.allclose(b.zeta1, b.zeta1.T)
+    assert np.allclose(b.exim, -b.exim.T) and np.allclose(b.zeta2, -b.zeta2.T)
+    assert b.biased() and b.ml == 1 and b.kernel.shape == (1, 4, 4)
+    b2 = ebath([0, 1, 2, 3], 300.0, 0.38, 16, bias=0.3, efric=m, exim=m)  # zeta None: inactive
+    assert not b2.biased()
+    with pytest.raises(ValueError):
+        ebath([0, 1, 2], 300.0, 0.38, 16, efric=m)
+
+
+def test_initialise_matches_reference():
+    from sclmd_amd import md as MD
+    from sclmd_amd import synthetic
+
+    g = load_golden("run_seeded")
+    natom = int(g["natom"])
+    m = MD.md(float(g["dt"]), int(g["nmd"]), float(g["T"]), axyz=synthetic.axyz_chain(natom),
+              dyn=g["dyn"], verbose=False)
+    assert rel(m.dyn, g["dyn_md"]) < 1e-14
+    m.AddConstr([range(6, 8)])
+    np.random.seed(int(g["seed"]))
+    m.initialise()
+    assert rel(m.p, g["p0"]) < 1e-14 and rel(m.q, g["q0"]) < 1e-14
+
+
+def test_tools_files(tmp_path, monkeypatch):
+    from sclmd_amd import tools
+
+    g = load_golden("tools")
+    kb, T = g["kb"], int(g["T"])
+    monkeypatch.chdir(tmp_path)
+    for i in range(3):
+        for j in range(int(g["nrun"])):
+            with open("kappa.%d.bath%d.run%d.dat" % (T, i, j), "w") as f:
+                f.write("%i %f    %f \n" % (j, float(T), kb[i, j]))
+    tools.calHF(dlist=2, bathnum=2)
+    tools.calTC(delta=0.1, dlist=2, bathnum=2, L=10.0, A=4.0)
+    np.testing.assert_allclose(np.loadtxt("heatflux.%d.dat" % T), g["heatflux_2"], rtol=1e-12)
+    np.testing.assert_allclose(np.loadtxt("thermalconductance.%d.dat" % T), g["tc_2"], rtol=1e-12)
+    np.testing.assert_allclose(np.loadtxt("thermalconductivity.%d.dat" % T), g["tcy_2"], rtol=1e-12)
+    np.testing.assert_allclose(np.loadtxt("heatflux-between-baths.%d.dat" % T), g["hfb_2"], rtol=1e-12)
+    tools.calHF(dlist=1, bathnum=3)
+    tools.calTC(delta=0.1, dlist=1, bathnum=3)
+    np.testing.assert_allclose(np.loadtxt("heatflux.%d.dat" % T), g["heatflux_3"], rtol=1e-12)
+    np.testing.assert_allclose(np.loadtxt("thermalconductance.%d.dat" % T), g["tc_3"], rtol=1e-12)
+    np.testing.assert_allclose(np.loadtxt("heatflux-between-baths.%d.dat" % T), g["hfb_3"], rtol=1e-12)
+
+
+@pytest.mark.parametrize("n,w", [(64, 1), (64, 8), (512, 8), (7, 3), (3, 8)])
+def test_shard_covers_ensemble(n, w):
+    from sclmd_amd.ensemble import shard
+
+    seen = []
+    for r in range(w):
+        off, cnt = shard(n, r, w)
+        seen.extend(range(off, off + cnt))
+    assert seen == list(range(n))
+
+
+def test_synthetic_junction_shapes():
+    from sclmd_amd import synthetic
+
+    dyn, axyz, baths, meta = synthetic.junction("C3", ml=16, nmd=64, natom=30, nw=50)
+    assert dyn.shape == (90, 90) and len(axyz) == 30
+    assert [b.nc for b in baths] == [30, 30] and baths[0].kernel.shape == (16, 30, 30)
+    assert np.allclose(dyn, dyn.T) and np.linalg.eigvalsh(dyn).min() > 0
+    dyn, axyz, baths, meta = synthetic.junction("C5", ml=8, nmd=32, natom=30, nw=50)
+    assert len(baths) == 3 and baths[2].kind == "ebath" and baths[2].biased()
