@@ -193,6 +193,7 @@ struct Gemm {
   int64_t lda = 0;
   int add_cs = 0;
   bool force_reduce = false;
+  int Kd = 0;  // true (unpadded) reduction length, for the algorithmic flop/byte count
 };
 
 // Split policy: target ~target_items work items in total for this product, each with at least
@@ -220,22 +221,29 @@ void plan_gemm(Op& op, const Gemm& g, int target_items, int min_work) {
   }
   const int nsplit = (ni > 0) ? si * sk : 0;
   const bool use_partial = g.force_reduce || g.add != nullptr || nsplit > 1;
+  // item order: (column tile, slice range, k range) outer, row group inner -- consecutive items
+  // share the staged history window (and, with the kernel's XCD-aware mapping, one L2)
+  std::vector<size_t> slot0s((size_t)ngroups * ncol, 0);
+  std::vector<int> nslot((size_t)ngroups * ncol, 0);
   for (int gi = 0; gi < ngroups; ++gi)
     for (int ct = 0; ct < ncol; ++ct) {
-      const int col0 = ct * NT;
-      const int ncols = std::min<int>(NT, g.N - col0);
-      const int nrows = std::min(64, g.M - 64 * gi);
-      if (nrows <= 0) continue;
-      const size_t slot0 = op.partial_doubles;
+      slot0s[(size_t)gi * ncol + ct] = op.partial_doubles;
       if (use_partial) op.partial_doubles += (size_t)nsplit * 64 * NT;
-      int slot = 0;
-      for (int a = 0; a < si && ni > 0; ++a) {
-        const int ia = g.i0 + (int)((int64_t)ni * a / si);
-        const int ib = g.i0 + (int)((int64_t)ni * (a + 1) / si);
-        if (ib <= ia) continue;
-        for (int b = 0; b < sk; ++b) {
-          const int kp0 = (int)((int64_t)nkp * b / sk), kp1 = (int)((int64_t)nkp * (b + 1) / sk);
-          if (kp1 <= kp0) continue;
+    }
+  for (int ct = 0; ct < ncol; ++ct) {
+    const int col0 = ct * NT;
+    const int ncols = std::min<int>(NT, g.N - col0);
+    for (int a = 0; a < si && ni > 0; ++a) {
+      const int ia = g.i0 + (int)((int64_t)ni * a / si);
+      const int ib = g.i0 + (int)((int64_t)ni * (a + 1) / si);
+      if (ib <= ia) continue;
+      for (int b = 0; b < sk; ++b) {
+        const int kp0 = (int)((int64_t)nkp * b / sk), kp1 = (int)((int64_t)nkp * (b + 1) / sk);
+        if (kp1 <= kp0) continue;
+        for (int gi = 0; gi < ngroups; ++gi) {
+          const int nrows = std::min(64, g.M - 64 * gi);
+          if (nrows <= 0) continue;
+          const size_t key = (size_t)gi * ncol + ct;
           CItem it{};
           it.A = g.A + (int64_t)(4 * gi) * g.a_rt + (int64_t)(2 * kp0) * g.a_ks + (int64_t)ia * 64;
           it.X = g.X + (int64_t)(8 * kp0) * g.ldx;
@@ -253,36 +261,44 @@ void plan_gemm(Op& op, const Gemm& g, int target_items, int min_work) {
           it.ncols = ncols;
           it.nrows = nrows;
           if (use_partial) {
-            it.out = (double*)(uintptr_t)((slot0 + (size_t)slot * 64 * NT) * sizeof(double));  // offset, fixed up later
+            // offset into the op's partial buffer, fixed up in materialize()
+            it.out = (double*)(uintptr_t)((slot0s[key] + (size_t)nslot[key] * 64 * NT) * sizeof(double));
             it.ldo = NT;
           } else {
             it.out = g.dst + (int64_t)(64 * gi) * g.ldd + col0;
             it.ldo = (int32_t)g.ldd;
           }
           op.items.push_back(it);
-          ++slot;
+          ++nslot[key];
         }
       }
-      if (use_partial) {
+    }
+  }
+  if (use_partial)
+    for (int gi = 0; gi < ngroups; ++gi)
+      for (int ct = 0; ct < ncol; ++ct) {
+        const int col0 = ct * NT;
+        const int nrows = std::min(64, g.M - 64 * gi);
+        if (nrows <= 0) continue;
+        const size_t key = (size_t)gi * ncol + ct;
         RItem r{};
         r.dst = g.dst + (int64_t)(64 * gi) * g.ldd + col0;
-        r.src = (const double*)(uintptr_t)(slot0 * sizeof(double));  // offset, fixed up later
+        r.src = (const double*)(uintptr_t)(slot0s[key] * sizeof(double));  // offset, fixed up later
         r.add = g.add ? g.add + (int64_t)(64 * gi) * g.lda + col0 : nullptr;
         r.ldd = (int32_t)g.ldd;
         r.lds = NT;
         r.lda = (int32_t)g.lda;
-        r.nslots = slot;
+        r.nslots = nslot[key];
         r.slot_stride = (int64_t)64 * NT;
         r.rows = nrows;
-        r.cols = ncols;
+        r.cols = std::min<int>(NT, g.N - col0);
         r.add_cs = g.add_cs;
         op.ritems.push_back(r);
       }
-    }
   // algorithmic work of this product: each kernel entry read once, X read
   // once, output written once.
   if (ni > 0) {
-    const double kd = 4.0 * g.nks_total;
+    const double kd = g.Kd > 0 ? g.Kd : 4.0 * g.nks_total;
     op.flops += 2.0 * g.M * kd * g.N * ni;
     op.bytes += 8.0 * ((double)ni * g.M * kd + kd * (g.ring ? (double)(ni + (g.N + g.cs - 1) / std::max(1, g.cs) - 1) * g.cs : g.N) + (double)g.M * g.N);
   }
@@ -306,6 +322,20 @@ int materialize(gle_handle* h, Op& op, const std::vector<bool>& is_partial) {
   }
   for (size_t i = 0; i < op.items.size(); ++i)
     if (is_partial[i]) op.items[i].out = op.partial + (uintptr_t)op.items[i].out / sizeof(double);
+  // pad the grid to a multiple of 8 (XCD-aware block mapping) with empty items
+  while (op.items.size() % 8) {
+    CItem e{};
+    e.A = op.items.empty() ? nullptr : op.items[0].A;
+    e.X = op.items.empty() ? nullptr : op.items[0].X;
+    e.out = nullptr;
+    e.nks = 0;
+    e.ni = 0;
+    e.nrt = 0;
+    e.ldx = 1;
+    e.ldo = 1;
+    e.cs = 1;
+    op.items.push_back(e);
+  }
   for (auto& r : op.ritems) r.src = op.partial + (uintptr_t)r.src / sizeof(double);
   if (!op.items.empty()) {
     int rc = dalloc_n(h, &op.d_items, op.items.size());
@@ -484,6 +514,7 @@ int freeze(gle_handle* h) {
     g.cs = (int)B;
     g.tshift = tshift;
     g.M = b.nc;
+    g.Kd = b.nc;
     g.N = N;
     g.dst = dst;
     g.ldd = ldd;
@@ -539,6 +570,7 @@ int freeze(gle_handle* h) {
       g.X = h->d_Q;
       g.ldx = B;
       g.M = (int)h->nph;
+      g.Kd = (int)h->nph;
       g.N = (int)B;
       g.dst = h->d_Ypot;
       g.ldd = B;
@@ -575,6 +607,7 @@ int freeze(gle_handle* h) {
       g.X = h->d_Qt;
       g.ldx = B;
       g.M = (int)h->nph;
+      g.Kd = (int)h->nph;
       g.N = (int)B;
       g.dst = h->d_Ypot;
       g.ldd = B;
@@ -612,6 +645,8 @@ int build_near(gle_handle* h) {
       g.cs = (int)B;
       g.tshift = 1;
       g.M = b.nc;
+      g.Kd = b.nc;
+    g.Kd = b.nc;
       g.N = (int)B;
       g.dst = b.d_S + (int64_t)par * b.ncp * B;
       g.ldd = B;
@@ -1143,6 +1178,7 @@ int gle_noise_generate(gle_handle* h, int32_t bath, const double* x_host, uint64
       g.X = d_x + (size_t)w * ncp * B;
       g.ldx = B;
       g.M = b.fac_rows;
+      g.Kd = b.nc;
       g.N = (int)B;
       g.dst = d_a + (size_t)w * b.fac_rows * B;
       g.ldd = B;

@@ -44,7 +44,12 @@ __global__ __launch_bounds__(WG, 2) void contract_kernel(const CItem* __restrict
   __shared__ double lds[KROWS * LDS_COLS];
   constexpr int NT = 16 * RN;
   constexpr int WWCAP = (256 * CU < LDS_WW_MAX) ? 256 * CU : LDS_WW_MAX;
-  const CItem it = items[blockIdx.x];
+  // XCD-aware order (grids are padded to a multiple of 8): blocks b, b+8, b+16, ... share an XCD
+  // and its L2, so they take consecutive work items -- the row groups of one slice range, which
+  // stage the same history window.
+  const int nblk = gridDim.x;
+  const int bid = (nblk & 7) ? (int)blockIdx.x : (int)(blockIdx.x & 7) * (nblk >> 3) + (int)(blockIdx.x >> 3);
+  const CItem it = items[bid];
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
   const int lane = tid & 63;

@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes into HBM bytes per launch of the
+dominant kernel.  gfx950 correction (MI355X_MICROARCH.md, HBM section; re-calibrated here with
+tools/peak_probe's known 4 GiB read streams: 8 B/lane and 16 B/lane coalesced reads both report
+exactly half): hbm_read = 2 * FETCH_SIZE * 1024, hbm_write = WRITE_SIZE * 1024.
+
+    python scripts/pmc_summary.py gpurun_out/pmc OUT.json --kernel 'contract_kernel<16' \
+        --config C3 --ntraj 64
+"""
+import argparse
+import csv
+import json
+import os
+
+
+def per_launch(path, kernel, grid=None):
+    vals = []
+    for r in csv.DictReader(open(path)):
+        if kernel in r["Kernel_Name"] and (grid is None or r["Grid_Size"] == grid):
+            vals.append(float(r["Counter_Value"]))
+    return vals
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("pmcdir")
+    ap.add_argument("out")
+    ap.add_argument("--kernel", default="contract_kernel<16")
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--ntraj", type=int, default=64)
+    a = ap.parse_args()
+    f = per_launch(os.path.join(a.pmcdir, "FETCH_SIZE", "run_counter_collection.csv"), a.kernel)
+    w = per_launch(os.path.join(a.pmcdir, "WRITE_SIZE", "run_counter_collection.csv"), a.kernel)
+    fetch = sum(f) / len(f) * 1024.0
+    write = sum(w) / len(w) * 1024.0
+    res = {"config": a.config, "ntraj": a.ntraj, "kernel": a.kernel, "launches": [len(f), len(w)],
+           "fetch_size_bytes_raw": fetch, "write_size_bytes": write,
+           "hbm_bytes_per_launch": 2.0 * fetch + write,
+           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "
+                     "read bytes = 2 x FETCH_SIZE (gfx950 half-count, calibrated on 4 GiB 8 B/lane and "
+                     "16 B/lane streams), write bytes = WRITE_SIZE"}
+    json.dump(res, open(a.out, "w"), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -3,24 +3,59 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <vector>
+#include <algorithm>
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
+template <int NACC>
 __global__ __launch_bounds__(256) void mfma_loop(double* out, int iters, double seed) {
-  d4 acc[8];
-  for (int i = 0; i < 8; ++i) acc[i] = d4{0, 0, 0, 0};
+  d4 acc[NACC];
+  for (int i = 0; i < NACC; ++i) acc[i] = d4{0, 0, 0, 0};
   double a = seed + threadIdx.x * 1e-3, b = seed - threadIdx.x * 2e-3;
   for (int it = 0; it < iters; ++it) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[i], 0, 0, 0);
+    for (int i = 0; i < NACC; ++i) acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[i], 0, 0, 0);
   }
   double s = 0;
-  for (int i = 0; i < 8; ++i) s += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
+  for (int i = 0; i < NACC; ++i) s += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+template <int NACC>
+static double mfma_tflops(int ncu, int wg_per_cu, double* out) {
+  const int blocks = ncu * wg_per_cu, iters = 32768 / NACC;
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  mfma_loop<NACC><<<blocks, 256>>>(out, 16, 1.0);
+  hipDeviceSynchronize();
+  float best = 1e30f;
+  for (int r = 0; r < 3; ++r) {
+    hipEventRecord(e0);
+    mfma_loop<NACC><<<blocks, 256>>>(out, iters, 1.0 + r);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    if (ms < best) best = ms;
+  }
+  return (double)blocks * 4 * iters * NACC * 2048.0 / (best * 1e-3) / 1e12;
 }
 
 __global__ void copy4(const float4* __restrict__ a, float4* __restrict__ b, size_t n) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) b[i] = a[i];
+}
+
+// known-byte read streams for calibrating rocprofv3 FETCH_SIZE per access width
+__global__ void read8(const double* __restrict__ a, double* out, size_t n) {
+  double s = 0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) s += a[i];
+  if (s == 12345.678) out[0] = s;
+}
+__global__ void read16(const double2* __restrict__ a, double* out, size_t n) {
+  double s = 0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) s += a[i].x + a[i].y;
+  if (s == 12345.678) out[0] = s;
 }
 
 int main() {
@@ -28,25 +63,18 @@ int main() {
   hipGetDeviceProperties(&p, 0);
   const int ncu = p.multiProcessorCount;
   double* out;
-  const int blocks = ncu * 8, iters = 4096;
-  hipMalloc(&out, (size_t)blocks * 256 * 8);
+  hipMalloc(&out, (size_t)ncu * 8 * 256 * 8);
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  mfma_loop<<<blocks, 256>>>(out, 64, 1.0);
-  hipDeviceSynchronize();
-  float best = 1e30f;
-  for (int r = 0; r < 5; ++r) {
-    hipEventRecord(e0);
-    mfma_loop<<<blocks, 256>>>(out, iters, 1.0 + r);
-    hipEventRecord(e1);
-    hipEventSynchronize(e1);
-    float ms;
-    hipEventElapsedTime(&ms, e0, e1);
-    if (ms < best) best = ms;
+  double tf = 0;
+  char sweep[512];
+  int pos = 0;
+  for (int w = 1; w <= 8; w *= 2) {
+    const double a = mfma_tflops<4>(ncu, w, out), b = mfma_tflops<8>(ncu, w, out), c = mfma_tflops<16>(ncu, w, out);
+    pos += snprintf(sweep + pos, sizeof(sweep) - pos, "%s\"wg%d\": [%.1f, %.1f, %.1f]", w > 1 ? ", " : "", w, a, b, c);
+    tf = std::max(tf, std::max(a, std::max(b, c)));
   }
-  const double flops = (double)blocks * 4 /*waves*/ * iters * 8 * 2048.0;
-  const double tf = flops / (best * 1e-3) / 1e12;
   const size_t n = (size_t)1 << 28;  // 4 GiB per buffer of float4? -> 2^28 * 16 B = 4 GiB
   float4 *a, *b;
   hipMalloc(&a, n * 16);
@@ -65,6 +93,10 @@ int main() {
     if (ms < bms) bms = ms;
   }
   const double gbs = 2.0 * n * 16 / (bms * 1e-3) / 1e9;
-  printf("{\"device\": \"%s\", \"cus\": %d, \"fp64_mfma_tflops\": %.2f, \"hbm_copy_gbs\": %.1f}\n", p.name, ncu, tf, gbs);
+  // calibration streams: exactly 4 GiB read each (run under rocprofv3 --pmc FETCH_SIZE)
+  read8<<<ncu * 8, 256>>>((const double*)a, out, n * 2);
+  read16<<<ncu * 8, 256>>>((const double2*)a, out, n);
+  hipDeviceSynchronize();
+  printf("{\"cus\": %d, \"fp64_mfma_tflops_best\": %.2f, \"fp64_mfma_sweep_acc4_8_16\": {%s}, \"hbm_copy_gbs\": %.1f}\n", ncu, tf, sweep, gbs);
   return 0;
 }
