@@ -52,8 +52,20 @@ typedef struct gle_config {
     int64_t nmd;        /* MD steps per run = noise period, md.nmd (md.py:59); even          */
     double dt;          /* MD time step, md.dt (md.py:59)                                    */
     int32_t device;     /* HIP device ordinal                                                */
-    int32_t block_len;  /* far-field time block L for the memory-kernel contraction; 0=auto  */
+    int32_t block_len;  /* far-field time block L (= partition length P in spectral mode); 0=auto */
+    int32_t far_mode;   /* GLE_FAR_AUTO / GLE_FAR_DIRECT / GLE_FAR_SPECTRAL                      */
+    int32_t reserved;
 } gle_config;
+
+/* far-field memory sum  sum_{i>=L} K_i p_{t-i}  (SURVEY.md section 8a R3):
+ *   DIRECT    one time-blocked MFMA contraction over the kernel slices every L steps;
+ *   SPECTRAL  uniformly partitioned overlap-save: kernel partitions of P = L slices are
+ *             transformed once (length 2P), every P steps one new input segment is transformed and
+ *             the far field is a per-frequency MFMA contraction of the spectra (~4(P+1)/P^2 of the
+ *             direct flops), then inverse-transformed.  Same result to fp64 rounding. */
+#define GLE_FAR_AUTO 0
+#define GLE_FAR_DIRECT 1
+#define GLE_FAR_SPECTRAL 2
 
 /* ---- lifetime ------------------------------------------------------------------------- */
 int gle_abi_version(void);
@@ -147,8 +159,9 @@ int gle_profile(gle_handle* h, int32_t enable);
 int gle_profile_read(gle_handle* h, int64_t* nlaunch, double* total_ms, double* flops,
                      double* bytes);
 /* Planner summary of the current configuration: block length L, far-field work items, bytes of
- * device memory in use. */
-int gle_plan_info(gle_handle* h, int64_t* block_len, int64_t* far_items, int64_t* device_bytes);
+ * device memory in use, far-field mode actually chosen. */
+int gle_plan_info(gle_handle* h, int64_t* block_len, int64_t* far_items, int64_t* device_bytes,
+                  int32_t* far_mode);
 
 #ifdef __cplusplus
 }

@@ -35,7 +35,11 @@ class GLEError(RuntimeError):
 
 class gle_config(ctypes.Structure):
     _fields_ = [("nph", ctypes.c_int64), ("ntraj", ctypes.c_int64), ("nmd", ctypes.c_int64),
-                ("dt", ctypes.c_double), ("device", ctypes.c_int32), ("block_len", ctypes.c_int32)]
+                ("dt", ctypes.c_double), ("device", ctypes.c_int32), ("block_len", ctypes.c_int32),
+                ("far_mode", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+FAR_AUTO, FAR_DIRECT, FAR_SPECTRAL = 0, 1, 2
+FAR_MODES = {"auto": FAR_AUTO, "direct": FAR_DIRECT, "spectral": FAR_SPECTRAL}
 
 
 _P = ctypes.c_void_p
@@ -70,7 +74,7 @@ _SIGS = {
     "gle_current_sums": (ctypes.c_int, [_P, _D]),
     "gle_profile": (ctypes.c_int, [_P, ctypes.c_int32]),
     "gle_profile_read": (ctypes.c_int, [_P, _I64, _D, _D, _D]),
-    "gle_plan_info": (ctypes.c_int, [_P, _I64, _I64, _I64]),
+    "gle_plan_info": (ctypes.c_int, [_P, _I64, _I64, _I64, ctypes.POINTER(ctypes.c_int32)]),
 }
 
 _lib = None
@@ -116,10 +120,11 @@ def device_count():
 class Stepper:
     """Owner of one gle_handle: a batch of ntraj trajectories of one system on one device."""
 
-    def __init__(self, nph, ntraj, nmd, dt, device=0, block_len=0):
+    def __init__(self, nph, ntraj, nmd, dt, device=0, block_len=0, far_mode="auto"):
         self.lib = load()
         self.nph, self.ntraj, self.nmd, self.dt = int(nph), int(ntraj), int(nmd), float(dt)
-        cfg = gle_config(self.nph, self.ntraj, self.nmd, self.dt, int(device), int(block_len))
+        fm = FAR_MODES[far_mode] if isinstance(far_mode, str) else int(far_mode)
+        cfg = gle_config(self.nph, self.ntraj, self.nmd, self.dt, int(device), int(block_len), fm, 0)
         h = _P()
         rc = self.lib.gle_create(ctypes.byref(cfg), ctypes.byref(h))
         if rc != 0:
@@ -269,6 +274,9 @@ class Stepper:
 
     def plan_info(self):
         a, b, c = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int64(0)
-        self._chk(self.lib.gle_plan_info(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
-                  "gle_plan_info")
-        return {"block_len": int(a.value), "far_items": int(b.value), "device_bytes": int(c.value)}
+        m = ctypes.c_int32(0)
+        self._chk(self.lib.gle_plan_info(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c),
+                                         ctypes.byref(m)), "gle_plan_info")
+        names = {v: k for k, v in FAR_MODES.items()}
+        return {"block_len": int(a.value), "far_items": int(b.value), "device_bytes": int(c.value),
+                "far_mode": names.get(int(m.value), int(m.value))}

@@ -57,6 +57,10 @@ struct Bath {
   int64_t ldh = 0;
   int R = 1;
   bool noise_set = false;
+  // spectral far field
+  int M = 0, nrt2 = 0, nks2 = 0, Rseg = 0;
+  int64_t ldseg = 0, khat_fstride = 0, seg_fstride = 0, yfstride = 0;
+  double *d_khat = nullptr, *d_seg = nullptr, *d_Yspec = nullptr;
   // noise generator
   int64_t nfreq = 0;
   bool fac_complex = false;
@@ -81,7 +85,7 @@ struct gle_handle {
   uint8_t* d_cmask = nullptr;
   double *d_P = nullptr, *d_Q = nullptr, *d_Ph = nullptr, *d_Qt = nullptr, *d_Fc = nullptr;
   double *d_Flast = nullptr, *d_etot = nullptr, *d_Q0 = nullptr, *d_part = nullptr, *d_Ypot = nullptr;
-  double* d_pdiff = nullptr;
+  unsigned long long* d_pmax = nullptr;
   int32_t* d_qvalid = nullptr;
   Clock* d_clk = nullptr;
   StepDev* d_sd = nullptr;
@@ -96,6 +100,10 @@ struct gle_handle {
   bool host_force_step = false;
   Op op_far, op_prime, op0, op0p, op1a, op1a_np, op1b;
   Op op_near[2];  // S(t+1) into S[(t+1)&1]: one plan per destination parity
+  Op op_spec;     // spectral far field: per-frequency contraction of kernel and segment spectra
+  int far_mode = GLE_FAR_DIRECT;
+  bool seg_ready = false;
+  double* d_cstab = nullptr;
   std::vector<void*> allocs;
   size_t dev_bytes = 0;
   // profiling of the dominant contraction
@@ -194,6 +202,8 @@ struct Gemm {
   int add_cs = 0;
   bool force_reduce = false;
   int Kd = 0;  // true (unpadded) reduction length, for the algorithmic flop/byte count
+  int tdiv = 1;
+  bool lat = false;  // per-step product: minimise sequential LDS stages per item
 };
 
 // Split policy: target ~target_items work items in total for this product, each with at least
@@ -206,17 +216,27 @@ void plan_gemm(Op& op, const Gemm& g, int target_items, int min_work) {
   const int ni = g.i1 - g.i0;
   const int nkp = g.nks_total / 2;  // k-step pairs
   const int base = ngroups * ncol;
-  int split = std::max(1, target_items / std::max(1, base));
-  const int64_t work = (int64_t)std::max(ni, 0) * g.nks_total;
-  split = (int)std::min<int64_t>(split, std::max<int64_t>(1, work / std::max(1, min_work)));
   int si = 1, sk = 1;
-  if (ni > 0) {
-    if (g.ring) {
-      si = std::min(split, ni);
-      sk = std::max(1, std::min(nkp, split / si));
-    } else {
-      sk = std::min(split, nkp);
-      si = std::max(1, std::min(ni, split / sk));
+  if (g.lat && ni > 0) {
+    // latency-bound per-step product: each item stages ONE window of slices (as many as fit the
+    // LDS row) for ONE or a few k-stages, so an item is a couple of LDS round trips long
+    const int ns_cap = g.ring ? std::max(1, (LDS_WW_MAX - NT) / std::max(1, g.cs) + 1) : 1;
+    si = (ni + ns_cap - 1) / ns_cap;
+    int kp_per = 1;
+    while ((int64_t)base * si * ((nkp + kp_per - 1) / kp_per) > target_items && kp_per < nkp) kp_per *= 2;
+    sk = (nkp + kp_per - 1) / kp_per;
+  } else {
+    int split = std::max(1, target_items / std::max(1, base));
+    const int64_t work = (int64_t)std::max(ni, 0) * g.nks_total;
+    split = (int)std::min<int64_t>(split, std::max<int64_t>(1, work / std::max(1, min_work)));
+    if (ni > 0) {
+      if (g.ring) {
+        si = std::min(split, ni);
+        sk = std::max(1, std::min(nkp, split / si));
+      } else {
+        sk = std::min(split, nkp);
+        si = std::max(1, std::min(ni, split / sk));
+      }
     }
   }
   const int nsplit = (ni > 0) ? si * sk : 0;
@@ -257,6 +277,7 @@ void plan_gemm(Op& op, const Gemm& g, int target_items, int min_work) {
           it.ring = g.ring;
           it.cs = g.cs;
           it.tshift = g.tshift;
+          it.tdiv = g.tdiv;
           it.col0 = col0;
           it.ncols = ncols;
           it.nrows = nrows;
@@ -334,6 +355,7 @@ int materialize(gle_handle* h, Op& op, const std::vector<bool>& is_partial) {
     e.ldx = 1;
     e.ldo = 1;
     e.cs = 1;
+    e.tdiv = 1;
     op.items.push_back(e);
   }
   for (auto& r : op.ritems) r.src = op.partial + (uintptr_t)r.src / sizeof(double);
@@ -357,8 +379,11 @@ struct Planner {
   gle_handle* h;
   Op& op;
   std::vector<bool> partial;
-  Planner(gle_handle* hh, Op& o, int rn) : h(hh), op(o) { op.rn = rn; }
-  void add(const Gemm& g, int target, int min_work) {
+  bool lat;
+  Planner(gle_handle* hh, Op& o, int rn, bool latency = false) : h(hh), op(o), lat(latency) { op.rn = rn; }
+  void add(const Gemm& g0, int target, int min_work) {
+    Gemm g = g0;
+    if (lat) g.lat = true;
     const size_t n0 = op.items.size();
     const size_t r0 = op.ritems.size();
     plan_gemm(op, g, target, min_work);
@@ -412,8 +437,16 @@ int freeze(gle_handle* h) {
   // streamed kernel slice, bounded so the per-step near-field stays small
   int mlmax = 1;
   for (auto& b : h->baths) mlmax = std::max(mlmax, b.ml);
+  // far-field mode: the spectral form pays when the contraction is compute-bound (many
+  // trajectories) and the kernel is long compared with the partition; the direct form streams the
+  // kernel once per L steps and wins when the step is bandwidth-bound (few trajectories)
+  int mode = h->cfg.far_mode;
+  const int Pdef = 32;
+  if (mode == GLE_FAR_AUTO) mode = (B >= 8 && mlmax >= 4 * Pdef) ? GLE_FAR_SPECTRAL : GLE_FAR_DIRECT;
   if (h->cfg.block_len > 0) {
     h->L = h->cfg.block_len;
+  } else if (mode == GLE_FAR_SPECTRAL) {
+    h->L = Pdef;
   } else {
     int L = 1;
     while (L * B < 256 && L < 32) L *= 2;
@@ -421,15 +454,62 @@ int freeze(gle_handle* h) {
   }
   const int L = h->L;
   const int rn_step = rn_for(B);
+  if (mode == GLE_FAR_SPECTRAL) {
+    // device-memory check: transformed kernels + segment rings
+    size_t need = 0;
+    for (auto& b : h->baths) {
+      if (b.ml <= L) continue;
+      const int M = (b.ml + L - 1) / L - 1;
+      const int64_t nrt2 = (2 * b.nc + 15) / 16, nks2 = rup(2 * b.nc, 8) / 4;
+      need += (size_t)(L + 1) * nrt2 * nks2 * M * 64 * 8;
+      need += (size_t)(L + 1) * rup(2 * b.nc, 8) * (2 * (M + 4) * B + 1024) * 8;
+    }
+    size_t fr = 0, tot = 0;
+    hipMemGetInfo(&fr, &tot);
+    if (need > fr / 2) {
+      if (h->cfg.far_mode == GLE_FAR_SPECTRAL)
+        return fail(h, GLE_ERR_NOMEM, "spectral far field needs " + std::to_string(need >> 20) + " MiB");
+      mode = GLE_FAR_DIRECT;
+    }
+  }
+  h->far_mode = mode;
   // ring sizes and buffers that depend on L
   for (auto& b : h->baths) {
-    b.R = b.ml + 2 * L + 2;
+    b.R = b.ml + 3 * L + 2;
     b.ldh = 2 * (int64_t)b.R * B + 512 + 16 * rn_for(L * B);
     int rc = dalloc_n(h, &b.d_H, (size_t)b.ncp * b.ldh + 4096);
     if (rc) return rc;
     if (b.ml > L) {
       rc = dalloc_n(h, &b.d_far, (size_t)b.ncp * L * B + 4096);
       if (rc) return rc;
+    }
+  }
+  if (mode == GLE_FAR_SPECTRAL) {
+    std::vector<double> cst((size_t)4 * L);
+    for (int q = 0; q < 2 * L; ++q) {
+      const long double a = 3.14159265358979323846264338327950288L * (long double)q / (long double)L;
+      cst[2 * q] = (double)cosl(a);
+      cst[2 * q + 1] = (double)sinl(a);
+    }
+    int rc = dalloc_n(h, &h->d_cstab, cst.size());
+    if (!rc) rc = upload(h, h->d_cstab, cst.data(), cst.size() * 8);
+    if (rc) return rc;
+    for (auto& b : h->baths) {
+      if (b.ml <= L) continue;
+      b.M = (b.ml + L - 1) / L - 1;
+      b.nrt2 = (2 * b.nc + 15) / 16;
+      b.nks2 = (int)(rup(2 * b.nc, 8) / 4);
+      b.Rseg = b.M + 4;
+      b.ldseg = 2 * (int64_t)b.Rseg * B + 1024;
+      b.khat_fstride = (int64_t)b.nrt2 * b.nks2 * b.M * 64;
+      b.seg_fstride = (int64_t)rup(2 * b.nc, 8) * b.ldseg;
+      b.yfstride = (int64_t)2 * b.nc * B;
+      rc = dalloc_n(h, &b.d_khat, (size_t)(L + 1) * b.khat_fstride);
+      if (!rc) rc = dalloc_n(h, &b.d_seg, (size_t)(L + 1) * b.seg_fstride + 4096);
+      if (!rc) rc = dalloc_n(h, &b.d_Yspec, (size_t)(L + 1) * b.yfstride + 4096);
+      if (rc) return rc;
+      launch_khat_pack(b.d_K, b.ml, b.nks, b.d_khat, L, b.M, b.nc, b.nrt2, b.nks2, h->d_cstab, h->stream);
+      HIPCHK(h, hipStreamSynchronize(h->stream));
     }
   }
   // StepDev
@@ -453,17 +533,17 @@ int freeze(gle_handle* h) {
   // DOF chunking of the phase kernels: ~ one 256-thread block per 64x(256/BT) elements
   const int BT = (int)std::min<int64_t>(B, 64);
   const int DL = 256 / BT;
-  h->dchunk = std::max(DL, (int)rup(std::max<int64_t>(1, h->nph / 64), DL));
-  h->dchunk = std::max(h->dchunk, DL * 4);
+  // two DOFs per thread: enough blocks to fill the chip for the elementwise phases
+  h->dchunk = 2 * DL;
   h->ndblk = (int)((h->nph + h->dchunk - 1) / h->dchunk);
   sd.ndblk = h->ndblk;
   sd.dchunk = h->dchunk;
-  int rc = dalloc_n(h, &h->d_part, (size_t)h->ndblk * (h->baths.size() + 1) * B);
+  int rc = dalloc_n(h, &h->d_part, (size_t)h->nmd * h->ndblk * (h->baths.size() + 1) * B);
   if (rc) return rc;
   sd.part = h->d_part;
-  rc = dalloc_n(h, &h->d_pdiff, (size_t)2 * h->ndblk * B);
+  rc = dalloc_n(h, &h->d_pmax, (size_t)4 * B);
   if (rc) return rc;
-  sd.pdiff = h->d_pdiff;
+  sd.pmax = h->d_pmax;
   // constraint mask
   std::vector<uint8_t> mask(h->nph, 0);
   for (auto d : h->constr) mask[d] = 1;
@@ -530,6 +610,40 @@ int freeze(gle_handle* h) {
         g.force_reduce = true;
         p.add(g, TGT_BIG, 16);
       }
+    rc = p.done();
+    if (rc) return rc;
+  }
+  // SPECTRAL: per frequency f, Y_f = sum_{m=1..M} Khat_m(f) Xhat_{T/P-m+1}(f) on [[Re,-Im],[Im,Re]]
+  if (h->far_mode == GLE_FAR_SPECTRAL) {
+    Planner p(h, h->op_spec, rn_step);
+    int nprod = 0;
+    for (auto& b : h->baths)
+      if (b.d_khat) nprod += L + 1;
+    for (auto& b : h->baths) {
+      if (!b.d_khat) continue;
+      for (int f = 0; f <= L; ++f) {
+        Gemm g{};
+        g.A = b.d_khat + (int64_t)f * b.khat_fstride;
+        g.a_ks = (int64_t)b.M * 64;
+        g.a_rt = (int64_t)b.nks2 * g.a_ks;
+        g.nrt_total = b.nrt2;
+        g.nks_total = b.nks2;
+        g.i0 = 0;
+        g.i1 = b.M;
+        g.X = b.d_seg + (int64_t)f * b.seg_fstride;
+        g.ldx = b.ldseg;
+        g.ring = b.Rseg;
+        g.cs = (int)B;
+        g.tshift = 0;
+        g.tdiv = L;
+        g.M = 2 * b.nc;
+        g.Kd = 2 * b.nc;
+        g.N = (int)B;
+        g.dst = b.d_Yspec + (int64_t)f * b.yfstride;
+        g.ldd = B;
+        p.add(g, std::max(1, 1536 / std::max(1, nprod)), 16);
+      }
+    }
     rc = p.done();
     if (rc) return rc;
   }
@@ -628,7 +742,7 @@ int build_near(gle_handle* h) {
   const int64_t B = h->B;
   const int L = h->L;
   for (int par = 0; par < 2; ++par) {
-    Planner p(h, h->op_near[par], rn_for(B));
+    Planner p(h, h->op_near[par], rn_for(B), true);
     for (auto& b : h->baths) {
       if (b.ml <= 1) continue;
       Gemm g{};
@@ -677,6 +791,7 @@ int prime(gle_handle* h) {
   }
   h->need_prime = false;
   h->far_due = true;
+  h->seg_ready = false;
   return GLE_OK;
 }
 
@@ -690,7 +805,23 @@ int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
     if (rc) return rc;
   }
   if (h->far_due) {
-    if (!h->op_far.items.empty()) run_op(h, h->op_far, 1, true);
+    const int L = h->L;
+    if (h->far_mode == GLE_FAR_SPECTRAL && h->t % L == 0 && !h->op_spec.items.empty()) {
+      for (auto& b : h->baths)
+        if (b.d_khat)
+          launch_seg_fft(b.d_H, b.ldh, b.R, (int)h->B, b.nc, L, h->t, h->seg_ready ? 1 : b.M, b.d_seg,
+                         b.seg_fstride, b.ldseg, b.Rseg, h->d_cstab, h->stream);
+      h->seg_ready = true;
+      run_op(h, h->op_spec, 0, true);
+      for (auto& b : h->baths)
+        if (b.d_khat)
+          launch_far_ifft(b.d_Yspec, b.yfstride, b.nc, (int)h->B, L, b.d_far, (int64_t)L * h->B,
+                          h->d_cstab, h->d_clk, h->stream);
+    } else if (!h->op_far.items.empty()) {
+      // direct block (every L steps in direct mode; the partial block before the first aligned
+      // spectral block otherwise)
+      run_op(h, h->op_far, 1, h->far_mode != GLE_FAR_SPECTRAL);
+    }
     h->far_due = false;
     h->steps_since_far = 0;
   }
@@ -698,7 +829,7 @@ int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
   if (fpot_host_T == nullptr && !h->has_dyn)
     return fail(h, GLE_ERR_STATE, "no potential force: pass fpot or call gle_set_dyn (md.py:468-470)");
   Op& op0 = need_pot ? h->op0p : h->op0;
-  run_op(h, op0, 0, h->op_far.items.empty());
+  run_op(h, op0, 0, h->op_far.items.empty() && h->op_spec.items.empty());
   run_op(h, h->op_near[(h->t + 1) & 1], 0, false);
   if (fpot_host_T)
     HIPCHK(h, hipMemcpyAsync(h->d_Fc, fpot_host_T, (size_t)h->nph * h->B * 8, hipMemcpyHostToDevice, h->stream));
@@ -723,7 +854,11 @@ int step_end_impl(gle_handle* h, const double* fpot_host_T) {
   launch_phaseC(h->d_sd, h->d_clk, (int)h->B, h->ndblk, mode1, mode1, h->stream);
   h->t += 1;
   h->pot_cache_exact = (fpot_host_T == nullptr) && h->constr.empty();
-  if (++h->steps_since_far >= h->L) h->far_due = true;
+  if (h->far_mode == GLE_FAR_SPECTRAL) {
+    if (h->t % h->L == 0) h->far_due = true;
+  } else if (++h->steps_since_far >= h->L) {
+    h->far_due = true;
+  }
   HIPCHK(h, hipGetLastError());
   return GLE_OK;
 }
@@ -775,6 +910,8 @@ int gle_create(const gle_config* cfg, gle_handle** out) {
   if (cfg->nph <= 0 || cfg->ntraj <= 0 || cfg->nmd <= 0 || !(cfg->dt > 0))
     return fail(nullptr, GLE_ERR_ARG, "nph, ntraj, nmd must be > 0 and dt > 0");
   if (cfg->nmd % 2) return fail(nullptr, GLE_ERR_ARG, "nmd must be even (functions.py:47-50 length check)");
+  if (cfg->far_mode < GLE_FAR_AUTO || cfg->far_mode > GLE_FAR_SPECTRAL) return fail(nullptr, GLE_ERR_ARG, "bad far_mode");
+  if (cfg->block_len < 0 || cfg->block_len > 4096) return fail(nullptr, GLE_ERR_ARG, "bad block_len");
   if (cfg->nph > (1 << 24) || cfg->ntraj > (1 << 20)) return fail(nullptr, GLE_ERR_UNSUP, "size too large");
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
@@ -963,6 +1100,7 @@ int gle_set_state(gle_handle* h, const double* p, const double* q, int64_t t) {
   rc = upload(h, h->d_clk, &c, sizeof(c));
   if (rc) return rc;
   HIPCHK(h, hipMemsetAsync(h->d_qvalid, 0, (size_t)B * 4, h->stream));
+  HIPCHK(h, hipMemsetAsync(h->d_pmax, 0, (size_t)B * 4 * 8, h->stream));
   // p_t into the history ring slot of t; q_t into the q gather
   for (auto& b : h->baths) {
     std::vector<double> col((size_t)b.nc * B), colq((size_t)b.ncp * B, 0.0);
@@ -1274,6 +1412,7 @@ int gle_sync(gle_handle* h) {
 int gle_get_current(gle_handle* h, double* cur) {
   if (!h || !cur) return GLE_ERR_ARG;
   hipSetDevice(h->cfg.device);
+  if (h->frozen) launch_finalize(h->d_sd, (int)h->B, (int)h->nmd, (int)h->baths.size(), h->stream);
   const int64_t B = h->B, nmd = h->nmd;
   std::vector<double> buf((size_t)nmd * B);
   for (size_t j = 0; j < h->baths.size(); ++j) {
@@ -1288,6 +1427,7 @@ int gle_get_current(gle_handle* h, double* cur) {
 int gle_get_energy(gle_handle* h, double* etot) {
   if (!h || !etot) return GLE_ERR_ARG;
   hipSetDevice(h->cfg.device);
+  if (h->frozen) launch_finalize(h->d_sd, (int)h->B, (int)h->nmd, (int)h->baths.size(), h->stream);
   const int64_t B = h->B, nmd = h->nmd;
   std::vector<double> buf((size_t)nmd * B);
   int rc = download(h, buf.data(), h->d_etot, buf.size() * 8);
@@ -1350,10 +1490,12 @@ int gle_profile_read(gle_handle* h, int64_t* nlaunch, double* total_ms, double* 
   return GLE_OK;
 }
 
-int gle_plan_info(gle_handle* h, int64_t* block_len, int64_t* far_items, int64_t* device_bytes) {
+int gle_plan_info(gle_handle* h, int64_t* block_len, int64_t* far_items, int64_t* device_bytes,
+                  int32_t* far_mode) {
   if (!h) return GLE_ERR_ARG;
   if (block_len) *block_len = h->frozen ? h->L : 0;
-  if (far_items) *far_items = (int64_t)h->op_far.items.size();
+  if (far_mode) *far_mode = h->frozen ? h->far_mode : h->cfg.far_mode;
+  if (far_items) *far_items = (int64_t)(h->far_mode == GLE_FAR_SPECTRAL ? h->op_spec.items.size() : h->op_far.items.size());
   if (device_bytes) *device_bytes = (int64_t)h->dev_bytes;
   return GLE_OK;
 }

@@ -44,6 +44,8 @@ struct CItem {
   int32_t col0;      // column offset of this tile inside the window
   int32_t ncols;     // valid columns to store
   int32_t nrows;     // valid rows to store (<= 64)
+  int32_t tdiv;      // ring index = floor(clock.t / tdiv) + tshift - slice (1: steps, P: segments)
+  int32_t pad;
 };
 
 // Deterministic fixed-order sum of split partial tiles (+ optional far-field addend).
@@ -92,8 +94,8 @@ struct StepDev {
   double* Q0;             // last q the potential force was evaluated at (md.q0)
   int32_t* qvalid;        // [B] md.q0 != [] flag
   double* Ypot;           // dyn . x of the latest potential product [nph][B]
-  double* pdiff;          // [2][ndblk][B] partial max |x - q0| (slot 0: id0, slot 1: id1)
-  double* part;           // [ndblk][nbath+1][B] current / energy partial sums
+  unsigned long long* pmax;  // [2 (id0,id1)][2 (parity)][B] max |x - q0| as ordered bit patterns
+  double* part;           // [nmd][ndblk][nbath+1][B] current / energy partial sums per step
   const uint8_t* cmask;   // [nph] constraint mask
   int32_t ndblk;          // DOF chunks of the phase kernels
   int32_t dchunk;         // DOFs per chunk
@@ -109,10 +111,18 @@ void launch_phaseA(const StepDev* sd, const Clock* clk, int B, int ndblk, int mo
 void launch_phaseB(const StepDev* sd, const Clock* clk, int B, int ndblk, int mode1, hipStream_t s);
 void launch_phaseC(const StepDev* sd, Clock* clk, int B, int ndblk, int mode1, int diff0,
                    hipStream_t s);
+void launch_finalize(const StepDev* sd, int B, int nmd, int nbath, hipStream_t s);
 void launch_philox_normal(double* x, int64_t nfreq, int64_t ncp, int64_t nc, int64_t B,
                           uint64_t seed, uint64_t traj_offset, hipStream_t s);
 void launch_ring_copy(double* H, int64_t ldh, int R, int B, int nc, int64_t tau0, int nt, double* buf,
                       int dir, hipStream_t s);
+void launch_khat_pack(const double* Kf, int ml, int nks_k, double* khat, int P, int M, int nc,
+                      int nrt2, int nks2, const double* cstab, hipStream_t s);
+void launch_seg_fft(const double* H, int64_t ldh, int R, int B, int nc, int P, int64_t T, int nseg,
+                    double* seg, int64_t seg_fstride, int64_t ldseg, int Rseg, const double* cstab,
+                    hipStream_t s);
+void launch_far_ifft(const double* Y, int64_t yfstride, int nc, int B, int P, double* far,
+                     int64_t ldfar, const double* cstab, Clock* clk, hipStream_t s);
 int launch_fft_noise(const double* a, double* noise, const double* tw, int64_t nmd, int64_t nc,
                      int64_t arows, int64_t B, int is_complex, double scale, hipStream_t s);
 

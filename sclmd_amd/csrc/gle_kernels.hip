@@ -73,7 +73,8 @@ __global__ __launch_bounds__(WG, 2) void contract_kernel(const CItem* __restrict
                                              // complementary LDS bank halves for ds_read_b64
     int64_t wbase = it.col0;
     if (it.ring) {
-      const int64_t tau = t + it.tshift - (int64_t)(it.ia + s0 + ns - 1);
+      const int64_t tt = it.tdiv > 1 ? t / it.tdiv : t;
+      const int64_t tau = tt + it.tshift - (int64_t)(it.ia + s0 + ns - 1);
       wbase += pmod(tau, it.ring) * it.cs;
     }
     const double* xs0 = it.X + wbase;
@@ -267,18 +268,23 @@ struct Lanes {
 };
 
 // md.potforce's cache (md.py:449-450, 767-779) for the harmonic force, per trajectory: hit iff the
-// cache is valid and max_d |q - q0| < 1e-9; the max over DOF chunks comes from the partial maxima
-// the previous phase kernel wrote (pdiff[slot][dblk][b]).
-__device__ __forceinline__ bool pot_hit(const StepDev* sd, int slot, int b, bool need_valid) {
-  if (need_valid && sd->qvalid[b] == 0) return false;
-  bool nan = false;
-  const double m = max_slots(sd->pdiff + (int64_t)slot * sd->ndblk * sd->B + b, sd->B, sd->ndblk, nan);
-  return !nan && m < 10e-10;
+// cache is valid and max_d |q - q0| < 1e-9.  The max over all DOFs is one word per trajectory,
+// accumulated with atomicMax on the bit pattern (non-negative doubles order like their bits; a NaN
+// pattern exceeds every finite value and reads back as NaN -> miss).  Words are double-buffered by
+// step parity and zeroed one kernel ahead of their producer.
+__device__ __forceinline__ unsigned long long* pmax_word(const StepDev* sd, int id, int par, int b) {
+  return sd->pmax + ((int64_t)(id * 2 + par)) * sd->B + b;
 }
 
-// block max of v over the DOF lanes of each trajectory -> pdiff[slot][blockIdx.y][b]
-__device__ __forceinline__ void block_max_store(const StepDev* sd, const Lanes& L, double v, int slot,
-                                                double* red) {
+__device__ __forceinline__ bool pot_hit(const StepDev* sd, int id, int par, int b, bool need_valid) {
+  if (need_valid && sd->qvalid[b] == 0) return false;
+  const double m = __longlong_as_double((long long)*pmax_word(sd, id, par, b));
+  return m == m && m < 10e-10;
+}
+
+// block max of v over the DOF lanes of each trajectory, then one atomicMax per trajectory
+__device__ __forceinline__ void block_max_atomic(const StepDev* sd, const Lanes& L, double v, int id,
+                                                 int par, double* red) {
   red[threadIdx.x] = L.ok ? v : 0.0;
   __syncthreads();
   if (L.dl == 0 && L.ok) {
@@ -289,7 +295,8 @@ __device__ __forceinline__ void block_max_store(const StepDev* sd, const Lanes& 
       nan |= (w != w);
       m = fmax(m, w);
     }
-    sd->pdiff[((int64_t)slot * sd->ndblk + blockIdx.y) * sd->B + L.b] = nan ? NAN : m;
+    const unsigned long long bits = nan ? 0x7FF8000000000000ull : (unsigned long long)__double_as_longlong(m);
+    atomicMax(pmax_word(sd, id, par, L.b), bits);
   }
   __syncthreads();
 }
@@ -320,7 +327,8 @@ __global__ __launch_bounds__(256) void phaseA_kernel(const StepDev* __restrict__
   const double dt = sd->dt, dt2 = dt * dt;
   const int d0 = blockIdx.y * sd->dchunk;
   const int d1 = min(nph, d0 + sd->dchunk);
-  const bool hit = (mode0 == 1 && L.ok) ? pot_hit(sd, 0, L.b, true) : true;
+  const bool hit = (mode0 == 1 && L.ok) ? pot_hit(sd, 0, par, L.b, true) : true;
+  if (L.ok && blockIdx.y == 0 && L.dl == 0) *pmax_word(sd, 0, par ^ 1, L.b) = 0ull;
   double cur[MAXBATH];
 #pragma unroll
   for (int j = 0; j < MAXBATH; ++j) cur[j] = 0.0;
@@ -377,11 +385,11 @@ __global__ __launch_bounds__(256) void phaseA_kernel(const StepDev* __restrict__
     if (L.dl == 0 && L.ok) {
       double s = 0.0;
       for (int x = 0; x < L.DL; ++x) s += red[x * L.BT + L.bl];
-      sd->part[((int64_t)blockIdx.y * (nb + 1) + qd) * B + L.b] = s;
+      sd->part[(((int64_t)tn * sd->ndblk + blockIdx.y) * (nb + 1) + qd) * B + L.b] = s;
     }
     __syncthreads();
   }
-  if (diff1) block_max_store(sd, L, dq, 1, red);
+  if (diff1) block_max_atomic(sd, L, dq, 1, par, red);
 }
 
 // potential force at q~ for DOF d: mode1 0 = in Fc (host force), 1 = harmonic cache select
@@ -414,7 +422,7 @@ __global__ __launch_bounds__(256) void phaseB_kernel(const StepDev* __restrict__
   const int d0 = blockIdx.y * sd->dchunk;
   const int d1 = min(nph, d0 + sd->dchunk);
   if (!L.ok) return;
-  const bool hit1 = (mode1 == 1) ? pot_hit(sd, 1, L.b, false) : true;
+  const bool hit1 = (mode1 == 1) ? pot_hit(sd, 1, (int)(t & 1), L.b, false) : true;
   for (int d = d0 + L.dl; d < d1; d += L.DL) {
     bool inb = false;
 #pragma unroll
@@ -448,7 +456,9 @@ __global__ __launch_bounds__(256) void phaseC_kernel(const StepDev* __restrict__
   const double dt = sd->dt;
   const int d0 = blockIdx.y * sd->dchunk;
   const int d1 = min(nph, d0 + sd->dchunk);
-  const bool hit1 = (mode1 == 1 && L.ok) ? pot_hit(sd, 1, L.b, false) : true;
+  const int par = (int)(t & 1);
+  const bool hit1 = (mode1 == 1 && L.ok) ? pot_hit(sd, 1, par, L.b, false) : true;
+  if (L.ok && blockIdx.y == 0 && L.dl == 0) *pmax_word(sd, 1, par ^ 1, L.b) = 0ull;
   double dq = 0.0;
   if (L.ok) {
     for (int d = d0 + L.dl; d < d1; d += L.DL) {
@@ -488,19 +498,9 @@ __global__ __launch_bounds__(256) void phaseC_kernel(const StepDev* __restrict__
         }
       }
     }
-    // close step t's heat current and kinetic energy from phase A's partial sums (fixed order)
-    if (blockIdx.y == 0) {
-      for (int qd = L.dl; qd <= nb; qd += L.DL) {
-        const double s = sum_slots(0.0, sd->part + (int64_t)qd * B + L.b, (int64_t)(nb + 1) * B, sd->ndblk);
-        if (qd < nb) {
-          sd->bath[qd].cur[(int64_t)tn * B + L.b] = s;
-        } else {
-          sd->etot[(int64_t)tn * B + L.b] = 0.5 * s;  // md.py:161-165, 383
-        }
-      }
-    }
   }
-  if (diff0) block_max_store(sd, L, dq, 0, red);
+  (void)tn;
+  if (diff0) block_max_atomic(sd, L, dq, 0, par ^ 1, red);
   if (mode1 == 1 && L.ok && blockIdx.y == 0 && L.dl == 0) sd->qvalid[L.b] = 1;
   // the last block to finish advances the step counter (all blocks read t before arriving)
   __syncthreads();
@@ -514,6 +514,29 @@ __global__ __launch_bounds__(256) void phaseC_kernel(const StepDev* __restrict__
       __threadfence();
     }
   }
+}
+
+// bath.cur[t] and md.etot[t] (md.py:383, 397) for every step of the run from phase A's per-step
+// partial sums, added in fixed DOF-chunk order (deterministic); launched when outputs are read.
+__global__ void finalize_kernel(const StepDev* __restrict__ sd) {
+  const int B = sd->B, nb = sd->nbath, nmd = sd->nmd, nd = sd->ndblk;
+  const int64_t total = (int64_t)nmd * (nb + 1) * B;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int b = (int)(e % B);
+    const int qd = (int)((e / B) % (nb + 1));
+    const int tn = (int)(e / ((int64_t)B * (nb + 1)));
+    const double s = sum_slots(0.0, sd->part + ((int64_t)tn * nd * (nb + 1) + qd) * B + b,
+                               (int64_t)(nb + 1) * B, nd);
+    if (qd < nb) sd->bath[qd].cur[(int64_t)tn * B + b] = s;
+    else sd->etot[(int64_t)tn * B + b] = 0.5 * s;  // md.py:161-165, 383
+  }
+}
+
+void launch_finalize(const StepDev* sd, int B, int nmd, int nbath, hipStream_t s) {
+  const int64_t total = (int64_t)nmd * (nbath + 1) * B;
+  const int64_t blocks = std::min<int64_t>((total + 255) / 256, 4096);
+  finalize_kernel<<<(unsigned)blocks, 256, 0, s>>>(sd);
 }
 
 static inline dim3 phase_grid(int B, int ndblk) {
@@ -693,6 +716,141 @@ void launch_ring_copy(double* H, int64_t ldh, int R, int B, int nc, int64_t tau0
   if (n <= 0) return;
   const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
   ring_copy_kernel<<<(unsigned)blocks, 256, 0, s>>>(H, ldh, R, B, nc, tau0, nt, buf, dir);
+}
+
+}  // namespace gle
+
+namespace gle {
+
+// ------------------------------------------------------------------------------------------
+// Spectral (overlap-save) far field.  cstab[q] = (cos(pi q / P), sin(pi q / P)), q < 2P.
+//
+// Kernel partitions k_m[i'] = K_{mP+i'} (i' < P, zero-padded to 2P), m = 1..M, transformed:
+//   Khat_m(f) = sum_i' k_m[i'] e^{-i pi f i'/P}, f = 0..P.
+// Packed as the real block [[Re, -Im], [Im, Re]] (2nc x 2nc) in fragment-native order
+// [f][rt][ks][m-1][64], read straight out of the fragment-native K already on the device.
+__global__ void khat_pack_kernel(const double* __restrict__ Kf, int ml, int nks_k,
+                                 double* __restrict__ khat, int P, int M, int nc, int nrt2, int nks2,
+                                 const double2* __restrict__ cstab) {
+  const int64_t total = (int64_t)(P + 1) * nrt2 * nks2 * M * 64;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int lane = (int)(e & 63);
+    int64_t r_ = e >> 6;
+    const int mm = (int)(r_ % M);
+    r_ /= M;
+    const int ks2 = (int)(r_ % nks2);
+    r_ /= nks2;
+    const int rt2 = (int)(r_ % nrt2);
+    const int f = (int)(r_ / nrt2);
+    const int r = 16 * rt2 + (lane & 15);
+    const int k = 4 * ks2 + (lane >> 4);
+    double v = 0.0;
+    if (r < 2 * nc && k < 2 * nc) {
+      const int rb = r >= nc, kb = k >= nc;
+      const int rr = r - rb * nc, kk = k - kb * nc;
+      const int64_t base = (((int64_t)(rr >> 4) * nks_k + (kk >> 2)) * ml) * 64 + (rr & 15) + 16 * (kk & 3);
+      double re = 0.0, im = 0.0;
+      const int m = mm + 1;
+      for (int ip = 0; ip < P; ++ip) {
+        const int i = m * P + ip;
+        if (i >= ml) break;
+        const double kv = Kf[base + (int64_t)i * 64];
+        const double2 cs = cstab[(f * ip) % (2 * P)];
+        re += kv * cs.x;
+        im -= kv * cs.y;
+      }
+      v = (rb == kb) ? re : (rb ? im : -im);
+    }
+    khat[e] = v;
+  }
+}
+
+void launch_khat_pack(const double* Kf, int ml, int nks_k, double* khat, int P, int M, int nc,
+                      int nrt2, int nks2, const double* cstab, hipStream_t s) {
+  khat_pack_kernel<<<8192, 256, 0, s>>>(Kf, ml, nks_k, khat, P, M, nc, nrt2, nks2,
+                                        (const double2*)cstab);
+}
+
+// Segment spectra for the nseg newest segments (sigma = T/P - s): x[n] = p at time
+// sigma*P - 2P + 2 + n (n < 2P-1), x[2P-1] = 0; Xhat(f) = sum_n x[n] e^{-i pi f n/P} written as rows
+// [k] = Re and [nc+k] = Im of the frequency-f segment ring (mirrored slots).
+__global__ void seg_fft_kernel(const double* __restrict__ H, int64_t ldh, int R, int B, int nc,
+                               int P, int64_t T, int nseg, double* __restrict__ seg,
+                               int64_t seg_fstride, int64_t ldseg, int Rseg,
+                               const double2* __restrict__ cstab) {
+  const int64_t total = (int64_t)nseg * (P + 1) * nc * B;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int b = (int)(e % B);
+    int64_t r_ = e / B;
+    const int k = (int)(r_ % nc);
+    r_ /= nc;
+    const int f = (int)(r_ % (P + 1));
+    const int sidx = (int)(r_ / (P + 1));
+    const int64_t sigma = T / P - sidx;
+    const int64_t t0 = sigma * P - 2 * P + 2;
+    const double* hk = H + (int64_t)k * ldh + b;
+    double re = 0.0, im = 0.0;
+    for (int n = 0; n < 2 * P - 1; ++n) {
+      const double x = hk[pmod(t0 + n, R) * B];
+      const double2 cs = cstab[(f * n) % (2 * P)];
+      re += x * cs.x;
+      im -= x * cs.y;
+    }
+    const int64_t slot = pmod(sigma, Rseg);
+    double* sf = seg + (int64_t)f * seg_fstride + b;
+    sf[(int64_t)k * ldseg + slot * B] = re;
+    sf[(int64_t)k * ldseg + (slot + Rseg) * B] = re;
+    sf[(int64_t)(nc + k) * ldseg + slot * B] = im;
+    sf[(int64_t)(nc + k) * ldseg + (slot + Rseg) * B] = im;
+  }
+}
+
+void launch_seg_fft(const double* H, int64_t ldh, int R, int B, int nc, int P, int64_t T, int nseg,
+                    double* seg, int64_t seg_fstride, int64_t ldseg, int Rseg, const double* cstab,
+                    hipStream_t s) {
+  const int64_t total = (int64_t)nseg * (P + 1) * nc * B;
+  const int64_t blocks = std::min<int64_t>((total + 255) / 256, 16384);
+  seg_fft_kernel<<<(unsigned)blocks, 256, 0, s>>>(H, ldh, R, B, nc, P, T, nseg, seg, seg_fstride,
+                                                  ldseg, Rseg, (const double2*)cstab);
+}
+
+// far(T+1+j) = y[j+P-1],  y[n] = (1/2P) [Y0 + (-1)^n Y_P + 2 sum_{0<f<P} Re(Y_f e^{+i pi f n/P})]
+// (the real inverse transform of the Hermitian spectrum; Im Y_0, Im Y_P ignored as by irfft).
+__global__ void far_ifft_kernel(const double* __restrict__ Y, int64_t yfstride, int nc, int B, int P,
+                                double* __restrict__ far, int64_t ldfar,
+                                const double2* __restrict__ cstab, Clock* clk) {
+  const int64_t total = (int64_t)nc * P * B;
+  if (blockIdx.x == 0 && threadIdx.x == 0) clk->t_far = load_t(clk);
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int b = (int)(e % B);
+    int64_t r_ = e / B;
+    const int j = (int)(r_ % P);
+    const int k = (int)(r_ / P);
+    const int n = j + P - 1;
+    const double* yk = Y + (int64_t)k * B + b;
+    const int64_t im_off = (int64_t)nc * B;
+    double acc = 0.0;
+    for (int f = 1; f < P; ++f) {
+      const double2 cs = cstab[(f * n) % (2 * P)];
+      const double* yf = yk + (int64_t)f * yfstride;
+      acc += yf[0] * cs.x - yf[im_off] * cs.y;
+    }
+    const double y0 = yk[0];
+    const double yp = yk[(int64_t)P * yfstride];
+    const double v = (y0 + ((n & 1) ? -yp : yp) + 2.0 * acc) / (2.0 * P);
+    far[(int64_t)k * ldfar + (int64_t)j * B + b] = v;
+  }
+}
+
+void launch_far_ifft(const double* Y, int64_t yfstride, int nc, int B, int P, double* far,
+                     int64_t ldfar, const double* cstab, Clock* clk, hipStream_t s) {
+  const int64_t total = (int64_t)nc * P * B;
+  const int64_t blocks = std::min<int64_t>((total + 255) / 256, 16384);
+  far_ifft_kernel<<<(unsigned)blocks, 256, 0, s>>>(Y, yfstride, nc, B, P, far, ldfar,
+                                                   (const double2*)cstab, clk);
 }
 
 }  // namespace gle

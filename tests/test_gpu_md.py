@@ -165,22 +165,23 @@ def test_device_noise_covariance(kind):
     assert np.array_equal(nz2, nz[:4]) and not np.allclose(nz3, nz2)
 
 
-def _c3_stepper(ntraj, ml=1024, nmd=4096, block_len=0):
+def _c3_stepper(ntraj, ml=1024, nmd=4096, block_len=0, far_mode="auto"):
     from sclmd_amd import _native as N
     from sclmd_amd import synthetic
 
     dyn, axyz, baths, meta = synthetic.junction("C3", ml=ml, nmd=nmd)
-    st = N.Stepper(meta["nph"], ntraj, meta["nmd"], meta["dt"], 0, block_len)
+    st = N.Stepper(meta["nph"], ntraj, meta["nmd"], meta["dt"], 0, block_len, far_mode)
     for b in baths:
         st.add_bath(N.GLE_BATH_PHONON, b.cids, b.kernel)
     st.set_dyn(dyn)
     return st, baths, meta
 
 
-def test_c3_linearity_full_size():
+@pytest.mark.parametrize("far_mode", ["direct", "spectral"])
+def test_c3_linearity_full_size(far_mode):
     """At the full C3 shape (nph 900, 2 x nc 300, ml 1024): the step is linear in (state, noise), so
     trajectory(s1+s2, n1+n2) == trajectory(s1, n1) + trajectory(s2, n2) within fp64 rounding."""
-    st, baths, meta = _c3_stepper(3)
+    st, baths, meta = _c3_stepper(3, far_mode=far_mode)
     nph, nmd = meta["nph"], meta["nmd"]
     rng = np.random.default_rng(5)
     p = rng.normal(size=(3, nph)) * 1e-3
@@ -192,18 +193,19 @@ def test_c3_linearity_full_size():
         n = rng.normal(size=(3, nmd, b.nc)) * 1e-3
         n[2] = n[0] + n[1]
         st.set_noise(i, n)
-    st.run(40)
+    st.run(70)
     p, q, t = st.get_state()
-    assert t == 40
+    assert t == 70
     assert rel(q[2], q[0] + q[1]) < 1e-11 and rel(p[2], p[0] + p[1]) < 1e-11
     st.close()
 
 
-def test_c3_trajectory_vs_oracle_short():
+@pytest.mark.parametrize("far_mode", ["direct", "spectral"])
+def test_c3_trajectory_vs_oracle_short(far_mode):
     """Full C3 shape, 1 trajectory, a few steps against the oracle (reference-shaped numpy)."""
     from oracle import sclmd_oracle as O
 
-    st, baths, meta = _c3_stepper(1)
+    st, baths, meta = _c3_stepper(1, far_mode=far_mode)
     nph, nmd, dt = meta["nph"], meta["nmd"], meta["dt"]
     rng = np.random.default_rng(9)
     p = rng.normal(size=nph) * 1e-3
@@ -218,25 +220,26 @@ def test_c3_trajectory_vs_oracle_short():
 
     sim = O.GLE(nph, dt, nmd, bs, dyn=synthetic.chain_dyn(meta["natom"]))
     sim.p, sim.q = p.copy(), q.copy()
-    for _ in range(6):
+    nst = 40  # crosses the first spectral block boundary (P = 32)
+    for _ in range(nst):
         sim.step()
-    st.run(6)
+    st.run(nst)
     pg, qg, _ = st.get_state()
     assert rel(qg[0], sim.q) < 1e-10 and rel(pg[0], sim.p) < 1e-10
-    cur = st.get_current()[:, 0, :6]
-    assert rel(cur, np.array([b.cur[:6] for b in bs])) < 1e-9
+    cur = st.get_current()[:, 0, :nst]
+    assert rel(cur, np.array([b.cur[:nst] for b in bs])) < 1e-9
     st.close()
 
 
-@pytest.mark.parametrize("block_len", [0, 5])
-def test_ring_wraparound_vs_oracle(block_len):
-    """Run well past the history ring length (R = ml + 2L + 2 slots) and across the noise period."""
+@pytest.mark.parametrize("far_mode,block_len", [("auto", 0), ("direct", 5), ("spectral", 4), ("spectral", 7)])
+def test_ring_wraparound_vs_oracle(far_mode, block_len):
+    """Run well past the history ring length (R = ml + 3L + 2 slots) and across the noise period."""
     from sclmd_amd import _native as N
     from oracle import sclmd_oracle as O
 
     g = load_golden("vv_twoph")
     nph, nmd, dt = 3 * int(g["natom"]), int(g["nmd"]), float(g["dt"])
-    st = N.Stepper(nph, 2, nmd, dt, 0, block_len)
+    st = N.Stepper(nph, 2, nmd, dt, 0, block_len, far_mode)
     for i in range(int(g["nbath"])):
         st.add_bath(N.GLE_BATH_PHONON, g["b%d_cids" % i], g["b%d_kernel" % i])
     st.set_dyn(g["dyn_md"])

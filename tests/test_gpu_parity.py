@@ -16,11 +16,11 @@ def relerr(a, b):
     return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
 
 
-def stepper_from_golden(g, ntraj=1, block_len=0):
+def stepper_from_golden(g, ntraj=1, block_len=0, far_mode="auto"):
     from sclmd_amd import _native as N
 
     nph = 3 * int(g["natom"])
-    st = N.Stepper(nph, ntraj, int(g["nmd"]), float(g["dt"]), 0, block_len)
+    st = N.Stepper(nph, ntraj, int(g["nmd"]), float(g["dt"]), 0, block_len, far_mode)
     for i in range(int(g["nbath"])):
         kind = str(g["b%d_kind" % i])
         if kind == "ebath":
@@ -40,11 +40,16 @@ def stepper_from_golden(g, ntraj=1, block_len=0):
     return st
 
 
+FAR_VARIANTS = [("auto", 0), ("direct", 1), ("direct", 3), ("spectral", 2), ("spectral", 5)]
+
+
 @pytest.mark.parametrize("case", vv_cases())
-@pytest.mark.parametrize("block_len", [0, 1, 3])
-def test_vv_golden(case, block_len):
+@pytest.mark.parametrize("far_mode,block_len", FAR_VARIANTS)
+def test_vv_golden(case, far_mode, block_len):
     g = load_golden(case)
-    st = stepper_from_golden(g, 1, block_len)
+    st = stepper_from_golden(g, 1, block_len, far_mode)
+    if far_mode == "spectral" and max(int(g["b%d_ml" % i]) for i in range(int(g["nbath"]))) > block_len:
+        assert st.plan_info()["far_mode"] == "spectral"
     nmd = int(g["nmd"])
     qs, ps = [], []
     for _ in range(int(g["nsteps"])):
@@ -65,13 +70,14 @@ def test_vv_golden(case, block_len):
     st.close()
 
 
-@pytest.mark.parametrize("case", ["vv_mixed", "vv_biased"])
-def test_vv_batched_trajectories(case):
+@pytest.mark.parametrize("case", ["vv_mixed", "vv_biased", "vv_twoph"])
+@pytest.mark.parametrize("far_mode", ["direct", "spectral"])
+def test_vv_batched_trajectories(case, far_mode):
     """B trajectories with different initial states and noise vs the oracle, one by one."""
     g = load_golden(case)
     B = 5
     rng = np.random.default_rng(7)
-    st = stepper_from_golden(g, B)
+    st = stepper_from_golden(g, B, 4 if far_mode == "spectral" else 0, far_mode)
     p0 = g["p0"][None] * (1 + 0.1 * rng.normal(size=(B, 1)))
     q0 = g["q0"][None] * (1 + 0.1 * rng.normal(size=(B, 1)))
     st.set_state(p0, q0, 0)
