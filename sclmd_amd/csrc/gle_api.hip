@@ -28,6 +28,7 @@ namespace {
 thread_local std::string g_create_error;
 
 struct Op {
+  bool cplx = false;   // complex items (contract_cplx_kernel)
   int rn = 1;
   int cu = 1;          // staged X columns per thread per row (contract_kernel template)
   int max_elems = 0;   // largest reduce tile
@@ -54,6 +55,7 @@ struct Bath {
   int32_t* d_inv = nullptr;
   double *d_noise = nullptr, *d_Y = nullptr, *d_S = nullptr, *d_Yq = nullptr;
   double *d_Xcur = nullptr, *d_Xq = nullptr, *d_H = nullptr, *d_cur = nullptr, *d_far = nullptr;
+  double* d_mid = nullptr;
   int64_t ldh = 0;
   int R = 1;
   bool noise_set = false;
@@ -98,9 +100,12 @@ struct gle_handle {
   bool far_due = true;
   bool pot_cache_exact = false;  // q_t == q~_{t-1} bitwise (no constraints): id0 cache hit
   bool host_force_step = false;
-  Op op_far, op_prime, op0, op0p, op1a, op1a_np, op1b;
-  Op op_near[2];  // S(t+1) into S[(t+1)&1]: one plan per destination parity
+  Op op_far, op_prime, op1a, op1a_np, op1b;
+  Op op0[2], op0p[2];  // {K0 p_t, Kq q_t, near S(t+1) into S[par]} (+ dyn q_t), par = (t+1)&1
   Op op_spec;     // spectral far field: per-frequency contraction of kernel and segment spectra
+  Op op_mid;      // mid-level block: lags [P1, L) every P1 steps, P1*B columns
+  int P1 = 0;     // mid-level block length (0: none, near field covers [1, L))
+  bool mid_due = true;
   int far_mode = GLE_FAR_DIRECT;
   bool seg_ready = false;
   double* d_cstab = nullptr;
@@ -200,10 +205,15 @@ struct Gemm {
   const double* add = nullptr;  // far addend
   int64_t lda = 0;
   int add_cs = 0;
+  const double* add2 = nullptr;  // mid-level addend
+  int64_t lda2 = 0;
+  int add2_cs = 0;
   bool force_reduce = false;
   int Kd = 0;  // true (unpadded) reduction length, for the algorithmic flop/byte count
   int tdiv = 1;
   bool lat = false;  // per-step product: minimise sequential LDS stages per item
+  bool cplx = false; // complex product: Im parts of A, X, dst at a_im, x_im, dst_im
+  int64_t a_im = 0, x_im = 0, dst_im = 0;
 };
 
 // Split policy: target ~target_items work items in total for this product, each with at least
@@ -216,7 +226,7 @@ void plan_gemm(Op& op, const Gemm& g, int target_items, int min_work) {
   const int ni = g.i1 - g.i0;
   const int nkp = g.nks_total / 2;  // k-step pairs
   const int base = ngroups * ncol;
-  int si = 1, sk = 1;
+  int si = 1, sk = 1, chunk = 0;  // chunk > 0: fixed slices per item (last one shorter)
   if (g.lat && ni > 0) {
     // latency-bound per-step product: each item stages ONE window of slices (as many as fit the
     // LDS row) for ONE or a few k-stages, so an item is a couple of LDS round trips long
@@ -231,7 +241,13 @@ void plan_gemm(Op& op, const Gemm& g, int target_items, int min_work) {
     split = (int)std::min<int64_t>(split, std::max<int64_t>(1, work / std::max(1, min_work)));
     if (ni > 0) {
       if (g.ring) {
-        si = std::min(split, ni);
+        // slice chunks are whole multiples of what one LDS window holds, so no item runs its
+        // k-stages with a short remainder window
+        const int wcap = g.cplx ? CPLX_WW_CAP : std::min(LDS_WW_MAX, 256 * (op.rn >= 16 ? 3 : 4));
+        const int ns_cap = std::max(1, (wcap - NT) / std::max(1, g.cs) + 1);
+        const int q = std::max(1, (int)((double)ni / ((double)split * ns_cap) + 0.5));
+        chunk = ns_cap * q;
+        si = (ni + chunk - 1) / chunk;
         sk = std::max(1, std::min(nkp, split / si));
       } else {
         sk = std::min(split, nkp);
@@ -240,7 +256,7 @@ void plan_gemm(Op& op, const Gemm& g, int target_items, int min_work) {
     }
   }
   const int nsplit = (ni > 0) ? si * sk : 0;
-  const bool use_partial = g.force_reduce || g.add != nullptr || nsplit > 1;
+  const bool use_partial = g.force_reduce || g.add != nullptr || g.add2 != nullptr || nsplit > 1;
   // item order: (column tile, slice range, k range) outer, row group inner -- consecutive items
   // share the staged history window (and, with the kernel's XCD-aware mapping, one L2)
   std::vector<size_t> slot0s((size_t)ngroups * ncol, 0);
@@ -248,14 +264,14 @@ void plan_gemm(Op& op, const Gemm& g, int target_items, int min_work) {
   for (int gi = 0; gi < ngroups; ++gi)
     for (int ct = 0; ct < ncol; ++ct) {
       slot0s[(size_t)gi * ncol + ct] = op.partial_doubles;
-      if (use_partial) op.partial_doubles += (size_t)nsplit * 64 * NT;
+      if (use_partial) op.partial_doubles += (size_t)nsplit * (g.cplx ? 2 : 1) * 64 * NT;
     }
   for (int ct = 0; ct < ncol; ++ct) {
     const int col0 = ct * NT;
     const int ncols = std::min<int>(NT, g.N - col0);
     for (int a = 0; a < si && ni > 0; ++a) {
-      const int ia = g.i0 + (int)((int64_t)ni * a / si);
-      const int ib = g.i0 + (int)((int64_t)ni * (a + 1) / si);
+      const int ia = g.i0 + (chunk ? std::min(ni, a * chunk) : (int)((int64_t)ni * a / si));
+      const int ib = g.i0 + (chunk ? std::min(ni, (a + 1) * chunk) : (int)((int64_t)ni * (a + 1) / si));
       if (ib <= ia) continue;
       for (int b = 0; b < sk; ++b) {
         const int kp0 = (int)((int64_t)nkp * b / sk), kp1 = (int)((int64_t)nkp * (b + 1) / sk);
@@ -281,13 +297,18 @@ void plan_gemm(Op& op, const Gemm& g, int target_items, int min_work) {
           it.col0 = col0;
           it.ncols = ncols;
           it.nrows = nrows;
+          const size_t slot_sz = (size_t)(g.cplx ? 2 : 1) * 64 * NT;
+          it.a_im = g.a_im;
+          it.x_im = g.x_im;
           if (use_partial) {
             // offset into the op's partial buffer, fixed up in materialize()
-            it.out = (double*)(uintptr_t)((slot0s[key] + (size_t)nslot[key] * 64 * NT) * sizeof(double));
+            it.out = (double*)(uintptr_t)((slot0s[key] + (size_t)nslot[key] * slot_sz) * sizeof(double));
             it.ldo = NT;
+            it.o_im = 64 * NT;
           } else {
             it.out = g.dst + (int64_t)(64 * gi) * g.ldd + col0;
             it.ldo = (int32_t)g.ldd;
+            it.o_im = g.dst_im;
           }
           op.items.push_back(it);
           ++nslot[key];
@@ -302,26 +323,33 @@ void plan_gemm(Op& op, const Gemm& g, int target_items, int min_work) {
         const int nrows = std::min(64, g.M - 64 * gi);
         if (nrows <= 0) continue;
         const size_t key = (size_t)gi * ncol + ct;
-        RItem r{};
-        r.dst = g.dst + (int64_t)(64 * gi) * g.ldd + col0;
-        r.src = (const double*)(uintptr_t)(slot0s[key] * sizeof(double));  // offset, fixed up later
-        r.add = g.add ? g.add + (int64_t)(64 * gi) * g.lda + col0 : nullptr;
-        r.ldd = (int32_t)g.ldd;
-        r.lds = NT;
-        r.lda = (int32_t)g.lda;
-        r.nslots = nslot[key];
-        r.slot_stride = (int64_t)64 * NT;
-        r.rows = nrows;
-        r.cols = std::min<int>(NT, g.N - col0);
-        r.add_cs = g.add_cs;
-        op.ritems.push_back(r);
+        for (int part = 0; part < (g.cplx ? 2 : 1); ++part) {
+          RItem r{};
+          r.dst = g.dst + part * g.dst_im + (int64_t)(64 * gi) * g.ldd + col0;
+          // offset, fixed up in materialize()
+          r.src = (const double*)(uintptr_t)((slot0s[key] + (size_t)part * 64 * NT) * sizeof(double));
+          r.add = (g.add && part == 0) ? g.add + (int64_t)(64 * gi) * g.lda + col0 : nullptr;
+          r.add2 = (g.add2 && part == 0) ? g.add2 + (int64_t)(64 * gi) * g.lda2 + col0 : nullptr;
+          r.lda2 = (int32_t)g.lda2;
+          r.add2_cs = g.add2_cs;
+          r.ldd = (int32_t)g.ldd;
+          r.lds = NT;
+          r.lda = (int32_t)g.lda;
+          r.nslots = nslot[key];
+          r.slot_stride = (int64_t)(g.cplx ? 2 : 1) * 64 * NT;
+          r.rows = nrows;
+          r.cols = std::min<int>(NT, g.N - col0);
+          r.add_cs = g.add_cs;
+          op.ritems.push_back(r);
+        }
       }
   // algorithmic work of this product: each kernel entry read once, X read
   // once, output written once.
   if (ni > 0) {
     const double kd = g.Kd > 0 ? g.Kd : 4.0 * g.nks_total;
-    op.flops += 2.0 * g.M * kd * g.N * ni;
-    op.bytes += 8.0 * ((double)ni * g.M * kd + kd * (g.ring ? (double)(ni + (g.N + g.cs - 1) / std::max(1, g.cs) - 1) * g.cs : g.N) + (double)g.M * g.N);
+    const double cf = g.cplx ? 4.0 : 1.0, cb = g.cplx ? 2.0 : 1.0;  // complex: 4 real products
+    op.flops += cf * 2.0 * g.M * kd * g.N * ni;
+    op.bytes += cb * 8.0 * ((double)ni * g.M * kd + kd * (g.ring ? (double)(ni + (g.N + g.cs - 1) / std::max(1, g.cs) - 1) * g.cs : g.N) + (double)g.M * g.N);
   }
 }
 
@@ -335,7 +363,7 @@ int materialize(gle_handle* h, Op& op, const std::vector<bool>& is_partial) {
     maxww = std::max(maxww, std::min(ww, LDS_WW_MAX));
   }
   const int cap = op.rn >= 16 ? 3 : 4;
-  op.cu = std::max(1, std::min(cap, (maxww + 255) / 256));
+  op.cu = op.cplx ? 2 : std::max(1, std::min(cap, (maxww + 255) / 256));
   for (const auto& r : op.ritems) op.max_elems = std::max(op.max_elems, r.rows * r.cols);
   if (op.partial_doubles) {
     int rc = dalloc_n(h, &op.partial, op.partial_doubles);
@@ -411,7 +439,10 @@ void run_op(gle_handle* h, Op& op, int set_tfar, bool profile) {
     h->ev_used += 2;
     hipEventRecord(e0, h->stream);
   }
-  launch_contract(op.rn, op.cu, op.d_items, (int)op.items.size(), h->d_clk, h->stream);
+  if (op.cplx)
+    launch_contract_cplx(op.rn, op.d_items, (int)op.items.size(), h->d_clk, h->stream);
+  else
+    launch_contract(op.rn, op.cu, op.d_items, (int)op.items.size(), h->d_clk, h->stream);
   if (e1) {
     hipEventRecord(e1, h->stream);
     h->prof_n += 1;
@@ -426,8 +457,6 @@ int check_bath(gle_handle* h, int32_t b) {
   if (b < 0 || b >= (int)h->baths.size()) return fail(h, GLE_ERR_ARG, "bad bath id");
   return GLE_OK;
 }
-
-int build_near(gle_handle* h);
 
 // Build every work plan once the system is fixed (first state / step call).
 int freeze(gle_handle* h) {
@@ -460,9 +489,8 @@ int freeze(gle_handle* h) {
     for (auto& b : h->baths) {
       if (b.ml <= L) continue;
       const int M = (b.ml + L - 1) / L - 1;
-      const int64_t nrt2 = (2 * b.nc + 15) / 16, nks2 = rup(2 * b.nc, 8) / 4;
-      need += (size_t)(L + 1) * nrt2 * nks2 * M * 64 * 8;
-      need += (size_t)(L + 1) * rup(2 * b.nc, 8) * (2 * (M + 4) * B + 1024) * 8;
+      need += (size_t)(L + 1) * 2 * b.nrt * b.nks * M * 64 * 8;
+      need += (size_t)(L + 1) * 2 * b.ncp * (2 * (M + 4) * B + 1024) * 8;
     }
     size_t fr = 0, tot = 0;
     hipMemGetInfo(&fr, &tot);
@@ -473,6 +501,8 @@ int freeze(gle_handle* h) {
     }
   }
   h->far_mode = mode;
+  // mid-level block: when the near field would otherwise sweep many kernel slices every step
+  h->P1 = (L >= 16) ? 8 : 0;
   // ring sizes and buffers that depend on L
   for (auto& b : h->baths) {
     b.R = b.ml + 3 * L + 2;
@@ -481,6 +511,10 @@ int freeze(gle_handle* h) {
     if (rc) return rc;
     if (b.ml > L) {
       rc = dalloc_n(h, &b.d_far, (size_t)b.ncp * L * B + 4096);
+      if (rc) return rc;
+    }
+    if (h->P1 && b.ml > h->P1) {
+      rc = dalloc_n(h, &b.d_mid, (size_t)b.ncp * h->P1 * B + 4096);
       if (rc) return rc;
     }
   }
@@ -497,12 +531,12 @@ int freeze(gle_handle* h) {
     for (auto& b : h->baths) {
       if (b.ml <= L) continue;
       b.M = (b.ml + L - 1) / L - 1;
-      b.nrt2 = (2 * b.nc + 15) / 16;
-      b.nks2 = (int)(rup(2 * b.nc, 8) / 4);
+      b.nrt2 = b.nrt;
+      b.nks2 = b.nks;
       b.Rseg = b.M + 4;
       b.ldseg = 2 * (int64_t)b.Rseg * B + 1024;
-      b.khat_fstride = (int64_t)b.nrt2 * b.nks2 * b.M * 64;
-      b.seg_fstride = (int64_t)rup(2 * b.nc, 8) * b.ldseg;
+      b.khat_fstride = (int64_t)2 * b.nrt2 * b.nks2 * b.M * 64;  // Re block then Im block
+      b.seg_fstride = (int64_t)2 * b.ncp * b.ldseg;              // Re rows then Im rows
       b.yfstride = (int64_t)2 * b.nc * B;
       rc = dalloc_n(h, &b.d_khat, (size_t)(L + 1) * b.khat_fstride);
       if (!rc) rc = dalloc_n(h, &b.d_seg, (size_t)(L + 1) * b.seg_fstride + 4096);
@@ -613,9 +647,24 @@ int freeze(gle_handle* h) {
     rc = p.done();
     if (rc) return rc;
   }
+  // MID: lags [P1, min(L, ml)) for targets t+1..t+P1, every P1 steps
+  if (h->P1) {
+    const int P1 = h->P1;
+    Planner p(h, h->op_mid, rn_for((int64_t)P1 * B));
+    for (auto& b : h->baths)
+      if (b.ml > P1) {
+        Gemm g = kgemm(b, b.d_K, P1, std::min(b.ml, L), b.d_H, b.ldh, b.R, 1, (int)(P1 * B), b.d_mid,
+                       (int64_t)P1 * B);
+        g.force_reduce = true;
+        p.add(g, 512, 8);
+      }
+    rc = p.done();
+    if (rc) return rc;
+  }
   // SPECTRAL: per frequency f, Y_f = sum_{m=1..M} Khat_m(f) Xhat_{T/P-m+1}(f) on [[Re,-Im],[Im,Re]]
   if (h->far_mode == GLE_FAR_SPECTRAL) {
     Planner p(h, h->op_spec, rn_step);
+    h->op_spec.cplx = true;
     int nprod = 0;
     for (auto& b : h->baths)
       if (b.d_khat) nprod += L + 1;
@@ -623,23 +672,27 @@ int freeze(gle_handle* h) {
       if (!b.d_khat) continue;
       for (int f = 0; f <= L; ++f) {
         Gemm g{};
+        g.cplx = true;
         g.A = b.d_khat + (int64_t)f * b.khat_fstride;
         g.a_ks = (int64_t)b.M * 64;
         g.a_rt = (int64_t)b.nks2 * g.a_ks;
+        g.a_im = (int64_t)b.nrt2 * b.nks2 * b.M * 64;
         g.nrt_total = b.nrt2;
         g.nks_total = b.nks2;
         g.i0 = 0;
         g.i1 = b.M;
         g.X = b.d_seg + (int64_t)f * b.seg_fstride;
+        g.x_im = (int64_t)b.ncp * b.ldseg;
         g.ldx = b.ldseg;
         g.ring = b.Rseg;
         g.cs = (int)B;
         g.tshift = 0;
         g.tdiv = L;
-        g.M = 2 * b.nc;
-        g.Kd = 2 * b.nc;
+        g.M = b.nc;
+        g.Kd = b.nc;
         g.N = (int)B;
         g.dst = b.d_Yspec + (int64_t)f * b.yfstride;
+        g.dst_im = (int64_t)b.nc * B;
         g.ldd = B;
         p.add(g, std::max(1, 1536 / std::max(1, nprod)), 16);
       }
@@ -659,40 +712,78 @@ int freeze(gle_handle* h) {
     rc = p.done();
     if (rc) return rc;
   }
-  // OP0 (+ pot variant): K0 p_t, near S(t+1) (+ far addend), Kq q_t, [dyn q_t]
-  for (int variant = 0; variant < 2; ++variant) {
-    Op& op = variant ? h->op0p : h->op0;
-    Planner p(h, op, rn_step);
-    for (auto& b : h->baths) {
-      p.add(kgemm(b, b.d_K, 0, 1, b.d_H, b.ldh, b.R, 0, (int)B, b.d_Y, B), TGT_STEP, 4);
-      if (b.has_q) {
-        Gemm g = kgemm(b, b.d_Kq, 0, 1, b.d_Xq, B, 0, 0, (int)B, b.d_Yq, B);
+  // OP0 (+ pot variant) per destination parity: K0 p_t, Kq q_t, [dyn q_t] and the near field
+  // S(t+1) = far(t+1) + sum_{1<=i<L} K_i p_{t+1-i} (only phases B/C need it, but it depends only
+  // on p_t, so it shares this launch)
+  for (int par = 0; par < 2; ++par)
+    for (int variant = 0; variant < 2; ++variant) {
+      Op& op = variant ? h->op0p[par] : h->op0[par];
+      Planner p(h, op, rn_step);
+      for (auto& b : h->baths) {
+        p.add(kgemm(b, b.d_K, 0, 1, b.d_H, b.ldh, b.R, 0, (int)B, b.d_Y, B), TGT_STEP, 4);
+        if (b.has_q) {
+          Gemm g = kgemm(b, b.d_Kq, 0, 1, b.d_Xq, B, 0, 0, (int)B, b.d_Yq, B);
+          g.a_ks = 64;
+          g.a_rt = (int64_t)b.nks * 64;
+          p.add(g, TGT_STEP, 4);
+        }
+      }
+      if (variant && h->has_dyn) {
+        Gemm g{};
+        g.A = h->d_dyn;
         g.a_ks = 64;
-        g.a_rt = (int64_t)b.nks * 64;
+        g.a_rt = (int64_t)h->dyn_nks * 64;
+        g.nrt_total = h->dyn_nrt;
+        g.nks_total = h->dyn_nks;
+        g.i0 = 0;
+        g.i1 = 1;
+        g.X = h->d_Q;
+        g.ldx = B;
+        g.M = (int)h->nph;
+        g.Kd = (int)h->nph;
+        g.N = (int)B;
+        g.dst = h->d_Ypot;
+        g.ldd = B;
         p.add(g, TGT_STEP, 4);
       }
+      p.lat = true;
+      for (auto& b : h->baths) {
+        if (b.ml <= 1) continue;
+        Gemm g{};
+        g.A = b.d_K;
+        g.a_ks = (int64_t)b.ml * 64;
+        g.a_rt = (int64_t)b.nks * g.a_ks;
+        g.nrt_total = b.nrt;
+        g.nks_total = b.nks;
+        g.i0 = 1;
+        // no near slices: the reduce copies far(t+1) (+ mid(t+1))
+        g.i1 = std::max(1, std::min(b.ml, h->P1 ? h->P1 : L));
+        g.X = b.d_H;
+        g.ldx = b.ldh;
+        g.ring = b.R;
+        g.cs = (int)B;
+        g.tshift = 1;
+        g.M = b.nc;
+        g.Kd = b.nc;
+        g.N = (int)B;
+        g.dst = b.d_S + (int64_t)par * b.ncp * B;
+        g.ldd = B;
+        if (b.ml > L) {
+          g.add = b.d_far;
+          g.lda = (int64_t)L * B;
+          g.add_cs = (int)B;
+        }
+        if (b.d_mid) {
+          g.add2 = b.d_mid;
+          g.lda2 = (int64_t)h->P1 * B;
+          g.add2_cs = (int)B;
+        }
+        g.force_reduce = true;
+        p.add(g, 256, 4);
+      }
+      rc = p.done();
+      if (rc) return rc;
     }
-    if (variant && h->has_dyn) {
-      Gemm g{};
-      g.A = h->d_dyn;
-      g.a_ks = 64;
-      g.a_rt = (int64_t)h->dyn_nks * 64;
-      g.nrt_total = h->dyn_nrt;
-      g.nks_total = h->dyn_nks;
-      g.i0 = 0;
-      g.i1 = 1;
-      g.X = h->d_Q;
-      g.ldx = B;
-      g.M = (int)h->nph;
-      g.Kd = (int)h->nph;
-      g.N = (int)B;
-      g.dst = h->d_Ypot;
-      g.ldd = B;
-      p.add(g, TGT_STEP, 4);
-    }
-    rc = p.done();
-    if (rc) return rc;
-  }
   // OP1a (+/- pot), OP1b
   for (int variant = 0; variant < 3; ++variant) {
     Op& op = variant == 0 ? h->op1a : (variant == 1 ? h->op1a_np : h->op1b);
@@ -730,52 +821,7 @@ int freeze(gle_handle* h) {
     rc = p.done();
     if (rc) return rc;
   }
-  rc = build_near(h);
-  if (rc) return rc;
   h->frozen = true;
-  return GLE_OK;
-}
-
-// The near-field S(t+1) product writes S[(t+1)&1]; its destination alternates every step, so it
-// is planned once per destination parity.
-int build_near(gle_handle* h) {
-  const int64_t B = h->B;
-  const int L = h->L;
-  for (int par = 0; par < 2; ++par) {
-    Planner p(h, h->op_near[par], rn_for(B), true);
-    for (auto& b : h->baths) {
-      if (b.ml <= 1) continue;
-      Gemm g{};
-      g.A = b.d_K;
-      g.a_ks = (int64_t)b.ml * 64;
-      g.a_rt = (int64_t)b.nks * g.a_ks;
-      g.nrt_total = b.nrt;
-      g.nks_total = b.nks;
-      g.i0 = 1;
-      g.i1 = std::min(b.ml, L);
-      g.X = b.d_H;
-      g.ldx = b.ldh;
-      g.ring = b.R;
-      g.cs = (int)B;
-      g.tshift = 1;
-      g.M = b.nc;
-      g.Kd = b.nc;
-    g.Kd = b.nc;
-      g.N = (int)B;
-      g.dst = b.d_S + (int64_t)par * b.ncp * B;
-      g.ldd = B;
-      if (b.ml > L) {
-        g.add = b.d_far;
-        g.lda = (int64_t)L * B;
-        g.add_cs = (int)B;
-      }
-      g.force_reduce = true;
-      if (g.i1 <= g.i0) g.i1 = g.i0;  // no near slices: the reduce copies far(t+1)
-      p.add(g, 256, 4);
-    }
-    int rc = p.done();
-    if (rc) return rc;
-  }
   return GLE_OK;
 }
 
@@ -791,6 +837,7 @@ int prime(gle_handle* h) {
   }
   h->need_prime = false;
   h->far_due = true;
+  h->mid_due = true;
   h->seg_ready = false;
   return GLE_OK;
 }
@@ -825,12 +872,16 @@ int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
     h->far_due = false;
     h->steps_since_far = 0;
   }
+  if (h->mid_due) {
+    if (!h->op_mid.items.empty()) run_op(h, h->op_mid, 2, false);
+    h->mid_due = false;
+  }
   const bool need_pot = (fpot_host_T == nullptr) && !h->pot_cache_exact;
   if (fpot_host_T == nullptr && !h->has_dyn)
     return fail(h, GLE_ERR_STATE, "no potential force: pass fpot or call gle_set_dyn (md.py:468-470)");
-  Op& op0 = need_pot ? h->op0p : h->op0;
+  const int par = (int)((h->t + 1) & 1);
+  Op& op0 = need_pot ? h->op0p[par] : h->op0[par];
   run_op(h, op0, 0, h->op_far.items.empty() && h->op_spec.items.empty());
-  run_op(h, h->op_near[(h->t + 1) & 1], 0, false);
   if (fpot_host_T)
     HIPCHK(h, hipMemcpyAsync(h->d_Fc, fpot_host_T, (size_t)h->nph * h->B * 8, hipMemcpyHostToDevice, h->stream));
   launch_phaseA(h->d_sd, h->d_clk, (int)h->B, h->ndblk, need_pot ? 1 : 0, fpot_host_T ? 0 : 1, h->stream);
@@ -854,6 +905,7 @@ int step_end_impl(gle_handle* h, const double* fpot_host_T) {
   launch_phaseC(h->d_sd, h->d_clk, (int)h->B, h->ndblk, mode1, mode1, h->stream);
   h->t += 1;
   h->pot_cache_exact = (fpot_host_T == nullptr) && h->constr.empty();
+  if (h->P1 && h->t % h->P1 == 0) h->mid_due = true;
   if (h->far_mode == GLE_FAR_SPECTRAL) {
     if (h->t % h->L == 0) h->far_due = true;
   } else if (++h->steps_since_far >= h->L) {
@@ -1097,6 +1149,7 @@ int gle_set_state(gle_handle* h, const double* p, const double* q, int64_t t) {
   Clock c{};
   c.t = t;
   c.t_far = t;
+  c.t_mid = t;
   rc = upload(h, h->d_clk, &c, sizeof(c));
   if (rc) return rc;
   HIPCHK(h, hipMemsetAsync(h->d_qvalid, 0, (size_t)B * 4, h->stream));

@@ -22,6 +22,7 @@ constexpr int KROWS = 4 * KC;      // 8 staged X rows
 constexpr int LDS_COLS = 1000;     // padded staged row length (doubles): 8*1000*8 = 62.5 KB
 constexpr int LDS_WW_MAX = 960;    // usable window width: roundup32(960) + 16 <= LDS_COLS
 constexpr int MAXBATH = 8;
+constexpr int CPLX_WW_CAP = 512;   // contract_cplx_kernel window (doubles per staged row)
 constexpr int ROWS_PER_WG = 64;    // 4 waves x 16 rows
 
 // One workgroup's share of a contraction  out[r][c] = sum_{i in slices} sum_k A_i[r][k] X_i[k][c]
@@ -46,6 +47,8 @@ struct CItem {
   int32_t nrows;     // valid rows to store (<= 64)
   int32_t tdiv;      // ring index = floor(clock.t / tdiv) + tshift - slice (1: steps, P: segments)
   int32_t pad;
+  // complex items (contract_cplx_kernel): imaginary parts at these offsets (doubles) from A, X, out
+  int64_t a_im, x_im, o_im;
 };
 
 // Deterministic fixed-order sum of split partial tiles (+ optional far-field addend).
@@ -61,11 +64,15 @@ struct RItem {
   int32_t rows, cols;
   int32_t add_cs;      // add column offset = (t - t_far) * add_cs
   int32_t pad;
+  const double* add2;  // mid-level block buffer or nullptr, column offset (t - t_mid) * add2_cs
+  int32_t lda2;
+  int32_t add2_cs;
 };
 
 struct Clock {
   int64_t t;        // md.t
   int64_t t_far;    // step at which the current far-field block was computed
+  int64_t t_mid;    // step at which the current mid-level block was computed
   uint32_t arrive;  // ticket counter of the step-closing kernel
   uint32_t pad;
 };
@@ -116,6 +123,7 @@ void launch_philox_normal(double* x, int64_t nfreq, int64_t ncp, int64_t nc, int
                           uint64_t seed, uint64_t traj_offset, hipStream_t s);
 void launch_ring_copy(double* H, int64_t ldh, int R, int B, int nc, int64_t tau0, int nt, double* buf,
                       int dir, hipStream_t s);
+void launch_contract_cplx(int rn, const CItem* items, int nitems, const Clock* clk, hipStream_t s);
 void launch_khat_pack(const double* Kf, int ml, int nks_k, double* khat, int P, int M, int nc,
                       int nrt2, int nks2, const double* cstab, hipStream_t s);
 void launch_seg_fft(const double* H, int64_t ldh, int R, int B, int nc, int P, int64_t T, int nseg,

@@ -163,6 +163,150 @@ __global__ __launch_bounds__(WG, 2) void contract_kernel(const CItem* __restrict
   }
 }
 
+// Complex contraction  (Yr + i Yi) = sum_slices sum_k (Ar + i Ai)(Xr + i Xi): each wave loads the Ar
+// and Ai fragments of its 16-row tile once and issues the four real MFMAs of the complex product;
+// the LDS stage holds 8 rows of Xr and 8 rows of Xi.  Used for the per-frequency spectral far field.
+constexpr int CPLX_WW_MAX = CPLX_WW_CAP;  // 16 rows x (512+16) doubles = 66 KB (2 WGs per CU)
+template <int RN>
+__global__ __launch_bounds__(WG, 2) void contract_cplx_kernel(const CItem* __restrict__ items,
+                                                              const Clock* __restrict__ clk) {
+  __shared__ double lds[2 * KROWS * (CPLX_WW_MAX + 16)];
+  constexpr int NT = 16 * RN;
+  constexpr int CU = 2;
+  const int nblk = gridDim.x;
+  const int bid = (nblk & 7) ? (int)blockIdx.x : (int)(blockIdx.x & 7) * (nblk >> 3) + (int)(blockIdx.x >> 3);
+  const CItem it = items[bid];
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int64_t t = load_t(clk);
+
+  d4 accr[RN], acci[RN];
+#pragma unroll
+  for (int n = 0; n < RN; ++n) {
+    accr[n] = d4{0.0, 0.0, 0.0, 0.0};
+    acci[n] = d4{0.0, 0.0, 0.0, 0.0};
+  }
+  const int ns_max = it.ring ? (CPLX_WW_MAX - NT) / it.cs + 1 : 1;
+  const bool active = wave < it.nrt;
+  const double* Aw = it.A + (int64_t)wave * it.a_rt + lane;
+  const int brow = lane >> 4;
+  const int bcol = lane & 15;
+  const int nst = it.nks / KC;
+
+  for (int s0 = 0; s0 < it.ni; s0 += ns_max) {
+    const int ns = min(ns_max, it.ni - s0);
+    const int ww = (ns - 1) * it.cs + NT;
+    const int wwp = ((ww + 31) & ~31) + 16;
+    int64_t wbase = it.col0;
+    if (it.ring) {
+      const int64_t tt = it.tdiv > 1 ? t / it.tdiv : t;
+      const int64_t tau = tt + it.tshift - (int64_t)(it.ia + s0 + ns - 1);
+      wbase += pmod(tau, it.ring) * it.cs;
+    }
+    const double* xs0 = it.X + wbase;
+    const double* As0 = Aw + (int64_t)s0 * 64;
+    double xr[2 * KROWS * CU];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int r = 0; r < KROWS; ++r)
+#pragma unroll
+        for (int u = 0; u < CU; ++u) {
+          const int c = tid + WG * u;
+          xr[(h * KROWS + r) * CU + u] = (c < ww) ? xs0[h * it.x_im + (int64_t)r * it.ldx + c] : 0.0;
+        }
+    for (int st = 0; st < nst; ++st) {
+      __syncthreads();
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < KROWS; ++r)
+#pragma unroll
+          for (int u = 0; u < CU; ++u) {
+            const int c = tid + WG * u;
+            if (c < ww) lds[(h * KROWS + r) * wwp + c] = xr[(h * KROWS + r) * CU + u];
+          }
+      __syncthreads();
+      const double* Ak = As0 + (int64_t)(st * KC) * it.a_ks;
+      if (st + 1 < nst) {
+        const double* xs = xs0 + (int64_t)(4 * KC * (st + 1)) * it.ldx;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int r = 0; r < KROWS; ++r)
+#pragma unroll
+            for (int u = 0; u < CU; ++u) {
+              const int c = tid + WG * u;
+              xr[(h * KROWS + r) * CU + u] = (c < ww) ? xs[h * it.x_im + (int64_t)r * it.ldx + c] : 0.0;
+            }
+      }
+      if (active) {
+        // Re/Im fragments of the next slice are in flight while this slice's MFMAs run
+        double ar[KC], ai[KC];
+#pragma unroll
+        for (int kk = 0; kk < KC; ++kk) {
+          ar[kk] = Ak[kk * it.a_ks];
+          ai[kk] = Ak[it.a_im + kk * it.a_ks];
+        }
+        for (int ss = 0; ss < ns; ++ss) {
+          double nr[KC], ni_[KC];
+#pragma unroll
+          for (int kk = 0; kk < KC; ++kk) {
+            nr[kk] = (ss + 1 < ns) ? Ak[kk * it.a_ks + (ss + 1) * 64] : 0.0;
+            ni_[kk] = (ss + 1 < ns) ? Ak[it.a_im + kk * it.a_ks + (ss + 1) * 64] : 0.0;
+          }
+          const int off = (ns - 1 - ss) * it.cs;
+#pragma unroll
+          for (int kk = 0; kk < KC; ++kk) {
+            const double nai = -ai[kk];
+            const double* br = lds + (kk * 4 + brow) * wwp + off + bcol;
+            const double* bi = br + KROWS * wwp;
+#pragma unroll
+            for (int n = 0; n < RN; ++n) {
+              const double vr = br[16 * n], vi = bi[16 * n];
+              accr[n] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[kk], vr, accr[n], 0, 0, 0);
+              accr[n] = __builtin_amdgcn_mfma_f64_16x16x4f64(nai, vi, accr[n], 0, 0, 0);
+              acci[n] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[kk], vr, acci[n], 0, 0, 0);
+              acci[n] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[kk], vi, acci[n], 0, 0, 0);
+            }
+          }
+#pragma unroll
+          for (int kk = 0; kk < KC; ++kk) {
+            ar[kk] = nr[kk];
+            ai[kk] = ni_[kk];
+          }
+        }
+      }
+    }
+  }
+  if (active) {
+#pragma unroll
+    for (int n = 0; n < RN; ++n) {
+      const int col = 16 * n + bcol;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wave * 16 + brow + 4 * r;
+        if (row < it.nrows && col < it.ncols) {
+          it.out[(int64_t)row * it.ldo + col] = accr[n][r];
+          it.out[it.o_im + (int64_t)row * it.ldo + col] = acci[n][r];
+        }
+      }
+    }
+  }
+}
+
+void launch_contract_cplx(int rn, const CItem* items, int nitems, const Clock* clk, hipStream_t s) {
+  if (nitems <= 0) return;
+  dim3 g(nitems), b(WG);
+  switch (rn) {
+    case 1: contract_cplx_kernel<1><<<g, b, 0, s>>>(items, clk); break;
+    case 2: contract_cplx_kernel<2><<<g, b, 0, s>>>(items, clk); break;
+    case 4: contract_cplx_kernel<4><<<g, b, 0, s>>>(items, clk); break;
+    default: contract_cplx_kernel<8><<<g, b, 0, s>>>(items, clk); break;
+  }
+}
+
 template <int RN>
 static void launch_rn(int cu, const CItem* items, int nitems, const Clock* clk, hipStream_t s) {
   dim3 g(nitems), b(WG);
@@ -231,14 +375,21 @@ __global__ __launch_bounds__(256) void reduce_kernel(const RItem* __restrict__ i
   const int n = it.rows * it.cols;
   const int e0 = blockIdx.y * RED_PER_BLOCK;
   const int64_t t = load_t(clk);
-  if (set_tfar && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) clk->t_far = t;
+  // set_tfar: 1 = this reduce completes a far-field block, 2 = a mid-level block
+  if (set_tfar && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    if (set_tfar == 1) clk->t_far = t;
+    else clk->t_mid = t;
+  }
   if (e0 >= n) return;
   const double* add = nullptr;
+  const double* add2 = nullptr;
   if (it.add) add = it.add + (t - clk->t_far) * it.add_cs;
+  if (it.add2) add2 = it.add2 + (t - clk->t_mid) * it.add2_cs;
   for (int e = e0 + threadIdx.x; e < min(n, e0 + RED_PER_BLOCK); e += blockDim.x) {
     const int r = e / it.cols;
     const int c = e - r * it.cols;
-    const double s0 = add ? add[(int64_t)r * it.lda + c] : 0.0;
+    double s0 = add ? add[(int64_t)r * it.lda + c] : 0.0;
+    if (add2) s0 += add2[(int64_t)r * it.lda2 + c];
     it.dst[(int64_t)r * it.ldd + c] = sum_slots(s0, it.src + (int64_t)r * it.lds + c, it.slot_stride, it.nslots);
   }
 }
@@ -732,7 +883,8 @@ namespace gle {
 __global__ void khat_pack_kernel(const double* __restrict__ Kf, int ml, int nks_k,
                                  double* __restrict__ khat, int P, int M, int nc, int nrt2, int nks2,
                                  const double2* __restrict__ cstab) {
-  const int64_t total = (int64_t)(P + 1) * nrt2 * nks2 * M * 64;
+  // layout [f][part (0 = Re, 1 = Im)][rt][ks][m-1][64] over the nc x nc bath block
+  const int64_t total = (int64_t)(P + 1) * 2 * nrt2 * nks2 * M * 64;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int lane = (int)(e & 63);
@@ -742,25 +894,22 @@ __global__ void khat_pack_kernel(const double* __restrict__ Kf, int ml, int nks_
     const int ks2 = (int)(r_ % nks2);
     r_ /= nks2;
     const int rt2 = (int)(r_ % nrt2);
-    const int f = (int)(r_ / nrt2);
+    r_ /= nrt2;
+    const int part = (int)(r_ & 1);
+    const int f = (int)(r_ >> 1);
     const int r = 16 * rt2 + (lane & 15);
     const int k = 4 * ks2 + (lane >> 4);
     double v = 0.0;
-    if (r < 2 * nc && k < 2 * nc) {
-      const int rb = r >= nc, kb = k >= nc;
-      const int rr = r - rb * nc, kk = k - kb * nc;
-      const int64_t base = (((int64_t)(rr >> 4) * nks_k + (kk >> 2)) * ml) * 64 + (rr & 15) + 16 * (kk & 3);
-      double re = 0.0, im = 0.0;
+    if (r < nc && k < nc) {
+      const int64_t base = (((int64_t)(r >> 4) * nks_k + (k >> 2)) * ml) * 64 + (r & 15) + 16 * (k & 3);
       const int m = mm + 1;
       for (int ip = 0; ip < P; ++ip) {
         const int i = m * P + ip;
         if (i >= ml) break;
         const double kv = Kf[base + (int64_t)i * 64];
         const double2 cs = cstab[(f * ip) % (2 * P)];
-        re += kv * cs.x;
-        im -= kv * cs.y;
+        v += part ? -kv * cs.y : kv * cs.x;
       }
-      v = (rb == kb) ? re : (rb ? im : -im);
     }
     khat[e] = v;
   }
@@ -802,8 +951,9 @@ __global__ void seg_fft_kernel(const double* __restrict__ H, int64_t ldh, int R,
     double* sf = seg + (int64_t)f * seg_fstride + b;
     sf[(int64_t)k * ldseg + slot * B] = re;
     sf[(int64_t)k * ldseg + (slot + Rseg) * B] = re;
-    sf[(int64_t)(nc + k) * ldseg + slot * B] = im;
-    sf[(int64_t)(nc + k) * ldseg + (slot + Rseg) * B] = im;
+    const int64_t ir = (int64_t)(((nc + 7) / 8) * 8 + k) * ldseg;  // Im rows start at ncp
+    sf[ir + slot * B] = im;
+    sf[ir + (slot + Rseg) * B] = im;
   }
 }
 

@@ -40,7 +40,7 @@ def stepper_from_golden(g, ntraj=1, block_len=0, far_mode="auto"):
     return st
 
 
-FAR_VARIANTS = [("auto", 0), ("direct", 1), ("direct", 3), ("spectral", 2), ("spectral", 5)]
+FAR_VARIANTS = [("auto", 0), ("direct", 1), ("direct", 3), ("direct", 16), ("spectral", 2), ("spectral", 5), ("spectral", 16)]
 
 
 @pytest.mark.parametrize("case", vv_cases())
