@@ -80,6 +80,8 @@ def main():
     ap.add_argument("--ntraj", type=int, default=64, help="trajectories per GPU")
     ap.add_argument("--config", default="C3")
     ap.add_argument("--block-len", type=int, default=0)
+    ap.add_argument("--mid-len", type=int, default=0)
+    ap.add_argument("--far-mode", default="auto", choices=["auto", "direct", "spectral"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
@@ -105,7 +107,8 @@ def main():
     dyn, axyz, baths, meta = synthetic.junction(args.config, seed=1234)
     m = MD.md(meta["dt"], meta["nmd"], meta["T"], axyz=axyz, dyn=dyn, ntraj=args.ntraj,
               seed=1000 + rank * args.ntraj, traj_offset=rank * args.ntraj, device=local_rank,
-              noise_mode="device", block_len=args.block_len, verbose=False)
+              noise_mode="device", block_len=args.block_len, far_mode=args.far_mode,
+              mid_len=args.mid_len, verbose=False)
     for b in baths:
         m.AddBath(b)
     m.initialise()
@@ -160,7 +163,8 @@ def main():
                                "%d traj/GPU" % (args.config, meta["natom"], len(baths), meta["nc"],
                                                 meta["ml"], meta["nmd"], args.ntraj),
                    "ntraj_per_gpu": args.ntraj, "ntraj_total": world * args.ntraj,
-                   "block_len": st.plan_info()["block_len"], "parallelism": "ensemble-dp%d" % world},
+                   "block_len": st.plan_info()["block_len"], "far_mode": st.plan_info()["far_mode"],
+                   "parallelism": "ensemble-dp%d" % world},
         "value_per_gpu": value / world,
         "setup_s": setup_s,
     }

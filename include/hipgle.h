@@ -54,7 +54,7 @@ typedef struct gle_config {
     int32_t device;     /* HIP device ordinal                                                */
     int32_t block_len;  /* far-field time block L (= partition length P in spectral mode); 0=auto */
     int32_t far_mode;   /* GLE_FAR_AUTO / GLE_FAR_DIRECT / GLE_FAR_SPECTRAL                      */
-    int32_t reserved;
+    int32_t mid_len;    /* P1: lags [P1, L) every P1 steps as one blocked contraction; 0=auto, -1=off */
 } gle_config;
 
 /* far-field memory sum  sum_{i>=L} K_i p_{t-i}  (SURVEY.md section 8a R3):

@@ -470,7 +470,7 @@ int freeze(gle_handle* h) {
   // trajectories) and the kernel is long compared with the partition; the direct form streams the
   // kernel once per L steps and wins when the step is bandwidth-bound (few trajectories)
   int mode = h->cfg.far_mode;
-  const int Pdef = 32;
+  const int Pdef = 64;
   if (mode == GLE_FAR_AUTO) mode = (B >= 8 && mlmax >= 4 * Pdef) ? GLE_FAR_SPECTRAL : GLE_FAR_DIRECT;
   if (h->cfg.block_len > 0) {
     h->L = h->cfg.block_len;
@@ -502,7 +502,9 @@ int freeze(gle_handle* h) {
   }
   h->far_mode = mode;
   // mid-level block: when the near field would otherwise sweep many kernel slices every step
-  h->P1 = (L >= 16) ? 8 : 0;
+  if (h->cfg.mid_len > 0) h->P1 = h->cfg.mid_len < L ? h->cfg.mid_len : 0;
+  else if (h->cfg.mid_len < 0) h->P1 = 0;
+  else h->P1 = (L >= 16) ? 8 : 0;
   // ring sizes and buffers that depend on L
   for (auto& b : h->baths) {
     b.R = b.ml + 3 * L + 2;
@@ -964,6 +966,7 @@ int gle_create(const gle_config* cfg, gle_handle** out) {
   if (cfg->nmd % 2) return fail(nullptr, GLE_ERR_ARG, "nmd must be even (functions.py:47-50 length check)");
   if (cfg->far_mode < GLE_FAR_AUTO || cfg->far_mode > GLE_FAR_SPECTRAL) return fail(nullptr, GLE_ERR_ARG, "bad far_mode");
   if (cfg->block_len < 0 || cfg->block_len > 4096) return fail(nullptr, GLE_ERR_ARG, "bad block_len");
+  if (cfg->mid_len < -1 || cfg->mid_len > 4096) return fail(nullptr, GLE_ERR_ARG, "bad mid_len");
   if (cfg->nph > (1 << 24) || cfg->ntraj > (1 << 20)) return fail(nullptr, GLE_ERR_UNSUP, "size too large");
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);

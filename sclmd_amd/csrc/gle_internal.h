@@ -51,6 +51,23 @@ struct CItem {
   int64_t a_im, x_im, o_im;
 };
 
+// One 16-row output tile of a latency-bound per-step product, computed by one 1024-thread
+// workgroup (16 waves split the slice x k-step space; fixed-order LDS tree reduction; far / mid
+// addends in the epilogue).  Same operand conventions as CItem.
+struct TItem {
+  const double* A;     // fragment base for (row tile, k-step 0, slice ia)
+  const double* X;     // X base (row 0)
+  double* out;         // tile output (row 0 of the tile, column 0)
+  const double* add;   // far-field addend (column offset (t - t_far) * add_cs) or nullptr
+  const double* add2;  // mid-level addend (column offset (t - t_mid) * add2_cs) or nullptr
+  int64_t a_ks;        // doubles between k-steps in A (slice stride is 64)
+  int64_t ldx;
+  int32_t ldo, lda, lda2, add_cs, add2_cs;
+  int32_t ia, ni, nks; // slices [ia, ia+ni), k-steps
+  int32_t ring, cs, tshift;
+  int32_t nrows, ncols;
+};
+
 // Deterministic fixed-order sum of split partial tiles (+ optional far-field addend).
 struct RItem {
   double* dst;
@@ -123,6 +140,7 @@ void launch_philox_normal(double* x, int64_t nfreq, int64_t ncp, int64_t nc, int
                           uint64_t seed, uint64_t traj_offset, hipStream_t s);
 void launch_ring_copy(double* H, int64_t ldh, int R, int B, int nc, int64_t tau0, int nt, double* buf,
                       int dir, hipStream_t s);
+void launch_tile(int rn, const TItem* items, int nitems, const Clock* clk, hipStream_t s);
 void launch_contract_cplx(int rn, const CItem* items, int nitems, const Clock* clk, hipStream_t s);
 void launch_khat_pack(const double* Kf, int ml, int nks_k, double* khat, int P, int M, int nc,
                       int nrt2, int nks2, const double* cstab, hipStream_t s);

@@ -330,6 +330,97 @@ void launch_contract(int rn, int cu, const CItem* items, int nitems, const Clock
 }
 
 // ------------------------------------------------------------------------------------------
+// Latency-optimised per-step products.  Work step s in [0, ni*nks) is (slice s / nks, k-step
+// s % nks); wave w owns the contiguous range [w*S/16, (w+1)*S/16).  Operands come straight from
+// global memory (L2-resident per-step data), loads issued 4 steps ahead of their MFMAs.
+constexpr int TILE_NW = 16;
+template <int RN>
+__global__ __launch_bounds__(1024) void tile_kernel(const TItem* __restrict__ items,
+                                                     const Clock* __restrict__ clk) {
+  __shared__ double red[(TILE_NW / 2) * 16 * 16 * RN];
+  const TItem it = items[blockIdx.x];
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int brow = lane >> 4, bcol = lane & 15;
+  const int64_t t = load_t(clk);
+  d4 acc[RN];
+#pragma unroll
+  for (int n = 0; n < RN; ++n) acc[n] = d4{0.0, 0.0, 0.0, 0.0};
+  const int S = it.ni * it.nks;
+  const int s0 = (int)((int64_t)S * wave / TILE_NW), s1 = (int)((int64_t)S * (wave + 1) / TILE_NW);
+  constexpr int U = 4;
+  for (int sb = s0; sb < s1; sb += U) {
+    double a[U], b[U][RN];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int s = sb + u;
+      a[u] = 0.0;
+#pragma unroll
+      for (int n = 0; n < RN; ++n) b[u][n] = 0.0;
+      if (s < s1) {
+        const int i = s / it.nks, ks = s - i * it.nks;
+        a[u] = it.A[(int64_t)ks * it.a_ks + (int64_t)i * 64 + lane];
+        int64_t cb = 0;
+        if (it.ring) cb = pmod(t + it.tshift - (it.ia + i), it.ring) * it.cs;
+        const double* xr = it.X + (int64_t)(4 * ks + brow) * it.ldx + cb + bcol;
+#pragma unroll
+        for (int n = 0; n < RN; ++n) b[u][n] = xr[16 * n];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int n = 0; n < RN; ++n) acc[n] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b[u][n], acc[n], 0, 0, 0);
+  }
+  // fixed-order tree over the 16 waves: w += w + half for half = 8, 4, 2, 1
+  for (int half = TILE_NW / 2; half >= 1; half >>= 1) {
+    if (wave >= half && wave < 2 * half) {
+      double* r = red + (wave - half) * 256 * RN;
+#pragma unroll
+      for (int n = 0; n < RN; ++n)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) r[(n * 4 + q) * 64 + lane] = acc[n][q];
+    }
+    __syncthreads();
+    if (wave < half) {
+      const double* r = red + wave * 256 * RN;
+#pragma unroll
+      for (int n = 0; n < RN; ++n)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[n][q] += r[(n * 4 + q) * 64 + lane];
+    }
+    __syncthreads();
+  }
+  if (wave == 0) {
+    const double* add = it.add ? it.add + (t - clk->t_far) * it.add_cs : nullptr;
+    const double* add2 = it.add2 ? it.add2 + (t - clk->t_mid) * it.add2_cs : nullptr;
+#pragma unroll
+    for (int n = 0; n < RN; ++n) {
+      const int col = 16 * n + bcol;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = brow + 4 * q;
+        if (row < it.nrows && col < it.ncols) {
+          double v = acc[n][q];
+          if (add) v = add[(int64_t)row * it.lda + col] + v;
+          if (add2) v += add2[(int64_t)row * it.lda2 + col];
+          it.out[(int64_t)row * it.ldo + col] = v;
+        }
+      }
+    }
+  }
+}
+
+void launch_tile(int rn, const TItem* items, int nitems, const Clock* clk, hipStream_t s) {
+  if (nitems <= 0) return;
+  switch (rn) {
+    case 1: tile_kernel<1><<<nitems, 1024, 0, s>>>(items, clk); break;
+    case 2: tile_kernel<2><<<nitems, 1024, 0, s>>>(items, clk); break;
+    default: tile_kernel<4><<<nitems, 1024, 0, s>>>(items, clk); break;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // grid (item, chunk): each block sums RED_PER_BLOCK consecutive elements of one tile over all of
 // its partial slots in slot order (deterministic).
 constexpr int RED_PER_BLOCK = 256;

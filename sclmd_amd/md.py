@@ -39,7 +39,7 @@ def ApplyConstraint(f, constr=None):
 class md:
     def __init__(self, dt, nmd, T, syslist=None, axyz=None, dyn=None, nstart=0, nstop=1, npie=1,
                  md2ang=0.06466, *, ntraj=1, seed=None, traj_offset=0, device=None,
-                 noise_mode="numpy", block_len=0, comm=None, verbose=True):
+                 noise_mode="numpy", block_len=0, far_mode="auto", mid_len=0, comm=None, verbose=True):
         self.nstart, self.nstop = nstart, nstop
         self.dt, self.nmd = dt, nmd
         self.T = T
@@ -58,6 +58,8 @@ class md:
         self.noise_mode = noise_mode
         self.device = device
         self.block_len = int(block_len)
+        self.far_mode = far_mode
+        self.mid_len = int(mid_len)
         self.comm = comm
         self.SetXyz(axyz)
         if syslist is not None:
@@ -339,7 +341,8 @@ class md:
         dev = self.device
         if dev is None:
             dev = int(os.environ.get("LOCAL_RANK", "0")) if _native.device_count() > 1 else 0
-        st = _native.Stepper(self.nph, self.ntraj, self.nmd, self.dt, dev, self.block_len)
+        st = _native.Stepper(self.nph, self.ntraj, self.nmd, self.dt, dev, self.block_len, self.far_mode,
+                             self.mid_len)
         for b in self.baths:
             if b.kernel is None:
                 raise ValueError("md: bath %s has no kernel (call phbath.gmem())" % b)
