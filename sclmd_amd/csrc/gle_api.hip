@@ -39,7 +39,14 @@ struct Op {
   double* partial = nullptr;
   size_t partial_doubles = 0;
   double flops = 0, bytes = 0;  // algorithmic, per launch
-  bool empty() const { return items.empty() && ritems.empty(); }
+  bool tile = false;   // latency-bound per-step op: tile_kernel items, no partials / reduce
+  std::vector<TItem> titems;
+  TItem* d_titems = nullptr;
+  size_t tpart_doubles = 0;   // tile partial slots (offsets fixed up in materialize)
+  int tcnt = 0;               // tile arrival counters
+  double* d_tpart = nullptr;
+  unsigned* d_tcnt = nullptr;
+  bool empty() const { return items.empty() && ritems.empty() && titems.empty(); }
 };
 
 struct Bath {
@@ -51,6 +58,8 @@ struct Bath {
   std::vector<double> K;  // host copy [ml][nc][nc] of the p-channel kernel (bias folded)
   std::vector<double> Kq; // [nc][nc] q-channel
   double* d_K = nullptr;
+  double* d_Kn = nullptr;  // compact fragment copy of the per-step slices [0, nn): [rt][ks][i][64]
+  int nn = 1;
   double* d_Kq = nullptr;
   int32_t* d_inv = nullptr;
   double *d_noise = nullptr, *d_Y = nullptr, *d_S = nullptr, *d_Yq = nullptr;
@@ -89,11 +98,11 @@ struct gle_handle {
   double *d_Flast = nullptr, *d_etot = nullptr, *d_Q0 = nullptr, *d_part = nullptr, *d_Ypot = nullptr;
   unsigned long long* d_pmax = nullptr;
   int32_t* d_qvalid = nullptr;
-  Clock* d_clk = nullptr;
   StepDev* d_sd = nullptr;
   double* d_tw = nullptr;
   int ndblk = 1, dchunk = 1;
   int64_t t = 0;
+  int64_t t_far = 0, t_mid = 0;  // steps at which the current far / mid blocks were computed
   bool frozen = false, state_set = false;
   bool need_prime = true;
   int steps_since_far = 0;
@@ -353,6 +362,60 @@ void plan_gemm(Op& op, const Gemm& g, int target_items, int min_work) {
   }
 }
 
+// Per-step product as tile_kernel items: per (16-row tile, column tile of 16*rn), ngrp shares of
+// the slice x k-step space, sized so each wave runs about TILE_STEPS steps.
+constexpr int TILE_WAVES = 4, TILE_STEPS = 8, TILE_MAXGRP = 64;
+void plan_tile(Op& op, const Gemm& g) {
+  const int NT = 16 * op.rn;
+  const int ni = std::max(0, g.i1 - g.i0);
+  const int64_t S = (int64_t)ni * g.nks_total;
+  const int ngrp = (int)std::max<int64_t>(1, std::min<int64_t>(TILE_MAXGRP, (S + TILE_WAVES * TILE_STEPS - 1) / (TILE_WAVES * TILE_STEPS)));
+  for (int c0 = 0; c0 < g.N; c0 += NT)
+    for (int rt = 0; rt < (g.M + 15) / 16; ++rt) {
+      TItem it{};
+      it.A = g.A + (int64_t)rt * g.a_rt + (int64_t)g.i0 * 64;
+      it.a_ks = g.a_ks;
+      it.X = g.X + c0;
+      it.ldx = g.ldx;
+      it.out = g.dst + (int64_t)(16 * rt) * g.ldd + c0;
+      it.ldo = (int32_t)g.ldd;
+      if (g.add) {
+        it.add = g.add + (int64_t)(16 * rt) * g.lda + c0;
+        it.lda = (int32_t)g.lda;
+        it.add_cs = g.add_cs;
+      }
+      if (g.add2) {
+        it.add2 = g.add2 + (int64_t)(16 * rt) * g.lda2 + c0;
+        it.lda2 = (int32_t)g.lda2;
+        it.add2_cs = g.add2_cs;
+      }
+      it.ia = g.i0;
+      it.ni = ni;
+      it.nks = g.nks_total;
+      it.ring = g.ring;
+      it.cs = g.cs;
+      it.tshift = g.tshift;
+      it.nrows = std::min(16, g.M - 16 * rt);
+      it.ncols = std::min(NT, g.N - c0);
+      it.ngrp = ngrp;
+      if (ngrp > 1) {
+        it.part = (double*)(uintptr_t)(op.tpart_doubles * sizeof(double));  // offset, fixed up later
+        it.cnt = (unsigned*)(uintptr_t)(op.tcnt * sizeof(unsigned));
+        op.tpart_doubles += (size_t)ngrp * 256 * op.rn;
+        op.tcnt += 1;
+      }
+      for (int gi = 0; gi < ngrp; ++gi) {
+        it.grp = gi;
+        op.titems.push_back(it);
+      }
+    }
+  if (ni > 0) {
+    const double kd = g.Kd > 0 ? g.Kd : 4.0 * g.nks_total;
+    op.flops += 2.0 * g.M * kd * g.N * ni;
+    op.bytes += 8.0 * ((double)ni * g.M * kd + kd * (g.ring ? (double)(ni + (g.N + g.cs - 1) / std::max(1, g.cs) - 1) * g.cs : g.N) + (double)g.M * g.N);
+  }
+}
+
 // Fix up partial-slot offsets once the partial buffer exists.  Items that write partials were
 // tagged with ldo == NT and an offset pointer smaller than the partial size.
 int materialize(gle_handle* h, Op& op, const std::vector<bool>& is_partial) {
@@ -387,6 +450,22 @@ int materialize(gle_handle* h, Op& op, const std::vector<bool>& is_partial) {
     op.items.push_back(e);
   }
   for (auto& r : op.ritems) r.src = op.partial + (uintptr_t)r.src / sizeof(double);
+  if (!op.titems.empty()) {
+    if (op.tcnt) {
+      int rc = dalloc_n(h, &op.d_tpart, op.tpart_doubles);
+      if (!rc) rc = dalloc_n(h, &op.d_tcnt, (size_t)op.tcnt);
+      if (rc) return rc;
+      for (auto& it : op.titems)
+        if (it.ngrp > 1) {
+          it.part = op.d_tpart + (uintptr_t)it.part / sizeof(double);
+          it.cnt = op.d_tcnt + (uintptr_t)it.cnt / sizeof(unsigned);
+        }
+    }
+    int rc = dalloc_n(h, &op.d_titems, op.titems.size());
+    if (rc) return rc;
+    rc = upload(h, op.d_titems, op.titems.data(), op.titems.size() * sizeof(TItem));
+    if (rc) return rc;
+  }
   if (!op.items.empty()) {
     int rc = dalloc_n(h, &op.d_items, op.items.size());
     if (rc) return rc;
@@ -410,6 +489,10 @@ struct Planner {
   bool lat;
   Planner(gle_handle* hh, Op& o, int rn, bool latency = false) : h(hh), op(o), lat(latency) { op.rn = rn; }
   void add(const Gemm& g0, int target, int min_work) {
+    if (op.tile) {
+      plan_tile(op, g0);
+      return;
+    }
     Gemm g = g0;
     if (lat) g.lat = true;
     const size_t n0 = op.items.size();
@@ -420,6 +503,14 @@ struct Planner {
   }
   int done() { return materialize(h, op, partial); }
 };
+
+StepArgs step_args(const gle_handle* h) {
+  StepArgs a;
+  a.t = h->t;
+  a.t_far = h->t_far;
+  a.t_mid = h->t_mid;
+  return a;
+}
 
 void run_op(gle_handle* h, Op& op, int set_tfar, bool profile) {
   hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -439,17 +530,27 @@ void run_op(gle_handle* h, Op& op, int set_tfar, bool profile) {
     h->ev_used += 2;
     hipEventRecord(e0, h->stream);
   }
+  if (op.tile) {
+    launch_tile(op.rn, op.d_titems, (int)op.titems.size(), step_args(h), h->stream);
+    if (e1) {
+      hipEventRecord(e1, h->stream);
+      h->prof_n += 1;
+      h->prof_flops += op.flops;
+      h->prof_bytes += op.bytes;
+    }
+    return;
+  }
   if (op.cplx)
-    launch_contract_cplx(op.rn, op.d_items, (int)op.items.size(), h->d_clk, h->stream);
+    launch_contract_cplx(op.rn, op.d_items, (int)op.items.size(), step_args(h), h->stream);
   else
-    launch_contract(op.rn, op.cu, op.d_items, (int)op.items.size(), h->d_clk, h->stream);
+    launch_contract(op.rn, op.cu, op.d_items, (int)op.items.size(), step_args(h), h->stream);
   if (e1) {
     hipEventRecord(e1, h->stream);
     h->prof_n += 1;
     h->prof_flops += op.flops;
     h->prof_bytes += op.bytes;
   }
-  launch_reduce(op.d_ritems, (int)op.ritems.size(), op.max_elems, h->d_clk, set_tfar, h->stream);
+  launch_reduce(op.d_ritems, (int)op.ritems.size(), op.max_elems, step_args(h), h->stream);
 }
 
 int check_bath(gle_handle* h, int32_t b) {
@@ -612,13 +713,25 @@ int freeze(gle_handle* h) {
   rc = upload(h, h->d_sd, &sd, sizeof(sd));
   if (rc) return rc;
 
+  // compact copy of the slices every step reads (K_0 and the near field): the full fragment-native
+  // kernel puts consecutive k-steps of one slice ml*512 B apart, so a per-step product touching
+  // only a few slices would hit a new page (TLB miss) on nearly every fragment
+  for (auto& b : h->baths) {
+    b.nn = std::max(1, std::min(b.ml, h->P1 ? h->P1 : L));
+    rc = dalloc_n(h, &b.d_Kn, (size_t)b.nrt * b.nks * b.nn * 64);
+    if (rc) return rc;
+    HIPCHK(h, hipMemcpy2DAsync(b.d_Kn, (size_t)b.nn * 64 * 8, b.d_K, (size_t)b.ml * 64 * 8,
+                               (size_t)b.nn * 64 * 8, (size_t)b.nrt * b.nks, hipMemcpyDeviceToDevice,
+                               h->stream));
+  }
+
   // ---- plans
   const int TGT_STEP = 256, TGT_BIG = 512;
   auto kgemm = [&](Bath& b, const double* A, int i0, int i1, const double* X, int64_t ldx, int ring,
                    int tshift, int N, double* dst, int64_t ldd) {
     Gemm g{};
     g.A = A;
-    g.a_ks = (int64_t)(A == b.d_K ? b.ml : 1) * 64;
+    g.a_ks = (int64_t)(A == b.d_K ? b.ml : (A == b.d_Kn ? b.nn : 1)) * 64;
     g.a_rt = (int64_t)b.nks * g.a_ks;
     g.nrt_total = b.nrt;
     g.nks_total = b.nks;
@@ -720,9 +833,10 @@ int freeze(gle_handle* h) {
   for (int par = 0; par < 2; ++par)
     for (int variant = 0; variant < 2; ++variant) {
       Op& op = variant ? h->op0p[par] : h->op0[par];
-      Planner p(h, op, rn_step);
+      op.tile = true;
+      Planner p(h, op, std::min(rn_step, 4));
       for (auto& b : h->baths) {
-        p.add(kgemm(b, b.d_K, 0, 1, b.d_H, b.ldh, b.R, 0, (int)B, b.d_Y, B), TGT_STEP, 4);
+        p.add(kgemm(b, b.d_Kn, 0, 1, b.d_H, b.ldh, b.R, 0, (int)B, b.d_Y, B), TGT_STEP, 4);
         if (b.has_q) {
           Gemm g = kgemm(b, b.d_Kq, 0, 1, b.d_Xq, B, 0, 0, (int)B, b.d_Yq, B);
           g.a_ks = 64;
@@ -752,8 +866,8 @@ int freeze(gle_handle* h) {
       for (auto& b : h->baths) {
         if (b.ml <= 1) continue;
         Gemm g{};
-        g.A = b.d_K;
-        g.a_ks = (int64_t)b.ml * 64;
+        g.A = b.d_Kn;
+        g.a_ks = (int64_t)b.nn * 64;
         g.a_rt = (int64_t)b.nks * g.a_ks;
         g.nrt_total = b.nrt;
         g.nks_total = b.nks;
@@ -789,11 +903,10 @@ int freeze(gle_handle* h) {
   // OP1a (+/- pot), OP1b
   for (int variant = 0; variant < 3; ++variant) {
     Op& op = variant == 0 ? h->op1a : (variant == 1 ? h->op1a_np : h->op1b);
-    Planner p(h, op, rn_step);
+    op.tile = true;
+    Planner p(h, op, std::min(rn_step, 4));
     for (auto& b : h->baths) {
-      Gemm g = kgemm(b, b.d_K, 0, 1, b.d_Xcur, B, 0, 0, (int)B, b.d_Y, B);
-      g.a_ks = (int64_t)b.ml * 64;
-      g.a_rt = (int64_t)b.nks * g.a_ks;
+      Gemm g = kgemm(b, b.d_Kn, 0, 1, b.d_Xcur, B, 0, 0, (int)B, b.d_Y, B);
       p.add(g, TGT_STEP, 4);
       if (b.has_q && variant < 2) {
         Gemm gq = kgemm(b, b.d_Kq, 0, 1, b.d_Xq, B, 0, 0, (int)B, b.d_Yq, B);
@@ -865,17 +978,20 @@ int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
       for (auto& b : h->baths)
         if (b.d_khat)
           launch_far_ifft(b.d_Yspec, b.yfstride, b.nc, (int)h->B, L, b.d_far, (int64_t)L * h->B,
-                          h->d_cstab, h->d_clk, h->stream);
+                          h->d_cstab, h->stream);
+      h->t_far = h->t;
     } else if (!h->op_far.items.empty()) {
       // direct block (every L steps in direct mode; the partial block before the first aligned
       // spectral block otherwise)
       run_op(h, h->op_far, 1, h->far_mode != GLE_FAR_SPECTRAL);
+      h->t_far = h->t;
     }
     h->far_due = false;
     h->steps_since_far = 0;
   }
   if (h->mid_due) {
     if (!h->op_mid.items.empty()) run_op(h, h->op_mid, 2, false);
+    h->t_mid = h->t;
     h->mid_due = false;
   }
   const bool need_pot = (fpot_host_T == nullptr) && !h->pot_cache_exact;
@@ -886,7 +1002,7 @@ int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
   run_op(h, op0, 0, h->op_far.items.empty() && h->op_spec.items.empty());
   if (fpot_host_T)
     HIPCHK(h, hipMemcpyAsync(h->d_Fc, fpot_host_T, (size_t)h->nph * h->B * 8, hipMemcpyHostToDevice, h->stream));
-  launch_phaseA(h->d_sd, h->d_clk, (int)h->B, h->ndblk, need_pot ? 1 : 0, fpot_host_T ? 0 : 1, h->stream);
+  launch_phaseA(h->d_sd, step_args(h), (int)h->B, h->ndblk, need_pot ? 1 : 0, fpot_host_T ? 0 : 1, h->stream);
   h->host_force_step = fpot_host_T != nullptr;
   return GLE_OK;
 }
@@ -902,9 +1018,9 @@ int step_end_impl(gle_handle* h, const double* fpot_host_T) {
     if (h->host_force_step) return fail(h, GLE_ERR_STATE, "step begun with a host force must end with one");
     run_op(h, h->op1a, 0, false);
   }
-  launch_phaseB(h->d_sd, h->d_clk, (int)h->B, h->ndblk, mode1, h->stream);
+  launch_phaseB(h->d_sd, step_args(h), (int)h->B, h->ndblk, mode1, h->stream);
   run_op(h, h->op1b, 0, false);
-  launch_phaseC(h->d_sd, h->d_clk, (int)h->B, h->ndblk, mode1, mode1, h->stream);
+  launch_phaseC(h->d_sd, step_args(h), (int)h->B, h->ndblk, mode1, mode1, h->stream);
   h->t += 1;
   h->pot_cache_exact = (fpot_host_T == nullptr) && h->constr.empty();
   if (h->P1 && h->t % h->P1 == 0) h->mid_due = true;
@@ -999,7 +1115,6 @@ int gle_create(const gle_config* cfg, gle_handle** out) {
   rc |= dalloc_n(h, &h->d_Ypot, nst);
   rc |= dalloc_n(h, &h->d_etot, (size_t)h->nmd * h->B);
   rc |= dalloc_n(h, &h->d_qvalid, (size_t)h->B);
-  rc |= dalloc_n(h, &h->d_clk, 1);
   if (rc) {
     g_create_error = h->err;
     gle_destroy(h);
@@ -1149,12 +1264,8 @@ int gle_set_state(gle_handle* h, const double* p, const double* q, int64_t t) {
   if (!rc) rc = upload(h, h->d_Q, tq.data(), tq.size() * 8);
   if (rc) return rc;
   h->t = t;
-  Clock c{};
-  c.t = t;
-  c.t_far = t;
-  c.t_mid = t;
-  rc = upload(h, h->d_clk, &c, sizeof(c));
-  if (rc) return rc;
+  h->t_far = t;
+  h->t_mid = t;
   HIPCHK(h, hipMemsetAsync(h->d_qvalid, 0, (size_t)B * 4, h->stream));
   HIPCHK(h, hipMemsetAsync(h->d_pmax, 0, (size_t)B * 4 * 8, h->stream));
   // p_t into the history ring slot of t; q_t into the q gather
@@ -1391,7 +1502,7 @@ int gle_noise_generate(gle_handle* h, int32_t bath, const double* x_host, uint64
     // chunk the grid to stay well inside launch limits
     const int CH = 1 << 20;
     for (size_t s = 0; s < op.items.size(); s += CH)
-      launch_contract(op.rn, 1, d_items + s, (int)std::min<size_t>(CH, op.items.size() - s), h->d_clk, h->stream);
+      launch_contract(op.rn, 1, d_items + s, (int)std::min<size_t>(CH, op.items.size() - s), step_args(h), h->stream);
     const double scale = 1.0 / (h->dt * (double)h->nmd);  // dw/2pi (functions.py:51)
     int frc = launch_fft_noise(d_a, b.d_noise, h->d_tw, h->nmd, nc, b.fac_rows, B, b.fac_complex ? 1 : 0, scale, h->stream);
     e = hipStreamSynchronize(h->stream);

@@ -51,10 +51,13 @@ struct CItem {
   int64_t a_im, x_im, o_im;
 };
 
-// One 16-row output tile of a latency-bound per-step product, computed by one 1024-thread
-// workgroup (16 waves split the slice x k-step space; fixed-order LDS tree reduction; far / mid
-// addends in the epilogue).  Same operand conventions as CItem.
+// One share of a 16-row output tile of a latency-bound per-step product.  The tile's slice x
+// k-step space is split over ngrp workgroups of 4 waves; waves reduce through LDS, groups through
+// partial slots summed in fixed order by the last group to arrive (far / mid addends in its
+// epilogue).  Same operand conventions as CItem.
 struct TItem {
+  double* part;        // [ngrp][256*RN] partial slots of this tile (ngrp > 1)
+  unsigned* cnt;       // arrival counter of this tile (ngrp > 1)
   const double* A;     // fragment base for (row tile, k-step 0, slice ia)
   const double* X;     // X base (row 0)
   double* out;         // tile output (row 0 of the tile, column 0)
@@ -66,6 +69,7 @@ struct TItem {
   int32_t ia, ni, nks; // slices [ia, ia+ni), k-steps
   int32_t ring, cs, tshift;
   int32_t nrows, ncols;
+  int32_t grp, ngrp;   // this workgroup's share, number of shares
 };
 
 // Deterministic fixed-order sum of split partial tiles (+ optional far-field addend).
@@ -86,13 +90,6 @@ struct RItem {
   int32_t add2_cs;
 };
 
-struct Clock {
-  int64_t t;        // md.t
-  int64_t t_far;    // step at which the current far-field block was computed
-  int64_t t_mid;    // step at which the current mid-level block was computed
-  uint32_t arrive;  // ticket counter of the step-closing kernel
-  uint32_t pad;
-};
 
 struct BathDev {
   const int32_t* inv;  // [nph] -> bath-local index k or -1
@@ -127,28 +124,35 @@ struct StepDev {
 };
 
 // launchers (gle_kernels.hip)
-void launch_contract(int rn, int cu, const CItem* items, int nitems, const Clock* clk, hipStream_t s);
-void launch_reduce(const RItem* items, int nitems, int max_elems, const Clock* clk, int set_tfar,
+// Every kernel takes the step counter by value: the host knows md.t and the steps at which the
+// current far / mid blocks were computed, so no kernel starts with a dependent load of a clock
+struct StepArgs {
+  int64_t t;      // md.t of this step
+  int64_t t_far;  // step of the current far-field block
+  int64_t t_mid;  // step of the current mid-level block
+};
+void launch_contract(int rn, int cu, const CItem* items, int nitems, StepArgs ta, hipStream_t s);
+void launch_reduce(const RItem* items, int nitems, int max_elems, StepArgs ta,
                    hipStream_t s);
-void launch_phaseA(const StepDev* sd, const Clock* clk, int B, int ndblk, int mode0, int diff1,
+void launch_phaseA(const StepDev* sd, StepArgs ta, int B, int ndblk, int mode0, int diff1,
                    hipStream_t s);
-void launch_phaseB(const StepDev* sd, const Clock* clk, int B, int ndblk, int mode1, hipStream_t s);
-void launch_phaseC(const StepDev* sd, Clock* clk, int B, int ndblk, int mode1, int diff0,
+void launch_phaseB(const StepDev* sd, StepArgs ta, int B, int ndblk, int mode1, hipStream_t s);
+void launch_phaseC(const StepDev* sd, StepArgs ta, int B, int ndblk, int mode1, int diff0,
                    hipStream_t s);
 void launch_finalize(const StepDev* sd, int B, int nmd, int nbath, hipStream_t s);
 void launch_philox_normal(double* x, int64_t nfreq, int64_t ncp, int64_t nc, int64_t B,
                           uint64_t seed, uint64_t traj_offset, hipStream_t s);
 void launch_ring_copy(double* H, int64_t ldh, int R, int B, int nc, int64_t tau0, int nt, double* buf,
                       int dir, hipStream_t s);
-void launch_tile(int rn, const TItem* items, int nitems, const Clock* clk, hipStream_t s);
-void launch_contract_cplx(int rn, const CItem* items, int nitems, const Clock* clk, hipStream_t s);
+void launch_tile(int rn, const TItem* items, int nitems, StepArgs ta, hipStream_t s);
+void launch_contract_cplx(int rn, const CItem* items, int nitems, StepArgs ta, hipStream_t s);
 void launch_khat_pack(const double* Kf, int ml, int nks_k, double* khat, int P, int M, int nc,
                       int nrt2, int nks2, const double* cstab, hipStream_t s);
 void launch_seg_fft(const double* H, int64_t ldh, int R, int B, int nc, int P, int64_t T, int nseg,
                     double* seg, int64_t seg_fstride, int64_t ldseg, int Rseg, const double* cstab,
                     hipStream_t s);
 void launch_far_ifft(const double* Y, int64_t yfstride, int nc, int B, int P, double* far,
-                     int64_t ldfar, const double* cstab, Clock* clk, hipStream_t s);
+                     int64_t ldfar, const double* cstab, hipStream_t s);
 int launch_fft_noise(const double* a, double* noise, const double* tw, int64_t nmd, int64_t nc,
                      int64_t arows, int64_t B, int is_complex, double scale, hipStream_t s);
 

@@ -27,9 +27,11 @@ __device__ __forceinline__ int64_t pmod(int64_t a, int64_t m) {
   return r < 0 ? r + m : r;
 }
 
-__device__ __forceinline__ int64_t load_t(const Clock* clk) {
-  return __hip_atomic_load(&clk->t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// explicit global-address-space load (pointers read from work-item structs are otherwise flat)
+__device__ __forceinline__ double gld(const double* p) {
+  return *(const __attribute__((address_space(1))) double*)p;
 }
+
 
 // ------------------------------------------------------------------------------------------
 // contraction
@@ -40,7 +42,7 @@ __device__ __forceinline__ int64_t load_t(const Clock* clk) {
 // into registers (software pipelining without a second LDS buffer).
 template <int RN, int CU>
 __global__ __launch_bounds__(WG, 2) void contract_kernel(const CItem* __restrict__ items,
-                                                         const Clock* __restrict__ clk) {
+                                                         StepArgs ta) {
   __shared__ double lds[KROWS * LDS_COLS];
   constexpr int NT = 16 * RN;
   constexpr int WWCAP = (256 * CU < LDS_WW_MAX) ? 256 * CU : LDS_WW_MAX;
@@ -53,7 +55,7 @@ __global__ __launch_bounds__(WG, 2) void contract_kernel(const CItem* __restrict
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
   const int lane = tid & 63;
-  const int64_t t = load_t(clk);
+  const int64_t t = ta.t;
 
   d4 acc[RN];
 #pragma unroll
@@ -169,7 +171,7 @@ __global__ __launch_bounds__(WG, 2) void contract_kernel(const CItem* __restrict
 constexpr int CPLX_WW_MAX = CPLX_WW_CAP;  // 16 rows x (512+16) doubles = 66 KB (2 WGs per CU)
 template <int RN>
 __global__ __launch_bounds__(WG, 2) void contract_cplx_kernel(const CItem* __restrict__ items,
-                                                              const Clock* __restrict__ clk) {
+                                                              StepArgs ta) {
   __shared__ double lds[2 * KROWS * (CPLX_WW_MAX + 16)];
   constexpr int NT = 16 * RN;
   constexpr int CU = 2;
@@ -179,7 +181,7 @@ __global__ __launch_bounds__(WG, 2) void contract_cplx_kernel(const CItem* __res
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
   const int lane = tid & 63;
-  const int64_t t = load_t(clk);
+  const int64_t t = ta.t;
 
   d4 accr[RN], acci[RN];
 #pragma unroll
@@ -296,83 +298,105 @@ __global__ __launch_bounds__(WG, 2) void contract_cplx_kernel(const CItem* __res
   }
 }
 
-void launch_contract_cplx(int rn, const CItem* items, int nitems, const Clock* clk, hipStream_t s) {
+void launch_contract_cplx(int rn, const CItem* items, int nitems, StepArgs ta, hipStream_t s) {
   if (nitems <= 0) return;
   dim3 g(nitems), b(WG);
   switch (rn) {
-    case 1: contract_cplx_kernel<1><<<g, b, 0, s>>>(items, clk); break;
-    case 2: contract_cplx_kernel<2><<<g, b, 0, s>>>(items, clk); break;
-    case 4: contract_cplx_kernel<4><<<g, b, 0, s>>>(items, clk); break;
-    default: contract_cplx_kernel<8><<<g, b, 0, s>>>(items, clk); break;
+    case 1: contract_cplx_kernel<1><<<g, b, 0, s>>>(items, ta); break;
+    case 2: contract_cplx_kernel<2><<<g, b, 0, s>>>(items, ta); break;
+    case 4: contract_cplx_kernel<4><<<g, b, 0, s>>>(items, ta); break;
+    default: contract_cplx_kernel<8><<<g, b, 0, s>>>(items, ta); break;
   }
 }
 
 template <int RN>
-static void launch_rn(int cu, const CItem* items, int nitems, const Clock* clk, hipStream_t s) {
+static void launch_rn(int cu, const CItem* items, int nitems, StepArgs ta, hipStream_t s) {
   dim3 g(nitems), b(WG);
   switch (cu) {
-    case 1: contract_kernel<RN, 1><<<g, b, 0, s>>>(items, clk); break;
-    case 2: contract_kernel<RN, 2><<<g, b, 0, s>>>(items, clk); break;
-    case 3: contract_kernel<RN, 3><<<g, b, 0, s>>>(items, clk); break;
-    default: contract_kernel<RN, 4><<<g, b, 0, s>>>(items, clk); break;
+    case 1: contract_kernel<RN, 1><<<g, b, 0, s>>>(items, ta); break;
+    case 2: contract_kernel<RN, 2><<<g, b, 0, s>>>(items, ta); break;
+    case 3: contract_kernel<RN, 3><<<g, b, 0, s>>>(items, ta); break;
+    default: contract_kernel<RN, 4><<<g, b, 0, s>>>(items, ta); break;
   }
 }
 
-void launch_contract(int rn, int cu, const CItem* items, int nitems, const Clock* clk, hipStream_t s) {
+void launch_contract(int rn, int cu, const CItem* items, int nitems, StepArgs ta, hipStream_t s) {
   if (nitems <= 0) return;
   switch (rn) {
-    case 1: launch_rn<1>(cu, items, nitems, clk, s); break;
-    case 2: launch_rn<2>(cu, items, nitems, clk, s); break;
-    case 4: launch_rn<4>(cu, items, nitems, clk, s); break;
-    case 8: launch_rn<8>(cu, items, nitems, clk, s); break;
-    default: launch_rn<16>(cu, items, nitems, clk, s); break;
+    case 1: launch_rn<1>(cu, items, nitems, ta, s); break;
+    case 2: launch_rn<2>(cu, items, nitems, ta, s); break;
+    case 4: launch_rn<4>(cu, items, nitems, ta, s); break;
+    case 8: launch_rn<8>(cu, items, nitems, ta, s); break;
+    default: launch_rn<16>(cu, items, nitems, ta, s); break;
   }
 }
 
 // ------------------------------------------------------------------------------------------
 // Latency-optimised per-step products.  Work step s in [0, ni*nks) is (slice s / nks, k-step
-// s % nks); wave w owns the contiguous range [w*S/16, (w+1)*S/16).  Operands come straight from
-// global memory (L2-resident per-step data), loads issued 4 steps ahead of their MFMAs.
-constexpr int TILE_NW = 16;
+// s % nks); share g of ngrp owns [g*S/ngrp, (g+1)*S/ngrp), split contiguously over the 4 waves.
+// Operands come straight from global memory (L2/MALL-resident per-step data).
+constexpr int TILE_NW = 4;
+constexpr int TILE_U = 8;  // work steps per wave with all operand loads in flight
 template <int RN>
-__global__ __launch_bounds__(1024) void tile_kernel(const TItem* __restrict__ items,
-                                                     const Clock* __restrict__ clk) {
-  __shared__ double red[(TILE_NW / 2) * 16 * 16 * RN];
+__global__ __launch_bounds__(TILE_NW * 64) void tile_kernel(const TItem* __restrict__ items,
+                                                            StepArgs ta) {
+  __shared__ double red[(TILE_NW / 2) * 256 * RN];
+  __shared__ unsigned last;
   const TItem it = items[blockIdx.x];
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const int brow = lane >> 4, bcol = lane & 15;
-  const int64_t t = load_t(clk);
+  const int64_t t = ta.t;
+  // epilogue addends (far + mid field) for this thread's output elements, fetched up front
+  double pre[RN];
+#pragma unroll
+  for (int j = 0; j < RN; ++j) {
+    const int e = j * TILE_NW * 64 + threadIdx.x;  // element (n*4+q)*64 + lane'
+    const int nq = e >> 6, ln = e & 63;
+    const int row = (ln >> 4) + 4 * (nq & 3), col = 16 * (nq >> 2) + (ln & 15);
+    double v = 0.0;
+    if (row < it.nrows && col < it.ncols) {
+      if (it.add) v = gld(it.add + (t - ta.t_far) * it.add_cs + (int64_t)row * it.lda + col);
+      if (it.add2) v += gld(it.add2 + (t - ta.t_mid) * it.add2_cs + (int64_t)row * it.lda2 + col);
+    }
+    pre[j] = v;
+  }
   d4 acc[RN];
 #pragma unroll
   for (int n = 0; n < RN; ++n) acc[n] = d4{0.0, 0.0, 0.0, 0.0};
-  const int S = it.ni * it.nks;
-  const int s0 = (int)((int64_t)S * wave / TILE_NW), s1 = (int)((int64_t)S * (wave + 1) / TILE_NW);
-  constexpr int U = 4;
-  for (int sb = s0; sb < s1; sb += U) {
-    double a[U], b[U][RN];
+  const int64_t S = (int64_t)it.ni * it.nks;
+  const int64_t g0 = S * it.grp / it.ngrp, g1 = S * (it.grp + 1) / it.ngrp;
+  const int s0 = (int)(g0 + (g1 - g0) * wave / TILE_NW), s1 = (int)(g0 + (g1 - g0) * (wave + 1) / TILE_NW);
+  const int tm = it.ring ? (int)pmod(t + it.tshift - it.ia, it.ring) : 0;
+  for (int sb = s0; sb < s1; sb += TILE_U) {
+    double a[TILE_U], b[TILE_U][RN];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
+    for (int u = 0; u < TILE_U; ++u) {
       const int s = sb + u;
       a[u] = 0.0;
 #pragma unroll
       for (int n = 0; n < RN; ++n) b[u][n] = 0.0;
       if (s < s1) {
         const int i = s / it.nks, ks = s - i * it.nks;
-        a[u] = it.A[(int64_t)ks * it.a_ks + (int64_t)i * 64 + lane];
+        a[u] = gld(it.A + (int64_t)ks * it.a_ks + (int64_t)i * 64 + lane);
         int64_t cb = 0;
-        if (it.ring) cb = pmod(t + it.tshift - (it.ia + i), it.ring) * it.cs;
+        if (it.ring) {
+          int c = tm - i;
+          if (c < 0) c += it.ring;
+          cb = (int64_t)c * it.cs;
+        }
         const double* xr = it.X + (int64_t)(4 * ks + brow) * it.ldx + cb + bcol;
 #pragma unroll
-        for (int n = 0; n < RN; ++n) b[u][n] = xr[16 * n];
+        for (int n = 0; n < RN; ++n) b[u][n] = gld(xr + 16 * n);
       }
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+    for (int u = 0; u < TILE_U; ++u)
 #pragma unroll
       for (int n = 0; n < RN; ++n) acc[n] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b[u][n], acc[n], 0, 0, 0);
   }
-  // fixed-order tree over the 16 waves: w += w + half for half = 8, 4, 2, 1
+  // fixed-order tree over the waves
+#pragma unroll
   for (int half = TILE_NW / 2; half >= 1; half >>= 1) {
     if (wave >= half && wave < 2 * half) {
       double* r = red + (wave - half) * 256 * RN;
@@ -391,32 +415,70 @@ __global__ __launch_bounds__(1024) void tile_kernel(const TItem* __restrict__ it
     }
     __syncthreads();
   }
-  if (wave == 0) {
-    const double* add = it.add ? it.add + (t - clk->t_far) * it.add_cs : nullptr;
-    const double* add2 = it.add2 ? it.add2 + (t - clk->t_mid) * it.add2_cs : nullptr;
+  if (it.ngrp == 1) {
+    if (wave == 0) {
 #pragma unroll
-    for (int n = 0; n < RN; ++n) {
-      const int col = 16 * n + bcol;
+      for (int n = 0; n < RN; ++n)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int row = brow + 4 * q;
-        if (row < it.nrows && col < it.ncols) {
-          double v = acc[n][q];
-          if (add) v = add[(int64_t)row * it.lda + col] + v;
-          if (add2) v += add2[(int64_t)row * it.lda2 + col];
-          it.out[(int64_t)row * it.ldo + col] = v;
-        }
-      }
+        for (int q = 0; q < 4; ++q) red[(n * 4 + q) * 64 + lane] = acc[n][q];
     }
+    __syncthreads();
+  } else {
+    // publish this share; the last share to arrive sums all shares in share order.  Partials move
+    // through agent-coherent (L2-bypassing) atomic stores / loads, so no cache-wide fence is
+    // needed (an agent-scope fence writes back and invalidates the XCD's L2, evicting the kernel
+    // slices the other workgroups stream).
+    if (wave == 0) {
+      double* slot = it.part + (int64_t)it.grp * 256 * RN;
+#pragma unroll
+      for (int n = 0; n < RN; ++n)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          __hip_atomic_store(slot + (n * 4 + q) * 64 + lane, acc[n][q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_s_waitcnt(0);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned old = __hip_atomic_fetch_add(it.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = (old == (unsigned)it.ngrp - 1) ? 1u : 0u;
+      if (last) __hip_atomic_store(it.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!last) return;
+  }
+#pragma unroll
+  for (int j = 0; j < RN; ++j) {
+    const int e = j * TILE_NW * 64 + threadIdx.x;
+    double v = 0.0;
+    if (it.ngrp == 1) {
+      v = red[e];
+    } else {
+      double* p = it.part + e;
+      int g = 0;
+      for (; g + 4 <= it.ngrp; g += 4) {
+        const double x0 = __hip_atomic_load(p + (int64_t)(g + 0) * 256 * RN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const double x1 = __hip_atomic_load(p + (int64_t)(g + 1) * 256 * RN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const double x2 = __hip_atomic_load(p + (int64_t)(g + 2) * 256 * RN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const double x3 = __hip_atomic_load(p + (int64_t)(g + 3) * 256 * RN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v += x0;
+        v += x1;
+        v += x2;
+        v += x3;
+      }
+      for (; g < it.ngrp; ++g) v += __hip_atomic_load(p + (int64_t)g * 256 * RN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const int nq = e >> 6, ln = e & 63;
+    const int row = (ln >> 4) + 4 * (nq & 3), col = 16 * (nq >> 2) + (ln & 15);
+    if (row < it.nrows && col < it.ncols) it.out[(int64_t)row * it.ldo + col] = pre[j] + v;
   }
 }
 
-void launch_tile(int rn, const TItem* items, int nitems, const Clock* clk, hipStream_t s) {
+void launch_tile(int rn, const TItem* items, int nitems, StepArgs ta, hipStream_t s) {
   if (nitems <= 0) return;
   switch (rn) {
-    case 1: tile_kernel<1><<<nitems, 1024, 0, s>>>(items, clk); break;
-    case 2: tile_kernel<2><<<nitems, 1024, 0, s>>>(items, clk); break;
-    default: tile_kernel<4><<<nitems, 1024, 0, s>>>(items, clk); break;
+    case 1: tile_kernel<1><<<nitems, TILE_NW * 64, 0, s>>>(items, ta); break;
+    case 2: tile_kernel<2><<<nitems, TILE_NW * 64, 0, s>>>(items, ta); break;
+    default: tile_kernel<4><<<nitems, TILE_NW * 64, 0, s>>>(items, ta); break;
   }
 }
 
@@ -461,21 +523,16 @@ __device__ __forceinline__ double max_slots(const double* p, int64_t st, int n, 
   return m;
 }
 __global__ __launch_bounds__(256) void reduce_kernel(const RItem* __restrict__ items,
-                                                     Clock* __restrict__ clk, int set_tfar) {
+                                                     StepArgs ta) {
   const RItem it = items[blockIdx.x];
   const int n = it.rows * it.cols;
   const int e0 = blockIdx.y * RED_PER_BLOCK;
-  const int64_t t = load_t(clk);
-  // set_tfar: 1 = this reduce completes a far-field block, 2 = a mid-level block
-  if (set_tfar && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
-    if (set_tfar == 1) clk->t_far = t;
-    else clk->t_mid = t;
-  }
+  const int64_t t = ta.t;
   if (e0 >= n) return;
   const double* add = nullptr;
   const double* add2 = nullptr;
-  if (it.add) add = it.add + (t - clk->t_far) * it.add_cs;
-  if (it.add2) add2 = it.add2 + (t - clk->t_mid) * it.add2_cs;
+  if (it.add) add = it.add + (t - ta.t_far) * it.add_cs;
+  if (it.add2) add2 = it.add2 + (t - ta.t_mid) * it.add2_cs;
   for (int e = e0 + threadIdx.x; e < min(n, e0 + RED_PER_BLOCK); e += blockDim.x) {
     const int r = e / it.cols;
     const int c = e - r * it.cols;
@@ -485,11 +542,11 @@ __global__ __launch_bounds__(256) void reduce_kernel(const RItem* __restrict__ i
   }
 }
 
-void launch_reduce(const RItem* items, int nitems, int max_elems, const Clock* clk, int set_tfar,
+void launch_reduce(const RItem* items, int nitems, int max_elems, StepArgs ta,
                    hipStream_t s) {
   if (nitems <= 0) return;
   dim3 g(nitems, (max_elems + RED_PER_BLOCK - 1) / RED_PER_BLOCK);
-  reduce_kernel<<<g, 256, 0, s>>>(items, const_cast<Clock*>(clk), set_tfar);
+  reduce_kernel<<<g, 256, 0, s>>>(items, ta);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -557,13 +614,12 @@ __device__ __forceinline__ double bath_force(const BathDev& bd, int k, int b, in
 // mode0: 0 = potential force at q_t already in Fc (exact cache hit or host force)
 //        1 = harmonic: select between the cache and -dyn.q_t (Ypot) per trajectory
 // diff1: write the per-chunk max |q~ - q0| for the id1 cache decision
-__global__ __launch_bounds__(256) void phaseA_kernel(const StepDev* __restrict__ sd,
-                                                     const Clock* __restrict__ clk, int mode0,
-                                                     int diff1) {
+__global__ __launch_bounds__(256) void phaseA_kernel(const StepDev* __restrict__ sd, StepArgs ta,
+                                                     int mode0, int diff1) {
   __shared__ double red[WG];
   const int B = sd->B, nph = sd->nph, nb = sd->nbath;
   Lanes L(B);
-  const int64_t t = load_t(clk);
+  const int64_t t = ta.t;
   const int tn = (int)(t % sd->nmd);
   const int par = (int)(t & 1);
   const double dt = sd->dt, dt2 = dt * dt;
@@ -653,11 +709,11 @@ __device__ __forceinline__ double id1_force(const StepDev* sd, int d, int b, int
   return f;
 }
 
-__global__ __launch_bounds__(256) void phaseB_kernel(const StepDev* __restrict__ sd,
-                                                     const Clock* __restrict__ clk, int mode1) {
+__global__ __launch_bounds__(256) void phaseB_kernel(const StepDev* __restrict__ sd, StepArgs ta,
+                                                     int mode1) {
   const int B = sd->B, nph = sd->nph, nb = sd->nbath;
   Lanes L(B);
-  const int64_t t = load_t(clk);
+  const int64_t t = ta.t;
   const int t1 = (int)((t + 1) % sd->nmd);
   const int par1 = (int)((t + 1) & 1);
   const double dt = sd->dt;
@@ -687,11 +743,12 @@ __global__ __launch_bounds__(256) void phaseB_kernel(const StepDev* __restrict__
 
 // diff0: write the per-chunk max |q_{t+1} - q0| for the next step's id0 cache decision
 __global__ __launch_bounds__(256) void phaseC_kernel(const StepDev* __restrict__ sd,
-                                                     Clock* __restrict__ clk, int mode1, int diff0) {
+                                                     StepArgs ta, int mode1,
+                                                     int diff0) {
   __shared__ double red[WG];
   const int B = sd->B, nph = sd->nph, nb = sd->nbath;
   Lanes L(B);
-  const int64_t t = load_t(clk);
+  const int64_t t = ta.t;
   const int tn = (int)(t % sd->nmd);
   const int t1 = (int)((t + 1) % sd->nmd);
   const int par1 = (int)((t + 1) & 1);
@@ -744,18 +801,6 @@ __global__ __launch_bounds__(256) void phaseC_kernel(const StepDev* __restrict__
   (void)tn;
   if (diff0) block_max_atomic(sd, L, dq, 0, par ^ 1, red);
   if (mode1 == 1 && L.ok && blockIdx.y == 0 && L.dl == 0) sd->qvalid[L.b] = 1;
-  // the last block to finish advances the step counter (all blocks read t before arriving)
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    const unsigned total = gridDim.x * gridDim.y;
-    const unsigned old = atomicAdd(&clk->arrive, 1u);
-    if (old == total - 1) {
-      clk->arrive = 0;
-      __hip_atomic_store(&clk->t, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __threadfence();
-    }
-  }
 }
 
 // bath.cur[t] and md.etot[t] (md.py:383, 397) for every step of the run from phase A's per-step
@@ -786,16 +831,16 @@ static inline dim3 phase_grid(int B, int ndblk) {
   return dim3((B + BT - 1) / BT, ndblk);
 }
 
-void launch_phaseA(const StepDev* sd, const Clock* clk, int B, int ndblk, int mode0, int diff1,
+void launch_phaseA(const StepDev* sd, StepArgs ta, int B, int ndblk, int mode0, int diff1,
                    hipStream_t s) {
-  phaseA_kernel<<<phase_grid(B, ndblk), WG, 0, s>>>(sd, clk, mode0, diff1);
+  phaseA_kernel<<<phase_grid(B, ndblk), WG, 0, s>>>(sd, ta, mode0, diff1);
 }
-void launch_phaseB(const StepDev* sd, const Clock* clk, int B, int ndblk, int mode1, hipStream_t s) {
-  phaseB_kernel<<<phase_grid(B, ndblk), WG, 0, s>>>(sd, clk, mode1);
+void launch_phaseB(const StepDev* sd, StepArgs ta, int B, int ndblk, int mode1, hipStream_t s) {
+  phaseB_kernel<<<phase_grid(B, ndblk), WG, 0, s>>>(sd, ta, mode1);
 }
-void launch_phaseC(const StepDev* sd, Clock* clk, int B, int ndblk, int mode1, int diff0,
+void launch_phaseC(const StepDev* sd, StepArgs ta, int B, int ndblk, int mode1, int diff0,
                    hipStream_t s) {
-  phaseC_kernel<<<phase_grid(B, ndblk), WG, 0, s>>>(sd, clk, mode1, diff0);
+  phaseC_kernel<<<phase_grid(B, ndblk), WG, 0, s>>>(sd, ta, mode1, diff0);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1061,9 +1106,8 @@ void launch_seg_fft(const double* H, int64_t ldh, int R, int B, int nc, int P, i
 // (the real inverse transform of the Hermitian spectrum; Im Y_0, Im Y_P ignored as by irfft).
 __global__ void far_ifft_kernel(const double* __restrict__ Y, int64_t yfstride, int nc, int B, int P,
                                 double* __restrict__ far, int64_t ldfar,
-                                const double2* __restrict__ cstab, Clock* clk) {
+                                const double2* __restrict__ cstab) {
   const int64_t total = (int64_t)nc * P * B;
-  if (blockIdx.x == 0 && threadIdx.x == 0) clk->t_far = load_t(clk);
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int b = (int)(e % B);
@@ -1087,11 +1131,11 @@ __global__ void far_ifft_kernel(const double* __restrict__ Y, int64_t yfstride, 
 }
 
 void launch_far_ifft(const double* Y, int64_t yfstride, int nc, int B, int P, double* far,
-                     int64_t ldfar, const double* cstab, Clock* clk, hipStream_t s) {
+                     int64_t ldfar, const double* cstab, hipStream_t s) {
   const int64_t total = (int64_t)nc * P * B;
   const int64_t blocks = std::min<int64_t>((total + 255) / 256, 16384);
   far_ifft_kernel<<<(unsigned)blocks, 256, 0, s>>>(Y, yfstride, nc, B, P, far, ldfar,
-                                                   (const double2*)cstab, clk);
+                                                   (const double2*)cstab);
 }
 
 }  // namespace gle
