@@ -80,7 +80,7 @@ def main():
     ap.add_argument("--ntraj", type=int, default=64, help="trajectories per GPU")
     ap.add_argument("--config", default="C3")
     ap.add_argument("--block-len", type=int, default=0)
-    ap.add_argument("--mid-len", type=int, default=0)
+    ap.add_argument("--max-block", type=int, default=0)
     ap.add_argument("--far-mode", default="auto", choices=["auto", "direct", "spectral"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
@@ -108,7 +108,7 @@ def main():
     m = MD.md(meta["dt"], meta["nmd"], meta["T"], axyz=axyz, dyn=dyn, ntraj=args.ntraj,
               seed=1000 + rank * args.ntraj, traj_offset=rank * args.ntraj, device=local_rank,
               noise_mode="device", block_len=args.block_len, far_mode=args.far_mode,
-              mid_len=args.mid_len, verbose=False)
+              max_block=args.max_block, verbose=False)
     for b in baths:
         m.AddBath(b)
     m.initialise()

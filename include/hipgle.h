@@ -52,17 +52,23 @@ typedef struct gle_config {
     int64_t nmd;        /* MD steps per run = noise period, md.nmd (md.py:59); even          */
     double dt;          /* MD time step, md.dt (md.py:59)                                    */
     int32_t device;     /* HIP device ordinal                                                */
-    int32_t block_len;  /* far-field time block L (= partition length P in spectral mode); 0=auto */
+    int32_t block_len;  /* P0: first block length of the memory-sum ladder (near field = lags
+                           [1, 2 P0) every step); 0 = auto (4)                                  */
     int32_t far_mode;   /* GLE_FAR_AUTO / GLE_FAR_DIRECT / GLE_FAR_SPECTRAL                      */
-    int32_t mid_len;    /* P1: lags [P1, L) every P1 steps as one blocked contraction; 0=auto, -1=off */
+    int32_t max_block;  /* largest ladder block length; 0 = auto (256 spectral, direct: L with
+                           L * ntraj >= 256, L <= 32)                                           */
 } gle_config;
 
-/* far-field memory sum  sum_{i>=L} K_i p_{t-i}  (SURVEY.md section 8a R3):
- *   DIRECT    one time-blocked MFMA contraction over the kernel slices every L steps;
- *   SPECTRAL  uniformly partitioned overlap-save: kernel partitions of P = L slices are
- *             transformed once (length 2P), every P steps one new input segment is transformed and
- *             the far field is a per-frequency MFMA contraction of the spectra (~4(P+1)/P^2 of the
- *             direct flops), then inverse-transformed.  Same result to fp64 rounding. */
+/* memory sum  S(t+1) = sum_{i>=1} K_i p_{t+1-i}   as a ladder:
+ *   near field  lags [1, 2 P0) every step;
+ *   level l     block P = P0 2^l, lags [2P, 4P) (the last level up to ml): every P steps one block
+ *               of P future steps is computed one block ahead, on a background stream that
+ *               overlaps the per-step chain.  A level is
+ *   DIRECT      one time-blocked MFMA contraction over its kernel slices, or
+ *   SPECTRAL    uniformly partitioned overlap-save: kernel partitions of P slices transformed once
+ *               (length 2P), one new input segment transformed per block, a per-frequency MFMA
+ *               contraction of the spectra (~4(P+1)/P^2 of the direct flops), inverse transform.
+ *   AUTO        spectral for power-of-two P >= 8 when ntraj >= 8.  Same result to fp64 rounding. */
 #define GLE_FAR_AUTO 0
 #define GLE_FAR_DIRECT 1
 #define GLE_FAR_SPECTRAL 2

@@ -36,7 +36,7 @@ class GLEError(RuntimeError):
 class gle_config(ctypes.Structure):
     _fields_ = [("nph", ctypes.c_int64), ("ntraj", ctypes.c_int64), ("nmd", ctypes.c_int64),
                 ("dt", ctypes.c_double), ("device", ctypes.c_int32), ("block_len", ctypes.c_int32),
-                ("far_mode", ctypes.c_int32), ("mid_len", ctypes.c_int32)]
+                ("far_mode", ctypes.c_int32), ("max_block", ctypes.c_int32)]
 
 FAR_AUTO, FAR_DIRECT, FAR_SPECTRAL = 0, 1, 2
 FAR_MODES = {"auto": FAR_AUTO, "direct": FAR_DIRECT, "spectral": FAR_SPECTRAL}
@@ -120,12 +120,12 @@ def device_count():
 class Stepper:
     """Owner of one gle_handle: a batch of ntraj trajectories of one system on one device."""
 
-    def __init__(self, nph, ntraj, nmd, dt, device=0, block_len=0, far_mode="auto", mid_len=0):
+    def __init__(self, nph, ntraj, nmd, dt, device=0, block_len=0, far_mode="auto", max_block=0):
         self.lib = load()
         self.nph, self.ntraj, self.nmd, self.dt = int(nph), int(ntraj), int(nmd), float(dt)
         fm = FAR_MODES[far_mode] if isinstance(far_mode, str) else int(far_mode)
         cfg = gle_config(self.nph, self.ntraj, self.nmd, self.dt, int(device), int(block_len), fm,
-                         int(mid_len))
+                         int(max_block))
         h = _P()
         rc = self.lib.gle_create(ctypes.byref(cfg), ctypes.byref(h))
         if rc != 0:

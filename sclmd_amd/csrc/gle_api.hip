@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -63,20 +64,40 @@ struct Bath {
   double* d_Kq = nullptr;
   int32_t* d_inv = nullptr;
   double *d_noise = nullptr, *d_Y = nullptr, *d_S = nullptr, *d_Yq = nullptr;
-  double *d_Xcur = nullptr, *d_Xq = nullptr, *d_H = nullptr, *d_cur = nullptr, *d_far = nullptr;
-  double* d_mid = nullptr;
+  double *d_Xcur = nullptr, *d_Xq = nullptr, *d_H = nullptr, *d_cur = nullptr;
   int64_t ldh = 0;
   int R = 1;
   bool noise_set = false;
-  // spectral far field
-  int M = 0, nrt2 = 0, nks2 = 0, Rseg = 0;
-  int64_t ldseg = 0, khat_fstride = 0, seg_fstride = 0, yfstride = 0;
-  double *d_khat = nullptr, *d_seg = nullptr, *d_Yspec = nullptr;
   // noise generator
   int64_t nfreq = 0;
   bool fac_complex = false;
   int fac_rows = 0, fac_nrt = 0;
   double* d_fac = nullptr;
+};
+
+// One level of the memory-sum ladder for one bath.
+struct LevelBath {
+  bool active = false;  // the bath's kernel reaches this level's lags
+  int lag1 = 0;         // lags [lag0, lag1) of this bath
+  double* d_out = nullptr;  // block double buffer [ncp][2 P B]: block k at columns (k&1) P B
+  // spectral: partitions m in [2, 2+M), segment-spectra ring of Rseg slots
+  int M = 0, Rseg = 0;
+  int64_t ldseg = 0, khat_fstride = 0, seg_fstride = 0, yfstride = 0;
+  double *d_khat = nullptr, *d_seg = nullptr, *d_Yspec = nullptr;
+};
+
+// Level l of the ladder: block length P; lags [2P, lag1).  Block k (targets kP+1..kP+P) only needs
+// p up to (k-1)P, so it is computed one block ahead on the background stream.
+struct Level {
+  int P = 1, lag0 = 2, lag1 = 2;
+  bool spectral = false;
+  int cstride = 1;             // twiddle-table stride (Pspec / P)
+  int sidx = 0;                // background stream
+  std::vector<LevelBath> lb;   // per bath
+  Op op[2];                    // direct: per output parity; spectral: op[0] (per-frequency products)
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  int64_t last_block = INT64_MIN;
+  int64_t bg_block[2] = {INT64_MIN, INT64_MIN};  // block launched on the background stream
 };
 
 }  // namespace
@@ -102,22 +123,22 @@ struct gle_handle {
   double* d_tw = nullptr;
   int ndblk = 1, dchunk = 1;
   int64_t t = 0;
-  int64_t t_far = 0, t_mid = 0;  // steps at which the current far / mid blocks were computed
   bool frozen = false, state_set = false;
   bool need_prime = true;
-  int steps_since_far = 0;
-  bool far_due = true;
   bool pot_cache_exact = false;  // q_t == q~_{t-1} bitwise (no constraints): id0 cache hit
   bool host_force_step = false;
-  Op op_far, op_prime, op1a, op1a_np, op1b;
-  Op op0[2], op0p[2];  // {K0 p_t, Kq q_t, near S(t+1) into S[par]} (+ dyn q_t), par = (t+1)&1
-  Op op_spec;     // spectral far field: per-frequency contraction of kernel and segment spectra
-  Op op_mid;      // mid-level block: lags [P1, L) every P1 steps, P1*B columns
-  int P1 = 0;     // mid-level block length (0: none, near field covers [1, L))
-  bool mid_due = true;
-  int far_mode = GLE_FAR_DIRECT;
-  bool seg_ready = false;
+  Op op_prime, op1a, op1a_np, op1b;
+  Op op0[2], op0p[2];  // {K0 p_t, Kq q_t, S(t+1) = near + levels into S[par]} (+ dyn q_t), par = (t+1)&1
+  int P0 = 1;          // first level block; near field = lags [1, 2 P0)
+  int near_end = 1;
+  std::vector<Level> levels;
+  int far_mode = GLE_FAR_DIRECT;  // GLE_FAR_SPECTRAL if any level is spectral
   double* d_cstab = nullptr;
+  static constexpr int NBG = 3;    // background streams: ladder blocks, levels grouped by P so a
+                                   // small level never queues behind a much larger level's block
+  hipStream_t bg[NBG] = {};
+  hipEvent_t ev_step = nullptr;    // end of the latest block-boundary step on the main stream
+  hipEvent_t ev_bg[NBG] = {};      // join points of the background streams
   std::vector<void*> allocs;
   size_t dev_bytes = 0;
   // profiling of the dominant contraction
@@ -211,12 +232,9 @@ struct Gemm {
   int M, N;
   double* dst;
   int64_t ldd;
-  const double* add = nullptr;  // far addend
-  int64_t lda = 0;
-  int add_cs = 0;
-  const double* add2 = nullptr;  // mid-level addend
-  int64_t lda2 = 0;
-  int add2_cs = 0;
+  const double* adds[MAXLVL] = {};  // level block buffers added in the tile epilogue
+  int32_t add_ld[MAXLVL] = {};
+  int nadd = 0;
   bool force_reduce = false;
   int Kd = 0;  // true (unpadded) reduction length, for the algorithmic flop/byte count
   int tdiv = 1;
@@ -265,7 +283,7 @@ void plan_gemm(Op& op, const Gemm& g, int target_items, int min_work) {
     }
   }
   const int nsplit = (ni > 0) ? si * sk : 0;
-  const bool use_partial = g.force_reduce || g.add != nullptr || g.add2 != nullptr || nsplit > 1;
+  const bool use_partial = g.force_reduce || nsplit > 1;
   // item order: (column tile, slice range, k range) outer, row group inner -- consecutive items
   // share the staged history window (and, with the kernel's XCD-aware mapping, one L2)
   std::vector<size_t> slot0s((size_t)ngroups * ncol, 0);
@@ -337,18 +355,12 @@ void plan_gemm(Op& op, const Gemm& g, int target_items, int min_work) {
           r.dst = g.dst + part * g.dst_im + (int64_t)(64 * gi) * g.ldd + col0;
           // offset, fixed up in materialize()
           r.src = (const double*)(uintptr_t)((slot0s[key] + (size_t)part * 64 * NT) * sizeof(double));
-          r.add = (g.add && part == 0) ? g.add + (int64_t)(64 * gi) * g.lda + col0 : nullptr;
-          r.add2 = (g.add2 && part == 0) ? g.add2 + (int64_t)(64 * gi) * g.lda2 + col0 : nullptr;
-          r.lda2 = (int32_t)g.lda2;
-          r.add2_cs = g.add2_cs;
           r.ldd = (int32_t)g.ldd;
           r.lds = NT;
-          r.lda = (int32_t)g.lda;
           r.nslots = nslot[key];
           r.slot_stride = (int64_t)(g.cplx ? 2 : 1) * 64 * NT;
           r.rows = nrows;
           r.cols = std::min<int>(NT, g.N - col0);
-          r.add_cs = g.add_cs;
           op.ritems.push_back(r);
         }
       }
@@ -379,15 +391,10 @@ void plan_tile(Op& op, const Gemm& g) {
       it.ldx = g.ldx;
       it.out = g.dst + (int64_t)(16 * rt) * g.ldd + c0;
       it.ldo = (int32_t)g.ldd;
-      if (g.add) {
-        it.add = g.add + (int64_t)(16 * rt) * g.lda + c0;
-        it.lda = (int32_t)g.lda;
-        it.add_cs = g.add_cs;
-      }
-      if (g.add2) {
-        it.add2 = g.add2 + (int64_t)(16 * rt) * g.lda2 + c0;
-        it.lda2 = (int32_t)g.lda2;
-        it.add2_cs = g.add2_cs;
+      it.nadd = g.nadd;
+      for (int a = 0; a < g.nadd; ++a) {
+        it.add[a] = g.adds[a] ? g.adds[a] + (int64_t)(16 * rt) * g.add_ld[a] + c0 : nullptr;
+        it.add_ld[a] = g.add_ld[a];
       }
       it.ia = g.i0;
       it.ni = ni;
@@ -504,53 +511,73 @@ struct Planner {
   int done() { return materialize(h, op, partial); }
 };
 
-StepArgs step_args(const gle_handle* h) {
-  StepArgs a;
-  a.t = h->t;
-  a.t_far = h->t_far;
-  a.t_mid = h->t_mid;
+inline int64_t floordiv(int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+
+// Step arguments of step t: per level, the column offset of target t+1 in its block buffer
+// (block floor(t/P), parity half of the buffer, column (t mod P) * B).
+StepArgs step_args(const gle_handle* h, int64_t t) {
+  StepArgs a{};
+  a.t = t;
+  for (size_t l = 0; l < h->levels.size(); ++l) {
+    const int64_t P = h->levels[l].P;
+    const int64_t k = floordiv(t, P);
+    a.lvl_off[l] = ((k & 1) * P + (t - k * P)) * h->B;
+  }
   return a;
 }
+StepArgs step_args(const gle_handle* h) { return step_args(h, h->t); }
 
-void run_op(gle_handle* h, Op& op, int set_tfar, bool profile) {
+void drain_profile(gle_handle* h) {
+  hipStreamSynchronize(h->stream);
+  for (int i = 0; i < gle_handle::NBG; ++i)
+    if (h->bg[i]) hipStreamSynchronize(h->bg[i]);
+  for (size_t i = 0; i + 1 < h->ev_used; i += 2) {
+    float ms = 0;
+    hipEventElapsedTime(&ms, h->ev[i], h->ev[i + 1]);
+    h->prof_ms += ms;
+  }
+  h->ev_used = 0;
+}
+
+// Launch one op on stream s; profile: HIP events around the contraction launch (the dominant
+// kernel) on that same stream.
+void run_op(gle_handle* h, Op& op, hipStream_t s, const StepArgs& ta, bool profile) {
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (profile && h->prof && !op.items.empty()) {
-    if (h->ev_used + 2 > h->ev.size()) {
-      // drain the pool into the running sum
-      hipStreamSynchronize(h->stream);
-      for (size_t i = 0; i + 1 < h->ev_used; i += 2) {
-        float ms = 0;
-        hipEventElapsedTime(&ms, h->ev[i], h->ev[i + 1]);
-        h->prof_ms += ms;
-      }
-      h->ev_used = 0;
-    }
+  if (profile && h->prof && !(op.items.empty() && op.titems.empty())) {
+    if (h->ev_used + 2 > h->ev.size()) drain_profile(h);
     e0 = h->ev[h->ev_used];
     e1 = h->ev[h->ev_used + 1];
     h->ev_used += 2;
-    hipEventRecord(e0, h->stream);
+    hipEventRecord(e0, s);
   }
-  if (op.tile) {
-    launch_tile(op.rn, op.d_titems, (int)op.titems.size(), step_args(h), h->stream);
-    if (e1) {
-      hipEventRecord(e1, h->stream);
-      h->prof_n += 1;
-      h->prof_flops += op.flops;
-      h->prof_bytes += op.bytes;
-    }
-    return;
-  }
-  if (op.cplx)
-    launch_contract_cplx(op.rn, op.d_items, (int)op.items.size(), step_args(h), h->stream);
+  if (op.tile)
+    launch_tile(op.rn, op.d_titems, (int)op.titems.size(), ta, s);
+  else if (op.cplx)
+    launch_contract_cplx(op.rn, op.d_items, (int)op.items.size(), ta, s);
   else
-    launch_contract(op.rn, op.cu, op.d_items, (int)op.items.size(), step_args(h), h->stream);
+    launch_contract(op.rn, op.cu, op.d_items, (int)op.items.size(), ta, s);
   if (e1) {
-    hipEventRecord(e1, h->stream);
+    hipEventRecord(e1, s);
     h->prof_n += 1;
     h->prof_flops += op.flops;
     h->prof_bytes += op.bytes;
   }
-  launch_reduce(op.d_ritems, (int)op.ritems.size(), op.max_elems, step_args(h), h->stream);
+  if (!op.tile) launch_reduce(op.d_ritems, (int)op.ritems.size(), op.max_elems, ta, s);
+}
+
+// Make the main stream wait for everything queued on the background stream.
+void join_bg(gle_handle* h) {
+  for (int i = 0; i < gle_handle::NBG; ++i)
+    if (h->bg[i]) {
+      hipEventRecord(h->ev_bg[i], h->bg[i]);
+      hipStreamWaitEvent(h->stream, h->ev_bg[i], 0);
+    }
+}
+
+int sync_bg(gle_handle* h) {
+  for (int i = 0; i < gle_handle::NBG; ++i)
+    if (h->bg[i]) HIPCHK(h, hipStreamSynchronize(h->bg[i]));
+  return GLE_OK;
 }
 
 int check_bath(gle_handle* h, int32_t b) {
@@ -563,91 +590,125 @@ int check_bath(gle_handle* h, int32_t b) {
 int freeze(gle_handle* h) {
   if (h->frozen) return GLE_OK;
   const int64_t B = h->B;
-  // block length L of the far-field contraction: enough columns (L*B) for MFMA reuse of each
-  // streamed kernel slice, bounded so the per-step near-field stays small
   int mlmax = 1;
   for (auto& b : h->baths) mlmax = std::max(mlmax, b.ml);
-  // far-field mode: the spectral form pays when the contraction is compute-bound (many
-  // trajectories) and the kernel is long compared with the partition; the direct form streams the
-  // kernel once per L steps and wins when the step is bandwidth-bound (few trajectories)
-  int mode = h->cfg.far_mode;
-  const int Pdef = 64;
-  if (mode == GLE_FAR_AUTO) mode = (B >= 8 && mlmax >= 4 * Pdef) ? GLE_FAR_SPECTRAL : GLE_FAR_DIRECT;
-  if (h->cfg.block_len > 0) {
-    h->L = h->cfg.block_len;
-  } else if (mode == GLE_FAR_SPECTRAL) {
-    h->L = Pdef;
+  // ---- memory-sum ladder:  S(t+1) = near(t+1) + sum_l level_l(t+1)
+  //   near     lags [1, 2 P0), every step, in the step's first product (tile kernel)
+  //   level l  block P = P0 2^l, lags [2P, 4P) (the last level: [2P, ml)); block k (targets
+  //            kP+1..kP+P) needs p only up to (k-1)P, so it is computed one block AHEAD on the
+  //            background stream while the per-step chain runs
+  //   a level is SPECTRAL (uniformly partitioned overlap-save, partitions of P lags, transforms of
+  //   length 2P: ~4(P+1)/P^2 of the direct flops) or DIRECT (one MFMA contraction per block, each
+  //   kernel slice reused for P*B columns)
+  const int mode = h->cfg.far_mode;
+  const bool spec_ok = mode == GLE_FAR_SPECTRAL || (mode == GLE_FAR_AUTO && B >= 8);
+  const int P0 = h->cfg.block_len > 0 ? h->cfg.block_len : 4;
+  int Pmax;
+  if (h->cfg.max_block > 0) {
+    Pmax = std::max(P0, h->cfg.max_block);
+  } else if (spec_ok) {
+    Pmax = std::max(P0, 256);
   } else {
-    int L = 1;
+    // direct: enough columns per block for MFMA reuse of each streamed kernel slice
+    int L = P0;
     while (L * B < 256 && L < 32) L *= 2;
-    h->L = L;
+    Pmax = L;
   }
-  const int L = h->L;
-  const int rn_step = rn_for(B);
-  if (mode == GLE_FAR_SPECTRAL) {
-    // device-memory check: transformed kernels + segment rings
+  h->P0 = P0;
+  h->near_end = std::min(mlmax, 2 * P0);
+  h->levels.clear();
+  for (int64_t P = P0; 2 * P < mlmax; P *= 2) {
+    Level lv;
+    lv.P = (int)P;
+    lv.lag0 = (int)(2 * P);
+    const bool last = P >= Pmax || 4 * P >= mlmax || (int)h->levels.size() == MAXLVL - 1;
+    lv.lag1 = last ? mlmax : (int)(4 * P);
+    const bool pow2 = (P & (P - 1)) == 0;
+    lv.spectral = spec_ok && pow2 && P >= (mode == GLE_FAR_SPECTRAL ? 2 : 8) && 2 * P <= 8192;
+    h->levels.push_back(lv);
+    if (last) break;
+  }
+  // device-memory check of the spectral levels (transformed kernels, segment rings, spectra)
+  {
     size_t need = 0;
-    for (auto& b : h->baths) {
-      if (b.ml <= L) continue;
-      const int M = (b.ml + L - 1) / L - 1;
-      need += (size_t)(L + 1) * 2 * b.nrt * b.nks * M * 64 * 8;
-      need += (size_t)(L + 1) * 2 * b.ncp * (2 * (M + 4) * B + 1024) * 8;
+    for (auto& lv : h->levels) {
+      if (!lv.spectral) continue;
+      for (auto& b : h->baths) {
+        if (b.ml <= lv.lag0) continue;
+        const int M = (std::min(lv.lag1, b.ml) + lv.P - 1) / lv.P - 2;
+        need += (size_t)(lv.P + 1) * 2 * b.nrt * b.nks * M * 64 * 8;
+        need += (size_t)(lv.P + 1) * 2 * b.ncp * (2 * (M + 4) * B + 1024) * 8;
+        need += (size_t)(lv.P + 1) * 2 * b.nc * B * 8;
+      }
     }
     size_t fr = 0, tot = 0;
     hipMemGetInfo(&fr, &tot);
     if (need > fr / 2) {
-      if (h->cfg.far_mode == GLE_FAR_SPECTRAL)
-        return fail(h, GLE_ERR_NOMEM, "spectral far field needs " + std::to_string(need >> 20) + " MiB");
-      mode = GLE_FAR_DIRECT;
+      if (mode == GLE_FAR_SPECTRAL)
+        return fail(h, GLE_ERR_NOMEM, "spectral levels need " + std::to_string(need >> 20) + " MiB");
+      for (auto& lv : h->levels) lv.spectral = false;
     }
   }
-  h->far_mode = mode;
-  // mid-level block: when the near field would otherwise sweep many kernel slices every step
-  if (h->cfg.mid_len > 0) h->P1 = h->cfg.mid_len < L ? h->cfg.mid_len : 0;
-  else if (h->cfg.mid_len < 0) h->P1 = 0;
-  else h->P1 = (L >= 16) ? 8 : 0;
-  // ring sizes and buffers that depend on L
+  h->far_mode = GLE_FAR_DIRECT;
+  int Pspec = 1, Ptop = P0;
+  for (auto& lv : h->levels) {
+    Ptop = std::max(Ptop, lv.P);
+    if (lv.spectral) {
+      h->far_mode = GLE_FAR_SPECTRAL;
+      Pspec = std::max(Pspec, lv.P);
+    }
+  }
+  h->L = Ptop;
+  const int rn_step = rn_for(B);
+  // history rings: ml + the background lookahead (a block may read p P+1 steps older than the
+  // newest slot the main stream writes while it runs) + slack
   for (auto& b : h->baths) {
-    b.R = b.ml + 3 * L + 2;
-    b.ldh = 2 * (int64_t)b.R * B + 512 + 16 * rn_for(L * B);
+    b.R = b.ml + 3 * Ptop + 2;
+    b.ldh = 2 * (int64_t)b.R * B + 512 + 16 * rn_for((int64_t)Ptop * B);
     int rc = dalloc_n(h, &b.d_H, (size_t)b.ncp * b.ldh + 4096);
     if (rc) return rc;
-    if (b.ml > L) {
-      rc = dalloc_n(h, &b.d_far, (size_t)b.ncp * L * B + 4096);
-      if (rc) return rc;
-    }
-    if (h->P1 && b.ml > h->P1) {
-      rc = dalloc_n(h, &b.d_mid, (size_t)b.ncp * h->P1 * B + 4096);
-      if (rc) return rc;
-    }
   }
-  if (mode == GLE_FAR_SPECTRAL) {
-    std::vector<double> cst((size_t)4 * L);
-    for (int q = 0; q < 2 * L; ++q) {
-      const long double a = 3.14159265358979323846264338327950288L * (long double)q / (long double)L;
+  if (h->far_mode == GLE_FAR_SPECTRAL) {
+    // twiddles cstab[q] = (cos(pi q / Pspec), sin(pi q / Pspec)), q < 2 Pspec
+    std::vector<double> cst((size_t)4 * Pspec);
+    for (int q = 0; q < 2 * Pspec; ++q) {
+      const long double a = 3.14159265358979323846264338327950288L * (long double)q / (long double)Pspec;
       cst[2 * q] = (double)cosl(a);
       cst[2 * q + 1] = (double)sinl(a);
     }
     int rc = dalloc_n(h, &h->d_cstab, cst.size());
     if (!rc) rc = upload(h, h->d_cstab, cst.data(), cst.size() * 8);
     if (rc) return rc;
-    for (auto& b : h->baths) {
-      if (b.ml <= L) continue;
-      b.M = (b.ml + L - 1) / L - 1;
-      b.nrt2 = b.nrt;
-      b.nks2 = b.nks;
-      b.Rseg = b.M + 4;
-      b.ldseg = 2 * (int64_t)b.Rseg * B + 1024;
-      b.khat_fstride = (int64_t)2 * b.nrt2 * b.nks2 * b.M * 64;  // Re block then Im block
-      b.seg_fstride = (int64_t)2 * b.ncp * b.ldseg;              // Re rows then Im rows
-      b.yfstride = (int64_t)2 * b.nc * B;
-      rc = dalloc_n(h, &b.d_khat, (size_t)(L + 1) * b.khat_fstride);
-      if (!rc) rc = dalloc_n(h, &b.d_seg, (size_t)(L + 1) * b.seg_fstride + 4096);
-      if (!rc) rc = dalloc_n(h, &b.d_Yspec, (size_t)(L + 1) * b.yfstride + 4096);
+  }
+  for (auto& lv : h->levels) {
+    lv.cstride = lv.spectral ? Pspec / lv.P : 1;
+    lv.lb.assign(h->baths.size(), LevelBath{});
+    for (size_t j = 0; j < h->baths.size(); ++j) {
+      Bath& b = h->baths[j];
+      LevelBath& L = lv.lb[j];
+      if (b.ml <= lv.lag0) continue;
+      L.active = true;
+      L.lag1 = std::min(lv.lag1, b.ml);
+      int rc = dalloc_n(h, &L.d_out, (size_t)b.ncp * 2 * lv.P * B + 4096);
       if (rc) return rc;
-      launch_khat_pack(b.d_K, b.ml, b.nks, b.d_khat, L, b.M, b.nc, b.nrt2, b.nks2, h->d_cstab, h->stream);
+      if (!lv.spectral) continue;
+      L.M = (L.lag1 + lv.P - 1) / lv.P - 2;
+      L.Rseg = L.M + 4;
+      L.ldseg = 2 * (int64_t)L.Rseg * B + 512;
+      L.khat_fstride = (int64_t)2 * b.nrt * b.nks * L.M * 64;  // Re block then Im block
+      L.seg_fstride = (int64_t)2 * b.ncp * L.ldseg;             // Re rows then Im rows
+      L.yfstride = (int64_t)2 * b.nc * B;
+      rc = dalloc_n(h, &L.d_khat, (size_t)(lv.P + 1) * L.khat_fstride);
+      if (!rc) rc = dalloc_n(h, &L.d_seg, (size_t)(lv.P + 1) * L.seg_fstride + 4096);
+      if (!rc) rc = dalloc_n(h, &L.d_Yspec, (size_t)(lv.P + 1) * L.yfstride + 4096);
+      if (rc) return rc;
+      launch_khat_pack(b.d_K, b.ml, b.nks, L.d_khat, lv.P, 2, L.M, b.nc, b.nrt, b.nks, h->d_cstab,
+                       lv.cstride, h->stream);
       HIPCHK(h, hipStreamSynchronize(h->stream));
     }
+    lv.sidx = lv.P <= 8 * P0 ? 0 : (lv.P <= 64 * P0 ? 1 : 2);
+    for (int q = 0; q < 2; ++q)
+      HIPCHK(h, hipEventCreateWithFlags(&lv.ev[q], hipEventDisableTiming | hipEventReleaseToDevice));
   }
   // StepDev
   StepDev sd{};
@@ -717,7 +778,7 @@ int freeze(gle_handle* h) {
   // kernel puts consecutive k-steps of one slice ml*512 B apart, so a per-step product touching
   // only a few slices would hit a new page (TLB miss) on nearly every fragment
   for (auto& b : h->baths) {
-    b.nn = std::max(1, std::min(b.ml, h->P1 ? h->P1 : L));
+    b.nn = std::max(1, std::min(b.ml, h->near_end));
     rc = dalloc_n(h, &b.d_Kn, (size_t)b.nrt * b.nks * b.nn * 64);
     if (rc) return rc;
     HIPCHK(h, hipMemcpy2DAsync(b.d_Kn, (size_t)b.nn * 64 * 8, b.d_K, (size_t)b.ml * 64 * 8,
@@ -749,71 +810,68 @@ int freeze(gle_handle* h) {
     g.ldd = ldd;
     return g;
   };
-  // FAR: slices [L, ml), windows ending at t+1..t+L
-  {
-    const int rnf = rn_for((int64_t)L * B);
-    Planner p(h, h->op_far, rnf);
-    for (auto& b : h->baths)
-      if (b.ml > L) {
-        Gemm g = kgemm(b, b.d_K, L, b.ml, b.d_H, b.ldh, b.R, 1, (int)(L * B), b.d_far, (int64_t)L * B);
-        g.force_reduce = true;
-        p.add(g, TGT_BIG, 16);
+  // LEVEL blocks.  Block k is computed with the step argument t = T = (k-1)P.
+  //   direct:   out[c] = sum_{i in [2P, lag1)} K_i p_{T+P+1+c/B-i}, c < P*B (targets T+P+1..T+2P),
+  //             one op per output parity (block buffer half k&1)
+  //   spectral: per frequency f, Y_f = sum_{m>=2} Khat_m(f) Xhat_{T/P+2-m}(f) on [[Re,-Im],[Im,Re]]
+  //             (the segment ring holds Xhat of the segments ending at sigma*P)
+  for (auto& lv : h->levels) {
+    if (lv.spectral) {
+      Op& op = lv.op[0];
+      op.cplx = true;
+      Planner p(h, op, rn_step);
+      int nprod = 0;
+      for (auto& L : lv.lb)
+        if (L.active) nprod += lv.P + 1;
+      for (size_t j = 0; j < h->baths.size(); ++j) {
+        Bath& b = h->baths[j];
+        LevelBath& L = lv.lb[j];
+        if (!L.active) continue;
+        for (int f = 0; f <= lv.P; ++f) {
+          Gemm g{};
+          g.cplx = true;
+          g.A = L.d_khat + (int64_t)f * L.khat_fstride;
+          g.a_ks = (int64_t)L.M * 64;
+          g.a_rt = (int64_t)b.nks * g.a_ks;
+          g.a_im = (int64_t)b.nrt * b.nks * L.M * 64;
+          g.nrt_total = b.nrt;
+          g.nks_total = b.nks;
+          g.i0 = 0;
+          g.i1 = L.M;
+          g.X = L.d_seg + (int64_t)f * L.seg_fstride;
+          g.x_im = (int64_t)b.ncp * L.ldseg;
+          g.ldx = L.ldseg;
+          g.ring = L.Rseg;
+          g.cs = (int)B;
+          g.tshift = 0;
+          g.tdiv = lv.P;
+          g.M = b.nc;
+          g.Kd = b.nc;
+          g.N = (int)B;
+          g.dst = L.d_Yspec + (int64_t)f * L.yfstride;
+          g.dst_im = (int64_t)b.nc * B;
+          g.ldd = B;
+          p.add(g, std::max(1, 1536 / std::max(1, nprod)), 16);
+        }
       }
-    rc = p.done();
-    if (rc) return rc;
-  }
-  // MID: lags [P1, min(L, ml)) for targets t+1..t+P1, every P1 steps
-  if (h->P1) {
-    const int P1 = h->P1;
-    Planner p(h, h->op_mid, rn_for((int64_t)P1 * B));
-    for (auto& b : h->baths)
-      if (b.ml > P1) {
-        Gemm g = kgemm(b, b.d_K, P1, std::min(b.ml, L), b.d_H, b.ldh, b.R, 1, (int)(P1 * B), b.d_mid,
-                       (int64_t)P1 * B);
-        g.force_reduce = true;
-        p.add(g, 512, 8);
-      }
-    rc = p.done();
-    if (rc) return rc;
-  }
-  // SPECTRAL: per frequency f, Y_f = sum_{m=1..M} Khat_m(f) Xhat_{T/P-m+1}(f) on [[Re,-Im],[Im,Re]]
-  if (h->far_mode == GLE_FAR_SPECTRAL) {
-    Planner p(h, h->op_spec, rn_step);
-    h->op_spec.cplx = true;
-    int nprod = 0;
-    for (auto& b : h->baths)
-      if (b.d_khat) nprod += L + 1;
-    for (auto& b : h->baths) {
-      if (!b.d_khat) continue;
-      for (int f = 0; f <= L; ++f) {
-        Gemm g{};
-        g.cplx = true;
-        g.A = b.d_khat + (int64_t)f * b.khat_fstride;
-        g.a_ks = (int64_t)b.M * 64;
-        g.a_rt = (int64_t)b.nks2 * g.a_ks;
-        g.a_im = (int64_t)b.nrt2 * b.nks2 * b.M * 64;
-        g.nrt_total = b.nrt2;
-        g.nks_total = b.nks2;
-        g.i0 = 0;
-        g.i1 = b.M;
-        g.X = b.d_seg + (int64_t)f * b.seg_fstride;
-        g.x_im = (int64_t)b.ncp * b.ldseg;
-        g.ldx = b.ldseg;
-        g.ring = b.Rseg;
-        g.cs = (int)B;
-        g.tshift = 0;
-        g.tdiv = L;
-        g.M = b.nc;
-        g.Kd = b.nc;
-        g.N = (int)B;
-        g.dst = b.d_Yspec + (int64_t)f * b.yfstride;
-        g.dst_im = (int64_t)b.nc * B;
-        g.ldd = B;
-        p.add(g, std::max(1, 1536 / std::max(1, nprod)), 16);
+      rc = p.done();
+      if (rc) return rc;
+    } else {
+      for (int par = 0; par < 2; ++par) {
+        Planner p(h, lv.op[par], rn_for((int64_t)lv.P * B));
+        for (size_t j = 0; j < h->baths.size(); ++j) {
+          Bath& b = h->baths[j];
+          LevelBath& L = lv.lb[j];
+          if (!L.active) continue;
+          Gemm g = kgemm(b, b.d_K, lv.lag0, L.lag1, b.d_H, b.ldh, b.R, lv.P + 1, (int)(lv.P * B),
+                         L.d_out + (int64_t)par * lv.P * B, (int64_t)2 * lv.P * B);
+          g.force_reduce = true;
+          p.add(g, TGT_BIG, 16);
+        }
+        rc = p.done();
+        if (rc) return rc;
       }
     }
-    rc = p.done();
-    if (rc) return rc;
   }
   // PRIME: S(t) = sum_{i>=1} K_i p_{t-i} from the current history (after set_state/history)
   {
@@ -863,7 +921,8 @@ int freeze(gle_handle* h) {
         p.add(g, TGT_STEP, 4);
       }
       p.lat = true;
-      for (auto& b : h->baths) {
+      for (size_t j = 0; j < h->baths.size(); ++j) {
+        Bath& b = h->baths[j];
         if (b.ml <= 1) continue;
         Gemm g{};
         g.A = b.d_Kn;
@@ -872,8 +931,7 @@ int freeze(gle_handle* h) {
         g.nrt_total = b.nrt;
         g.nks_total = b.nks;
         g.i0 = 1;
-        // no near slices: the reduce copies far(t+1) (+ mid(t+1))
-        g.i1 = std::max(1, std::min(b.ml, h->P1 ? h->P1 : L));
+        g.i1 = b.nn;  // near field lags [1, near_end); none: the levels' sum only
         g.X = b.d_H;
         g.ldx = b.ldh;
         g.ring = b.R;
@@ -884,15 +942,11 @@ int freeze(gle_handle* h) {
         g.N = (int)B;
         g.dst = b.d_S + (int64_t)par * b.ncp * B;
         g.ldd = B;
-        if (b.ml > L) {
-          g.add = b.d_far;
-          g.lda = (int64_t)L * B;
-          g.add_cs = (int)B;
-        }
-        if (b.d_mid) {
-          g.add2 = b.d_mid;
-          g.lda2 = (int64_t)h->P1 * B;
-          g.add2_cs = (int)B;
+        g.nadd = (int)h->levels.size();
+        for (size_t l = 0; l < h->levels.size(); ++l) {
+          const LevelBath& L = h->levels[l].lb[j];
+          g.adds[l] = L.active ? L.d_out : nullptr;
+          g.add_ld[l] = 2 * h->levels[l].P * (int32_t)B;
         }
         g.force_reduce = true;
         p.add(g, 256, 4);
@@ -940,20 +994,61 @@ int freeze(gle_handle* h) {
   return GLE_OK;
 }
 
+// Block k of level lv on stream s.  Spectral: the newest segment spectrum is transformed first
+// (all M the block reads when priming).
+int launch_level_block(gle_handle* h, Level& lv, int64_t k, hipStream_t s, bool priming) {
+  const int64_t T = (k - 1) * (int64_t)lv.P;
+  const StepArgs ta = step_args(h, T);
+  const int par = (int)(k & 1);
+  if (lv.spectral) {
+    for (size_t j = 0; j < h->baths.size(); ++j) {
+      Bath& b = h->baths[j];
+      LevelBath& L = lv.lb[j];
+      if (!L.active) continue;
+      if (launch_seg_fft(b.d_H, b.ldh, b.R, (int)h->B, b.nc, b.ncp, lv.P, T, priming ? L.M : 1, L.d_seg,
+                         L.seg_fstride, L.ldseg, L.Rseg, h->d_cstab, lv.cstride, s))
+        return fail(h, GLE_ERR_UNSUP, "segment transform launch failed (P = " + std::to_string(lv.P) + ")");
+    }
+    run_op(h, lv.op[0], s, ta, true);
+    for (size_t j = 0; j < h->baths.size(); ++j) {
+      Bath& b = h->baths[j];
+      LevelBath& L = lv.lb[j];
+      if (!L.active) continue;
+      if (launch_far_ifft(L.d_Yspec, L.yfstride, b.nc, (int)h->B, lv.P, L.d_out + (int64_t)par * lv.P * h->B,
+                          (int64_t)2 * lv.P * h->B, h->d_cstab, lv.cstride, s))
+        return fail(h, GLE_ERR_UNSUP, "inverse transform launch failed (P = " + std::to_string(lv.P) + ")");
+    }
+  } else {
+    run_op(h, lv.op[par], s, ta, true);
+  }
+  HIPCHK(h, hipEventRecord(lv.ev[par], s));
+  return GLE_OK;
+}
+
+// After set_state / set_history: S(t) from the whole history, and the two level blocks that cover
+// targets t+1 .. (the next block boundary) + P, all on the main stream.
 int prime(gle_handle* h) {
+  join_bg(h);  // blocks still in flight read the ring and write the buffers recomputed here
+  const StepArgs ta = step_args(h);
   // S(t) into S[t&1]: the prime op writes S[0]; copy when t is odd
   if (!h->op_prime.empty()) {
-    run_op(h, h->op_prime, 0, false);
+    run_op(h, h->op_prime, h->stream, ta, false);
     if (h->t & 1)
       for (auto& b : h->baths)
         if (b.ml > 1)
           HIPCHK(h, hipMemcpyAsync(b.d_S + (int64_t)b.ncp * h->B, b.d_S, (size_t)b.ncp * h->B * 8,
                                    hipMemcpyDeviceToDevice, h->stream));
   }
+  for (auto& lv : h->levels) {
+    const int64_t k0 = floordiv(h->t, lv.P);
+    int rc = launch_level_block(h, lv, k0, h->stream, true);
+    if (!rc) rc = launch_level_block(h, lv, k0 + 1, h->stream, false);
+    if (rc) return rc;
+    lv.last_block = k0 + 1;
+    lv.bg_block[0] = lv.bg_block[1] = INT64_MIN;
+  }
+  if (!h->levels.empty()) HIPCHK(h, hipEventRecord(h->ev_step, h->stream));
   h->need_prime = false;
-  h->far_due = true;
-  h->mid_due = true;
-  h->seg_ready = false;
   return GLE_OK;
 }
 
@@ -961,74 +1056,67 @@ int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
   if (!h->state_set) return fail(h, GLE_ERR_STATE, "gle_set_state has not been called");
   for (size_t j = 0; j < h->baths.size(); ++j)
     if (!h->baths[j].noise_set) return fail(h, GLE_ERR_STATE, "bath " + std::to_string(j) + " has no noise");
+  if (fpot_host_T == nullptr && !h->has_dyn)
+    return fail(h, GLE_ERR_STATE, "no potential force: pass fpot or call gle_set_dyn (md.py:468-470)");
   int rc = 0;
   if (h->need_prime) {
     rc = prime(h);
     if (rc) return rc;
   }
-  if (h->far_due) {
-    const int L = h->L;
-    if (h->far_mode == GLE_FAR_SPECTRAL && h->t % L == 0 && !h->op_spec.items.empty()) {
-      for (auto& b : h->baths)
-        if (b.d_khat)
-          launch_seg_fft(b.d_H, b.ldh, b.R, (int)h->B, b.nc, L, h->t, h->seg_ready ? 1 : b.M, b.d_seg,
-                         b.seg_fstride, b.ldseg, b.Rseg, h->d_cstab, h->stream);
-      h->seg_ready = true;
-      run_op(h, h->op_spec, 0, true);
-      for (auto& b : h->baths)
-        if (b.d_khat)
-          launch_far_ifft(b.d_Yspec, b.yfstride, b.nc, (int)h->B, L, b.d_far, (int64_t)L * h->B,
-                          h->d_cstab, h->stream);
-      h->t_far = h->t;
-    } else if (!h->op_far.items.empty()) {
-      // direct block (every L steps in direct mode; the partial block before the first aligned
-      // spectral block otherwise)
-      run_op(h, h->op_far, 1, h->far_mode != GLE_FAR_SPECTRAL);
-      h->t_far = h->t;
+  const int64_t t = h->t;
+  // ladder: at each block boundary T = kP, start block k+1 (targets T+P+1..T+2P, data up to T) on
+  // the level's background stream once step T-1 has closed; consume block k from this step on
+  bool bg_waited[gle_handle::NBG] = {};
+  for (auto& lv : h->levels) {
+    if (t % lv.P != 0) continue;
+    const int64_t k = t / lv.P;
+    if (k + 1 > lv.last_block) {
+      hipStream_t bs = h->bg[lv.sidx];
+      if (!bg_waited[lv.sidx]) {
+        HIPCHK(h, hipStreamWaitEvent(bs, h->ev_step, 0));
+        bg_waited[lv.sidx] = true;
+      }
+      rc = launch_level_block(h, lv, k + 1, bs, false);
+      if (rc) return rc;
+      lv.last_block = k + 1;
+      lv.bg_block[(k + 1) & 1] = k + 1;
     }
-    h->far_due = false;
-    h->steps_since_far = 0;
-  }
-  if (h->mid_due) {
-    if (!h->op_mid.items.empty()) run_op(h, h->op_mid, 2, false);
-    h->t_mid = h->t;
-    h->mid_due = false;
+    if (lv.bg_block[k & 1] == k) {
+      HIPCHK(h, hipStreamWaitEvent(h->stream, lv.ev[k & 1], 0));
+      lv.bg_block[k & 1] = INT64_MIN;
+    }
   }
   const bool need_pot = (fpot_host_T == nullptr) && !h->pot_cache_exact;
-  if (fpot_host_T == nullptr && !h->has_dyn)
-    return fail(h, GLE_ERR_STATE, "no potential force: pass fpot or call gle_set_dyn (md.py:468-470)");
-  const int par = (int)((h->t + 1) & 1);
+  const int par = (int)((t + 1) & 1);
+  const StepArgs ta = step_args(h);
   Op& op0 = need_pot ? h->op0p[par] : h->op0[par];
-  run_op(h, op0, 0, h->op_far.items.empty() && h->op_spec.items.empty());
+  run_op(h, op0, h->stream, ta, h->levels.empty());
   if (fpot_host_T)
     HIPCHK(h, hipMemcpyAsync(h->d_Fc, fpot_host_T, (size_t)h->nph * h->B * 8, hipMemcpyHostToDevice, h->stream));
-  launch_phaseA(h->d_sd, step_args(h), (int)h->B, h->ndblk, need_pot ? 1 : 0, fpot_host_T ? 0 : 1, h->stream);
+  launch_phaseA(h->d_sd, ta, (int)h->B, h->ndblk, need_pot ? 1 : 0, fpot_host_T ? 0 : 1, h->stream);
   h->host_force_step = fpot_host_T != nullptr;
   return GLE_OK;
 }
 
 int step_end_impl(gle_handle* h, const double* fpot_host_T) {
   int mode1 = 1;
+  const StepArgs ta = step_args(h);
   if (fpot_host_T) {
-    run_op(h, h->op1a_np, 0, false);
+    run_op(h, h->op1a_np, h->stream, ta, false);
     HIPCHK(h, hipMemcpyAsync(h->d_Fc, fpot_host_T, (size_t)h->nph * h->B * 8, hipMemcpyHostToDevice, h->stream));
     mode1 = 0;
   } else {
     if (!h->has_dyn) return fail(h, GLE_ERR_STATE, "no potential force at q~");
     if (h->host_force_step) return fail(h, GLE_ERR_STATE, "step begun with a host force must end with one");
-    run_op(h, h->op1a, 0, false);
+    run_op(h, h->op1a, h->stream, ta, false);
   }
-  launch_phaseB(h->d_sd, step_args(h), (int)h->B, h->ndblk, mode1, h->stream);
-  run_op(h, h->op1b, 0, false);
-  launch_phaseC(h->d_sd, step_args(h), (int)h->B, h->ndblk, mode1, mode1, h->stream);
+  launch_phaseB(h->d_sd, ta, (int)h->B, h->ndblk, mode1, h->stream);
+  run_op(h, h->op1b, h->stream, ta, false);
+  launch_phaseC(h->d_sd, ta, (int)h->B, h->ndblk, mode1, mode1, h->stream);
+  // the next step is a block boundary: the background blocks started there wait for this step
+  if (!h->levels.empty() && (h->t + 1) % h->P0 == 0) HIPCHK(h, hipEventRecord(h->ev_step, h->stream));
   h->t += 1;
   h->pot_cache_exact = (fpot_host_T == nullptr) && h->constr.empty();
-  if (h->P1 && h->t % h->P1 == 0) h->mid_due = true;
-  if (h->far_mode == GLE_FAR_SPECTRAL) {
-    if (h->t % h->L == 0) h->far_due = true;
-  } else if (++h->steps_since_far >= h->L) {
-    h->far_due = true;
-  }
   HIPCHK(h, hipGetLastError());
   return GLE_OK;
 }
@@ -1082,7 +1170,7 @@ int gle_create(const gle_config* cfg, gle_handle** out) {
   if (cfg->nmd % 2) return fail(nullptr, GLE_ERR_ARG, "nmd must be even (functions.py:47-50 length check)");
   if (cfg->far_mode < GLE_FAR_AUTO || cfg->far_mode > GLE_FAR_SPECTRAL) return fail(nullptr, GLE_ERR_ARG, "bad far_mode");
   if (cfg->block_len < 0 || cfg->block_len > 4096) return fail(nullptr, GLE_ERR_ARG, "bad block_len");
-  if (cfg->mid_len < -1 || cfg->mid_len > 4096) return fail(nullptr, GLE_ERR_ARG, "bad mid_len");
+  if (cfg->max_block < 0 || cfg->max_block > 4096) return fail(nullptr, GLE_ERR_ARG, "bad max_block");
   if (cfg->nph > (1 << 24) || cfg->ntraj > (1 << 20)) return fail(nullptr, GLE_ERR_UNSUP, "size too large");
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
@@ -1098,10 +1186,22 @@ int gle_create(const gle_config* cfg, gle_handle** out) {
   h->nmd = cfg->nmd;
   h->dt = cfg->dt;
   h->nphp = rup(h->nph, 8);
-  e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+  // main stream (the latency-bound per-step chain) at the highest priority, background streams
+  // (ladder blocks) at the lowest
+  {
+    int lo = 0, hi = 0;
+    hipDeviceGetStreamPriorityRange(&lo, &hi);
+    e = hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, hi);
+    for (int i = 0; i < gle_handle::NBG && e == hipSuccess; ++i) {
+      e = hipStreamCreateWithPriority(&h->bg[i], hipStreamNonBlocking, lo);
+      if (e == hipSuccess)
+        e = hipEventCreateWithFlags(&h->ev_bg[i], hipEventDisableTiming | hipEventReleaseToDevice);
+    }
+  }
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_step, hipEventDisableTiming | hipEventReleaseToDevice);
   if (e != hipSuccess) {
-    delete h;
-    return fail(nullptr, GLE_ERR_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+    gle_destroy(h);
+    return fail(nullptr, GLE_ERR_HIP, std::string("stream/event creation: ") + hipGetErrorString(e));
   }
   const size_t nst = (size_t)(h->nphp + 64) * h->B + 1024;  // row slack for static windows
   int rc = 0;
@@ -1143,9 +1243,19 @@ int gle_create(const gle_config* cfg, gle_handle** out) {
 int gle_destroy(gle_handle* h) {
   if (!h) return GLE_OK;
   hipSetDevice(h->cfg.device);
+  for (int i = 0; i < gle_handle::NBG; ++i)
+    if (h->bg[i]) hipStreamSynchronize(h->bg[i]);
   if (h->stream) hipStreamSynchronize(h->stream);
   for (void* p : h->allocs) hipFree(p);
   for (auto e : h->ev) hipEventDestroy(e);
+  for (auto& lv : h->levels)
+    for (auto e : lv.ev)
+      if (e) hipEventDestroy(e);
+  if (h->ev_step) hipEventDestroy(h->ev_step);
+  for (int i = 0; i < gle_handle::NBG; ++i) {
+    if (h->ev_bg[i]) hipEventDestroy(h->ev_bg[i]);
+    if (h->bg[i]) hipStreamDestroy(h->bg[i]);
+  }
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;
   return GLE_OK;
@@ -1256,6 +1366,8 @@ int gle_set_state(gle_handle* h, const double* p, const double* q, int64_t t) {
   hipSetDevice(h->cfg.device);
   int rc = freeze(h);
   if (rc) return rc;
+  rc = sync_bg(h);  // background blocks read the ring rewritten here
+  if (rc) return rc;
   const int64_t B = h->B, n = h->nph;
   std::vector<double> tp, tq;
   to_dev_layout(p, tp, B, n, n);
@@ -1264,8 +1376,6 @@ int gle_set_state(gle_handle* h, const double* p, const double* q, int64_t t) {
   if (!rc) rc = upload(h, h->d_Q, tq.data(), tq.size() * 8);
   if (rc) return rc;
   h->t = t;
-  h->t_far = t;
-  h->t_mid = t;
   HIPCHK(h, hipMemsetAsync(h->d_qvalid, 0, (size_t)B * 4, h->stream));
   HIPCHK(h, hipMemsetAsync(h->d_pmax, 0, (size_t)B * 4 * 8, h->stream));
   // p_t into the history ring slot of t; q_t into the q gather
@@ -1315,6 +1425,8 @@ int gle_set_history(gle_handle* h, int32_t bath, const double* phis) {
   if (rc) return rc;
   if (!h->state_set) return fail(h, GLE_ERR_STATE, "call gle_set_state first (history slots are relative to t)");
   hipSetDevice(h->cfg.device);
+  rc = sync_bg(h);  // background blocks read the ring rewritten here
+  if (rc) return rc;
   Bath& b = h->baths[bath];
   const int64_t B = h->B;
   // phis[i] (newest first) is p at time t-1-i (md.phis between steps, md.py:386-387)
@@ -1571,6 +1683,8 @@ int gle_run(gle_handle* h, int64_t nsteps) {
 int gle_sync(gle_handle* h) {
   if (!h) return GLE_ERR_ARG;
   hipSetDevice(h->cfg.device);
+  int rc = sync_bg(h);
+  if (rc) return rc;
   HIPCHK(h, hipStreamSynchronize(h->stream));
   HIPCHK(h, hipGetLastError());
   return GLE_OK;
@@ -1643,13 +1757,8 @@ int gle_profile(gle_handle* h, int32_t enable) {
 int gle_profile_read(gle_handle* h, int64_t* nlaunch, double* total_ms, double* flops, double* bytes) {
   if (!h) return GLE_ERR_ARG;
   hipSetDevice(h->cfg.device);
-  HIPCHK(h, hipStreamSynchronize(h->stream));
-  for (size_t i = 0; i + 1 < h->ev_used; i += 2) {
-    float ms = 0;
-    HIPCHK(h, hipEventElapsedTime(&ms, h->ev[i], h->ev[i + 1]));
-    h->prof_ms += ms;
-  }
-  h->ev_used = 0;
+  drain_profile(h);
+  HIPCHK(h, hipGetLastError());
   if (nlaunch) *nlaunch = h->prof_n;
   if (total_ms) *total_ms = h->prof_ms;
   if (flops) *flops = h->prof_flops;
@@ -1660,9 +1769,11 @@ int gle_profile_read(gle_handle* h, int64_t* nlaunch, double* total_ms, double* 
 int gle_plan_info(gle_handle* h, int64_t* block_len, int64_t* far_items, int64_t* device_bytes,
                   int32_t* far_mode) {
   if (!h) return GLE_ERR_ARG;
-  if (block_len) *block_len = h->frozen ? h->L : 0;
+  int64_t items = 0;
+  for (auto& lv : h->levels) items += (int64_t)lv.op[0].items.size();
+  if (block_len) *block_len = h->frozen ? h->P0 : 0;
   if (far_mode) *far_mode = h->frozen ? h->far_mode : h->cfg.far_mode;
-  if (far_items) *far_items = (int64_t)(h->far_mode == GLE_FAR_SPECTRAL ? h->op_spec.items.size() : h->op_far.items.size());
+  if (far_items) *far_items = items;
   if (device_bytes) *device_bytes = (int64_t)h->dev_bytes;
   return GLE_OK;
 }

@@ -22,6 +22,7 @@ constexpr int KROWS = 4 * KC;      // 8 staged X rows
 constexpr int LDS_COLS = 1000;     // padded staged row length (doubles): 8*1000*8 = 62.5 KB
 constexpr int LDS_WW_MAX = 960;    // usable window width: roundup32(960) + 16 <= LDS_COLS
 constexpr int MAXBATH = 8;
+constexpr int MAXLVL = 12;         // levels of the memory-sum ladder
 constexpr int CPLX_WW_CAP = 512;   // contract_cplx_kernel window (doubles per staged row)
 constexpr int ROWS_PER_WG = 64;    // 4 waves x 16 rows
 
@@ -61,11 +62,13 @@ struct TItem {
   const double* A;     // fragment base for (row tile, k-step 0, slice ia)
   const double* X;     // X base (row 0)
   double* out;         // tile output (row 0 of the tile, column 0)
-  const double* add;   // far-field addend (column offset (t - t_far) * add_cs) or nullptr
-  const double* add2;  // mid-level addend (column offset (t - t_mid) * add2_cs) or nullptr
+  const double* add[MAXLVL];  // level block buffers (row 0 of the tile; the step's column
+                              // offset is StepArgs::lvl_off), first nadd used
   int64_t a_ks;        // doubles between k-steps in A (slice stride is 64)
   int64_t ldx;
-  int32_t ldo, lda, lda2, add_cs, add2_cs;
+  int32_t add_ld[MAXLVL];
+  int32_t nadd;
+  int32_t ldo;
   int32_t ia, ni, nks; // slices [ia, ia+ni), k-steps
   int32_t ring, cs, tshift;
   int32_t nrows, ncols;
@@ -76,18 +79,12 @@ struct TItem {
 struct RItem {
   double* dst;
   const double* src;   // first partial slot
-  const double* add;   // far-field buffer or nullptr
   int32_t ldd;         // dst row stride
   int32_t lds;         // partial row stride
-  int32_t lda;         // add row stride
   int32_t nslots;
+  int32_t pad;
   int64_t slot_stride; // doubles between partial slots
   int32_t rows, cols;
-  int32_t add_cs;      // add column offset = (t - t_far) * add_cs
-  int32_t pad;
-  const double* add2;  // mid-level block buffer or nullptr, column offset (t - t_mid) * add2_cs
-  int32_t lda2;
-  int32_t add2_cs;
 };
 
 
@@ -127,9 +124,8 @@ struct StepDev {
 // Every kernel takes the step counter by value: the host knows md.t and the steps at which the
 // current far / mid blocks were computed, so no kernel starts with a dependent load of a clock
 struct StepArgs {
-  int64_t t;      // md.t of this step
-  int64_t t_far;  // step of the current far-field block
-  int64_t t_mid;  // step of the current mid-level block
+  int64_t t;                 // md.t of this step
+  int64_t lvl_off[MAXLVL];   // per level: offset (doubles) of target t+1 in its block buffer
 };
 void launch_contract(int rn, int cu, const CItem* items, int nitems, StepArgs ta, hipStream_t s);
 void launch_reduce(const RItem* items, int nitems, int max_elems, StepArgs ta,
@@ -146,13 +142,13 @@ void launch_ring_copy(double* H, int64_t ldh, int R, int B, int nc, int64_t tau0
                       int dir, hipStream_t s);
 void launch_tile(int rn, const TItem* items, int nitems, StepArgs ta, hipStream_t s);
 void launch_contract_cplx(int rn, const CItem* items, int nitems, StepArgs ta, hipStream_t s);
-void launch_khat_pack(const double* Kf, int ml, int nks_k, double* khat, int P, int M, int nc,
-                      int nrt2, int nks2, const double* cstab, hipStream_t s);
-void launch_seg_fft(const double* H, int64_t ldh, int R, int B, int nc, int P, int64_t T, int nseg,
-                    double* seg, int64_t seg_fstride, int64_t ldseg, int Rseg, const double* cstab,
-                    hipStream_t s);
-void launch_far_ifft(const double* Y, int64_t yfstride, int nc, int B, int P, double* far,
-                     int64_t ldfar, const double* cstab, hipStream_t s);
+void launch_khat_pack(const double* Kf, int ml, int nks_k, double* khat, int P, int m0, int M,
+                      int nc, int nrt2, int nks2, const double* cstab, int cstride, hipStream_t s);
+int launch_seg_fft(const double* H, int64_t ldh, int R, int B, int nc, int ncp, int P, int64_t T,
+                   int nseg, double* seg, int64_t seg_fstride, int64_t ldseg, int Rseg,
+                   const double* cstab, int cstride, hipStream_t s);
+int launch_far_ifft(const double* Y, int64_t yfstride, int nc, int B, int P, double* out,
+                    int64_t ldout, const double* cstab, int cstride, hipStream_t s);
 int launch_fft_noise(const double* a, double* noise, const double* tw, int64_t nmd, int64_t nc,
                      int64_t arows, int64_t B, int is_complex, double scale, hipStream_t s);
 

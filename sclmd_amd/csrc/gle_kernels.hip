@@ -342,25 +342,11 @@ __global__ __launch_bounds__(TILE_NW * 64) void tile_kernel(const TItem* __restr
                                                             StepArgs ta) {
   __shared__ double red[(TILE_NW / 2) * 256 * RN];
   __shared__ unsigned last;
-  const TItem it = items[blockIdx.x];
+  const TItem& it = items[blockIdx.x];  // read in place: the addend arrays are indexed dynamically
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const int brow = lane >> 4, bcol = lane & 15;
   const int64_t t = ta.t;
-  // epilogue addends (far + mid field) for this thread's output elements, fetched up front
-  double pre[RN];
-#pragma unroll
-  for (int j = 0; j < RN; ++j) {
-    const int e = j * TILE_NW * 64 + threadIdx.x;  // element (n*4+q)*64 + lane'
-    const int nq = e >> 6, ln = e & 63;
-    const int row = (ln >> 4) + 4 * (nq & 3), col = 16 * (nq >> 2) + (ln & 15);
-    double v = 0.0;
-    if (row < it.nrows && col < it.ncols) {
-      if (it.add) v = gld(it.add + (t - ta.t_far) * it.add_cs + (int64_t)row * it.lda + col);
-      if (it.add2) v += gld(it.add2 + (t - ta.t_mid) * it.add2_cs + (int64_t)row * it.lda2 + col);
-    }
-    pre[j] = v;
-  }
   d4 acc[RN];
 #pragma unroll
   for (int n = 0; n < RN; ++n) acc[n] = d4{0.0, 0.0, 0.0, 0.0};
@@ -446,6 +432,31 @@ __global__ __launch_bounds__(TILE_NW * 64) void tile_kernel(const TItem* __restr
     __syncthreads();
     if (!last) return;
   }
+  // epilogue addends: the ladder levels' blocks at target t+1 (all loads issued together)
+  double pre[RN];
+  {
+    double av[MAXLVL][RN];
+#pragma unroll
+    for (int a = 0; a < MAXLVL; ++a) {
+      const double* ap = a < it.nadd ? it.add[a] : nullptr;
+      const int64_t off = ap ? ta.lvl_off[a] : 0;
+      const int ld = it.add_ld[a];
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        const int e = j * TILE_NW * 64 + threadIdx.x;  // element (n*4+q)*64 + lane'
+        const int nq = e >> 6, ln = e & 63;
+        const int row = (ln >> 4) + 4 * (nq & 3), col = 16 * (nq >> 2) + (ln & 15);
+        av[a][j] = (ap && row < it.nrows && col < it.ncols) ? gld(ap + off + (int64_t)row * ld + col) : 0.0;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      double v = 0.0;
+#pragma unroll
+      for (int a = 0; a < MAXLVL; ++a) v += av[a][j];
+      pre[j] = v;
+    }
+  }
 #pragma unroll
   for (int j = 0; j < RN; ++j) {
     const int e = j * TILE_NW * 64 + threadIdx.x;
@@ -527,18 +538,12 @@ __global__ __launch_bounds__(256) void reduce_kernel(const RItem* __restrict__ i
   const RItem it = items[blockIdx.x];
   const int n = it.rows * it.cols;
   const int e0 = blockIdx.y * RED_PER_BLOCK;
-  const int64_t t = ta.t;
+  (void)ta;
   if (e0 >= n) return;
-  const double* add = nullptr;
-  const double* add2 = nullptr;
-  if (it.add) add = it.add + (t - ta.t_far) * it.add_cs;
-  if (it.add2) add2 = it.add2 + (t - ta.t_mid) * it.add2_cs;
   for (int e = e0 + threadIdx.x; e < min(n, e0 + RED_PER_BLOCK); e += blockDim.x) {
     const int r = e / it.cols;
     const int c = e - r * it.cols;
-    double s0 = add ? add[(int64_t)r * it.lda + c] : 0.0;
-    if (add2) s0 += add2[(int64_t)r * it.lda2 + c];
-    it.dst[(int64_t)r * it.ldd + c] = sum_slots(s0, it.src + (int64_t)r * it.lds + c, it.slot_stride, it.nslots);
+    it.dst[(int64_t)r * it.ldd + c] = sum_slots(0.0, it.src + (int64_t)r * it.lds + c, it.slot_stride, it.nslots);
   }
 }
 
@@ -1010,16 +1015,17 @@ void launch_ring_copy(double* H, int64_t ldh, int R, int B, int nc, int64_t tau0
 namespace gle {
 
 // ------------------------------------------------------------------------------------------
-// Spectral (overlap-save) far field.  cstab[q] = (cos(pi q / P), sin(pi q / P)), q < 2P.
+// Spectral (overlap-save) levels.  A level of block length P covers the lags of partitions
+// m in [m0, m0 + M): k_m[i'] = K_{mP+i'} (i' < P, zero-padded to N = 2P).  Twiddles:
+// cstab[q] = (cos(pi q / Pmax), sin(pi q / Pmax)), q < 2 Pmax; a level reads it with stride
+// Pmax / P, so e^{-i pi f n / P} = (cs.x, -cs.y) at q = ((f n) mod 2P) * stride.
 //
-// Kernel partitions k_m[i'] = K_{mP+i'} (i' < P, zero-padded to 2P), m = 1..M, transformed:
-//   Khat_m(f) = sum_i' k_m[i'] e^{-i pi f i'/P}, f = 0..P.
-// Packed as the real block [[Re, -Im], [Im, Re]] (2nc x 2nc) in fragment-native order
-// [f][rt][ks][m-1][64], read straight out of the fragment-native K already on the device.
+//   Khat_m(f) = sum_i' k_m[i'] e^{-i pi f i'/P}, f = 0..P, packed as the real block
+//   [[Re, -Im], [Im, Re]] (2nc x 2nc) in fragment-native order [f][part][rt][ks][m-m0][64], read
+//   straight out of the fragment-native K already on the device (one-time setup).
 __global__ void khat_pack_kernel(const double* __restrict__ Kf, int ml, int nks_k,
-                                 double* __restrict__ khat, int P, int M, int nc, int nrt2, int nks2,
-                                 const double2* __restrict__ cstab) {
-  // layout [f][part (0 = Re, 1 = Im)][rt][ks][m-1][64] over the nc x nc bath block
+                                 double* __restrict__ khat, int P, int m0, int M, int nc, int nrt2,
+                                 int nks2, const double2* __restrict__ cstab, int cstride) {
   const int64_t total = (int64_t)(P + 1) * 2 * nrt2 * nks2 * M * 64;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
@@ -1038,12 +1044,12 @@ __global__ void khat_pack_kernel(const double* __restrict__ Kf, int ml, int nks_
     double v = 0.0;
     if (r < nc && k < nc) {
       const int64_t base = (((int64_t)(r >> 4) * nks_k + (k >> 2)) * ml) * 64 + (r & 15) + 16 * (k & 3);
-      const int m = mm + 1;
+      const int m = mm + m0;
       for (int ip = 0; ip < P; ++ip) {
         const int i = m * P + ip;
         if (i >= ml) break;
         const double kv = Kf[base + (int64_t)i * 64];
-        const double2 cs = cstab[(f * ip) % (2 * P)];
+        const double2 cs = cstab[((f * ip) % (2 * P)) * cstride];
         v += part ? -kv * cs.y : kv * cs.x;
       }
     }
@@ -1051,91 +1057,188 @@ __global__ void khat_pack_kernel(const double* __restrict__ Kf, int ml, int nks_
   }
 }
 
-void launch_khat_pack(const double* Kf, int ml, int nks_k, double* khat, int P, int M, int nc,
-                      int nrt2, int nks2, const double* cstab, hipStream_t s) {
-  khat_pack_kernel<<<8192, 256, 0, s>>>(Kf, ml, nks_k, khat, P, M, nc, nrt2, nks2,
-                                        (const double2*)cstab);
+void launch_khat_pack(const double* Kf, int ml, int nks_k, double* khat, int P, int m0, int M,
+                      int nc, int nrt2, int nks2, const double* cstab, int cstride, hipStream_t s) {
+  khat_pack_kernel<<<8192, 256, 0, s>>>(Kf, ml, nks_k, khat, P, m0, M, nc, nrt2, nks2,
+                                        (const double2*)cstab, cstride);
 }
 
-// Segment spectra for the nseg newest segments (sigma = T/P - s): x[n] = p at time
-// sigma*P - 2P + 2 + n (n < 2P-1), x[2P-1] = 0; Xhat(f) = sum_n x[n] e^{-i pi f n/P} written as rows
-// [k] = Re and [nc+k] = Im of the frequency-f segment ring (mirrored slots).
-__global__ void seg_fft_kernel(const double* __restrict__ H, int64_t ldh, int R, int B, int nc,
-                               int P, int64_t T, int nseg, double* __restrict__ seg,
-                               int64_t seg_fstride, int64_t ldseg, int Rseg,
-                               const double2* __restrict__ cstab) {
-  const int64_t total = (int64_t)nseg * (P + 1) * nc * B;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int b = (int)(e % B);
-    int64_t r_ = e / B;
-    const int k = (int)(r_ % nc);
-    r_ /= nc;
-    const int f = (int)(r_ % (P + 1));
-    const int sidx = (int)(r_ / (P + 1));
-    const int64_t sigma = T / P - sidx;
-    const int64_t t0 = sigma * P - 2 * P + 2;
-    const double* hk = H + (int64_t)k * ldh + b;
-    double re = 0.0, im = 0.0;
-    for (int n = 0; n < 2 * P - 1; ++n) {
-      const double x = hk[pmod(t0 + n, R) * B];
-      const double2 cs = cstab[(f * n) % (2 * P)];
-      re += x * cs.x;
-      im -= x * cs.y;
+// In-place radix-2 FFT of NS complex series of length N = 2^logn held bit-reversed in LDS
+// (buf[s * N + i]); sign -1 = forward, +1 = inverse (unscaled).
+template <int NS>
+__device__ __forceinline__ void lds_fft(double2* buf, int logn, const double2* __restrict__ cstab,
+                                        int cstride_n, double sign) {
+  const int N = 1 << logn, h = N >> 1;
+  for (int st = 1; st <= logn; ++st) {
+    const int half = 1 << (st - 1);
+    const int tstride = (N >> st) * cstride_n;  // twiddle e^{-2 pi i jj / 2^st} = table[jj * (N/2^st) * 2 * stride / 2]
+    for (int j = threadIdx.x; j < NS * h; j += blockDim.x) {
+      const int sidx = j / h, jb = j - sidx * h;
+      const int g = jb >> (st - 1);
+      const int jj = jb & (half - 1);
+      double2* bs = buf + sidx * N;
+      const int i0 = (g << st) + jj;
+      const int i1 = i0 + half;
+      const double2 c = cstab[jj * tstride];
+      const double wx = c.x, wy = sign * c.y;  // e^{sign i 2 pi jj / 2^st}
+      const double2 x0 = bs[i0];
+      const double2 x1 = bs[i1];
+      const double2 y = make_double2(x1.x * wx - x1.y * wy, x1.x * wy + x1.y * wx);
+      bs[i0] = make_double2(x0.x + y.x, x0.y + y.y);
+      bs[i1] = make_double2(x0.x - y.x, x0.y - y.y);
     }
-    const int64_t slot = pmod(sigma, Rseg);
+    __syncthreads();
+  }
+}
+
+// Segment spectra of the nseg newest segments sigma = T/P - sidx (grid: sidx x DOF k x 8-trajectory
+// chunk): x[n] = p at time sigma*P - 2P + 2 + n (n < 2P-1), x[2P-1] = 0;
+// Xhat(f) = sum_n x[n] e^{-i pi f n / P}, f = 0..P, written as rows [k] = Re and [ncp + k] = Im of
+// the frequency-f segment ring (mirrored slots).  Two real series per complex FFT.
+constexpr int FFT_BC = 8;  // trajectories per block
+__global__ __launch_bounds__(256) void seg_fft_kernel(const double* __restrict__ H, int64_t ldh, int R,
+                                                      int B, int nc, int ncp, int P, int logn,
+                                                      int64_t T, double* __restrict__ seg,
+                                                      int64_t seg_fstride, int64_t ldseg, int Rseg,
+                                                      const double2* __restrict__ cstab, int cstride) {
+  extern __shared__ double2 fbuf[];
+  const int N = 2 * P;
+  const int nbc = (B + FFT_BC - 1) / FFT_BC;
+  const int bc = blockIdx.x % nbc;
+  const int k = (blockIdx.x / nbc) % nc;
+  const int sidx = blockIdx.x / (nbc * nc);
+  const int64_t sigma = T / P - sidx;
+  const int64_t t0 = sigma * P - 2 * P + 2;
+  const int b0 = bc * FFT_BC;
+  const double* hk = H + (int64_t)k * ldh;
+  for (int e = threadIdx.x; e < N * FFT_BC / 2; e += blockDim.x) {
+    const int q = e % (FFT_BC / 2);
+    const int n = e / (FFT_BC / 2);
+    double xr = 0.0, xi = 0.0;
+    if (n < N - 1) {
+      const double* hs = hk + pmod(t0 + n, R) * B;
+      const int ba = b0 + 2 * q, bb = ba + 1;
+      if (ba < B) xr = hs[ba];
+      if (bb < B) xi = hs[bb];
+    }
+    const unsigned rev = __brev((unsigned)n) >> (32 - logn);
+    fbuf[q * N + rev] = make_double2(xr, xi);
+  }
+  __syncthreads();
+  lds_fft<FFT_BC / 2>(fbuf, logn, cstab, cstride, -1.0);
+  const int64_t slot = pmod(sigma, Rseg);
+  for (int e = threadIdx.x; e < (P + 1) * FFT_BC; e += blockDim.x) {
+    const int bl = e % FFT_BC;
+    const int f = e / FFT_BC;
+    const int b = b0 + bl;
+    if (b >= B) continue;
+    const int q = bl >> 1;
+    const double2 z = fbuf[q * N + f];
+    const double2 zc = fbuf[q * N + ((N - f) & (N - 1))];
+    // X_even = (Z[f] + conj Z[N-f]) / 2, X_odd = (Z[f] - conj Z[N-f]) / (2i)
+    double re, im;
+    if ((bl & 1) == 0) {
+      re = 0.5 * (z.x + zc.x);
+      im = 0.5 * (z.y - zc.y);
+    } else {
+      re = 0.5 * (z.y + zc.y);
+      im = -0.5 * (z.x - zc.x);
+    }
     double* sf = seg + (int64_t)f * seg_fstride + b;
     sf[(int64_t)k * ldseg + slot * B] = re;
     sf[(int64_t)k * ldseg + (slot + Rseg) * B] = re;
-    const int64_t ir = (int64_t)(((nc + 7) / 8) * 8 + k) * ldseg;  // Im rows start at ncp
+    const int64_t ir = (int64_t)(ncp + k) * ldseg;
     sf[ir + slot * B] = im;
     sf[ir + (slot + Rseg) * B] = im;
   }
 }
 
-void launch_seg_fft(const double* H, int64_t ldh, int R, int B, int nc, int P, int64_t T, int nseg,
-                    double* seg, int64_t seg_fstride, int64_t ldseg, int Rseg, const double* cstab,
-                    hipStream_t s) {
-  const int64_t total = (int64_t)nseg * (P + 1) * nc * B;
-  const int64_t blocks = std::min<int64_t>((total + 255) / 256, 16384);
-  seg_fft_kernel<<<(unsigned)blocks, 256, 0, s>>>(H, ldh, R, B, nc, P, T, nseg, seg, seg_fstride,
-                                                  ldseg, Rseg, (const double2*)cstab);
+int launch_seg_fft(const double* H, int64_t ldh, int R, int B, int nc, int ncp, int P, int64_t T,
+                   int nseg, double* seg, int64_t seg_fstride, int64_t ldseg, int Rseg,
+                   const double* cstab, int cstride, hipStream_t s) {
+  int logn = 0;
+  while ((1 << logn) < 2 * P) ++logn;
+  if ((1 << logn) != 2 * P) return -1;
+  const size_t shmem = (size_t)(FFT_BC / 2) * 2 * P * sizeof(double2);
+  if (shmem > 160 * 1024) return -2;
+  if (hipFuncSetAttribute((const void*)seg_fft_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)shmem) != hipSuccess)
+    return -3;
+  const int nbc = (B + FFT_BC - 1) / FFT_BC;
+  const int64_t blocks = (int64_t)nseg * nc * nbc;
+  seg_fft_kernel<<<(unsigned)blocks, 256, shmem, s>>>(H, ldh, R, B, nc, ncp, P, logn, T, seg,
+                                                      seg_fstride, ldseg, Rseg,
+                                                      (const double2*)cstab, cstride);
+  return 0;
 }
 
-// far(T+1+j) = y[j+P-1],  y[n] = (1/2P) [Y0 + (-1)^n Y_P + 2 sum_{0<f<P} Re(Y_f e^{+i pi f n/P})]
-// (the real inverse transform of the Hermitian spectrum; Im Y_0, Im Y_P ignored as by irfft).
-__global__ void far_ifft_kernel(const double* __restrict__ Y, int64_t yfstride, int nc, int B, int P,
-                                double* __restrict__ far, int64_t ldfar,
-                                const double2* __restrict__ cstab) {
-  const int64_t total = (int64_t)nc * P * B;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int b = (int)(e % B);
-    int64_t r_ = e / B;
-    const int j = (int)(r_ % P);
-    const int k = (int)(r_ / P);
-    const int n = j + P - 1;
-    const double* yk = Y + (int64_t)k * B + b;
-    const int64_t im_off = (int64_t)nc * B;
-    double acc = 0.0;
-    for (int f = 1; f < P; ++f) {
-      const double2 cs = cstab[(f * n) % (2 * P)];
-      const double* yf = yk + (int64_t)f * yfstride;
-      acc += yf[0] * cs.x - yf[im_off] * cs.y;
+// Block output out(kP + 1 + j) = y[j + P - 1] (j < P) of the real inverse transform of the
+// Hermitian spectrum Y(f), f = 0..P (Im Y_0, Im Y_P ignored as by irfft):
+//   y[n] = (1/2P) sum_{f<2P} Y(f) e^{+i pi f n / P},  Y(2P - f) = conj Y(f).
+// Grid: DOF k x 8-trajectory chunk; two real outputs per complex inverse FFT.
+__global__ __launch_bounds__(256) void far_ifft_kernel(const double* __restrict__ Y, int64_t yfstride,
+                                                       int nc, int B, int P, int logn,
+                                                       double* __restrict__ out, int64_t ldout,
+                                                       const double2* __restrict__ cstab, int cstride) {
+  extern __shared__ double2 fbuf[];
+  const int N = 2 * P;
+  const int nbc = (B + FFT_BC - 1) / FFT_BC;
+  const int bc = blockIdx.x % nbc;
+  const int k = blockIdx.x / nbc;
+  const int b0 = bc * FFT_BC;
+  const int64_t im_off = (int64_t)nc * B;
+  for (int e = threadIdx.x; e < N * FFT_BC / 2; e += blockDim.x) {
+    const int q = e % (FFT_BC / 2);
+    const int f = e / (FFT_BC / 2);
+    const bool cj = f > P;
+    const int fs = cj ? N - f : f;
+    const bool realonly = (fs == 0) || (fs == P);
+    const int ba = b0 + 2 * q, bb = ba + 1;
+    const double* yf = Y + (int64_t)fs * yfstride + (int64_t)k * B;
+    double ar = 0.0, ai = 0.0, br = 0.0, bi = 0.0;
+    if (ba < B) {
+      ar = yf[ba];
+      ai = realonly ? 0.0 : yf[im_off + ba];
     }
-    const double y0 = yk[0];
-    const double yp = yk[(int64_t)P * yfstride];
-    const double v = (y0 + ((n & 1) ? -yp : yp) + 2.0 * acc) / (2.0 * P);
-    far[(int64_t)k * ldfar + (int64_t)j * B + b] = v;
+    if (bb < B) {
+      br = yf[bb];
+      bi = realonly ? 0.0 : yf[im_off + bb];
+    }
+    if (cj) {
+      ai = -ai;
+      bi = -bi;
+    }
+    // Z = A + i B
+    const unsigned rev = __brev((unsigned)f) >> (32 - logn);
+    fbuf[q * N + rev] = make_double2(ar - bi, ai + br);
+  }
+  __syncthreads();
+  lds_fft<FFT_BC / 2>(fbuf, logn, cstab, cstride, 1.0);
+  const double scale = 1.0 / N;
+  for (int e = threadIdx.x; e < P * FFT_BC; e += blockDim.x) {
+    const int bl = e % FFT_BC;
+    const int j = e / FFT_BC;
+    const int b = b0 + bl;
+    if (b >= B) continue;
+    const double2 z = fbuf[(bl >> 1) * N + j + P - 1];
+    out[(int64_t)k * ldout + (int64_t)j * B + b] = ((bl & 1) ? z.y : z.x) * scale;
   }
 }
 
-void launch_far_ifft(const double* Y, int64_t yfstride, int nc, int B, int P, double* far,
-                     int64_t ldfar, const double* cstab, hipStream_t s) {
-  const int64_t total = (int64_t)nc * P * B;
-  const int64_t blocks = std::min<int64_t>((total + 255) / 256, 16384);
-  far_ifft_kernel<<<(unsigned)blocks, 256, 0, s>>>(Y, yfstride, nc, B, P, far, ldfar,
-                                                   (const double2*)cstab);
+int launch_far_ifft(const double* Y, int64_t yfstride, int nc, int B, int P, double* out,
+                    int64_t ldout, const double* cstab, int cstride, hipStream_t s) {
+  int logn = 0;
+  while ((1 << logn) < 2 * P) ++logn;
+  if ((1 << logn) != 2 * P) return -1;
+  const size_t shmem = (size_t)(FFT_BC / 2) * 2 * P * sizeof(double2);
+  if (shmem > 160 * 1024) return -2;
+  if (hipFuncSetAttribute((const void*)far_ifft_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)shmem) != hipSuccess)
+    return -3;
+  const int nbc = (B + FFT_BC - 1) / FFT_BC;
+  far_ifft_kernel<<<(unsigned)(nc * nbc), 256, shmem, s>>>(Y, yfstride, nc, B, P, logn, out, ldout,
+                                                          (const double2*)cstab, cstride);
+  return 0;
 }
 
 }  // namespace gle

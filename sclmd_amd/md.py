@@ -39,7 +39,7 @@ def ApplyConstraint(f, constr=None):
 class md:
     def __init__(self, dt, nmd, T, syslist=None, axyz=None, dyn=None, nstart=0, nstop=1, npie=1,
                  md2ang=0.06466, *, ntraj=1, seed=None, traj_offset=0, device=None,
-                 noise_mode="numpy", block_len=0, far_mode="auto", mid_len=0, comm=None, verbose=True):
+                 noise_mode="numpy", block_len=0, far_mode="auto", max_block=0, comm=None, verbose=True):
         self.nstart, self.nstop = nstart, nstop
         self.dt, self.nmd = dt, nmd
         self.T = T
@@ -59,7 +59,7 @@ class md:
         self.device = device
         self.block_len = int(block_len)
         self.far_mode = far_mode
-        self.mid_len = int(mid_len)
+        self.max_block = int(max_block)
         self.comm = comm
         self.SetXyz(axyz)
         if syslist is not None:
@@ -342,7 +342,7 @@ class md:
         if dev is None:
             dev = int(os.environ.get("LOCAL_RANK", "0")) if _native.device_count() > 1 else 0
         st = _native.Stepper(self.nph, self.ntraj, self.nmd, self.dt, dev, self.block_len, self.far_mode,
-                             self.mid_len)
+                             self.max_block)
         for b in self.baths:
             if b.kernel is None:
                 raise ValueError("md: bath %s has no kernel (call phbath.gmem())" % b)

@@ -43,7 +43,7 @@ def test_bad_config_rejected():
     from sclmd_amd import _native
 
     lib = _native.load()
-    cfg = _native.gle_config(12, 1, 15, 0.38, 0, 0, 0, 0)  # odd nmd (fields: ..., far_mode, mid_len)
+    cfg = _native.gle_config(12, 1, 15, 0.38, 0, 0, 0, 0)  # odd nmd (fields: ..., far_mode, max_block)
     h = ctypes.c_void_p()
     assert lib.gle_create(ctypes.byref(cfg), ctypes.byref(h)) == -1
     assert b"even" in lib.gle_last_error(None)

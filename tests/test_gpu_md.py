@@ -277,3 +277,50 @@ def test_deterministic():
         outs.append(st.get_state()[0])
         st.close()
     assert np.array_equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("far_mode,block_len,max_block",
+                         [("auto", 0, 0), ("direct", 0, 0), ("spectral", 0, 64), ("spectral", 2, 0), ("direct", 3, 16)])
+def test_ladder_long_kernel_vs_oracle(far_mode, block_len, max_block):
+    """Every rung of the memory-sum ladder against the oracle: a 1024-slice kernel on a small
+    junction, started at an unaligned t with a nonzero history, run past several blocks of the
+    largest level (block 256 at the defaults) and across the noise period."""
+    from sclmd_amd import _native as N
+    from sclmd_amd import synthetic
+    from oracle import sclmd_oracle as O
+
+    ml, nmd, t0, nst, B = 1024, 512, 37, 700, 8
+    dyn, _, baths, meta = synthetic.junction("C3", ml=ml, nmd=nmd, natom=12, nw=200)
+    nph, dt = meta["nph"], meta["dt"]
+    st = N.Stepper(nph, B, nmd, dt, 0, block_len, far_mode, max_block)
+    for b in baths:
+        st.add_bath(N.GLE_BATH_PHONON, b.cids, b.kernel)
+    st.set_dyn(dyn)
+    rng = np.random.default_rng(21)
+    # two distinct trajectories, tiled over the batch
+    p = rng.normal(size=(2, nph)) * 1e-3
+    q = rng.normal(size=(2, nph)) * 1e-3
+    hist = [rng.normal(size=(2, ml, b.nc)) * 1e-3 for b in baths]
+    noise = [rng.normal(size=(2, nmd, b.nc)) * 1e-3 for b in baths]
+    tile = np.arange(B) % 2
+    st.set_state(p[tile], q[tile], t0)
+    for i in range(len(baths)):
+        st.set_history(i, hist[i][tile])
+        st.set_noise(i, noise[i][tile])
+    info = st.plan_info()
+    if far_mode == "spectral":
+        assert info["far_mode"] == "spectral"
+    st.run(nst)
+    pg, qg, t = st.get_state()
+    assert t == t0 + nst
+    for j in range(2):
+        bs = [O.Bath("ph", b.cids, b.kernel, noise[i][j], dt, nmd) for i, b in enumerate(baths)]
+        sim = O.GLE(nph, dt, nmd, bs, dyn=dyn)
+        sim.p, sim.q, sim.t = p[j].copy(), q[j].copy(), t0
+        for i, b in enumerate(baths):
+            sim.phis[:, b.cids] = hist[i][j]
+        for _ in range(nst):
+            sim.step()
+        for b_ in (j, j + 2, B - 2 + j):
+            assert rel(qg[b_], sim.q) < 1e-9 and rel(pg[b_], sim.p) < 1e-9, (b_, rel(qg[b_], sim.q))
+    st.close()
