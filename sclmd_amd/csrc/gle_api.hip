@@ -1,12 +1,11 @@
 // Host side of the hipgle C-ABI: handle, device buffers, work planner, step orchestration.
 //
-// Step schedule (one md.vv, md.py:367-411), all on the handle's stream:
-//   [every L steps] FAR  : far(t+j) = sum_{i>=L} K_i p_{t+j-i}, j = 1..L      (one contraction)
-//   OP0  : Y0 = K0 p_t, near S(t+1) = sum_{1<=i<L} K_i p_{t+1-i}, Yq = Kq q_t, [dyn q_t]
-//   RED0 : S(t+1) = far(t+1) + near;  split-K sums
-//   [POTSEL(q_t)]  PHASE A : F0, heat current, p_half, q~, gathers
-//   OP1a : [dyn q~], Y = K0 p_half, Yq = Kq q~ ; RED1a ; [POTSEL(q~)] ; PHASE B : p1
-//   OP1b : Y = K0 p1 ; RED1b ; PHASE C : p2, constraints, history push, t+1
+// Step schedule (one md.vv, md.py:367-411): three launches on the handle's stream (gle_chain.hip)
+//   A : K0.p_t (+Kq.q_t, +dyn.q_t) and the id0 phase per DOF tile; S(t+1) = K_1.p_t + near-field
+//       partials + ladder levels per bath row tile
+//   B : K0.p_half, Kq.q~, dyn.q~ and the first velocity iteration; near-field partials for t+2
+//   C : K0.p1, second iteration, constraints, history push; near-field partials for t+2
+// plus, at block boundaries, the ladder blocks on background streams (one block ahead).
 // The memory sum S is computed once per step (the reference recomputes the whole history sum in
 // each of its three md.force calls, baths.py:453-457; the i>=1 tail is identical in all three).
 #include <hip/hip_runtime.h>
@@ -40,14 +39,14 @@ struct Op {
   double* partial = nullptr;
   size_t partial_doubles = 0;
   double flops = 0, bytes = 0;  // algorithmic, per launch
-  bool tile = false;   // latency-bound per-step op: tile_kernel items, no partials / reduce
-  std::vector<TItem> titems;
-  TItem* d_titems = nullptr;
-  size_t tpart_doubles = 0;   // tile partial slots (offsets fixed up in materialize)
-  int tcnt = 0;               // tile arrival counters
-  double* d_tpart = nullptr;
-  unsigned* d_tcnt = nullptr;
-  bool empty() const { return items.empty() && ritems.empty() && titems.empty(); }
+  bool empty() const { return items.empty() && ritems.empty(); }
+};
+
+// One launch of the per-step chain (gle_chain.hip).
+struct Chain {
+  std::vector<ChTile> tiles;
+  ChTile* d = nullptr;
+  double flops = 0;  // algorithmic flops of the launch's products
 };
 
 struct Bath {
@@ -56,15 +55,23 @@ struct Bath {
   double c = 1.0;
   bool has_q = false;
   std::vector<int64_t> cids;
+  std::vector<int32_t> inv;  // [nph] DOF -> k or -1
   std::vector<double> K;  // host copy [ml][nc][nc] of the p-channel kernel (bias folded)
+  std::vector<double> K0; // host copy of slice 0 (bias folded)
   std::vector<double> Kq; // [nc][nc] q-channel
   double* d_K = nullptr;
   double* d_Kn = nullptr;  // compact fragment copy of the per-step slices [0, nn): [rt][ks][i][64]
   int nn = 1;
   double* d_Kq = nullptr;
+  // K0 / Kq rows in DOF order for the chain's DOF tiles: tile rt at [tofs[rt]][ks][64]
+  double *d_K0d = nullptr, *d_Kqd = nullptr;
+  std::vector<int64_t> tofs;
   int32_t* d_inv = nullptr;
-  double *d_noise = nullptr, *d_Y = nullptr, *d_S = nullptr, *d_Yq = nullptr;
+  double *d_noise = nullptr, *d_S = nullptr, *d_Yq = nullptr;
   double *d_Xcur = nullptr, *d_Xq = nullptr, *d_H = nullptr, *d_cur = nullptr;
+  double* d_NP = nullptr;  // near-field partial slots [2][nqn][vs]
+  int nqn = 0;
+  int64_t vs = 0;          // doubles per bath-local [ncp][B] buffer (with slack)
   int64_t ldh = 0;
   int R = 1;
   bool noise_set = false;
@@ -113,22 +120,26 @@ struct gle_handle {
   bool has_dyn = false;
   int dyn_nrt = 0, dyn_nks = 0;
   double* d_dyn = nullptr;
+  std::vector<double> dyn_h;   // host copy [nph][nph]
+  double* d_dynd = nullptr;    // block-sparse DOF-tile fragments of dyn
+  std::vector<std::vector<std::pair<int, int>>> dyn_rng;  // per DOF tile: (first k-step, count)
+  std::vector<int64_t> dyn_tofs;
   std::vector<int64_t> constr;
   uint8_t* d_cmask = nullptr;
   double *d_P = nullptr, *d_Q = nullptr, *d_Ph = nullptr, *d_Qt = nullptr, *d_Fc = nullptr;
-  double *d_Flast = nullptr, *d_etot = nullptr, *d_Q0 = nullptr, *d_part = nullptr, *d_Ypot = nullptr;
+  double *d_Flast = nullptr, *d_etot = nullptr, *d_Q0 = nullptr, *d_part = nullptr;
   unsigned long long* d_pmax = nullptr;
   int32_t* d_qvalid = nullptr;
   StepDev* d_sd = nullptr;
   double* d_tw = nullptr;
-  int ndblk = 1, dchunk = 1;
+  int ndblk = 1;
   int64_t t = 0;
   bool frozen = false, state_set = false;
   bool need_prime = true;
   bool pot_cache_exact = false;  // q_t == q~_{t-1} bitwise (no constraints): id0 cache hit
   bool host_force_step = false;
-  Op op_prime, op1a, op1a_np, op1b;
-  Op op0[2], op0p[2];  // {K0 p_t, Kq q_t, S(t+1) = near + levels into S[par]} (+ dyn q_t), par = (t+1)&1
+  Op op_prime;
+  Chain chA[2], chB[2], chC, chNear;  // [with dyn.q]; chNear: all near-field partial tiles (priming)
   int P0 = 1;          // first level block; near field = lags [1, 2 P0)
   int near_end = 1;
   std::vector<Level> levels;
@@ -232,9 +243,6 @@ struct Gemm {
   int M, N;
   double* dst;
   int64_t ldd;
-  const double* adds[MAXLVL] = {};  // level block buffers added in the tile epilogue
-  int32_t add_ld[MAXLVL] = {};
-  int nadd = 0;
   bool force_reduce = false;
   int Kd = 0;  // true (unpadded) reduction length, for the algorithmic flop/byte count
   int tdiv = 1;
@@ -374,55 +382,6 @@ void plan_gemm(Op& op, const Gemm& g, int target_items, int min_work) {
   }
 }
 
-// Per-step product as tile_kernel items: per (16-row tile, column tile of 16*rn), ngrp shares of
-// the slice x k-step space, sized so each wave runs about TILE_STEPS steps.
-constexpr int TILE_WAVES = 4, TILE_STEPS = 8, TILE_MAXGRP = 64;
-void plan_tile(Op& op, const Gemm& g) {
-  const int NT = 16 * op.rn;
-  const int ni = std::max(0, g.i1 - g.i0);
-  const int64_t S = (int64_t)ni * g.nks_total;
-  const int ngrp = (int)std::max<int64_t>(1, std::min<int64_t>(TILE_MAXGRP, (S + TILE_WAVES * TILE_STEPS - 1) / (TILE_WAVES * TILE_STEPS)));
-  for (int c0 = 0; c0 < g.N; c0 += NT)
-    for (int rt = 0; rt < (g.M + 15) / 16; ++rt) {
-      TItem it{};
-      it.A = g.A + (int64_t)rt * g.a_rt + (int64_t)g.i0 * 64;
-      it.a_ks = g.a_ks;
-      it.X = g.X + c0;
-      it.ldx = g.ldx;
-      it.out = g.dst + (int64_t)(16 * rt) * g.ldd + c0;
-      it.ldo = (int32_t)g.ldd;
-      it.nadd = g.nadd;
-      for (int a = 0; a < g.nadd; ++a) {
-        it.add[a] = g.adds[a] ? g.adds[a] + (int64_t)(16 * rt) * g.add_ld[a] + c0 : nullptr;
-        it.add_ld[a] = g.add_ld[a];
-      }
-      it.ia = g.i0;
-      it.ni = ni;
-      it.nks = g.nks_total;
-      it.ring = g.ring;
-      it.cs = g.cs;
-      it.tshift = g.tshift;
-      it.nrows = std::min(16, g.M - 16 * rt);
-      it.ncols = std::min(NT, g.N - c0);
-      it.ngrp = ngrp;
-      if (ngrp > 1) {
-        it.part = (double*)(uintptr_t)(op.tpart_doubles * sizeof(double));  // offset, fixed up later
-        it.cnt = (unsigned*)(uintptr_t)(op.tcnt * sizeof(unsigned));
-        op.tpart_doubles += (size_t)ngrp * 256 * op.rn;
-        op.tcnt += 1;
-      }
-      for (int gi = 0; gi < ngrp; ++gi) {
-        it.grp = gi;
-        op.titems.push_back(it);
-      }
-    }
-  if (ni > 0) {
-    const double kd = g.Kd > 0 ? g.Kd : 4.0 * g.nks_total;
-    op.flops += 2.0 * g.M * kd * g.N * ni;
-    op.bytes += 8.0 * ((double)ni * g.M * kd + kd * (g.ring ? (double)(ni + (g.N + g.cs - 1) / std::max(1, g.cs) - 1) * g.cs : g.N) + (double)g.M * g.N);
-  }
-}
-
 // Fix up partial-slot offsets once the partial buffer exists.  Items that write partials were
 // tagged with ldo == NT and an offset pointer smaller than the partial size.
 int materialize(gle_handle* h, Op& op, const std::vector<bool>& is_partial) {
@@ -457,22 +416,6 @@ int materialize(gle_handle* h, Op& op, const std::vector<bool>& is_partial) {
     op.items.push_back(e);
   }
   for (auto& r : op.ritems) r.src = op.partial + (uintptr_t)r.src / sizeof(double);
-  if (!op.titems.empty()) {
-    if (op.tcnt) {
-      int rc = dalloc_n(h, &op.d_tpart, op.tpart_doubles);
-      if (!rc) rc = dalloc_n(h, &op.d_tcnt, (size_t)op.tcnt);
-      if (rc) return rc;
-      for (auto& it : op.titems)
-        if (it.ngrp > 1) {
-          it.part = op.d_tpart + (uintptr_t)it.part / sizeof(double);
-          it.cnt = op.d_tcnt + (uintptr_t)it.cnt / sizeof(unsigned);
-        }
-    }
-    int rc = dalloc_n(h, &op.d_titems, op.titems.size());
-    if (rc) return rc;
-    rc = upload(h, op.d_titems, op.titems.data(), op.titems.size() * sizeof(TItem));
-    if (rc) return rc;
-  }
   if (!op.items.empty()) {
     int rc = dalloc_n(h, &op.d_items, op.items.size());
     if (rc) return rc;
@@ -496,10 +439,6 @@ struct Planner {
   bool lat;
   Planner(gle_handle* hh, Op& o, int rn, bool latency = false) : h(hh), op(o), lat(latency) { op.rn = rn; }
   void add(const Gemm& g0, int target, int min_work) {
-    if (op.tile) {
-      plan_tile(op, g0);
-      return;
-    }
     Gemm g = g0;
     if (lat) g.lat = true;
     const size_t n0 = op.items.size();
@@ -543,16 +482,14 @@ void drain_profile(gle_handle* h) {
 // kernel) on that same stream.
 void run_op(gle_handle* h, Op& op, hipStream_t s, const StepArgs& ta, bool profile) {
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (profile && h->prof && !(op.items.empty() && op.titems.empty())) {
+  if (profile && h->prof && !op.items.empty()) {
     if (h->ev_used + 2 > h->ev.size()) drain_profile(h);
     e0 = h->ev[h->ev_used];
     e1 = h->ev[h->ev_used + 1];
     h->ev_used += 2;
     hipEventRecord(e0, s);
   }
-  if (op.tile)
-    launch_tile(op.rn, op.d_titems, (int)op.titems.size(), ta, s);
-  else if (op.cplx)
+  if (op.cplx)
     launch_contract_cplx(op.rn, op.d_items, (int)op.items.size(), ta, s);
   else
     launch_contract(op.rn, op.cu, op.d_items, (int)op.items.size(), ta, s);
@@ -562,7 +499,24 @@ void run_op(gle_handle* h, Op& op, hipStream_t s, const StepArgs& ta, bool profi
     h->prof_flops += op.flops;
     h->prof_bytes += op.bytes;
   }
-  if (!op.tile) launch_reduce(op.d_ritems, (int)op.ritems.size(), op.max_elems, ta, s);
+  launch_reduce(op.d_ritems, (int)op.ritems.size(), op.max_elems, ta, s);
+}
+
+// One chain launch; profiled (HIP events, same stream) when the ladder has no levels.
+void run_chain(gle_handle* h, int stage, Chain& c, const StepArgs& ta, int mode, bool profile) {
+  hipEvent_t e1 = nullptr;
+  if (profile && h->prof && !c.tiles.empty()) {
+    if (h->ev_used + 2 > h->ev.size()) drain_profile(h);
+    hipEventRecord(h->ev[h->ev_used], h->stream);
+    e1 = h->ev[h->ev_used + 1];
+    h->ev_used += 2;
+  }
+  launch_chain(stage, c.d, (int)c.tiles.size(), h->d_sd, ta, mode, h->stream);
+  if (e1) {
+    hipEventRecord(e1, h->stream);
+    h->prof_n += 1;
+    h->prof_flops += c.flops;
+  }
 }
 
 // Make the main stream wait for everything queued on the background stream.
@@ -587,6 +541,331 @@ int check_bath(gle_handle* h, int32_t b) {
 }
 
 // Build every work plan once the system is fixed (first state / step call).
+// ---- per-step chain planning (gle_chain.hip) ---------------------------------------------
+
+// A run of k-steps of one chain output: acc_o += sum_s A[s * a_ks] . X rows 4s..4s+3.
+struct Seg {
+  int o;
+  const double* A;
+  int a_ks;
+  const double* X;
+  int ldx, ring, tshift, nks;
+};
+
+// Split the k-steps [g_begin, g_end) of the concatenated segments evenly over the CH_NW waves of
+// tile T; every (wave, output) run gets its own LDS slot, slots of one output are contiguous.
+int fill_tasks(gle_handle* h, ChTile& T, const std::vector<Seg>& segs, int nout, int64_t g_begin,
+               int64_t g_end, double* flops) {
+  int slot = 0;
+  std::vector<int> nsl(nout, 0), first(nout, -1);
+  for (int w = 0; w < CH_NW; ++w) {
+    const int64_t g0 = g_begin + (g_end - g_begin) * w / CH_NW;
+    const int64_t g1 = g_begin + (g_end - g_begin) * (w + 1) / CH_NW;
+    int64_t pos = 0;
+    int cur_o = -1, cnt = 0, cur_slot = -1;
+    for (const Seg& sg : segs) {
+      const int64_t s0 = std::max(g0, pos), s1 = std::min(g1, pos + sg.nks);
+      if (s1 > s0) {
+        if (sg.o != cur_o) {
+          cur_o = sg.o;
+          cur_slot = slot++;
+          if (first[cur_o] < 0) first[cur_o] = cur_slot;
+          ++nsl[cur_o];
+        }
+        if (cnt >= CH_TPW) return fail(h, GLE_ERR_UNSUP, "chain plan: too many k-step runs per wave");
+        ChTask& tk = T.task[w][cnt++];
+        const int64_t kl = s0 - pos;
+        tk.A = sg.A + kl * sg.a_ks;
+        tk.a_ks = sg.a_ks;
+        tk.X = sg.X + 4 * kl * sg.ldx;
+        tk.ldx = sg.ldx;
+        tk.ring = sg.ring;
+        tk.tshift = sg.tshift;
+        tk.nks = (int32_t)(s1 - s0);
+        tk.slot = cur_slot;
+        *flops += 2048.0 * T.rn * (double)(s1 - s0);
+      }
+      pos += sg.nks;
+    }
+    T.ntw[w] = (int8_t)cnt;
+  }
+  if ((int64_t)slot * 256 * T.rn > CH_LDS) return fail(h, GLE_ERR_UNSUP, "chain plan: LDS slots");
+  int run = 0;
+  for (int o = 0; o < nout; ++o) {
+    if (nsl[o] && first[o] != run) return fail(h, GLE_ERR_UNSUP, "chain plan: slot order");
+    T.ob[o] = (int8_t)run;
+    run += nsl[o];
+  }
+  T.ob[nout] = (int8_t)run;
+  for (int o = nout + 1; o <= CH_NOUT; ++o) T.ob[o] = (int8_t)run;
+  return GLE_OK;
+}
+
+int upload_chain(gle_handle* h, Chain& c) {
+  if (c.tiles.empty()) return GLE_OK;
+  int rc = dalloc_n(h, &c.d, c.tiles.size());
+  if (!rc) rc = upload(h, c.d, c.tiles.data(), c.tiles.size() * sizeof(ChTile));
+  return rc;
+}
+
+int plan_chain(gle_handle* h) {
+  const int64_t B = h->B;
+  const int nb = (int)h->baths.size();
+  const int ntile = h->ndblk;
+  const int ncol1 = (int)((B + 15) / 16);
+  // K0 / Kq rows in DOF order: DOF tile rt of bath j at tofs[rt], [ks][64] fragments
+  for (auto& b : h->baths) {
+    b.tofs.assign(ntile, -1);
+    int64_t n = 0;
+    for (int rt = 0; rt < ntile; ++rt) {
+      bool any = false;
+      for (int r = 0; r < 16 && 16 * rt + r < h->nph; ++r) any |= b.inv[16 * rt + r] >= 0;
+      if (any) {
+        b.tofs[rt] = n;
+        n += (int64_t)b.nks * 64;
+      }
+    }
+    auto pack_dof = [&](const std::vector<double>& M) {
+      std::vector<double> f((size_t)n, 0.0);
+      for (int rt = 0; rt < ntile; ++rt) {
+        if (b.tofs[rt] < 0) continue;
+        for (int ks = 0; ks < b.nks; ++ks)
+          for (int l = 0; l < 64; ++l) {
+            const int64_t d = 16 * rt + (l & 15), kc = 4 * ks + (l >> 4);
+            if (d >= h->nph || kc >= b.nc || b.inv[d] < 0) continue;
+            f[(size_t)(b.tofs[rt] + ks * 64 + l)] = M[(size_t)b.inv[d] * b.nc + kc];
+          }
+      }
+      return f;
+    };
+    std::vector<double> f = pack_dof(b.K0);
+    int rc = dalloc_n(h, &b.d_K0d, f.size());
+    if (!rc) rc = upload(h, b.d_K0d, f.data(), f.size() * 8);
+    if (!rc && b.has_q) {
+      f = pack_dof(b.Kq);
+      rc = dalloc_n(h, &b.d_Kqd, f.size());
+      if (!rc) rc = upload(h, b.d_Kqd, f.data(), f.size() * 8);
+    }
+    if (rc) return rc;
+  }
+  // dyn as block-sparse DOF-tile fragments: per tile at most two runs of nonzero 16x4 blocks
+  if (h->has_dyn) {
+    const int nksd = (int)(h->nphp / 4);
+    h->dyn_rng.assign(ntile, {});
+    h->dyn_tofs.assign(ntile, 0);
+    int64_t n = 0;
+    for (int rt = 0; rt < ntile; ++rt) {
+      std::vector<std::pair<int, int>> rg;
+      for (int ks = 0; ks < nksd; ++ks) {
+        bool nz = false;
+        for (int r = 0; r < 16 && !nz; ++r) {
+          const int64_t d = 16 * rt + r;
+          if (d >= h->nph) break;
+          for (int c = 4 * ks; c < 4 * ks + 4 && c < h->nph; ++c) nz |= h->dyn_h[(size_t)d * h->nph + c] != 0.0;
+        }
+        if (!nz) continue;
+        if (!rg.empty() && rg.back().first + rg.back().second == ks) ++rg.back().second;
+        else rg.push_back({ks, 1});
+      }
+      while (rg.size() > 2) {  // merge across the smallest gap
+        size_t bi = 0;
+        int bg = INT32_MAX;
+        for (size_t i = 0; i + 1 < rg.size(); ++i) {
+          const int gap = rg[i + 1].first - (rg[i].first + rg[i].second);
+          if (gap < bg) {
+            bg = gap;
+            bi = i;
+          }
+        }
+        rg[bi].second = rg[bi + 1].first + rg[bi + 1].second - rg[bi].first;
+        rg.erase(rg.begin() + bi + 1);
+      }
+      h->dyn_tofs[rt] = n;
+      for (auto& r : rg) n += (int64_t)r.second * 64;
+      h->dyn_rng[rt] = rg;
+    }
+    std::vector<double> f((size_t)std::max<int64_t>(n, 64), 0.0);
+    for (int rt = 0; rt < ntile; ++rt) {
+      int64_t o = h->dyn_tofs[rt];
+      for (auto& r : h->dyn_rng[rt])
+        for (int ks = r.first; ks < r.first + r.second; ++ks, o += 64)
+          for (int l = 0; l < 64; ++l) {
+            const int64_t d = 16 * rt + (l & 15), c = 4 * ks + (l >> 4);
+            if (d < h->nph && c < h->nph) f[(size_t)(o + l)] = h->dyn_h[(size_t)d * h->nph + c];
+          }
+    }
+    int rc = dalloc_n(h, &h->d_dynd, f.size());
+    if (!rc) rc = upload(h, h->d_dynd, f.data(), f.size() * 8);
+    if (rc) return rc;
+  }
+  // near-field partial items (lags [2, nn), target t+2) per bath: sizes and slot counts
+  const int rn_raw = (int)std::min<int64_t>(4, (B + 15) / 16);
+  const int nt_raw = 16 * rn_raw;
+  const int ncolr = (int)((B + nt_raw - 1) / nt_raw);
+  const char* env = getenv("GLE_NEAR_KS");
+  const int raw_ks = env ? std::max(4, atoi(env)) : 24;
+  for (auto& b : h->baths) {
+    b.nqn = 0;
+    if (b.nn > 2) {
+      const int64_t W = (int64_t)(b.nn - 2) * b.nks;
+      int q = (int)((W + raw_ks - 1) / raw_ks);
+      q = std::max(q, (b.nn - 2 + 11) / 12);  // at most CH_TPW slice runs per wave
+      q = std::max(1, std::min<int>(q, (int)W));
+      if (q > CH_NPMAX) return fail(h, GLE_ERR_UNSUP, "near field too long for the chain (block_len)");
+      b.nqn = q;
+      int rc = dalloc_n(h, &b.d_NP, (size_t)2 * q * b.vs + 4096);
+      if (rc) return rc;
+    }
+  }
+  // ---- tiles
+  auto dof_tile = [&](int stage, bool withD, int rt, int ct, Chain& c) -> int {
+    ChTile T{};
+    T.kind = CH_DOF;
+    T.rn = 1;
+    T.row0 = 16 * rt;
+    T.c0 = 16 * ct;
+    T.tile = rt;
+    T.nrows = (int)std::min<int64_t>(16, h->nph - 16 * rt);
+    T.ncols = (int)std::min<int64_t>(16, B - 16 * ct);
+    T.first = rt == 0 ? 1 : 0;
+    std::vector<Seg> segs;
+    std::vector<Seg> qsegs;
+    int nu = 0;
+    for (int u = 0; u < CH_TB; ++u) T.tb[u] = -1;
+    for (int j = 0; j < nb; ++j) {
+      Bath& b = h->baths[j];
+      uint32_t m = 0;
+      bool affine = true;
+      int off = 0;
+      for (int r = 0; r < 16; ++r) {
+        const int64_t d = 16 * rt + r;
+        if (d >= h->nph || b.inv[d] < 0) continue;
+        const int o = b.inv[d] - (int)d;
+        if (m == 0) off = o;
+        else if (o != off) affine = false;
+        m |= 1u << r;
+      }
+      if (!m) continue;
+      if (nu == CH_TB) return fail(h, GLE_ERR_UNSUP, "chain plan: more than 3 baths meet one 16-DOF tile");
+      const int u = nu++;
+      T.tb[u] = j;
+      T.bmask[u] = m;
+      T.boff[u] = affine ? off : CH_INV;
+      Seg y{u, b.d_K0d + b.tofs[rt], 64, nullptr, (int)B, 0, 0, b.nks};
+      if (stage == 0) {
+        y.X = b.d_H;
+        y.ldx = (int)b.ldh;
+        y.ring = b.R;
+      } else {
+        y.X = b.d_Xcur + (stage == 2 ? b.vs : 0);
+      }
+      segs.push_back(y);
+      if (b.has_q && stage < 2)
+        qsegs.push_back(Seg{CH_TB + u, b.d_Kqd + b.tofs[rt], 64, b.d_Xq + (stage == 1 ? b.vs : 0), (int)B, 0, 0, b.nks});
+    }
+    segs.insert(segs.end(), qsegs.begin(), qsegs.end());
+    if (withD && h->has_dyn && stage < 2) {
+      int64_t o = h->dyn_tofs[rt];
+      for (auto& r : h->dyn_rng[rt]) {
+        segs.push_back(Seg{2 * CH_TB, h->d_dynd + o, 64, (stage == 0 ? h->d_Q : h->d_Qt) + (int64_t)4 * r.first * B,
+                           (int)B, 0, 0, r.second});
+        o += (int64_t)r.second * 64;
+      }
+    }
+    int64_t W = 0;
+    for (auto& sg : segs) W += sg.nks;
+    int rc = fill_tasks(h, T, segs, CH_NOUT, 0, W, &c.flops);
+    if (rc) return rc;
+    c.tiles.push_back(T);
+    return GLE_OK;
+  };
+  for (int v = 0; v < 2; ++v) {
+    for (Chain* c : {&h->chA[v], &h->chB[v]}) {
+      c->tiles.clear();
+      c->flops = 0;
+    }
+  }
+  h->chC.tiles.clear();
+  h->chC.flops = 0;
+  h->chNear.tiles.clear();
+  for (int rt = 0; rt < ntile; ++rt)
+    for (int ct = 0; ct < ncol1; ++ct) {
+      int rc = 0;
+      for (int v = 0; v < 2 && !rc; ++v) {
+        rc = dof_tile(0, v == 1, rt, ct, h->chA[v]);
+        if (!rc) rc = dof_tile(1, v == 1, rt, ct, h->chB[v]);
+      }
+      if (!rc) rc = dof_tile(2, false, rt, ct, h->chC);
+      if (rc) return rc;
+    }
+  // S(t+1) tiles (chain A): K_1.p_t + near-field partials + levels, per bath row tile
+  for (int j = 0; j < nb; ++j) {
+    Bath& b = h->baths[j];
+    if (b.ml < 2) continue;
+    for (int rt = 0; rt < b.nrt; ++rt)
+      for (int ct = 0; ct < ncol1; ++ct) {
+        ChTile T{};
+        T.kind = CH_SFIN;
+        T.rn = 1;
+        T.row0 = 16 * rt;
+        T.c0 = 16 * ct;
+        T.tile = j;
+        T.nrows = std::min(16, b.nc - 16 * rt);
+        T.ncols = (int)std::min<int64_t>(16, B - 16 * ct);
+        std::vector<Seg> segs{Seg{0, b.d_Kn + ((int64_t)rt * b.nks * b.nn + 1) * 64, b.nn * 64, b.d_H, (int)b.ldh,
+                                  b.R, 0, b.nks}};
+        for (int v = 0; v < 2; ++v) {
+          int rc = fill_tasks(h, T, segs, 1, 0, b.nks, &h->chA[v].flops);
+          if (rc) return rc;
+          h->chA[v].tiles.push_back(T);
+        }
+      }
+  }
+  // near-field partial tiles (chains B and C, alternating items)
+  for (int j = 0; j < nb; ++j) {
+    Bath& b = h->baths[j];
+    if (b.nqn == 0) continue;
+    std::vector<Seg> base;
+    for (int i = 2; i < b.nn; ++i)
+      base.push_back(Seg{0, nullptr, b.nn * 64, b.d_H, (int)b.ldh, b.R, 2 - i, b.nks});
+    const int64_t W = (int64_t)(b.nn - 2) * b.nks;
+    for (int rt = 0; rt < b.nrt; ++rt) {
+      std::vector<Seg> segs = base;
+      for (int i = 2; i < b.nn; ++i) segs[i - 2].A = b.d_Kn + ((int64_t)rt * b.nks * b.nn + i) * 64;
+      for (int ct = 0; ct < ncolr; ++ct)
+        for (int q = 0; q < b.nqn; ++q) {
+          ChTile T{};
+          T.kind = CH_RAW;
+          T.rn = rn_raw;
+          T.row0 = 16 * rt;
+          T.c0 = nt_raw * ct;
+          T.tile = j;
+          T.nrows = std::min(16, b.nc - 16 * rt);
+          T.ncols = (int)std::min<int64_t>(nt_raw, B - T.c0);
+          T.par_shift = 2;
+          T.par_stride = (int64_t)b.nqn * b.vs;
+          T.dst = b.d_NP + (int64_t)q * b.vs + (int64_t)16 * rt * B + T.c0;
+          T.ldd = (int)B;
+          Chain& c = (q & 1) ? h->chC : h->chB[0];
+          const double f0 = c.flops;
+          int rc = fill_tasks(h, T, segs, 1, W * q / b.nqn, W * (q + 1) / b.nqn, &c.flops);
+          if (rc) return rc;
+          c.tiles.push_back(T);
+          if (!(q & 1)) {
+            h->chB[1].tiles.push_back(T);
+            h->chB[1].flops += c.flops - f0;
+          }
+          h->chNear.tiles.push_back(T);
+        }
+    }
+  }
+  for (Chain* c : {&h->chA[0], &h->chA[1], &h->chB[0], &h->chB[1], &h->chC, &h->chNear}) {
+    int rc = upload_chain(h, *c);
+    if (rc) return rc;
+  }
+  return GLE_OK;
+}
+
 int freeze(gle_handle* h) {
   if (h->frozen) return GLE_OK;
   const int64_t B = h->B;
@@ -710,68 +989,18 @@ int freeze(gle_handle* h) {
     for (int q = 0; q < 2; ++q)
       HIPCHK(h, hipEventCreateWithFlags(&lv.ev[q], hipEventDisableTiming | hipEventReleaseToDevice));
   }
-  // StepDev
-  StepDev sd{};
-  sd.nph = (int32_t)h->nph;
-  sd.B = (int32_t)B;
-  sd.nmd = (int32_t)h->nmd;
-  sd.nbath = (int32_t)h->baths.size();
-  sd.dt = h->dt;
-  sd.P = h->d_P;
-  sd.Q = h->d_Q;
-  sd.Ph = h->d_Ph;
-  sd.Qt = h->d_Qt;
-  sd.G = nullptr;
-  sd.Fc = h->d_Fc;
-  sd.Flast = h->d_Flast;
-  sd.etot = h->d_etot;
-  sd.Q0 = h->d_Q0;
-  sd.qvalid = h->d_qvalid;
-  sd.Ypot = h->d_Ypot;
-  // DOF chunking of the phase kernels: ~ one 256-thread block per 64x(256/BT) elements
-  const int BT = (int)std::min<int64_t>(B, 64);
-  const int DL = 256 / BT;
-  // two DOFs per thread: enough blocks to fill the chip for the elementwise phases
-  h->dchunk = 2 * DL;
-  h->ndblk = (int)((h->nph + h->dchunk - 1) / h->dchunk);
-  sd.ndblk = h->ndblk;
-  sd.dchunk = h->dchunk;
+  // DOF tiles of the chain (16 DOFs each) = rows of the per-step current / energy partial table
+  h->ndblk = (int)((h->nph + 15) / 16);
   int rc = dalloc_n(h, &h->d_part, (size_t)h->nmd * h->ndblk * (h->baths.size() + 1) * B);
   if (rc) return rc;
-  sd.part = h->d_part;
   rc = dalloc_n(h, &h->d_pmax, (size_t)4 * B);
   if (rc) return rc;
-  sd.pmax = h->d_pmax;
   // constraint mask
   std::vector<uint8_t> mask(h->nph, 0);
   for (auto d : h->constr) mask[d] = 1;
   rc = dalloc_n(h, &h->d_cmask, h->nph);
   if (rc) return rc;
   rc = upload(h, h->d_cmask, mask.data(), h->nph);
-  if (rc) return rc;
-  sd.cmask = h->d_cmask;
-  for (size_t j = 0; j < h->baths.size(); ++j) {
-    Bath& b = h->baths[j];
-    BathDev& bd = sd.bath[j];
-    bd.inv = b.d_inv;
-    bd.noise = b.d_noise;
-    bd.Y = b.d_Y;
-    bd.S = b.d_S;
-    bd.Yq = b.d_Yq;
-    bd.Xcur = b.d_Xcur;
-    bd.Xq = b.d_Xq;
-    bd.H = b.d_H;
-    bd.cur = b.d_cur;
-    bd.c = b.c;
-    bd.nc = b.nc;
-    bd.ncp = b.ncp;
-    bd.ldh = (int32_t)b.ldh;
-    bd.R = b.R;
-    bd.has_q = b.has_q ? 1 : 0;
-  }
-  rc = dalloc_n(h, &h->d_sd, 1);
-  if (rc) return rc;
-  rc = upload(h, h->d_sd, &sd, sizeof(sd));
   if (rc) return rc;
 
   // compact copy of the slices every step reads (K_0 and the near field): the full fragment-native
@@ -787,7 +1016,7 @@ int freeze(gle_handle* h) {
   }
 
   // ---- plans
-  const int TGT_STEP = 256, TGT_BIG = 512;
+  const int TGT_BIG = 512;
   auto kgemm = [&](Bath& b, const double* A, int i0, int i1, const double* X, int64_t ldx, int ring,
                    int tshift, int N, double* dst, int64_t ldd) {
     Gemm g{};
@@ -885,111 +1114,59 @@ int freeze(gle_handle* h) {
     rc = p.done();
     if (rc) return rc;
   }
-  // OP0 (+ pot variant) per destination parity: K0 p_t, Kq q_t, [dyn q_t] and the near field
-  // S(t+1) = far(t+1) + sum_{1<=i<L} K_i p_{t+1-i} (only phases B/C need it, but it depends only
-  // on p_t, so it shares this launch)
-  for (int par = 0; par < 2; ++par)
-    for (int variant = 0; variant < 2; ++variant) {
-      Op& op = variant ? h->op0p[par] : h->op0[par];
-      op.tile = true;
-      Planner p(h, op, std::min(rn_step, 4));
-      for (auto& b : h->baths) {
-        p.add(kgemm(b, b.d_Kn, 0, 1, b.d_H, b.ldh, b.R, 0, (int)B, b.d_Y, B), TGT_STEP, 4);
-        if (b.has_q) {
-          Gemm g = kgemm(b, b.d_Kq, 0, 1, b.d_Xq, B, 0, 0, (int)B, b.d_Yq, B);
-          g.a_ks = 64;
-          g.a_rt = (int64_t)b.nks * 64;
-          p.add(g, TGT_STEP, 4);
-        }
-      }
-      if (variant && h->has_dyn) {
-        Gemm g{};
-        g.A = h->d_dyn;
-        g.a_ks = 64;
-        g.a_rt = (int64_t)h->dyn_nks * 64;
-        g.nrt_total = h->dyn_nrt;
-        g.nks_total = h->dyn_nks;
-        g.i0 = 0;
-        g.i1 = 1;
-        g.X = h->d_Q;
-        g.ldx = B;
-        g.M = (int)h->nph;
-        g.Kd = (int)h->nph;
-        g.N = (int)B;
-        g.dst = h->d_Ypot;
-        g.ldd = B;
-        p.add(g, TGT_STEP, 4);
-      }
-      p.lat = true;
-      for (size_t j = 0; j < h->baths.size(); ++j) {
-        Bath& b = h->baths[j];
-        if (b.ml <= 1) continue;
-        Gemm g{};
-        g.A = b.d_Kn;
-        g.a_ks = (int64_t)b.nn * 64;
-        g.a_rt = (int64_t)b.nks * g.a_ks;
-        g.nrt_total = b.nrt;
-        g.nks_total = b.nks;
-        g.i0 = 1;
-        g.i1 = b.nn;  // near field lags [1, near_end); none: the levels' sum only
-        g.X = b.d_H;
-        g.ldx = b.ldh;
-        g.ring = b.R;
-        g.cs = (int)B;
-        g.tshift = 1;
-        g.M = b.nc;
-        g.Kd = b.nc;
-        g.N = (int)B;
-        g.dst = b.d_S + (int64_t)par * b.ncp * B;
-        g.ldd = B;
-        g.nadd = (int)h->levels.size();
-        for (size_t l = 0; l < h->levels.size(); ++l) {
-          const LevelBath& L = h->levels[l].lb[j];
-          g.adds[l] = L.active ? L.d_out : nullptr;
-          g.add_ld[l] = 2 * h->levels[l].P * (int32_t)B;
-        }
-        g.force_reduce = true;
-        p.add(g, 256, 4);
-      }
-      rc = p.done();
-      if (rc) return rc;
+  rc = plan_chain(h);
+  if (rc) return rc;
+  // device step descriptor
+  StepDev sd{};
+  sd.nph = (int32_t)h->nph;
+  sd.B = (int32_t)B;
+  sd.nmd = (int32_t)h->nmd;
+  sd.nbath = (int32_t)h->baths.size();
+  sd.dt = h->dt;
+  sd.P = h->d_P;
+  sd.Q = h->d_Q;
+  sd.Ph = h->d_Ph;
+  sd.Qt = h->d_Qt;
+  sd.Fc = h->d_Fc;
+  sd.Flast = h->d_Flast;
+  sd.etot = h->d_etot;
+  sd.Q0 = h->d_Q0;
+  sd.qvalid = h->d_qvalid;
+  sd.pmax = h->d_pmax;
+  sd.part = h->d_part;
+  sd.cmask = h->d_cmask;
+  sd.ndblk = h->ndblk;
+  for (size_t j = 0; j < h->baths.size(); ++j) {
+    Bath& b = h->baths[j];
+    BathDev& bd = sd.bath[j];
+    bd.inv = b.d_inv;
+    bd.noise = b.d_noise;
+    bd.S = b.d_S;
+    bd.Yq = b.d_Yq;
+    bd.Xcur = b.d_Xcur;
+    bd.Xq = b.d_Xq;
+    bd.H = b.d_H;
+    bd.cur = b.d_cur;
+    bd.NP = b.d_NP;
+    bd.nlvl = (int32_t)h->levels.size();
+    for (size_t l = 0; l < h->levels.size(); ++l) {
+      const LevelBath& L = h->levels[l].lb[j];
+      bd.lvl[l] = L.active ? L.d_out : nullptr;
+      bd.lvl_ld[l] = 2 * h->levels[l].P * (int32_t)B;
     }
-  // OP1a (+/- pot), OP1b
-  for (int variant = 0; variant < 3; ++variant) {
-    Op& op = variant == 0 ? h->op1a : (variant == 1 ? h->op1a_np : h->op1b);
-    op.tile = true;
-    Planner p(h, op, std::min(rn_step, 4));
-    for (auto& b : h->baths) {
-      Gemm g = kgemm(b, b.d_Kn, 0, 1, b.d_Xcur, B, 0, 0, (int)B, b.d_Y, B);
-      p.add(g, TGT_STEP, 4);
-      if (b.has_q && variant < 2) {
-        Gemm gq = kgemm(b, b.d_Kq, 0, 1, b.d_Xq, B, 0, 0, (int)B, b.d_Yq, B);
-        gq.a_ks = 64;
-        gq.a_rt = (int64_t)b.nks * 64;
-        p.add(gq, TGT_STEP, 4);
-      }
-    }
-    if (variant == 0 && h->has_dyn) {
-      Gemm g{};
-      g.A = h->d_dyn;
-      g.a_ks = 64;
-      g.a_rt = (int64_t)h->dyn_nks * 64;
-      g.nrt_total = h->dyn_nrt;
-      g.nks_total = h->dyn_nks;
-      g.i0 = 0;
-      g.i1 = 1;
-      g.X = h->d_Qt;
-      g.ldx = B;
-      g.M = (int)h->nph;
-      g.Kd = (int)h->nph;
-      g.N = (int)B;
-      g.dst = h->d_Ypot;
-      g.ldd = B;
-      p.add(g, TGT_STEP, 4);
-    }
-    rc = p.done();
-    if (rc) return rc;
+    bd.c = b.c;
+    bd.vs = b.vs;
+    bd.nc = b.nc;
+    bd.ncp = b.ncp;
+    bd.ldh = (int32_t)b.ldh;
+    bd.R = b.R;
+    bd.has_q = b.has_q ? 1 : 0;
+    bd.nqn = b.nqn;
   }
+  rc = dalloc_n(h, &h->d_sd, 1);
+  if (rc) return rc;
+  rc = upload(h, h->d_sd, &sd, sizeof(sd));
+  if (rc) return rc;
   h->frozen = true;
   return GLE_OK;
 }
@@ -1036,7 +1213,7 @@ int prime(gle_handle* h) {
     if (h->t & 1)
       for (auto& b : h->baths)
         if (b.ml > 1)
-          HIPCHK(h, hipMemcpyAsync(b.d_S + (int64_t)b.ncp * h->B, b.d_S, (size_t)b.ncp * h->B * 8,
+          HIPCHK(h, hipMemcpyAsync(b.d_S + b.vs, b.d_S, (size_t)b.ncp * h->B * 8,
                                    hipMemcpyDeviceToDevice, h->stream));
   }
   for (auto& lv : h->levels) {
@@ -1047,6 +1224,8 @@ int prime(gle_handle* h) {
     lv.last_block = k0 + 1;
     lv.bg_block[0] = lv.bg_block[1] = INT64_MIN;
   }
+  // near-field partials of target t+1 (lags >= 2: p up to t-1), as the chain of step t-1 leaves them
+  launch_chain(1, h->chNear.d, (int)h->chNear.tiles.size(), h->d_sd, step_args(h, h->t - 1), 0, h->stream);
   if (!h->levels.empty()) HIPCHK(h, hipEventRecord(h->ev_step, h->stream));
   h->need_prime = false;
   return GLE_OK;
@@ -1087,13 +1266,10 @@ int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
     }
   }
   const bool need_pot = (fpot_host_T == nullptr) && !h->pot_cache_exact;
-  const int par = (int)((t + 1) & 1);
   const StepArgs ta = step_args(h);
-  Op& op0 = need_pot ? h->op0p[par] : h->op0[par];
-  run_op(h, op0, h->stream, ta, h->levels.empty());
   if (fpot_host_T)
     HIPCHK(h, hipMemcpyAsync(h->d_Fc, fpot_host_T, (size_t)h->nph * h->B * 8, hipMemcpyHostToDevice, h->stream));
-  launch_phaseA(h->d_sd, ta, (int)h->B, h->ndblk, need_pot ? 1 : 0, fpot_host_T ? 0 : 1, h->stream);
+  run_chain(h, 0, h->chA[need_pot ? 1 : 0], ta, (need_pot ? 1 : 0) | (fpot_host_T ? 0 : 2), h->levels.empty());
   h->host_force_step = fpot_host_T != nullptr;
   return GLE_OK;
 }
@@ -1102,17 +1278,14 @@ int step_end_impl(gle_handle* h, const double* fpot_host_T) {
   int mode1 = 1;
   const StepArgs ta = step_args(h);
   if (fpot_host_T) {
-    run_op(h, h->op1a_np, h->stream, ta, false);
     HIPCHK(h, hipMemcpyAsync(h->d_Fc, fpot_host_T, (size_t)h->nph * h->B * 8, hipMemcpyHostToDevice, h->stream));
     mode1 = 0;
   } else {
     if (!h->has_dyn) return fail(h, GLE_ERR_STATE, "no potential force at q~");
     if (h->host_force_step) return fail(h, GLE_ERR_STATE, "step begun with a host force must end with one");
-    run_op(h, h->op1a, h->stream, ta, false);
   }
-  launch_phaseB(h->d_sd, ta, (int)h->B, h->ndblk, mode1, h->stream);
-  run_op(h, h->op1b, h->stream, ta, false);
-  launch_phaseC(h->d_sd, ta, (int)h->B, h->ndblk, mode1, mode1, h->stream);
+  run_chain(h, 1, h->chB[mode1], ta, mode1, h->levels.empty());
+  run_chain(h, 2, h->chC, ta, mode1, h->levels.empty());
   // the next step is a block boundary: the background blocks started there wait for this step
   if (!h->levels.empty() && (h->t + 1) % h->P0 == 0) HIPCHK(h, hipEventRecord(h->ev_step, h->stream));
   h->t += 1;
@@ -1212,7 +1385,6 @@ int gle_create(const gle_config* cfg, gle_handle** out) {
   rc |= dalloc_n(h, &h->d_Fc, nst);
   rc |= dalloc_n(h, &h->d_Flast, nst);
   rc |= dalloc_n(h, &h->d_Q0, nst);
-  rc |= dalloc_n(h, &h->d_Ypot, nst);
   rc |= dalloc_n(h, &h->d_etot, (size_t)h->nmd * h->B);
   rc |= dalloc_n(h, &h->d_qvalid, (size_t)h->B);
   if (rc) {
@@ -1314,20 +1486,21 @@ int gle_add_bath(gle_handle* h, int32_t kind, const int64_t* cids, int64_t nc, i
       if (rc) return rc;
     }
   }
-  std::vector<int32_t> inv(h->nph, -1);
-  for (int64_t k = 0; k < nc; ++k) inv[cids[k]] = (int32_t)k;
+  b.inv.assign(h->nph, -1);
+  for (int64_t k = 0; k < nc; ++k) b.inv[cids[k]] = (int32_t)k;
   const int64_t B = h->B;
   const size_t nbuf = (size_t)(b.ncp + 64) * B + 1024;
+  b.vs = (int64_t)nbuf;
   rc |= dalloc_n(h, &b.d_inv, (size_t)h->nph);
-  if (!rc) rc = upload(h, b.d_inv, inv.data(), inv.size() * 4);
+  if (!rc) rc = upload(h, b.d_inv, b.inv.data(), b.inv.size() * 4);
   rc |= dalloc_n(h, &b.d_noise, (size_t)h->nmd * nc * B);
-  rc |= dalloc_n(h, &b.d_Y, nbuf);
   rc |= dalloc_n(h, &b.d_S, 2 * nbuf);
-  rc |= dalloc_n(h, &b.d_Xcur, nbuf);
-  rc |= dalloc_n(h, &b.d_Xq, nbuf);
+  rc |= dalloc_n(h, &b.d_Xcur, 2 * nbuf);
+  rc |= dalloc_n(h, &b.d_Xq, 2 * nbuf);
   rc |= dalloc_n(h, &b.d_cur, (size_t)h->nmd * B);
   if (b.has_q) rc |= dalloc_n(h, &b.d_Yq, nbuf);
   if (rc) return GLE_ERR_NOMEM;
+  b.K0.assign(b.K.begin(), b.K.begin() + nc * nc);
   b.K.clear();
   b.K.shrink_to_fit();
   h->baths.push_back(std::move(b));
@@ -1341,6 +1514,7 @@ int gle_set_dyn(gle_handle* h, const double* dyn) {
   hipSetDevice(h->cfg.device);
   h->dyn_nrt = (int)((h->nph + 15) / 16);
   h->dyn_nks = (int)(h->nphp / 4);
+  h->dyn_h.assign(dyn, dyn + h->nph * h->nph);
   std::vector<double> f = pack_frags(dyn, 1, h->nph, h->nph, h->dyn_nrt, h->dyn_nks);
   int rc = dalloc_n(h, &h->d_dyn, f.size());
   if (!rc) rc = upload(h, h->d_dyn, f.data(), f.size() * 8);

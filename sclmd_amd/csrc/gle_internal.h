@@ -52,29 +52,6 @@ struct CItem {
   int64_t a_im, x_im, o_im;
 };
 
-// One share of a 16-row output tile of a latency-bound per-step product.  The tile's slice x
-// k-step space is split over ngrp workgroups of 4 waves; waves reduce through LDS, groups through
-// partial slots summed in fixed order by the last group to arrive (far / mid addends in its
-// epilogue).  Same operand conventions as CItem.
-struct TItem {
-  double* part;        // [ngrp][256*RN] partial slots of this tile (ngrp > 1)
-  unsigned* cnt;       // arrival counter of this tile (ngrp > 1)
-  const double* A;     // fragment base for (row tile, k-step 0, slice ia)
-  const double* X;     // X base (row 0)
-  double* out;         // tile output (row 0 of the tile, column 0)
-  const double* add[MAXLVL];  // level block buffers (row 0 of the tile; the step's column
-                              // offset is StepArgs::lvl_off), first nadd used
-  int64_t a_ks;        // doubles between k-steps in A (slice stride is 64)
-  int64_t ldx;
-  int32_t add_ld[MAXLVL];
-  int32_t nadd;
-  int32_t ldo;
-  int32_t ia, ni, nks; // slices [ia, ia+ni), k-steps
-  int32_t ring, cs, tshift;
-  int32_t nrows, ncols;
-  int32_t grp, ngrp;   // this workgroup's share, number of shares
-};
-
 // Deterministic fixed-order sum of split partial tiles (+ optional far-field addend).
 struct RItem {
   double* dst;
@@ -91,34 +68,93 @@ struct RItem {
 struct BathDev {
   const int32_t* inv;  // [nph] -> bath-local index k or -1
   const double* noise; // [nmd][nc][B]
-  double* Y;           // K0 . x       [ncp][B]
-  double* S;           // memory sums S(t) double buffer [2][ncp][B]
-  double* Yq;          // q-channel K . q (biased ebath) [ncp][B] or nullptr
-  double* Xcur;        // gathered x (p half / p1) [ncp][B]
-  double* Xq;          // gathered q [ncp][B]
+  double* S;           // memory sums S(t) double buffer [2][ncp][B] (parity of t)
+  double* Yq;          // Kq . q~ (biased ebath) [ncp][B], chain B -> C
+  double* Xcur;        // gathered p half (buffer 0) / p1 (buffer 1), [2][ncp][B]
+  double* Xq;          // gathered q_t (buffer 0) / q~ (buffer 1), [2][ncp][B]
   double* H;           // history ring
   double* cur;         // heat current [nmd][B]
+  double* NP;          // near-field partial slots [2 parity][nqn][ncp][B] (lags [2, nn))
+  const double* lvl[MAXLVL];  // ladder level block buffers [ncp][2 P B] (nullptr: inactive)
+  int32_t lvl_ld[MAXLVL];
   double c;            // dt factor (dt if ml > 1 else 1, baths.py:454-457)
+  int64_t vs;          // doubles between the buffers of S / Xcur / Xq and between NP slots
   int32_t nc, ncp;
   int32_t ldh, R;
   int32_t has_q;
+  int32_t nqn;         // near-field partial slots per parity
+  int32_t nlvl;
   int32_t pad;
 };
 
 struct StepDev {
   int32_t nph, B, nmd, nbath;
   double dt;
-  double *P, *Q, *Ph, *Qt, *G, *Fc, *Flast, *etot;
+  double *P, *Q, *Ph, *Qt, *Fc, *Flast, *etot;
   double* Q0;             // last q the potential force was evaluated at (md.q0)
   int32_t* qvalid;        // [B] md.q0 != [] flag
-  double* Ypot;           // dyn . x of the latest potential product [nph][B]
   unsigned long long* pmax;  // [2 (id0,id1)][2 (parity)][B] max |x - q0| as ordered bit patterns
   double* part;           // [nmd][ndblk][nbath+1][B] current / energy partial sums per step
   const uint8_t* cmask;   // [nph] constraint mask
-  int32_t ndblk;          // DOF chunks of the phase kernels
-  int32_t dchunk;         // DOFs per chunk
+  int32_t ndblk;          // DOF tiles (16 DOFs each) = current partial rows per step
+  int32_t pad;
   BathDev bath[MAXBATH];
 };
+
+// ---- per-step chain (gle_chain.hip) ------------------------------------------------------
+// One md.vv is three launches A, B, C.  Every workgroup is one ChTile: a 16-row x 16*rn-column
+// output tile whose products are split over the 4 waves by k-steps (each wave's run of tasks
+// accumulates into an LDS partial slot; the epilogue adds the slots of an output in fixed order),
+// followed by an epilogue of its kind:
+//   CH_DOF   16 DOFs x 16 trajectories: the phase of md.vv for those elements (A: bath forces at
+//            t, heat current, half kick, drift; B: first velocity iteration; C: second iteration,
+//            constraints, history push)
+//   CH_SFIN  16 bath rows: S(t+1) = K_1 p_t + near-field partials + ladder levels
+//   CH_RAW   16 bath rows x 16*rn columns of a near-field partial (lags >= 2, target t+2)
+constexpr int CH_NW = 4;        // waves per chain workgroup
+constexpr int CH_TPW = 4;       // tasks per wave
+constexpr int CH_TB = 3;        // baths a DOF tile may intersect
+constexpr int CH_NOUT = 2 * CH_TB + 1;
+constexpr int CH_LDS = 4096;    // doubles of LDS partial slots (32 KB)
+constexpr int CH_NPMAX = 32;    // near-field partial slots read by one SFIN element
+enum { CH_DOF = 0, CH_SFIN = 1, CH_RAW = 2 };
+
+struct ChTask {
+  const double* A;   // fragment of the first k-step (lane offset added in the kernel)
+  const double* X;   // X at row 4 * (first k-step), column 0
+  int32_t a_ks;      // doubles between consecutive k-steps of A
+  int32_t ldx;       // X row stride (doubles)
+  int32_t nks;       // k-steps
+  int32_t ring;      // ring slots R of a history-ring X (0: static X)
+  int32_t tshift;    // ring: column slot pmod(t + tshift, ring)
+  int32_t slot;      // LDS partial slot
+};
+
+struct ChTile {
+  int32_t kind;      // CH_DOF / CH_SFIN / CH_RAW
+  int32_t rn;        // 16-column MFMA tiles (1, 2 or 4)
+  int32_t row0;      // CH_DOF: first DOF; otherwise first bath-local row
+  int32_t c0;        // first trajectory column
+  int32_t tile;      // CH_DOF: DOF-tile index (current partial row); otherwise the bath
+  int32_t nrows, ncols;  // valid rows / columns of the tile
+  int32_t par_shift; // CH_RAW: destination parity buffer ((t + par_shift) & 1)
+  int64_t par_stride;// CH_RAW: doubles between the parity buffers of dst
+  double* dst;       // CH_RAW: row 0, column 0 of the tile in parity buffer 0
+  int32_t ldd;
+  int32_t first;     // CH_DOF: the tile that zeroes the other-parity cache words
+  int8_t ntw[CH_NW]; // tasks of wave w
+  int8_t ob[CH_NOUT + 1];  // output o adds LDS slots [ob[o], ob[o+1]); outputs: Y of tile bath u
+                           // (u < CH_TB), YQ of tile bath u (CH_TB + u), YD (2 CH_TB);
+                           // CH_SFIN / CH_RAW use output 0
+  int8_t pad[8 - (CH_NW + CH_NOUT + 1) % 8];
+  // CH_DOF: the tile's baths tb[u] (-1: none); DOF row0 + r is in bath tb[u] iff bit r of bmask[u];
+  // bath-local k = DOF + boff[u] (CH_INV: k from the bath's inv table)
+  int32_t tb[CH_TB];
+  uint32_t bmask[CH_TB];
+  int32_t boff[CH_TB];
+  ChTask task[CH_NW][CH_TPW];
+};
+constexpr int32_t CH_INV = -0x40000000;
 
 // launchers (gle_kernels.hip)
 // Every kernel takes the step counter by value: the host knows md.t and the steps at which the
@@ -130,17 +166,16 @@ struct StepArgs {
 void launch_contract(int rn, int cu, const CItem* items, int nitems, StepArgs ta, hipStream_t s);
 void launch_reduce(const RItem* items, int nitems, int max_elems, StepArgs ta,
                    hipStream_t s);
-void launch_phaseA(const StepDev* sd, StepArgs ta, int B, int ndblk, int mode0, int diff1,
-                   hipStream_t s);
-void launch_phaseB(const StepDev* sd, StepArgs ta, int B, int ndblk, int mode1, hipStream_t s);
-void launch_phaseC(const StepDev* sd, StepArgs ta, int B, int ndblk, int mode1, int diff0,
-                   hipStream_t s);
+// stage 0/1/2 = A/B/C.  mode: A: 1 = harmonic id0 potential with md.potforce's cache rule (YD = dyn.q_t
+// present), 0 = potential force at q_t already in Fc; bit 1: write the id1 cache distance.
+// B / C: 1 = harmonic force at q~ (B computes YD = dyn.q~), 0 = host force in Fc.
+void launch_chain(int stage, const ChTile* tiles, int ntiles, const StepDev* sd, StepArgs ta, int mode,
+                  hipStream_t s);
 void launch_finalize(const StepDev* sd, int B, int nmd, int nbath, hipStream_t s);
 void launch_philox_normal(double* x, int64_t nfreq, int64_t ncp, int64_t nc, int64_t B,
                           uint64_t seed, uint64_t traj_offset, hipStream_t s);
 void launch_ring_copy(double* H, int64_t ldh, int R, int B, int nc, int64_t tau0, int nt, double* buf,
                       int dir, hipStream_t s);
-void launch_tile(int rn, const TItem* items, int nitems, StepArgs ta, hipStream_t s);
 void launch_contract_cplx(int rn, const CItem* items, int nitems, StepArgs ta, hipStream_t s);
 void launch_khat_pack(const double* Kf, int ml, int nks_k, double* khat, int P, int m0, int M,
                       int nc, int nrt2, int nks2, const double* cstab, int cstride, hipStream_t s);

@@ -6,10 +6,8 @@
 //                       the velocity-history ring staged once per k-chunk in LDS and shared by the
 //                       4 waves (one 16-row tile each) across all slices of the work item.
 //  reduce_kernel        fixed-order sum of split-K / split-slice partial tiles (+ far field).
-//  potsel_kernel        md.potforce's cache rule (sameq, md.py:449-450, 767-779) per trajectory.
-//  phaseA/B/C_kernel    the elementwise parts of md.vv (md.py:383-411): bath-force assembly
-//                       (baths.py:232-255, 452-458), heat current (md.py:397), Verlet kicks,
-//                       constraints (md.py:782-794), history push (md.py:386-387).
+//  finalize_kernel      heat current / kinetic energy per step from the chain's partial table.
+//  (the per-step chain of md.vv is in gle_chain.hip)
 //  philox / fft_noise   coloured-noise generator (noise.py:50-100, 149-206).
 #include <hip/hip_runtime.h>
 
@@ -332,168 +330,6 @@ void launch_contract(int rn, int cu, const CItem* items, int nitems, StepArgs ta
 }
 
 // ------------------------------------------------------------------------------------------
-// Latency-optimised per-step products.  Work step s in [0, ni*nks) is (slice s / nks, k-step
-// s % nks); share g of ngrp owns [g*S/ngrp, (g+1)*S/ngrp), split contiguously over the 4 waves.
-// Operands come straight from global memory (L2/MALL-resident per-step data).
-constexpr int TILE_NW = 4;
-constexpr int TILE_U = 8;  // work steps per wave with all operand loads in flight
-template <int RN>
-__global__ __launch_bounds__(TILE_NW * 64) void tile_kernel(const TItem* __restrict__ items,
-                                                            StepArgs ta) {
-  __shared__ double red[(TILE_NW / 2) * 256 * RN];
-  __shared__ unsigned last;
-  const TItem& it = items[blockIdx.x];  // read in place: the addend arrays are indexed dynamically
-  const int wave = threadIdx.x >> 6;
-  const int lane = threadIdx.x & 63;
-  const int brow = lane >> 4, bcol = lane & 15;
-  const int64_t t = ta.t;
-  d4 acc[RN];
-#pragma unroll
-  for (int n = 0; n < RN; ++n) acc[n] = d4{0.0, 0.0, 0.0, 0.0};
-  const int64_t S = (int64_t)it.ni * it.nks;
-  const int64_t g0 = S * it.grp / it.ngrp, g1 = S * (it.grp + 1) / it.ngrp;
-  const int s0 = (int)(g0 + (g1 - g0) * wave / TILE_NW), s1 = (int)(g0 + (g1 - g0) * (wave + 1) / TILE_NW);
-  const int tm = it.ring ? (int)pmod(t + it.tshift - it.ia, it.ring) : 0;
-  for (int sb = s0; sb < s1; sb += TILE_U) {
-    double a[TILE_U], b[TILE_U][RN];
-#pragma unroll
-    for (int u = 0; u < TILE_U; ++u) {
-      const int s = sb + u;
-      a[u] = 0.0;
-#pragma unroll
-      for (int n = 0; n < RN; ++n) b[u][n] = 0.0;
-      if (s < s1) {
-        const int i = s / it.nks, ks = s - i * it.nks;
-        a[u] = gld(it.A + (int64_t)ks * it.a_ks + (int64_t)i * 64 + lane);
-        int64_t cb = 0;
-        if (it.ring) {
-          int c = tm - i;
-          if (c < 0) c += it.ring;
-          cb = (int64_t)c * it.cs;
-        }
-        const double* xr = it.X + (int64_t)(4 * ks + brow) * it.ldx + cb + bcol;
-#pragma unroll
-        for (int n = 0; n < RN; ++n) b[u][n] = gld(xr + 16 * n);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < TILE_U; ++u)
-#pragma unroll
-      for (int n = 0; n < RN; ++n) acc[n] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b[u][n], acc[n], 0, 0, 0);
-  }
-  // fixed-order tree over the waves
-#pragma unroll
-  for (int half = TILE_NW / 2; half >= 1; half >>= 1) {
-    if (wave >= half && wave < 2 * half) {
-      double* r = red + (wave - half) * 256 * RN;
-#pragma unroll
-      for (int n = 0; n < RN; ++n)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) r[(n * 4 + q) * 64 + lane] = acc[n][q];
-    }
-    __syncthreads();
-    if (wave < half) {
-      const double* r = red + wave * 256 * RN;
-#pragma unroll
-      for (int n = 0; n < RN; ++n)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc[n][q] += r[(n * 4 + q) * 64 + lane];
-    }
-    __syncthreads();
-  }
-  if (it.ngrp == 1) {
-    if (wave == 0) {
-#pragma unroll
-      for (int n = 0; n < RN; ++n)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) red[(n * 4 + q) * 64 + lane] = acc[n][q];
-    }
-    __syncthreads();
-  } else {
-    // publish this share; the last share to arrive sums all shares in share order.  Partials move
-    // through agent-coherent (L2-bypassing) atomic stores / loads, so no cache-wide fence is
-    // needed (an agent-scope fence writes back and invalidates the XCD's L2, evicting the kernel
-    // slices the other workgroups stream).
-    if (wave == 0) {
-      double* slot = it.part + (int64_t)it.grp * 256 * RN;
-#pragma unroll
-      for (int n = 0; n < RN; ++n)
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          __hip_atomic_store(slot + (n * 4 + q) * 64 + lane, acc[n][q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_s_waitcnt(0);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const unsigned old = __hip_atomic_fetch_add(it.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last = (old == (unsigned)it.ngrp - 1) ? 1u : 0u;
-      if (last) __hip_atomic_store(it.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if (!last) return;
-  }
-  // epilogue addends: the ladder levels' blocks at target t+1 (all loads issued together)
-  double pre[RN];
-  {
-    double av[MAXLVL][RN];
-#pragma unroll
-    for (int a = 0; a < MAXLVL; ++a) {
-      const double* ap = a < it.nadd ? it.add[a] : nullptr;
-      const int64_t off = ap ? ta.lvl_off[a] : 0;
-      const int ld = it.add_ld[a];
-#pragma unroll
-      for (int j = 0; j < RN; ++j) {
-        const int e = j * TILE_NW * 64 + threadIdx.x;  // element (n*4+q)*64 + lane'
-        const int nq = e >> 6, ln = e & 63;
-        const int row = (ln >> 4) + 4 * (nq & 3), col = 16 * (nq >> 2) + (ln & 15);
-        av[a][j] = (ap && row < it.nrows && col < it.ncols) ? gld(ap + off + (int64_t)row * ld + col) : 0.0;
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < RN; ++j) {
-      double v = 0.0;
-#pragma unroll
-      for (int a = 0; a < MAXLVL; ++a) v += av[a][j];
-      pre[j] = v;
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < RN; ++j) {
-    const int e = j * TILE_NW * 64 + threadIdx.x;
-    double v = 0.0;
-    if (it.ngrp == 1) {
-      v = red[e];
-    } else {
-      double* p = it.part + e;
-      int g = 0;
-      for (; g + 4 <= it.ngrp; g += 4) {
-        const double x0 = __hip_atomic_load(p + (int64_t)(g + 0) * 256 * RN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const double x1 = __hip_atomic_load(p + (int64_t)(g + 1) * 256 * RN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const double x2 = __hip_atomic_load(p + (int64_t)(g + 2) * 256 * RN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const double x3 = __hip_atomic_load(p + (int64_t)(g + 3) * 256 * RN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        v += x0;
-        v += x1;
-        v += x2;
-        v += x3;
-      }
-      for (; g < it.ngrp; ++g) v += __hip_atomic_load(p + (int64_t)g * 256 * RN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    const int nq = e >> 6, ln = e & 63;
-    const int row = (ln >> 4) + 4 * (nq & 3), col = 16 * (nq >> 2) + (ln & 15);
-    if (row < it.nrows && col < it.ncols) it.out[(int64_t)row * it.ldo + col] = pre[j] + v;
-  }
-}
-
-void launch_tile(int rn, const TItem* items, int nitems, StepArgs ta, hipStream_t s) {
-  if (nitems <= 0) return;
-  switch (rn) {
-    case 1: tile_kernel<1><<<nitems, TILE_NW * 64, 0, s>>>(items, ta); break;
-    case 2: tile_kernel<2><<<nitems, TILE_NW * 64, 0, s>>>(items, ta); break;
-    default: tile_kernel<4><<<nitems, TILE_NW * 64, 0, s>>>(items, ta); break;
-  }
-}
-
-// ------------------------------------------------------------------------------------------
 // grid (item, chunk): each block sums RED_PER_BLOCK consecutive elements of one tile over all of
 // its partial slots in slot order (deterministic).
 constexpr int RED_PER_BLOCK = 256;
@@ -554,260 +390,6 @@ void launch_reduce(const RItem* items, int nitems, int max_elems, StepArgs ta,
   reduce_kernel<<<g, 256, 0, s>>>(items, ta);
 }
 
-// ------------------------------------------------------------------------------------------
-// Thread mapping shared by the per-step kernels: a block owns BT = min(B, 64) consecutive
-// trajectories (fastest index, so lanes are coalesced) and DL = 256/BT DOF lanes; blockIdx.y
-// selects a chunk of DOFs.
-struct Lanes {
-  int BT, DL, bl, dl, b;
-  bool ok;
-  __device__ Lanes(int B) {
-    BT = B < 64 ? B : 64;
-    DL = WG / BT;
-    bl = threadIdx.x % BT;
-    dl = threadIdx.x / BT;
-    b = blockIdx.x * BT + bl;
-    ok = (dl < DL) && (b < B);
-  }
-};
-
-// md.potforce's cache (md.py:449-450, 767-779) for the harmonic force, per trajectory: hit iff the
-// cache is valid and max_d |q - q0| < 1e-9.  The max over all DOFs is one word per trajectory,
-// accumulated with atomicMax on the bit pattern (non-negative doubles order like their bits; a NaN
-// pattern exceeds every finite value and reads back as NaN -> miss).  Words are double-buffered by
-// step parity and zeroed one kernel ahead of their producer.
-__device__ __forceinline__ unsigned long long* pmax_word(const StepDev* sd, int id, int par, int b) {
-  return sd->pmax + ((int64_t)(id * 2 + par)) * sd->B + b;
-}
-
-__device__ __forceinline__ bool pot_hit(const StepDev* sd, int id, int par, int b, bool need_valid) {
-  if (need_valid && sd->qvalid[b] == 0) return false;
-  const double m = __longlong_as_double((long long)*pmax_word(sd, id, par, b));
-  return m == m && m < 10e-10;
-}
-
-// block max of v over the DOF lanes of each trajectory, then one atomicMax per trajectory
-__device__ __forceinline__ void block_max_atomic(const StepDev* sd, const Lanes& L, double v, int id,
-                                                 int par, double* red) {
-  red[threadIdx.x] = L.ok ? v : 0.0;
-  __syncthreads();
-  if (L.dl == 0 && L.ok) {
-    double m = 0.0;
-    bool nan = false;
-    for (int x = 0; x < L.DL; ++x) {
-      const double w = red[x * L.BT + L.bl];
-      nan |= (w != w);
-      m = fmax(m, w);
-    }
-    const unsigned long long bits = nan ? 0x7FF8000000000000ull : (unsigned long long)__double_as_longlong(m);
-    atomicMax(pmax_word(sd, id, par, L.b), bits);
-  }
-  __syncthreads();
-}
-
-// bath force of bath j at DOF-local index k (baths.py:232-255, 452-458):
-//   noise[tn] - c*(K0.x + S) - Kq.q   (Kq = -V(exim - zeta1); V*zeta2 folded into K0)
-__device__ __forceinline__ double bath_force(const BathDev& bd, int k, int b, int B, int tn,
-                                             int par) {
-  const int64_t kb = (int64_t)k * B + b;
-  double f = bd.noise[((int64_t)tn * bd.nc + k) * B + b] -
-             bd.c * (bd.Y[kb] + bd.S[(int64_t)par * bd.ncp * B + kb]);
-  if (bd.has_q) f -= bd.Yq[kb];
-  return f;
-}
-
-// mode0: 0 = potential force at q_t already in Fc (exact cache hit or host force)
-//        1 = harmonic: select between the cache and -dyn.q_t (Ypot) per trajectory
-// diff1: write the per-chunk max |q~ - q0| for the id1 cache decision
-__global__ __launch_bounds__(256) void phaseA_kernel(const StepDev* __restrict__ sd, StepArgs ta,
-                                                     int mode0, int diff1) {
-  __shared__ double red[WG];
-  const int B = sd->B, nph = sd->nph, nb = sd->nbath;
-  Lanes L(B);
-  const int64_t t = ta.t;
-  const int tn = (int)(t % sd->nmd);
-  const int par = (int)(t & 1);
-  const double dt = sd->dt, dt2 = dt * dt;
-  const int d0 = blockIdx.y * sd->dchunk;
-  const int d1 = min(nph, d0 + sd->dchunk);
-  const bool hit = (mode0 == 1 && L.ok) ? pot_hit(sd, 0, par, L.b, true) : true;
-  if (L.ok && blockIdx.y == 0 && L.dl == 0) *pmax_word(sd, 0, par ^ 1, L.b) = 0ull;
-  double cur[MAXBATH];
-#pragma unroll
-  for (int j = 0; j < MAXBATH; ++j) cur[j] = 0.0;
-  double e = 0.0, dq = 0.0;
-  if (L.ok)
-    for (int d = d0 + L.dl; d < d1; d += L.DL) {
-      const int64_t i = (int64_t)d * B + L.b;
-      const double p = sd->P[i], q = sd->Q[i];
-      double f;  // potforce(q_t)
-      if (!hit) {
-        f = -1.0 * sd->Ypot[i];  // f = -1.0*mdot(dyn, q)  (md.py:467)
-        sd->Fc[i] = f;
-        sd->Q0[i] = q;
-      } else {
-        f = sd->Fc[i];
-      }
-#pragma unroll
-      for (int j = 0; j < MAXBATH; ++j) {
-        if (j < nb) {
-          const BathDev& bd = sd->bath[j];
-          const int k = bd.inv[d];
-          if (k >= 0) {
-            const double fb = bath_force(bd, k, L.b, B, tn, par);
-            f += fb;           // pf = pf + fbaths[i]   (md.py:432-434)
-            cur[j] += fb * p;  // cur[t] = fbaths[i].p  (md.py:397)
-          }
-        }
-      }
-      e += p * p;
-      const double ph = p + f * dt / 2.0;            // md.py:391
-      const double qt = q + p * dt + f * dt2 / 2.0;  // md.py:392
-      sd->Ph[i] = ph;
-      sd->Qt[i] = qt;
-      if (diff1) dq = fmax(dq, fabs(qt - (hit ? sd->Q0[i] : q)));
-#pragma unroll
-      for (int j = 0; j < MAXBATH; ++j) {
-        if (j < nb) {
-          const BathDev& bd = sd->bath[j];
-          const int k = bd.inv[d];
-          if (k >= 0) {
-            bd.Xcur[(int64_t)k * B + L.b] = ph;
-            if (bd.has_q) bd.Xq[(int64_t)k * B + L.b] = qt;
-          }
-        }
-      }
-    }
-  for (int qd = 0; qd <= nb; ++qd) {
-    double v = e;
-#pragma unroll
-    for (int j = 0; j < MAXBATH; ++j)
-      if (j == qd && j < nb) v = cur[j];
-    red[threadIdx.x] = L.ok ? v : 0.0;
-    __syncthreads();
-    if (L.dl == 0 && L.ok) {
-      double s = 0.0;
-      for (int x = 0; x < L.DL; ++x) s += red[x * L.BT + L.bl];
-      sd->part[(((int64_t)tn * sd->ndblk + blockIdx.y) * (nb + 1) + qd) * B + L.b] = s;
-    }
-    __syncthreads();
-  }
-  if (diff1) block_max_atomic(sd, L, dq, 1, par, red);
-}
-
-// potential force at q~ for DOF d: mode1 0 = in Fc (host force), 1 = harmonic cache select
-__device__ __forceinline__ double pot_qt(const StepDev* sd, int64_t i, bool hit1) {
-  return hit1 ? sd->Fc[i] : -1.0 * sd->Ypot[i];
-}
-
-__device__ __forceinline__ double id1_force(const StepDev* sd, int d, int b, int B, int t1,
-                                            int par1, double fpot) {
-  double f = fpot;
-#pragma unroll
-  for (int j = 0; j < MAXBATH; ++j) {
-    if (j < sd->nbath) {
-      const BathDev& bd = sd->bath[j];
-      const int k = bd.inv[d];
-      if (k >= 0) f += bath_force(bd, k, b, B, t1, par1);
-    }
-  }
-  return f;
-}
-
-__global__ __launch_bounds__(256) void phaseB_kernel(const StepDev* __restrict__ sd, StepArgs ta,
-                                                     int mode1) {
-  const int B = sd->B, nph = sd->nph, nb = sd->nbath;
-  Lanes L(B);
-  const int64_t t = ta.t;
-  const int t1 = (int)((t + 1) % sd->nmd);
-  const int par1 = (int)((t + 1) & 1);
-  const double dt = sd->dt;
-  const int d0 = blockIdx.y * sd->dchunk;
-  const int d1 = min(nph, d0 + sd->dchunk);
-  if (!L.ok) return;
-  const bool hit1 = (mode1 == 1) ? pot_hit(sd, 1, (int)(t & 1), L.b, false) : true;
-  for (int d = d0 + L.dl; d < d1; d += L.DL) {
-    bool inb = false;
-#pragma unroll
-    for (int j = 0; j < MAXBATH; ++j)
-      if (j < nb && sd->bath[j].inv[d] >= 0) inb = true;
-    if (!inb) continue;  // p1 only feeds the bath friction terms
-    const int64_t i = (int64_t)d * B + L.b;
-    const double f = id1_force(sd, d, L.b, B, t1, par1, pot_qt(sd, i, hit1));
-    const double p1 = sd->Ph[i] + dt * f / 2.0;  // md.py:402
-#pragma unroll
-    for (int j = 0; j < MAXBATH; ++j) {
-      if (j < nb) {
-        const BathDev& bd = sd->bath[j];
-        const int k = bd.inv[d];
-        if (k >= 0) bd.Xcur[(int64_t)k * B + L.b] = p1;
-      }
-    }
-  }
-}
-
-// diff0: write the per-chunk max |q_{t+1} - q0| for the next step's id0 cache decision
-__global__ __launch_bounds__(256) void phaseC_kernel(const StepDev* __restrict__ sd,
-                                                     StepArgs ta, int mode1,
-                                                     int diff0) {
-  __shared__ double red[WG];
-  const int B = sd->B, nph = sd->nph, nb = sd->nbath;
-  Lanes L(B);
-  const int64_t t = ta.t;
-  const int tn = (int)(t % sd->nmd);
-  const int t1 = (int)((t + 1) % sd->nmd);
-  const int par1 = (int)((t + 1) & 1);
-  const double dt = sd->dt;
-  const int d0 = blockIdx.y * sd->dchunk;
-  const int d1 = min(nph, d0 + sd->dchunk);
-  const int par = (int)(t & 1);
-  const bool hit1 = (mode1 == 1 && L.ok) ? pot_hit(sd, 1, par, L.b, false) : true;
-  if (L.ok && blockIdx.y == 0 && L.dl == 0) *pmax_word(sd, 1, par ^ 1, L.b) = 0ull;
-  double dq = 0.0;
-  if (L.ok) {
-    for (int d = d0 + L.dl; d < d1; d += L.DL) {
-      const int64_t i = (int64_t)d * B + L.b;
-      double fp;
-      double qt = sd->Qt[i];
-      if (!hit1) {  // md.potforce miss at q~: evaluate and cache (md.py:472-473)
-        fp = -1.0 * sd->Ypot[i];
-        sd->Fc[i] = fp;
-        sd->Q0[i] = qt;
-      } else {
-        fp = sd->Fc[i];
-      }
-      const double f = id1_force(sd, d, L.b, B, t1, par1, fp);
-      double p2 = sd->Ph[i] + dt * f / 2.0;  // md.py:404
-      if (sd->cmask[d]) {  // ApplyConstraint (md.py:407-408, 782-794)
-        p2 = 0.0;
-        qt = 0.0;
-      }
-      sd->P[i] = p2;
-      sd->Q[i] = qt;
-      sd->Flast[i] = f;
-      if (diff0) dq = fmax(dq, fabs(qt - sd->Q0[i]));
-#pragma unroll
-      for (int j = 0; j < MAXBATH; ++j) {
-        if (j < nb) {
-          const BathDev& bd = sd->bath[j];
-          const int k = bd.inv[d];
-          if (k >= 0) {
-            // history push of p_{t+1} (rpadleft, md.py:387 of the next step), mirrored slot
-            const int64_t slot = pmod(t + 1, bd.R);
-            double* h = bd.H + (int64_t)k * bd.ldh + L.b;
-            h[slot * B] = p2;
-            h[(slot + bd.R) * B] = p2;
-            if (bd.has_q) bd.Xq[(int64_t)k * B + L.b] = qt;
-          }
-        }
-      }
-    }
-  }
-  (void)tn;
-  if (diff0) block_max_atomic(sd, L, dq, 0, par ^ 1, red);
-  if (mode1 == 1 && L.ok && blockIdx.y == 0 && L.dl == 0) sd->qvalid[L.b] = 1;
-}
-
 // bath.cur[t] and md.etot[t] (md.py:383, 397) for every step of the run from phase A's per-step
 // partial sums, added in fixed DOF-chunk order (deterministic); launched when outputs are read.
 __global__ void finalize_kernel(const StepDev* __restrict__ sd) {
@@ -829,23 +411,6 @@ void launch_finalize(const StepDev* sd, int B, int nmd, int nbath, hipStream_t s
   const int64_t total = (int64_t)nmd * (nbath + 1) * B;
   const int64_t blocks = std::min<int64_t>((total + 255) / 256, 4096);
   finalize_kernel<<<(unsigned)blocks, 256, 0, s>>>(sd);
-}
-
-static inline dim3 phase_grid(int B, int ndblk) {
-  const int BT = B < 64 ? B : 64;
-  return dim3((B + BT - 1) / BT, ndblk);
-}
-
-void launch_phaseA(const StepDev* sd, StepArgs ta, int B, int ndblk, int mode0, int diff1,
-                   hipStream_t s) {
-  phaseA_kernel<<<phase_grid(B, ndblk), WG, 0, s>>>(sd, ta, mode0, diff1);
-}
-void launch_phaseB(const StepDev* sd, StepArgs ta, int B, int ndblk, int mode1, hipStream_t s) {
-  phaseB_kernel<<<phase_grid(B, ndblk), WG, 0, s>>>(sd, ta, mode1);
-}
-void launch_phaseC(const StepDev* sd, StepArgs ta, int B, int ndblk, int mode1, int diff0,
-                   hipStream_t s) {
-  phaseC_kernel<<<phase_grid(B, ndblk), WG, 0, s>>>(sd, ta, mode1, diff0);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -1,16 +1,63 @@
-"""Per-(kernel, grid) launch-duration summary of a rocprofv3 kernel trace CSV."""
+"""Per-(kernel, grid) launch-duration summary of a rocprofv3 kernel trace CSV.
+
+With --steps: steady-state per-step breakdown over the last N chain C launches, and the chain
+kernels split by whether a background (other-queue) kernel overlapped them."""
 import collections
 import csv
 import sys
 
+
+def short(name):
+    name = name.replace("(anonymous namespace)::", "").replace("void ", "").replace("gle::", "")
+    return name.split("(")[0]
+
+
 rows = list(csv.DictReader(open(sys.argv[1])))
+for r in rows:
+    r["s"] = int(r["Start_Timestamp"])
+    r["e"] = int(r["End_Timestamp"])
+    r["n"] = short(r["Kernel_Name"])
+    r["g"] = int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"]))
 d = collections.defaultdict(list)
 for r in rows:
-    name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("gle::", "")
-    key = (name[:40], int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"])), int(r["Grid_Size_Y"]))
-    d[key].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    d[(r["n"][:40], r["g"], int(r["Grid_Size_Y"]))].append((r["e"] - r["s"]) / 1e3)
 tot = sum(sum(v) for v in d.values())
-for k, v in sorted(d.items(), key=lambda kv: -sum(kv[1])):
+for k, v in sorted(d.items(), key=lambda kv: -sum(kv[1]))[:30]:
     v = sorted(v)
     print("%-40s grid %6d x %4d  n %5d  med %9.1f us  min %9.1f  total %10.1f us (%4.1f%%)"
           % (k[0], k[1], k[2], len(v), v[len(v) // 2], v[0], sum(v), 100 * sum(v) / tot))
+
+if "--steps" in sys.argv:
+    rows.sort(key=lambda r: r["s"])
+    cs = [r for r in rows if r["n"].startswith("chain_kernel<2>")]
+    n = min(100, len(cs) - 1)
+    if n > 0:
+        a, b = cs[-n - 1]["e"], cs[-1]["e"]
+        win = [r for r in rows if r["s"] >= a and r["e"] <= b]
+        per = collections.defaultdict(float)
+        cnt = collections.Counter()
+        for r in win:
+            per[(r["n"][:32], r["g"])] += (r["e"] - r["s"]) / 1e3
+            cnt[(r["n"][:32], r["g"])] += 1
+        print("\nsteady state: %.2f us per step over %d steps" % ((b - a) / 1e3 / n, n))
+        for k, v in sorted(per.items(), key=lambda kv: -kv[1]):
+            print("  %-32s grid %6d  n %4d  per-step %8.2f us  avg %8.2f us" % (k[0], k[1], cnt[k], v / n, v / cnt[k]))
+        chain = [r for r in win if r["n"].startswith("chain_kernel")]
+        bg = [r for r in win if not r["n"].startswith("chain_kernel")]
+        alone = collections.defaultdict(list)
+        over = collections.defaultdict(list)
+        for r in chain:
+            ov = any(x["s"] < r["e"] and x["e"] > r["s"] for x in bg)
+            (over if ov else alone)[r["n"]].append((r["e"] - r["s"]) / 1e3)
+        for k in sorted(set(alone) | set(over)):
+            fa = sorted(alone[k])
+            fo = sorted(over[k])
+            print("  %-18s alone n %4d med %6.1f us | beside background n %4d med %6.1f us"
+                  % (k, len(fa), fa[len(fa) // 2] if fa else 0, len(fo), fo[len(fo) // 2] if fo else 0))
+        gaps = []
+        ch = sorted(chain, key=lambda r: r["s"])
+        for x, y in zip(ch, ch[1:]):
+            gaps.append((y["s"] - x["e"]) / 1e3)
+        gaps.sort()
+        if gaps:
+            print("  chain launch gaps: med %.2f us  p90 %.2f us" % (gaps[len(gaps) // 2], gaps[int(len(gaps) * 0.9)]))
