@@ -47,6 +47,8 @@ struct Chain {
   std::vector<ChTile> tiles;
   ChTile* d = nullptr;
   double flops = 0;  // algorithmic flops of the launch's products
+  int nw = 4;        // waves per workgroup
+  size_t lds = 0;    // dynamic LDS bytes per workgroup
 };
 
 struct Bath {
@@ -71,6 +73,8 @@ struct Bath {
   double *d_Xcur = nullptr, *d_Xq = nullptr, *d_H = nullptr, *d_cur = nullptr;
   double* d_NP = nullptr;  // near-field partial slots [2][nqn][vs]
   int nqn = 0;
+  double* d_NR = nullptr;  // near ring [NRS][vs]: p of the newest NRS steps (slot t mod NRS)
+  int NRS = 2;
   int64_t vs = 0;          // doubles per bath-local [ncp][B] buffer (with slack)
   int64_t ldh = 0;
   int R = 1;
@@ -131,6 +135,11 @@ struct gle_handle {
   unsigned long long* d_pmax = nullptr;
   int32_t* d_qvalid = nullptr;
   StepDev* d_sd = nullptr;
+  unsigned long long* d_dbg = nullptr;  // GLE_CHAIN_DBG stamps
+  double* d_zero = nullptr;            // zero row (chain S(t+1) tiles' unused level slots)
+  bool dbg_no_ladder = false;  // GLE_DBG_NO_LADDER: skip the ladder blocks (timing experiments only)
+  int dbg_ntile = 0;
+  int64_t dbg_t = -1;
   double* d_tw = nullptr;
   int ndblk = 1;
   int64_t t = 0;
@@ -140,6 +149,8 @@ struct gle_handle {
   bool host_force_step = false;
   Op op_prime;
   Chain chA[2], chB[2], chC, chNear;  // [with dyn.q]; chNear: all near-field partial tiles (priming)
+  int ch_nw[3] = {4, 8, 4};            // chain workgroup waves per stage
+  int ch_drn = 1;                      // DOF-tile 16-column MFMA tiles
   int P0 = 1;          // first level block; near field = lags [1, 2 P0)
   int near_end = 1;
   std::vector<Level> levels;
@@ -457,6 +468,7 @@ inline int64_t floordiv(int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + 
 StepArgs step_args(const gle_handle* h, int64_t t) {
   StepArgs a{};
   a.t = t;
+  a.dbg = (h->d_dbg && t == h->dbg_t) ? 1 : 0;
   for (size_t l = 0; l < h->levels.size(); ++l) {
     const int64_t P = h->levels[l].P;
     const int64_t k = floordiv(t, P);
@@ -511,7 +523,7 @@ void run_chain(gle_handle* h, int stage, Chain& c, const StepArgs& ta, int mode,
     e1 = h->ev[h->ev_used + 1];
     h->ev_used += 2;
   }
-  launch_chain(stage, c.d, (int)c.tiles.size(), h->d_sd, ta, mode, h->stream);
+  launch_chain(stage, c.nw, h->ch_drn, c.lds, c.d, (int)c.tiles.size(), h->d_sd, ta, mode, h->stream);
   if (e1) {
     hipEventRecord(e1, h->stream);
     h->prof_n += 1;
@@ -550,17 +562,36 @@ struct Seg {
   int a_ks;
   const double* X;
   int ldx, ring, tshift, nks;
+  int sst;  // ring: doubles between slots
 };
 
 // Split the k-steps [g_begin, g_end) of the concatenated segments evenly over the CH_NW waves of
 // tile T; every (wave, output) run gets its own LDS slot, slots of one output are contiguous.
 int fill_tasks(gle_handle* h, ChTile& T, const std::vector<Seg>& segs, int nout, int64_t g_begin,
-               int64_t g_end, double* flops) {
+               int64_t g_end, Chain& c) {
   int slot = 0;
+  const int NW = c.nw;
+  double* flops = &c.flops;
   std::vector<int> nsl(nout, 0), first(nout, -1);
-  for (int w = 0; w < CH_NW; ++w) {
-    const int64_t g0 = g_begin + (g_end - g_begin) * w / CH_NW;
-    const int64_t g1 = g_begin + (g_end - g_begin) * (w + 1) / CH_NW;
+  int64_t g0 = g_begin;
+  for (int w = 0; w < NW; ++w) {
+    // wave w: [g0, g1) with g1 the even split point, cut short at a segment end if it would need
+    // more than CH_TPW runs (the following waves take the rest)
+    int64_t g1 = std::max(g0, g_begin + (g_end - g_begin) * (w + 1) / NW);
+    {
+      int64_t pos = 0;
+      int runs = 0;
+      for (const Seg& sg : segs) {
+        const int64_t s0 = std::max(g0, pos), s1 = std::min(g1, pos + sg.nks);
+        if (s1 > s0 && ++runs == CH_TPW) {
+          g1 = std::max(g1, std::min(pos + sg.nks, w == NW - 1 ? g_end : g1));
+          g1 = std::min(g1, pos + sg.nks);
+          break;
+        }
+        pos += sg.nks;
+      }
+    }
+    if (w == NW - 1 && g1 < g_end) return fail(h, GLE_ERR_UNSUP, "chain plan: too many k-step runs per wave");
     int64_t pos = 0;
     int cur_o = -1, cnt = 0, cur_slot = -1;
     for (const Seg& sg : segs) {
@@ -581,6 +612,7 @@ int fill_tasks(gle_handle* h, ChTile& T, const std::vector<Seg>& segs, int nout,
         tk.ldx = sg.ldx;
         tk.ring = sg.ring;
         tk.tshift = sg.tshift;
+        tk.sst = sg.sst;
         tk.nks = (int32_t)(s1 - s0);
         tk.slot = cur_slot;
         *flops += 2048.0 * T.rn * (double)(s1 - s0);
@@ -588,8 +620,10 @@ int fill_tasks(gle_handle* h, ChTile& T, const std::vector<Seg>& segs, int nout,
       pos += sg.nks;
     }
     T.ntw[w] = (int8_t)cnt;
+    g0 = g1;
   }
-  if ((int64_t)slot * 256 * T.rn > CH_LDS) return fail(h, GLE_ERR_UNSUP, "chain plan: LDS slots");
+  c.lds = std::max(c.lds, (size_t)slot * 256 * T.rn * 8);
+  if (c.lds > 64 * 1024) return fail(h, GLE_ERR_UNSUP, "chain plan: LDS slots");
   int run = 0;
   for (int o = 0; o < nout; ++o) {
     if (nsl[o] && first[o] != run) return fail(h, GLE_ERR_UNSUP, "chain plan: slot order");
@@ -612,7 +646,17 @@ int plan_chain(gle_handle* h) {
   const int64_t B = h->B;
   const int nb = (int)h->baths.size();
   const int ntile = h->ndblk;
-  const int ncol1 = (int)((B + 15) / 16);
+  if (const char* e = getenv("GLE_CHAIN_NW")) {
+    int v[3] = {4, 8, 4};
+    sscanf(e, "%d,%d,%d", &v[0], &v[1], &v[2]);
+    for (int i = 0; i < 3; ++i) h->ch_nw[i] = v[i] >= 16 ? 16 : (v[i] >= 8 ? 8 : 4);
+  }
+  if (const char* e = getenv("GLE_CHAIN_DRN")) h->ch_drn = atoi(e) >= 2 ? 2 : 1;
+  const char* near_in = getenv("GLE_NEAR_IN");
+  if (!near_in) near_in = "AC";
+  const int drn = (int)std::min<int64_t>(h->ch_drn, (B + 15) / 16);
+  h->ch_drn = drn;
+  const int ncol1 = (int)((B + 16 * drn - 1) / (16 * drn));
   // K0 / Kq rows in DOF order: DOF tile rt of bath j at tofs[rt], [ks][64] fragments
   for (auto& b : h->baths) {
     b.tofs.assign(ntile, -1);
@@ -698,6 +742,13 @@ int plan_chain(gle_handle* h) {
     if (!rc) rc = upload(h, h->d_dynd, f.data(), f.size() * 8);
     if (rc) return rc;
   }
+  // zero row for the S(t+1) tiles' unused level slots (read at column offsets up to 2 P B + B)
+  {
+    int Pt = 1;
+    for (auto& lv : h->levels) Pt = std::max(Pt, lv.P);
+    int rc = dalloc_n(h, &h->d_zero, (size_t)(2 * Pt + 2) * B + 64);
+    if (rc) return rc;
+  }
   // near-field partial items (lags [2, nn), target t+2) per bath: sizes and slot counts
   const int rn_raw = (int)std::min<int64_t>(4, (B + 15) / 16);
   const int nt_raw = 16 * rn_raw;
@@ -705,11 +756,15 @@ int plan_chain(gle_handle* h) {
   const char* env = getenv("GLE_NEAR_KS");
   const int raw_ks = env ? std::max(4, atoi(env)) : 24;
   for (auto& b : h->baths) {
+    b.NRS = std::max(2, b.nn + 1);
+    int rc0 = dalloc_n(h, &b.d_NR, (size_t)b.NRS * b.vs + 4096);
+    if (rc0) return rc0;
     b.nqn = 0;
     if (b.nn > 2) {
       const int64_t W = (int64_t)(b.nn - 2) * b.nks;
-      int q = (int)((W + raw_ks - 1) / raw_ks);
-      q = std::max(q, (b.nn - 2 + 11) / 12);  // at most CH_TPW slice runs per wave
+      int q = (int)std::min<int64_t>(CH_NPMAX, (W + raw_ks - 1) / raw_ks);
+      // at most CH_TPW - 1 whole slices per wave, so a wave's range spans at most CH_TPW slice runs
+      q = std::max(q, (b.nn - 2 + 4 * (CH_TPW - 1) - 1) / (4 * (CH_TPW - 1)));
       q = std::max(1, std::min<int>(q, (int)W));
       if (q > CH_NPMAX) return fail(h, GLE_ERR_UNSUP, "near field too long for the chain (block_len)");
       b.nqn = q;
@@ -721,17 +776,17 @@ int plan_chain(gle_handle* h) {
   auto dof_tile = [&](int stage, bool withD, int rt, int ct, Chain& c) -> int {
     ChTile T{};
     T.kind = CH_DOF;
-    T.rn = 1;
+    T.rn = drn;
     T.row0 = 16 * rt;
-    T.c0 = 16 * ct;
+    T.c0 = 16 * drn * ct;
     T.tile = rt;
     T.nrows = (int)std::min<int64_t>(16, h->nph - 16 * rt);
-    T.ncols = (int)std::min<int64_t>(16, B - 16 * ct);
+    T.ncols = (int)std::min<int64_t>(16 * drn, B - T.c0);
     T.first = rt == 0 ? 1 : 0;
     std::vector<Seg> segs;
     std::vector<Seg> qsegs;
     int nu = 0;
-    for (int u = 0; u < CH_TB; ++u) T.tb[u] = -1;
+    for (int u = 0; u < CH_TB; ++u) T.tb[u].bath = -1;
     for (int j = 0; j < nb; ++j) {
       Bath& b = h->baths[j];
       uint32_t m = 0;
@@ -748,33 +803,49 @@ int plan_chain(gle_handle* h) {
       if (!m) continue;
       if (nu == CH_TB) return fail(h, GLE_ERR_UNSUP, "chain plan: more than 3 baths meet one 16-DOF tile");
       const int u = nu++;
-      T.tb[u] = j;
-      T.bmask[u] = m;
-      T.boff[u] = affine ? off : CH_INV;
-      Seg y{u, b.d_K0d + b.tofs[rt], 64, nullptr, (int)B, 0, 0, b.nks};
+      ChBath& cb = T.tb[u];
+      cb.noise = b.d_noise;
+      cb.S = b.d_S;
+      cb.Xcur = b.d_Xcur;
+      cb.Xq = b.d_Xq;
+      cb.Yq = b.d_Yq;
+      cb.H = b.d_H;
+      cb.NR = b.d_NR;
+      cb.inv = b.d_inv;
+      cb.c = b.c;
+      cb.vs = b.vs;
+      cb.nc = b.nc;
+      cb.ldh = (int32_t)b.ldh;
+      cb.R = b.R;
+      cb.NRS = b.NRS;
+      cb.has_q = b.has_q ? 1 : 0;
+      cb.bath = j;
+      cb.bmask = m;
+      cb.boff = affine ? off : CH_INV;
+      Seg y{u, b.d_K0d + b.tofs[rt], 64, nullptr, (int)B, 0, 0, b.nks, 0};
       if (stage == 0) {
-        y.X = b.d_H;
-        y.ldx = (int)b.ldh;
-        y.ring = b.R;
+        y.X = b.d_NR;
+        y.ring = b.NRS;
+        y.sst = (int)b.vs;
       } else {
         y.X = b.d_Xcur + (stage == 2 ? b.vs : 0);
       }
       segs.push_back(y);
       if (b.has_q && stage < 2)
-        qsegs.push_back(Seg{CH_TB + u, b.d_Kqd + b.tofs[rt], 64, b.d_Xq + (stage == 1 ? b.vs : 0), (int)B, 0, 0, b.nks});
+        qsegs.push_back(Seg{CH_TB + u, b.d_Kqd + b.tofs[rt], 64, b.d_Xq + (stage == 1 ? b.vs : 0), (int)B, 0, 0, b.nks, 0});
     }
     segs.insert(segs.end(), qsegs.begin(), qsegs.end());
     if (withD && h->has_dyn && stage < 2) {
       int64_t o = h->dyn_tofs[rt];
       for (auto& r : h->dyn_rng[rt]) {
         segs.push_back(Seg{2 * CH_TB, h->d_dynd + o, 64, (stage == 0 ? h->d_Q : h->d_Qt) + (int64_t)4 * r.first * B,
-                           (int)B, 0, 0, r.second});
+                           (int)B, 0, 0, r.second, 0});
         o += (int64_t)r.second * 64;
       }
     }
     int64_t W = 0;
     for (auto& sg : segs) W += sg.nks;
-    int rc = fill_tasks(h, T, segs, CH_NOUT, 0, W, &c.flops);
+    int rc = fill_tasks(h, T, segs, CH_NOUT, 0, W, c);
     if (rc) return rc;
     c.tiles.push_back(T);
     return GLE_OK;
@@ -784,10 +855,19 @@ int plan_chain(gle_handle* h) {
       c->tiles.clear();
       c->flops = 0;
     }
+    h->chA[v].nw = h->ch_nw[0];
+    h->chB[v].nw = h->ch_nw[1];
+    // stage A's DOF epilogue reduces 5 quantities over the tile in LDS
+    h->chA[v].lds = (size_t)5 * 256 * drn * 8;
+    h->chB[v].lds = 0;
   }
   h->chC.tiles.clear();
   h->chC.flops = 0;
+  h->chC.nw = h->ch_nw[2];
+  h->chC.lds = (size_t)256 * drn * 8;
   h->chNear.tiles.clear();
+  h->chNear.nw = 4;
+  h->chNear.lds = 0;
   for (int rt = 0; rt < ntile; ++rt)
     for (int ct = 0; ct < ncol1; ++ct) {
       int rc = 0;
@@ -806,16 +886,27 @@ int plan_chain(gle_handle* h) {
       for (int ct = 0; ct < ncol1; ++ct) {
         ChTile T{};
         T.kind = CH_SFIN;
-        T.rn = 1;
+        T.rn = drn;
         T.row0 = 16 * rt;
-        T.c0 = 16 * ct;
+        T.c0 = 16 * drn * ct;
         T.tile = j;
         T.nrows = std::min(16, b.nc - 16 * rt);
-        T.ncols = (int)std::min<int64_t>(16, B - 16 * ct);
-        std::vector<Seg> segs{Seg{0, b.d_Kn + ((int64_t)rt * b.nks * b.nn + 1) * 64, b.nn * 64, b.d_H, (int)b.ldh,
-                                  b.R, 0, b.nks}};
+        T.ncols = (int)std::min<int64_t>(16 * drn, B - T.c0);
+        ChSfin& sf = T.sf;
+        sf.NP = b.nqn ? b.d_NP : h->d_zero;
+        sf.S = b.d_S;
+        sf.vs = b.vs;
+        sf.nqn = b.nqn;
+        sf.nc = b.nc;
+        for (int l = 0; l < MAXLVL; ++l) {
+          const bool act = l < (int)h->levels.size() && h->levels[l].lb[j].active;
+          sf.lvl[l] = act ? h->levels[l].lb[j].d_out : h->d_zero;
+          sf.lvl_ld[l] = act ? 2 * h->levels[l].P * (int32_t)B : 0;
+        }
+        std::vector<Seg> segs{Seg{0, b.d_Kn + ((int64_t)rt * b.nks * b.nn + 1) * 64, b.nn * 64, b.d_NR, (int)B,
+                                  b.NRS, 0, b.nks, (int)b.vs}};
         for (int v = 0; v < 2; ++v) {
-          int rc = fill_tasks(h, T, segs, 1, 0, b.nks, &h->chA[v].flops);
+          int rc = fill_tasks(h, T, segs, 1, 0, b.nks, h->chA[v]);
           if (rc) return rc;
           h->chA[v].tiles.push_back(T);
         }
@@ -827,7 +918,7 @@ int plan_chain(gle_handle* h) {
     if (b.nqn == 0) continue;
     std::vector<Seg> base;
     for (int i = 2; i < b.nn; ++i)
-      base.push_back(Seg{0, nullptr, b.nn * 64, b.d_H, (int)b.ldh, b.R, 2 - i, b.nks});
+      base.push_back(Seg{0, nullptr, b.nn * 64, b.d_NR, (int)B, b.NRS, 2 - i, b.nks, (int)b.vs});
     const int64_t W = (int64_t)(b.nn - 2) * b.nks;
     for (int rt = 0; rt < b.nrt; ++rt) {
       std::vector<Seg> segs = base;
@@ -846,16 +937,30 @@ int plan_chain(gle_handle* h) {
           T.par_stride = (int64_t)b.nqn * b.vs;
           T.dst = b.d_NP + (int64_t)q * b.vs + (int64_t)16 * rt * B + T.c0;
           T.ldd = (int)B;
-          Chain& c = (q & 1) ? h->chC : h->chB[0];
-          const double f0 = c.flops;
-          int rc = fill_tasks(h, T, segs, 1, W * q / b.nqn, W * (q + 1) / b.nqn, &c.flops);
-          if (rc) return rc;
-          c.tiles.push_back(T);
-          if (!(q & 1)) {
-            h->chB[1].tiles.push_back(T);
-            h->chB[1].flops += c.flops - f0;
+          // near-field tiles go to the stages named in GLE_NEAR_IN (default A and C), round robin
+          const int ns = (int)strlen(near_in);
+          const char st = near_in[q % std::max(1, ns)];
+          Chain* pair[2] = {nullptr, nullptr};
+          if (st == 'A') {
+            pair[0] = &h->chA[0];
+            pair[1] = &h->chA[1];
+          } else if (st == 'B') {
+            pair[0] = &h->chB[0];
+            pair[1] = &h->chB[1];
+          } else {
+            pair[0] = &h->chC;
           }
-          h->chNear.tiles.push_back(T);
+          for (Chain* c : pair) {
+            if (!c) continue;
+            ChTile Tc = T;
+            int rc = fill_tasks(h, Tc, segs, 1, W * q / b.nqn, W * (q + 1) / b.nqn, *c);
+            if (rc) return rc;
+            c->tiles.push_back(Tc);
+          }
+          ChTile Tn = T;
+          int rc = fill_tasks(h, Tn, segs, 1, W * q / b.nqn, W * (q + 1) / b.nqn, h->chNear);
+          if (rc) return rc;
+          h->chNear.tiles.push_back(Tn);
         }
     }
   }
@@ -1136,6 +1241,17 @@ int freeze(gle_handle* h) {
   sd.part = h->d_part;
   sd.cmask = h->d_cmask;
   sd.ndblk = h->ndblk;
+  if (const char* dbg = getenv("GLE_CHAIN_DBG")) {
+    size_t n = 0;
+    for (Chain* c : {&h->chA[1], &h->chB[1], &h->chC}) n = std::max(n, c->tiles.size());
+    sd.dbg_ntile = (int32_t)n;
+    sd.dbg_t = atoll(dbg);
+    rc = dalloc_n(h, &h->d_dbg, (size_t)3 * n * 4);
+    if (rc) return rc;
+    sd.dbg = h->d_dbg;
+    h->dbg_ntile = (int)n;
+    h->dbg_t = sd.dbg_t;
+  }
   for (size_t j = 0; j < h->baths.size(); ++j) {
     Bath& b = h->baths[j];
     BathDev& bd = sd.bath[j];
@@ -1148,6 +1264,8 @@ int freeze(gle_handle* h) {
     bd.H = b.d_H;
     bd.cur = b.d_cur;
     bd.NP = b.d_NP;
+    bd.NR = b.d_NR;
+    bd.NRS = b.NRS;
     bd.nlvl = (int32_t)h->levels.size();
     for (size_t l = 0; l < h->levels.size(); ++l) {
       const LevelBath& L = h->levels[l].lb[j];
@@ -1225,7 +1343,10 @@ int prime(gle_handle* h) {
     lv.bg_block[0] = lv.bg_block[1] = INT64_MIN;
   }
   // near-field partials of target t+1 (lags >= 2: p up to t-1), as the chain of step t-1 leaves them
-  launch_chain(1, h->chNear.d, (int)h->chNear.tiles.size(), h->d_sd, step_args(h, h->t - 1), 0, h->stream);
+  for (auto& b : h->baths)
+    launch_near_fill(b.d_H, b.ldh, b.R, (int)h->B, b.ncp, b.d_NR, b.vs, b.NRS, h->t, h->stream);
+  launch_chain(1, h->chNear.nw, h->ch_drn, h->chNear.lds, h->chNear.d, (int)h->chNear.tiles.size(), h->d_sd,
+               step_args(h, h->t - 1), 0, h->stream);
   if (!h->levels.empty()) HIPCHK(h, hipEventRecord(h->ev_step, h->stream));
   h->need_prime = false;
   return GLE_OK;
@@ -1247,7 +1368,7 @@ int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
   // the level's background stream once step T-1 has closed; consume block k from this step on
   bool bg_waited[gle_handle::NBG] = {};
   for (auto& lv : h->levels) {
-    if (t % lv.P != 0) continue;
+    if (t % lv.P != 0 || h->dbg_no_ladder) continue;
     const int64_t k = t / lv.P;
     if (k + 1 > lv.last_block) {
       hipStream_t bs = h->bg[lv.sidx];
@@ -1359,14 +1480,30 @@ int gle_create(const gle_config* cfg, gle_handle** out) {
   h->nmd = cfg->nmd;
   h->dt = cfg->dt;
   h->nphp = rup(h->nph, 8);
+  h->dbg_no_ladder = getenv("GLE_DBG_NO_LADDER") != nullptr;
   // main stream (the latency-bound per-step chain) at the highest priority, background streams
   // (ladder blocks) at the lowest
   {
     int lo = 0, hi = 0;
     hipDeviceGetStreamPriorityRange(&lo, &hi);
     e = hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, hi);
+    // GLE_BG_RESERVE=R: the background streams stay off CU mask bits [0, R), which the per-step
+    // chain then finds free at every launch
+    int reserve = 0;
+    if (const char* r = getenv("GLE_BG_RESERVE")) reserve = std::max(0, atoi(r));
+    std::vector<uint32_t> cumask;
+    if (reserve > 0) {
+      hipDeviceProp_t prop;
+      hipGetDeviceProperties(&prop, cfg->device);
+      const int ncu = prop.multiProcessorCount;
+      cumask.assign((ncu + 31) / 32, 0u);
+      for (int c = std::min(reserve, ncu - 8); c < ncu; ++c) cumask[c / 32] |= 1u << (c % 32);
+    }
     for (int i = 0; i < gle_handle::NBG && e == hipSuccess; ++i) {
-      e = hipStreamCreateWithPriority(&h->bg[i], hipStreamNonBlocking, lo);
+      if (reserve > 0)
+        e = hipExtStreamCreateWithCUMask(&h->bg[i], (uint32_t)cumask.size(), cumask.data());
+      else
+        e = hipStreamCreateWithPriority(&h->bg[i], hipStreamNonBlocking, lo);
       if (e == hipSuccess)
         e = hipEventCreateWithFlags(&h->ev_bg[i], hipEventDisableTiming | hipEventReleaseToDevice);
     }
@@ -1412,9 +1549,53 @@ int gle_create(const gle_config* cfg, gle_handle** out) {
   return GLE_OK;
 }
 
+// GLE_CHAIN_DBG: per-stage timeline of the recorded step's chain launches (stderr)
+static void dump_chain_dbg(gle_handle* h) {
+  const int n = h->dbg_ntile;
+  std::vector<unsigned long long> st((size_t)3 * n * 4);
+  if (hipMemcpy(st.data(), h->d_dbg, st.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+  const char* kn[3] = {"DOF", "SFIN", "RAW"};
+  for (int g = 0; g < 3; ++g) {
+    const Chain& c = g == 0 ? h->chA[1] : (g == 1 ? h->chB[1] : h->chC);
+    unsigned long long t0 = ~0ull, t1 = 0;
+    for (size_t i = 0; i < c.tiles.size(); ++i) {
+      const unsigned long long* r = &st[((size_t)g * n + i) * 4];
+      if (r[0]) t0 = std::min(t0, r[0]);
+      t1 = std::max(t1, r[3]);
+    }
+    if (t0 == ~0ull) continue;
+    fprintf(stderr, "[chain dbg] stage %c: %zu tiles, span %.2f us\n", "ABC"[g], c.tiles.size(), (t1 - t0) / 100.0);
+    for (int k = 0; k < 3; ++k) {
+      std::vector<double> v[5];
+      for (size_t i = 0; i < c.tiles.size(); ++i) {
+        if (c.tiles[i].kind != k) continue;
+        const unsigned long long* r = &st[((size_t)g * n + i) * 4];
+        if (!r[0] || !r[3]) continue;
+        v[0].push_back((r[0] - t0) / 100.0);
+        v[1].push_back((r[1] - r[0]) / 100.0);
+        v[2].push_back((r[2] - r[1]) / 100.0);
+        v[3].push_back((r[3] - r[2]) / 100.0);
+        v[4].push_back((r[3] - t0) / 100.0);
+      }
+      if (v[0].empty()) continue;
+      const char* nm[5] = {"start", "desc", "prod", "epi", "end"};
+      fprintf(stderr, "[chain dbg]   %-4s n %4zu", kn[k], v[0].size());
+      for (int q = 0; q < 5; ++q) {
+        std::sort(v[q].begin(), v[q].end());
+        fprintf(stderr, "  %s %.2f/%.2f/%.2f", nm[q], v[q][v[q].size() / 2], v[q][v[q].size() * 9 / 10], v[q].back());
+      }
+      fprintf(stderr, "\n");
+    }
+  }
+}
+
 int gle_destroy(gle_handle* h) {
   if (!h) return GLE_OK;
   hipSetDevice(h->cfg.device);
+  if (h->d_dbg) {
+    hipDeviceSynchronize();
+    dump_chain_dbg(h);
+  }
   for (int i = 0; i < gle_handle::NBG; ++i)
     if (h->bg[i]) hipStreamSynchronize(h->bg[i]);
   if (h->stream) hipStreamSynchronize(h->stream);

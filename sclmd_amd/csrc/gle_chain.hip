@@ -10,12 +10,15 @@
 //              (rpadleft, md.py:386-387), cache distances for the next step's id0 call
 //      CH_RAW  near-field partials for target t+2
 //
-// A workgroup owns a whole output tile (no split over workgroups): its 4 waves split the tile's
-// k-steps, each wave keeps all of its operand loads in flight at once, the partial tiles meet in LDS
-// and are added in a fixed order (deterministic).  Everything the epilogue reads that does not
-// depend on the products is loaded before the products start, so a launch costs one descriptor
-// round trip, one operand round trip, the MFMAs and the stores.
+// A workgroup owns a whole output tile (no split over workgroups): its NW waves split the tile's
+// k-steps, each wave keeps a batch of operand loads in flight at once, the partial tiles meet in
+// LDS and are added in a fixed order (deterministic).  Everything the epilogue reads that does not
+// depend on the products is loaded before the products start.  The newest p of every bath lives in
+// a small slot-major near ring, so per-step operands are contiguous (no TLB walk per k-step as in
+// the 2R-slot history ring the ladder reads).
 #include <hip/hip_runtime.h>
+
+#include <cstddef>
 
 #include "gle_internal.h"
 
@@ -24,24 +27,38 @@ namespace gle {
 namespace {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) double gdouble;
+
+// global-address-space view of a pointer: loads and stores become global_* instructions (flat ones
+// also count on lgkmcnt and would make every scalar-load wait drain the vector loads in flight)
+template <class T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* G(T* p) {
+  return (__attribute__((address_space(1))) T*)p;
+}
 
 __device__ __forceinline__ int64_t cmod(int64_t a, int64_t m) {
   int64_t r = a % m;
   return r < 0 ? r + m : r;
 }
 
-// k-steps a wave keeps in flight per batch
-template <int RN>
+// k-steps a wave keeps in flight per batch (16-wave workgroups have 128 registers per lane)
+template <int RN, int NW>
 struct Batch {
-  static constexpr int U = RN == 1 ? 16 : (RN == 2 ? 8 : 4);
+  static constexpr int U = NW >= 16 ? (RN == 1 ? 16 : (RN == 2 ? 6 : 3)) : (RN == 1 ? 24 : (RN == 2 ? 12 : 8));
 };
+
+// GLE_CHAIN_DBG timeline: stamp 0 entry, 1 descriptor read, 2 products done, 3 end (100 MHz)
+__device__ __forceinline__ void stamp(const StepDev* __restrict__ sd, int stage, int k, const StepArgs& ta) {
+  if (ta.dbg && threadIdx.x == 0 && (int)blockIdx.x < sd->dbg_ntile)
+    G(sd->dbg)[((int64_t)stage * sd->dbg_ntile + blockIdx.x) * 4 + k] = __builtin_amdgcn_s_memrealtime();
+}
 
 // The wave's tasks: acc += A_s . X rows 4s..4s+3 over each task's k-steps; a task run ends in its
 // LDS slot (16 x 16 RN doubles, row-major).
-template <int RN>
-__device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave, int lane, int64_t t, int B,
+template <int RN, int NW>
+__device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave, int lane, int64_t t,
                                          double* lds) {
-  constexpr int U = Batch<RN>::U;
+  constexpr int U = Batch<RN, NW>::U;
   constexpr int NT = 16 * RN;
   const int nt = T->ntw[wave];
   const int brow = lane >> 4, bcol = lane & 15;
@@ -65,9 +82,9 @@ __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave,
       cur = tk.slot;
     }
     int64_t col = T->c0;
-    if (tk.ring) col += cmod(t + tk.tshift, tk.ring) * (int64_t)B;
-    const double* A = tk.A + lane;
-    const double* X = tk.X + col + (int64_t)brow * tk.ldx + bcol;
+    if (tk.ring) col += cmod(t + tk.tshift, tk.ring) * (int64_t)tk.sst;
+    gdouble* A = (gdouble*)(tk.A + lane);
+    gdouble* X = (gdouble*)(tk.X + col + (int64_t)brow * tk.ldx + bcol);
     const int64_t xs = 4 * (int64_t)tk.ldx;
     for (int s0 = 0; s0 < tk.nks; s0 += U) {
       double a[U], b[U][RN];
@@ -97,20 +114,21 @@ __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave,
   }
 }
 
-__device__ __forceinline__ void run_products(const ChTile* __restrict__ T, int64_t t, int B, double* lds) {
+template <int NW>
+__device__ __forceinline__ void run_products(const ChTile* __restrict__ T, int64_t t, double* lds) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   switch (T->rn) {
-    case 1: products<1>(T, wave, lane, t, B, lds); break;
-    case 2: products<2>(T, wave, lane, t, B, lds); break;
-    default: products<4>(T, wave, lane, t, B, lds); break;
+    case 1: products<1, NW>(T, wave, lane, t, lds); break;
+    case 2: products<2, NW>(T, wave, lane, t, lds); break;
+    default: products<4, NW>(T, wave, lane, t, lds); break;
   }
 }
 
-// output o of a 16 x 16 tile at element e (slots of 256 doubles), added in slot order
-__device__ __forceinline__ double out_sum(const ChTile* __restrict__ T, const double* lds, int o, int e) {
+// output o at element e of a tile with slots of ss doubles, added in slot order
+__device__ __forceinline__ double out_sum(const ChTile* __restrict__ T, const double* lds, int o, int e, int ss) {
   double v = 0.0;
-  for (int s = T->ob[o]; s < T->ob[o + 1]; ++s) v += lds[s * 256 + e];
+  for (int s = T->ob[o]; s < T->ob[o + 1]; ++s) v += lds[s * ss + e];
   return v;
 }
 
@@ -126,406 +144,516 @@ __device__ __forceinline__ bool word_hit(unsigned long long w) {
   return m == m && m < 10e-10;
 }
 
-// per-trajectory reductions over the 16 rows of a DOF tile: thread e = r*16 + c holds row r,
-// column c.  red: 16 x 16 doubles of LDS scratch.
-__device__ __forceinline__ double col_sum(double v, double* red) {
-  __syncthreads();
-  red[threadIdx.x] = v;
-  __syncthreads();
-  double s = 0.0;
-  if (threadIdx.x < 16)
-    for (int r = 0; r < 16; ++r) s += red[r * 16 + threadIdx.x];
-  return s;
-}
-__device__ __forceinline__ double col_max(double v, double* red, bool& nan) {
-  __syncthreads();
-  red[threadIdx.x] = v;
-  __syncthreads();
-  double m = 0.0;
-  nan = false;
-  if (threadIdx.x < 16)
-    for (int r = 0; r < 16; ++r) {
-      const double w = red[r * 16 + threadIdx.x];
-      nan |= (w != w);
-      m = fmax(m, w);
-    }
-  return m;
-}
+// ------------------------------------------------------------------------------------------
+// DOF tiles: 16 DOFs x NT = 16 DRN trajectories; thread element i is e = threadIdx.x + i NW 64
+// (row e / NT, column e % NT).
+template <int NW, int DRN>
+struct DofGeo {
+  static constexpr int NT = 16 * DRN;
+  static constexpr int NE = 16 * NT;
+  static constexpr int EPT = (NE + NW * 64 - 1) / (NW * 64);
+};
 
 struct Elem {
   int r, d, b;
   int64_t i;
-  bool ok;
+  bool ok, in;  // in: inside the tile's element range; ok: a real (DOF, trajectory)
 };
 
-__device__ __forceinline__ Elem elem_of(const ChTile* __restrict__ T, const StepDev* __restrict__ sd) {
+template <int NW, int DRN>
+__device__ __forceinline__ Elem elem_of(const ChTile* __restrict__ T, const StepDev* __restrict__ sd, int k) {
+  using Geo = DofGeo<NW, DRN>;
   Elem E;
-  E.r = threadIdx.x >> 4;
+  const int e = threadIdx.x + k * NW * 64;
+  E.in = e < Geo::NE;
+  E.r = e / Geo::NT;
   E.d = T->row0 + E.r;
-  E.b = T->c0 + (threadIdx.x & 15);
-  E.ok = E.d < sd->nph && E.b < sd->B;
+  E.b = T->c0 + (e % Geo::NT);
+  E.ok = E.in && E.d < sd->nph && E.b < sd->B;
   E.i = (int64_t)E.d * sd->B + E.b;
   return E;
 }
 
-// bath-local row of the element's DOF in tile bath u (bath bd), or -1
-__device__ __forceinline__ int bath_row(const ChTile* __restrict__ T, const BathDev& bd, int u, const Elem& E) {
-  if (!E.ok || !((T->bmask[u] >> E.r) & 1u)) return -1;
-  const int off = T->boff[u];
-  return off == CH_INV ? bd.inv[E.d] : E.d + off;
+// bath-local row of the element's DOF in tile bath bd, or -1
+__device__ __forceinline__ int bath_row(const ChBath& bd, const Elem& E) {
+  if (bd.bath < 0 || !E.ok || !((bd.bmask >> E.r) & 1u)) return -1;
+  return bd.boff == CH_INV ? G(bd.inv)[E.d] : E.d + bd.boff;
 }
 
-// ------------------------------------------------------------------------------------------
+// Per-trajectory reductions over the tile's 16 rows, one LDS pass: quantity q of element e at
+// red[q * NE + e]; column sums (fixed row order) / maxima by threads < NT.
+template <int NW, int DRN>
+__device__ __forceinline__ double col_red(const double* red, int q, int c, bool max, bool& nan) {
+  using Geo = DofGeo<NW, DRN>;
+  double v = 0.0;
+  nan = false;
+  for (int r = 0; r < 16; ++r) {
+    const double w = red[q * Geo::NE + r * Geo::NT + c];
+    if (max) {
+      nan |= (w != w);
+      v = fmax(v, w);
+    } else {
+      v += w;
+    }
+  }
+  return v;
+}
+
 // stage A, DOF tile
+template <int NW, int DRN>
 __device__ __forceinline__ void dof_A(const ChTile* __restrict__ T, const StepDev* __restrict__ sd,
                                       const StepArgs& ta, int mode, double* lds) {
+  using Geo = DofGeo<NW, DRN>;
+  constexpr int EPT = Geo::EPT;
   const int B = sd->B, nb = sd->nbath;
   const int64_t t = ta.t;
   const int tn = (int)(t % sd->nmd);
   const int par = (int)(t & 1);
   const double dt = sd->dt, dt2 = dt * dt;
   const bool harm = (mode & 1) != 0, diff1 = (mode & 2) != 0;
-  const Elem E = elem_of(T, sd);
   // ---- loads that do not depend on the products
-  double p = 0.0, q = 0.0, fc = 0.0, q0 = 0.0;
-  unsigned long long w0 = 0;
-  if (E.ok) {
-    p = sd->P[E.i];
-    q = sd->Q[E.i];
-    fc = sd->Fc[E.i];
-    if (harm || diff1) q0 = sd->Q0[E.i];
-    if (harm) w0 = (sd->qvalid[E.b] != 0) ? *pmax_word(sd, 0, par, E.b) : 0x7FF8000000000000ull;
-  }
-  int kk[CH_TB];
-  double nz[CH_TB], sv[CH_TB];
+  Elem E[EPT];
+  double p[EPT], q[EPT], fc[EPT], q0[EPT];
+  unsigned long long w0[EPT];
+  int qv[EPT];
+  int kk[EPT][CH_TB];
+  double nz[EPT][CH_TB], sv[EPT][CH_TB];
 #pragma unroll
-  for (int u = 0; u < CH_TB; ++u) {
-    kk[u] = -1;
-    nz[u] = sv[u] = 0.0;
-    const int j = T->tb[u];
-    if (j >= 0) {
-      const BathDev& bd = sd->bath[j];
-      kk[u] = bath_row(T, bd, u, E);
-      if (kk[u] >= 0) {
-        nz[u] = bd.noise[((int64_t)tn * bd.nc + kk[u]) * B + E.b];
-        sv[u] = bd.S[(int64_t)par * bd.vs + (int64_t)kk[u] * B + E.b];
+  for (int x = 0; x < EPT; ++x) {
+    E[x] = elem_of<NW, DRN>(T, sd, x);
+    p[x] = q[x] = fc[x] = q0[x] = 0.0;
+    w0[x] = 0;
+    qv[x] = 0;
+    if (E[x].ok) {
+      p[x] = G(sd->P)[E[x].i];
+      q[x] = G(sd->Q)[E[x].i];
+      fc[x] = G(sd->Fc)[E[x].i];
+      if (harm || diff1) q0[x] = G(sd->Q0)[E[x].i];
+      if (harm) {
+        qv[x] = G(sd->qvalid)[E[x].b];
+        w0[x] = *G(pmax_word(sd, 0, par, E[x].b));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < CH_TB; ++u) {
+      kk[x][u] = -1;
+      nz[x][u] = sv[x][u] = 0.0;
+      {
+        const ChBath& bd = T->tb[u];
+        kk[x][u] = bath_row(bd, E[x]);
+        if (kk[x][u] >= 0) {
+          nz[x][u] = G(bd.noise)[((int64_t)tn * bd.nc + kk[x][u]) * B + E[x].b];
+          sv[x][u] = G(bd.S)[(int64_t)par * bd.vs + (int64_t)kk[x][u] * B + E[x].b];
+        }
       }
     }
   }
-  if (T->first && threadIdx.x < 16 && E.b < B) *pmax_word(sd, 0, par ^ 1, E.b) = 0ull;
-  run_products(T, t, B, lds);
+  if (T->first && threadIdx.x < Geo::NT && T->c0 + (int)threadIdx.x < B)
+    *G(pmax_word(sd, 0, par ^ 1, T->c0 + threadIdx.x)) = 0ull;
+  run_products<NW>(T, t, lds);
   __syncthreads();
+  stamp(sd, 0, 2, ta);
   // ---- epilogue (md.vv id0, md.py:383-397)
-  const int e = threadIdx.x;
-  const bool hit = harm ? word_hit(w0) : true;
-  double f = fc;  // potforce(q_t)
-  if (!hit) {
-    f = -1.0 * out_sum(T, lds, 2 * CH_TB, e);  // f = -1.0*mdot(dyn, q)  (md.py:467)
-    if (E.ok) {
-      sd->Fc[E.i] = f;
-      sd->Q0[E.i] = q;
-    }
-  }
-  double cur[CH_TB];
+  double cur[EPT][CH_TB], ee[EPT], dq[EPT];
 #pragma unroll
-  for (int u = 0; u < CH_TB; ++u) {
-    cur[u] = 0.0;
-    if (kk[u] >= 0) {
-      const BathDev& bd = sd->bath[T->tb[u]];
-      double fb = nz[u] - bd.c * (out_sum(T, lds, u, e) + sv[u]);
-      if (bd.has_q) fb -= out_sum(T, lds, CH_TB + u, e);
-      f += fb;           // pf = pf + fbaths[i]  (md.py:432-434)
-      cur[u] = fb * p;   // cur[t] = fbaths[i].p (md.py:397)
+  for (int x = 0; x < EPT; ++x) {
+    const int e = threadIdx.x + x * NW * 64;
+    const bool hit = harm ? (qv[x] != 0 && word_hit(w0[x])) : true;
+    double f = fc[x];  // potforce(q_t)
+    if (!hit && E[x].in) {
+      f = -1.0 * out_sum(T, lds, 2 * CH_TB, e, Geo::NE);  // f = -1.0*mdot(dyn, q)  (md.py:467)
+      if (E[x].ok) {
+        G(sd->Fc)[E[x].i] = f;
+        G(sd->Q0)[E[x].i] = q[x];
+      }
     }
-  }
-  const double ph = p + f * dt / 2.0;            // md.py:391
-  const double qt = q + p * dt + f * dt2 / 2.0;  // md.py:392
-  if (E.ok) {
-    sd->Ph[E.i] = ph;
-    sd->Qt[E.i] = qt;
-  }
 #pragma unroll
-  for (int u = 0; u < CH_TB; ++u) {
-    if (kk[u] >= 0) {
-      const BathDev& bd = sd->bath[T->tb[u]];
-      const int64_t kb = (int64_t)kk[u] * B + E.b;
-      bd.Xcur[kb] = ph;
-      if (bd.has_q) bd.Xq[bd.vs + kb] = qt;
+    for (int u = 0; u < CH_TB; ++u) {
+      cur[x][u] = 0.0;
+      if (kk[x][u] >= 0) {
+        const ChBath& bd = T->tb[u];
+        double fb = nz[x][u] - bd.c * (out_sum(T, lds, u, e, Geo::NE) + sv[x][u]);
+        if (bd.has_q) fb -= out_sum(T, lds, CH_TB + u, e, Geo::NE);
+        f += fb;                 // pf = pf + fbaths[i]  (md.py:432-434)
+        cur[x][u] = fb * p[x];   // cur[t] = fbaths[i].p (md.py:397)
+      }
     }
+    const double ph = p[x] + f * dt / 2.0;               // md.py:391
+    const double qt = q[x] + p[x] * dt + f * dt2 / 2.0;  // md.py:392
+    if (E[x].ok) {
+      G(sd->Ph)[E[x].i] = ph;
+      G(sd->Qt)[E[x].i] = qt;
+    }
+#pragma unroll
+    for (int u = 0; u < CH_TB; ++u) {
+      if (kk[x][u] >= 0) {
+        const ChBath& bd = T->tb[u];
+        const int64_t kb = (int64_t)kk[x][u] * B + E[x].b;
+        G(bd.Xcur)[kb] = ph;
+        if (bd.has_q) G(bd.Xq)[bd.vs + kb] = qt;
+      }
+    }
+    ee[x] = E[x].ok ? p[x] * p[x] : 0.0;
+    dq[x] = E[x].ok ? fabs(qt - (hit ? q0[x] : q[x])) : 0.0;
   }
-  // per-trajectory sums over the tile's DOFs (fixed order), one row of the step's partial table
+  // per-trajectory sums over the tile's DOFs (fixed order): one row of the step's partial table
   // [tile][bath | energy]; baths that miss the tile get zeros
+  __syncthreads();
   double* red = lds;
-  double* prow = sd->part + (((int64_t)tn * sd->ndblk + T->tile) * (nb + 1)) * B;
-  const bool wcol = threadIdx.x < 16 && E.b < B;
-  for (int j = 0; j < nb; ++j) {
-    int uj = -1;
 #pragma unroll
-    for (int u = 0; u < CH_TB; ++u)
-      if (T->tb[u] == j) uj = u;
-    double s = 0.0;
-    if (uj >= 0) {
-      double cj = 0.0;
+  for (int x = 0; x < EPT; ++x) {
+    const int e = threadIdx.x + x * NW * 64;
+    if (E[x].in) {
+#pragma unroll
+      for (int u = 0; u < CH_TB; ++u) red[u * Geo::NE + e] = cur[x][u];
+      red[CH_TB * Geo::NE + e] = ee[x];
+      red[(CH_TB + 1) * Geo::NE + e] = dq[x];
+    }
+  }
+  __syncthreads();
+  const int c = threadIdx.x;
+  const int b = T->c0 + c;
+  if (c < Geo::NT && b < B) {
+    double* prow = sd->part + (((int64_t)tn * sd->ndblk + T->tile) * (nb + 1)) * B;
+    bool nan;
+    for (int j = 0; j < nb; ++j) {
+      int uj = -1;
 #pragma unroll
       for (int u = 0; u < CH_TB; ++u)
-        if (u == uj) cj = cur[u];
-      s = col_sum(cj, red);
+        if (T->tb[u].bath == j) uj = u;
+      prow[(int64_t)j * B + b] = uj >= 0 ? col_red<NW, DRN>(red, uj, c, false, nan) : 0.0;
     }
-    if (wcol) prow[(int64_t)j * B + E.b] = s;
-  }
-  {
-    const double s = col_sum(E.ok ? p * p : 0.0, red);
-    if (wcol) prow[(int64_t)nb * B + E.b] = s;
-  }
-  if (diff1) {
-    const double dq = E.ok ? fabs(qt - (hit ? q0 : q)) : 0.0;
-    bool nan;
-    const double m = col_max(dq, red, nan);
-    if (wcol) {
+    prow[(int64_t)nb * B + b] = col_red<NW, DRN>(red, CH_TB, c, false, nan);
+    if (diff1) {
+      const double m = col_red<NW, DRN>(red, CH_TB + 1, c, true, nan);
       const unsigned long long bits = nan ? 0x7FF8000000000000ull : (unsigned long long)__double_as_longlong(m);
-      atomicMax(pmax_word(sd, 1, par, E.b), bits);
+      atomicMax(pmax_word(sd, 1, par, b), bits);
     }
   }
 }
 
 // stage B, DOF tile
+template <int NW, int DRN>
 __device__ __forceinline__ void dof_B(const ChTile* __restrict__ T, const StepDev* __restrict__ sd,
                                       const StepArgs& ta, int mode, double* lds) {
+  using Geo = DofGeo<NW, DRN>;
+  constexpr int EPT = Geo::EPT;
   const int B = sd->B;
   const int64_t t = ta.t;
   const int t1 = (int)((t + 1) % sd->nmd);
   const int par = (int)(t & 1), par1 = par ^ 1;
   const double dt = sd->dt;
   const bool harm = mode != 0;
-  const Elem E = elem_of(T, sd);
-  double ph = 0.0, qt = 0.0, fc = 0.0;
-  unsigned long long w1 = 0;
-  if (E.ok) {
-    ph = sd->Ph[E.i];
-    qt = sd->Qt[E.i];
-    fc = sd->Fc[E.i];
-    if (harm) w1 = *pmax_word(sd, 1, par, E.b);
-  }
-  int kk[CH_TB];
-  double nz[CH_TB], sv[CH_TB];
+  Elem E[EPT];
+  double ph[EPT], qt[EPT], fc[EPT];
+  unsigned long long w1[EPT];
+  int kk[EPT][CH_TB];
+  double nz[EPT][CH_TB], sv[EPT][CH_TB];
 #pragma unroll
-  for (int u = 0; u < CH_TB; ++u) {
-    kk[u] = -1;
-    nz[u] = sv[u] = 0.0;
-    const int j = T->tb[u];
-    if (j >= 0) {
-      const BathDev& bd = sd->bath[j];
-      kk[u] = bath_row(T, bd, u, E);
-      if (kk[u] >= 0) {
-        nz[u] = bd.noise[((int64_t)t1 * bd.nc + kk[u]) * B + E.b];
-        sv[u] = bd.S[(int64_t)par1 * bd.vs + (int64_t)kk[u] * B + E.b];
+  for (int x = 0; x < EPT; ++x) {
+    E[x] = elem_of<NW, DRN>(T, sd, x);
+    ph[x] = qt[x] = fc[x] = 0.0;
+    w1[x] = 0;
+    if (E[x].ok) {
+      ph[x] = G(sd->Ph)[E[x].i];
+      qt[x] = G(sd->Qt)[E[x].i];
+      fc[x] = G(sd->Fc)[E[x].i];
+      if (harm) w1[x] = *G(pmax_word(sd, 1, par, E[x].b));
+    }
+#pragma unroll
+    for (int u = 0; u < CH_TB; ++u) {
+      kk[x][u] = -1;
+      nz[x][u] = sv[x][u] = 0.0;
+      {
+        const ChBath& bd = T->tb[u];
+        kk[x][u] = bath_row(bd, E[x]);
+        if (kk[x][u] >= 0) {
+          nz[x][u] = G(bd.noise)[((int64_t)t1 * bd.nc + kk[x][u]) * B + E[x].b];
+          sv[x][u] = G(bd.S)[(int64_t)par1 * bd.vs + (int64_t)kk[x][u] * B + E[x].b];
+        }
       }
     }
   }
-  run_products(T, t, B, lds);
+  run_products<NW>(T, t, lds);
   __syncthreads();
-  const int e = threadIdx.x;
-  const bool hit1 = harm ? word_hit(w1) : true;
-  double f = fc;  // potforce(q~)
-  if (!hit1) {
-    f = -1.0 * out_sum(T, lds, 2 * CH_TB, e);
-    if (E.ok) {  // md.potforce miss at q~: evaluate and cache (md.py:472-473)
-      sd->Fc[E.i] = f;
-      sd->Q0[E.i] = qt;
-    }
-  }
-  bool inb = false;
+  stamp(sd, 1, 2, ta);
 #pragma unroll
-  for (int u = 0; u < CH_TB; ++u) {
-    if (kk[u] >= 0) {
-      const BathDev& bd = sd->bath[T->tb[u]];
-      const int64_t kb = (int64_t)kk[u] * B + E.b;
-      double fb = nz[u] - bd.c * (out_sum(T, lds, u, e) + sv[u]);
-      if (bd.has_q) {
-        const double yq = out_sum(T, lds, CH_TB + u, e);
-        fb -= yq;
-        bd.Yq[kb] = yq;  // Kq.q~ is the same in both id1 calls
+  for (int x = 0; x < EPT; ++x) {
+    const int e = threadIdx.x + x * NW * 64;
+    const bool hit1 = harm ? word_hit(w1[x]) : true;
+    double f = fc[x];  // potforce(q~)
+    if (!hit1 && E[x].in) {
+      f = -1.0 * out_sum(T, lds, 2 * CH_TB, e, Geo::NE);
+      if (E[x].ok) {  // md.potforce miss at q~: evaluate and cache (md.py:472-473)
+        G(sd->Fc)[E[x].i] = f;
+        G(sd->Q0)[E[x].i] = qt[x];
       }
-      f += fb;
-      inb = true;
     }
-  }
-  if (inb) {
-    const double p1 = ph + dt * f / 2.0;  // md.py:402 (p1 only feeds the bath friction terms)
+    bool inb = false;
 #pragma unroll
-    for (int u = 0; u < CH_TB; ++u)
-      if (kk[u] >= 0) {
-        const BathDev& bd = sd->bath[T->tb[u]];
-        bd.Xcur[bd.vs + (int64_t)kk[u] * B + E.b] = p1;
+    for (int u = 0; u < CH_TB; ++u) {
+      if (kk[x][u] >= 0) {
+        const ChBath& bd = T->tb[u];
+        const int64_t kb = (int64_t)kk[x][u] * B + E[x].b;
+        double fb = nz[x][u] - bd.c * (out_sum(T, lds, u, e, Geo::NE) + sv[x][u]);
+        if (bd.has_q) {
+          const double yq = out_sum(T, lds, CH_TB + u, e, Geo::NE);
+          fb -= yq;
+          G(bd.Yq)[kb] = yq;  // Kq.q~ is the same in both id1 calls
+        }
+        f += fb;
+        inb = true;
       }
+    }
+    if (inb) {
+      const double p1 = ph[x] + dt * f / 2.0;  // md.py:402 (p1 only feeds the bath friction terms)
+#pragma unroll
+      for (int u = 0; u < CH_TB; ++u)
+        if (kk[x][u] >= 0) {
+          const ChBath& bd = T->tb[u];
+          G(bd.Xcur)[bd.vs + (int64_t)kk[x][u] * B + E[x].b] = p1;
+        }
+    }
   }
 }
 
 // stage C, DOF tile
+template <int NW, int DRN>
 __device__ __forceinline__ void dof_C(const ChTile* __restrict__ T, const StepDev* __restrict__ sd,
                                       const StepArgs& ta, int mode, double* lds) {
+  using Geo = DofGeo<NW, DRN>;
+  constexpr int EPT = Geo::EPT;
   const int B = sd->B;
   const int64_t t = ta.t;
   const int t1 = (int)((t + 1) % sd->nmd);
   const int par = (int)(t & 1), par1 = par ^ 1;
   const double dt = sd->dt;
   const bool harm = mode != 0;
-  const Elem E = elem_of(T, sd);
-  double ph = 0.0, qt = 0.0, fc = 0.0, q0 = 0.0;
-  bool cons = false;
-  if (E.ok) {
-    ph = sd->Ph[E.i];
-    qt = sd->Qt[E.i];
-    fc = sd->Fc[E.i];
-    cons = sd->cmask[E.d] != 0;
-    if (harm) q0 = sd->Q0[E.i];
-  }
-  int kk[CH_TB];
-  double nz[CH_TB], sv[CH_TB], yq[CH_TB];
+  Elem E[EPT];
+  double ph[EPT], qt[EPT], fc[EPT], q0[EPT];
+  int cons[EPT];
+  int kk[EPT][CH_TB];
+  double nz[EPT][CH_TB], sv[EPT][CH_TB], yq[EPT][CH_TB];
 #pragma unroll
-  for (int u = 0; u < CH_TB; ++u) {
-    kk[u] = -1;
-    nz[u] = sv[u] = yq[u] = 0.0;
-    const int j = T->tb[u];
-    if (j >= 0) {
-      const BathDev& bd = sd->bath[j];
-      kk[u] = bath_row(T, bd, u, E);
-      if (kk[u] >= 0) {
-        const int64_t kb = (int64_t)kk[u] * B + E.b;
-        nz[u] = bd.noise[((int64_t)t1 * bd.nc + kk[u]) * B + E.b];
-        sv[u] = bd.S[(int64_t)par1 * bd.vs + kb];
-        if (bd.has_q) yq[u] = bd.Yq[kb];
+  for (int x = 0; x < EPT; ++x) {
+    E[x] = elem_of<NW, DRN>(T, sd, x);
+    ph[x] = qt[x] = fc[x] = q0[x] = 0.0;
+    cons[x] = 0;
+    if (E[x].ok) {
+      ph[x] = G(sd->Ph)[E[x].i];
+      qt[x] = G(sd->Qt)[E[x].i];
+      fc[x] = G(sd->Fc)[E[x].i];
+      cons[x] = G(sd->cmask)[E[x].d];
+      if (harm) q0[x] = G(sd->Q0)[E[x].i];
+    }
+#pragma unroll
+    for (int u = 0; u < CH_TB; ++u) {
+      kk[x][u] = -1;
+      nz[x][u] = sv[x][u] = yq[x][u] = 0.0;
+      {
+        const ChBath& bd = T->tb[u];
+        kk[x][u] = bath_row(bd, E[x]);
+        if (kk[x][u] >= 0) {
+          const int64_t kb = (int64_t)kk[x][u] * B + E[x].b;
+          nz[x][u] = G(bd.noise)[((int64_t)t1 * bd.nc + kk[x][u]) * B + E[x].b];
+          sv[x][u] = G(bd.S)[(int64_t)par1 * bd.vs + kb];
+          if (bd.has_q) yq[x][u] = G(bd.Yq)[kb];
+        }
       }
     }
   }
-  if (T->first && threadIdx.x < 16 && E.b < B) {
-    *pmax_word(sd, 1, par1, E.b) = 0ull;
-    if (harm) sd->qvalid[E.b] = 1;
+  if (T->first && threadIdx.x < Geo::NT && T->c0 + (int)threadIdx.x < B) {
+    *G(pmax_word(sd, 1, par1, T->c0 + threadIdx.x)) = 0ull;
+    if (harm) G(sd->qvalid)[T->c0 + threadIdx.x] = 1;
   }
-  run_products(T, t, B, lds);
+  run_products<NW>(T, t, lds);
   __syncthreads();
-  const int e = threadIdx.x;
-  double f = fc;
+  stamp(sd, 2, 2, ta);
+  double dq[EPT];
 #pragma unroll
-  for (int u = 0; u < CH_TB; ++u) {
-    if (kk[u] >= 0) {
-      const BathDev& bd = sd->bath[T->tb[u]];
-      f += nz[u] - bd.c * (out_sum(T, lds, u, e) + sv[u]) - yq[u];
-    }
-  }
-  double p2 = ph + dt * f / 2.0;  // md.py:404
-  double qn = qt;
-  if (cons) {  // ApplyConstraint (md.py:407-408, 782-794)
-    p2 = 0.0;
-    qn = 0.0;
-  }
-  if (E.ok) {
-    sd->P[E.i] = p2;
-    sd->Q[E.i] = qn;
-    sd->Flast[E.i] = f;
-  }
+  for (int x = 0; x < EPT; ++x) {
+    const int e = threadIdx.x + x * NW * 64;
+    double f = fc[x];
 #pragma unroll
-  for (int u = 0; u < CH_TB; ++u) {
-    if (kk[u] >= 0) {
-      const BathDev& bd = sd->bath[T->tb[u]];
-      // history push of p_{t+1} (rpadleft, md.py:387 of the next step), mirrored slot
-      const int64_t slot = cmod(t + 1, bd.R);
-      double* h = bd.H + (int64_t)kk[u] * bd.ldh + E.b;
-      h[slot * B] = p2;
-      h[(slot + bd.R) * B] = p2;
-      if (bd.has_q) bd.Xq[(int64_t)kk[u] * B + E.b] = qn;
+    for (int u = 0; u < CH_TB; ++u) {
+      if (kk[x][u] >= 0) {
+        const ChBath& bd = T->tb[u];
+        f += nz[x][u] - bd.c * (out_sum(T, lds, u, e, Geo::NE) + sv[x][u]) - yq[x][u];
+      }
     }
+    double p2 = ph[x] + dt * f / 2.0;  // md.py:404
+    double qn = qt[x];
+    if (cons[x] != 0) {  // ApplyConstraint (md.py:407-408, 782-794)
+      p2 = 0.0;
+      qn = 0.0;
+    }
+    if (E[x].ok) {
+      G(sd->P)[E[x].i] = p2;
+      G(sd->Q)[E[x].i] = qn;
+      G(sd->Flast)[E[x].i] = f;
+    }
+#pragma unroll
+    for (int u = 0; u < CH_TB; ++u) {
+      if (kk[x][u] >= 0) {
+        const ChBath& bd = T->tb[u];
+        // history push of p_{t+1} (rpadleft, md.py:387 of the next step): mirrored slot of the
+        // ladder's ring and the chain's near ring
+        const int64_t kb = (int64_t)kk[x][u] * B + E[x].b;
+        const int64_t slot = cmod(t + 1, bd.R);
+        __attribute__((address_space(1))) double* h = G(bd.H + (int64_t)kk[x][u] * bd.ldh + E[x].b);
+        h[slot * B] = p2;
+        h[(slot + bd.R) * B] = p2;
+        G(bd.NR)[cmod(t + 1, bd.NRS) * bd.vs + kb] = p2;
+        if (bd.has_q) G(bd.Xq)[kb] = qn;
+      }
+    }
+    dq[x] = E[x].ok ? fabs(qn - q0[x]) : 0.0;
   }
   if (harm) {  // cache distance of q_{t+1} for the next step's id0 call
-    const double dq = E.ok ? fabs(qn - q0) : 0.0;
-    bool nan;
-    const double m = col_max(dq, lds, nan);
-    if (threadIdx.x < 16 && E.b < B) {
+    __syncthreads();
+#pragma unroll
+    for (int x = 0; x < EPT; ++x) {
+      const int e = threadIdx.x + x * NW * 64;
+      if (E[x].in) lds[e] = dq[x];
+    }
+    __syncthreads();
+    const int c = threadIdx.x;
+    const int b = T->c0 + c;
+    if (c < Geo::NT && b < B) {
+      bool nan;
+      const double m = col_red<NW, DRN>(lds, 0, c, true, nan);
       const unsigned long long bits = nan ? 0x7FF8000000000000ull : (unsigned long long)__double_as_longlong(m);
-      atomicMax(pmax_word(sd, 0, par1, E.b), bits);
+      atomicMax(pmax_word(sd, 0, par1, b), bits);
     }
   }
 }
 
-// S(t+1) of bath rows [row0, row0+16): K_1.p_t (the products) + near-field partials + levels
+// S(t+1) of bath rows [row0, row0+16) x 16 rn columns: K_1.p_t (the products) + near-field
+// partials + levels
+template <int NW, int DRN>
 __device__ __forceinline__ void sfin(const ChTile* __restrict__ T, const StepDev* __restrict__ sd,
-                                     const StepArgs& ta, double* lds) {
+                                     const StepArgs& ta, double* lds, int stage) {
   const int B = sd->B;
   const int64_t t = ta.t;
   const int par1 = (int)((t + 1) & 1);
-  const BathDev& bd = sd->bath[T->tile];
-  const int r = threadIdx.x >> 4;
-  const int k = T->row0 + r;
-  const int b = T->c0 + (threadIdx.x & 15);
-  const bool ok = k < bd.nc && b < B;
-  const int64_t kb = (int64_t)k * B + b;
-  // near-field partials and level blocks, added in slot / level order (8 loads in flight)
-  double sn = 0.0, pre = 0.0;
-  if (ok) {
-    const double* np = bd.NP + (int64_t)par1 * bd.nqn * bd.vs + kb;
-    for (int q0 = 0; q0 < bd.nqn; q0 += 8) {
-      double v[8];
+  const ChSfin& sf = T->sf;
+  constexpr int NT = 16 * DRN, NE = 16 * NT;  // S(t+1) tiles have the DOF tiles' width
+  constexpr int EPT = (NE + NW * 64 - 1) / (NW * 64);
+  double pre[EPT];
+  int64_t kb[EPT];
+  bool ok[EPT];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = (q0 + u < bd.nqn) ? np[(int64_t)(q0 + u) * bd.vs] : 0.0;
+  for (int x = 0; x < EPT; ++x) {
+    const int e = threadIdx.x + x * NW * 64;
+    const int k = T->row0 + e / NT;
+    const int b = T->c0 + e % NT;
+    ok[x] = e < NE && k < sf.nc && b < B;
+    kb[x] = (int64_t)k * B + b;
+    // near-field partials and level blocks, all loads in flight together, added in slot / level
+    // order
+    double v[CH_NPMAX], lv[MAXLVL];
+    gdouble* np = G(sf.NP) + (sf.nqn > 0 ? (int64_t)par1 * sf.nqn * sf.vs + (ok[x] ? kb[x] : 0) : 0);
+    // unconditional loads (slot min(q, nqn-1); nqn == 0 reads the zero row), masked in the sum
 #pragma unroll
-      for (int u = 0; u < 8; ++u) sn += v[u];
-    }
-    double lv[MAXLVL];
+    for (int q = 0; q < CH_NPMAX; ++q) v[q] = np[(int64_t)min(q, max(sf.nqn - 1, 0)) * sf.vs];
 #pragma unroll
     for (int l = 0; l < MAXLVL; ++l)
-      lv[l] = (l < bd.nlvl && bd.lvl[l]) ? bd.lvl[l][(int64_t)k * bd.lvl_ld[l] + ta.lvl_off[l] + b] : 0.0;
+      lv[l] = G(sf.lvl[l])[(ok[x] ? (int64_t)k * sf.lvl_ld[l] + b : 0) + ta.lvl_off[l]];
+    double sn = 0.0, lvs = 0.0;
 #pragma unroll
-    for (int l = 0; l < MAXLVL; ++l) pre += lv[l];
+    for (int q = 0; q < CH_NPMAX; ++q) sn += (q < sf.nqn) ? v[q] : 0.0;
+#pragma unroll
+    for (int l = 0; l < MAXLVL; ++l) lvs += lv[l];
+    pre[x] = lvs + sn;
   }
-  run_products(T, t, B, lds);
+  run_products<NW>(T, t, lds);
   __syncthreads();
-  const double s = out_sum(T, lds, 0, threadIdx.x) + sn;
-  if (ok) bd.S[(int64_t)par1 * bd.vs + kb] = pre + s;
+  stamp(sd, stage, 2, ta);
+#pragma unroll
+  for (int x = 0; x < EPT; ++x) {
+    const int e = threadIdx.x + x * NW * 64;
+    if (ok[x]) G(sf.S)[(int64_t)par1 * sf.vs + kb[x]] = out_sum(T, lds, 0, e, NE) + pre[x];
+  }
 }
 
 // near-field partial tile: rows [0, nrows) x columns [0, ncols) of the parity buffer of t + par_shift
-__device__ __forceinline__ void raw(const ChTile* __restrict__ T, const StepDev* __restrict__ sd, const StepArgs& ta, double* lds) {
+template <int NW>
+__device__ __forceinline__ void raw(const ChTile* __restrict__ T, const StepDev* __restrict__ sd, const StepArgs& ta,
+                                    double* lds, int stage) {
   const int64_t t = ta.t;
-  run_products(T, t, sd->B, lds);
+  run_products<NW>(T, t, lds);
   __syncthreads();
-  const int rn = T->rn, NT = 16 * rn;
+  stamp(sd, stage, 2, ta);
+  const int NT = 16 * T->rn;
   double* dst = T->dst + ((t + T->par_shift) & 1) * T->par_stride;
-  for (int e = threadIdx.x; e < 16 * NT; e += CH_NW * 64) {
+  for (int e = threadIdx.x; e < 16 * NT; e += NW * 64) {
     double v = 0.0;
     for (int s = T->ob[0]; s < T->ob[1]; ++s) v += lds[s * 16 * NT + e];
     const int row = e / NT, col = e - row * NT;
-    if (row < T->nrows && col < T->ncols) dst[(int64_t)row * T->ldd + col] = v;
+    if (row < T->nrows && col < T->ncols) G(dst)[(int64_t)row * T->ldd + col] = v;
   }
 }
 
-template <int STAGE>
-__global__ __launch_bounds__(CH_NW * 64) void chain_kernel(const ChTile* __restrict__ tiles,
-                                                           const StepDev* __restrict__ sd, StepArgs ta,
-                                                           int mode) {
-  __shared__ double lds[CH_LDS];
-  const ChTile* T = tiles + blockIdx.x;
-  const int kind = T->kind;
-  if (kind == CH_DOF) {
-    if (STAGE == 0) dof_A(T, sd, ta, mode, lds);
-    else if (STAGE == 1) dof_B(T, sd, ta, mode, lds);
-    else dof_C(T, sd, ta, mode, lds);
-  } else if (kind == CH_SFIN) {
-    sfin(T, sd, ta, lds);
-  } else {
-    raw(T, sd, ta, lds);
+template <int STAGE, int NW, int DRN>
+__global__ __launch_bounds__(NW * 64) void chain_kernel(const ChTile* __restrict__ tiles, const StepDev* sd,
+                                                        StepArgs ta, int mode) {
+  extern __shared__ double lds[];
+  // The tile descriptor and the step descriptor's header are copied into LDS with one round of
+  // coalesced vector loads: every later field access is an LDS read instead of a chain of
+  // dependent scalar loads.
+  constexpr int NTW = sizeof(ChTile) / 8, NSW = (offsetof(StepDev, bath) + 7) / 8;
+  __shared__ unsigned long long tdw[NTW], sdw[NSW];
+  stamp(sd, STAGE, 0, ta);
+  {
+    const __attribute__((address_space(1))) unsigned long long* tsrc =
+        (const __attribute__((address_space(1))) unsigned long long*)(tiles + blockIdx.x);
+    const __attribute__((address_space(1))) unsigned long long* ssrc =
+        (const __attribute__((address_space(1))) unsigned long long*)sd;
+    for (int i = threadIdx.x; i < NTW + NSW; i += NW * 64) {
+      if (i < NTW) tdw[i] = tsrc[i];
+      else sdw[i - NTW] = ssrc[i - NTW];
+    }
   }
+  __syncthreads();
+  const ChTile* T = (const ChTile*)tdw;
+  sd = (const StepDev*)sdw;  // header only: bath[] is not copied (tiles carry their baths)
+  const int kind = T->kind;
+  stamp(sd, STAGE, 1, ta);
+  if (kind == CH_DOF) {
+    if (STAGE == 0) dof_A<NW, DRN>(T, sd, ta, mode, lds);
+    else if (STAGE == 1) dof_B<NW, DRN>(T, sd, ta, mode, lds);
+    else dof_C<NW, DRN>(T, sd, ta, mode, lds);
+  } else if (kind == CH_SFIN) {
+    sfin<NW, DRN>(T, sd, ta, lds, STAGE);
+  } else {
+    raw<NW>(T, sd, ta, lds, STAGE);
+  }
+  stamp(sd, STAGE, 3, ta);
+}
+
+template <int STAGE, int NW>
+void launch_nd(int drn, size_t lds, const ChTile* tiles, int ntiles, const StepDev* sd, StepArgs ta, int mode,
+               hipStream_t s) {
+  if (drn == 2) chain_kernel<STAGE, NW, 2><<<ntiles, NW * 64, lds, s>>>(tiles, sd, ta, mode);
+  else chain_kernel<STAGE, NW, 1><<<ntiles, NW * 64, lds, s>>>(tiles, sd, ta, mode);
+}
+
+template <int STAGE>
+void launch_st(int nw, int drn, size_t lds, const ChTile* tiles, int ntiles, const StepDev* sd, StepArgs ta,
+               int mode, hipStream_t s) {
+  if (nw == 16) launch_nd<STAGE, 16>(drn, lds, tiles, ntiles, sd, ta, mode, s);
+  else if (nw == 8) launch_nd<STAGE, 8>(drn, lds, tiles, ntiles, sd, ta, mode, s);
+  else launch_nd<STAGE, 4>(drn, lds, tiles, ntiles, sd, ta, mode, s);
 }
 
 }  // namespace
 
-void launch_chain(int stage, const ChTile* tiles, int ntiles, const StepDev* sd, StepArgs ta, int mode,
-                  hipStream_t s) {
+void launch_chain(int stage, int nw, int drn, size_t lds_bytes, const ChTile* tiles, int ntiles, const StepDev* sd,
+                  StepArgs ta, int mode, hipStream_t s) {
   if (ntiles <= 0) return;
-  switch (stage) {
-    case 0: chain_kernel<0><<<ntiles, CH_NW * 64, 0, s>>>(tiles, sd, ta, mode); break;
-    case 1: chain_kernel<1><<<ntiles, CH_NW * 64, 0, s>>>(tiles, sd, ta, mode); break;
-    default: chain_kernel<2><<<ntiles, CH_NW * 64, 0, s>>>(tiles, sd, ta, mode); break;
-  }
+  if (stage == 0) launch_st<0>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
+  else if (stage == 1) launch_st<1>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
+  else launch_st<2>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
 }
 
 }  // namespace gle

@@ -75,6 +75,7 @@ struct BathDev {
   double* H;           // history ring
   double* cur;         // heat current [nmd][B]
   double* NP;          // near-field partial slots [2 parity][nqn][ncp][B] (lags [2, nn))
+  double* NR;          // near ring: p of the newest NRS steps, slot-major [NRS][vs] (slot = t mod NRS)
   const double* lvl[MAXLVL];  // ladder level block buffers [ncp][2 P B] (nullptr: inactive)
   int32_t lvl_ld[MAXLVL];
   double c;            // dt factor (dt if ml > 1 else 1, baths.py:454-457)
@@ -84,7 +85,7 @@ struct BathDev {
   int32_t has_q;
   int32_t nqn;         // near-field partial slots per parity
   int32_t nlvl;
-  int32_t pad;
+  int32_t NRS;         // near-ring slots
 };
 
 struct StepDev {
@@ -97,7 +98,9 @@ struct StepDev {
   double* part;           // [nmd][ndblk][nbath+1][B] current / energy partial sums per step
   const uint8_t* cmask;   // [nph] constraint mask
   int32_t ndblk;          // DOF tiles (16 DOFs each) = current partial rows per step
-  int32_t pad;
+  int32_t dbg_ntile;      // stamp slots per stage
+  unsigned long long* dbg;   // GLE_CHAIN_DBG: [3 stages][dbg_ntile][4] s_memrealtime stamps, or nullptr
+  int64_t dbg_t;          // step whose launches record stamps
   BathDev bath[MAXBATH];
 };
 
@@ -111,12 +114,12 @@ struct StepDev {
 //            constraints, history push)
 //   CH_SFIN  16 bath rows: S(t+1) = K_1 p_t + near-field partials + ladder levels
 //   CH_RAW   16 bath rows x 16*rn columns of a near-field partial (lags >= 2, target t+2)
-constexpr int CH_NW = 4;        // waves per chain workgroup
-constexpr int CH_TPW = 4;       // tasks per wave
+constexpr int CH_NW = 16;       // waves per chain workgroup (max)
+constexpr int CH_TPW = 3;       // tasks per wave
 constexpr int CH_TB = 3;        // baths a DOF tile may intersect
 constexpr int CH_NOUT = 2 * CH_TB + 1;
-constexpr int CH_LDS = 4096;    // doubles of LDS partial slots (32 KB)
-constexpr int CH_NPMAX = 32;    // near-field partial slots read by one SFIN element
+constexpr int CH_LDS_PER_WAVE = 1024;  // doubles of LDS partial slots per wave
+constexpr int CH_NPMAX = 16;    // near-field partial slots read by one SFIN element
 enum { CH_DOF = 0, CH_SFIN = 1, CH_RAW = 2 };
 
 struct ChTask {
@@ -125,9 +128,37 @@ struct ChTask {
   int32_t a_ks;      // doubles between consecutive k-steps of A
   int32_t ldx;       // X row stride (doubles)
   int32_t nks;       // k-steps
-  int32_t ring;      // ring slots R of a history-ring X (0: static X)
-  int32_t tshift;    // ring: column slot pmod(t + tshift, ring)
+  int32_t ring;      // ring slots of a ring X (0: static X)
+  int32_t tshift;    // ring: slot pmod(t + tshift, ring)
+  int32_t sst;       // ring: doubles between slots
   int32_t slot;      // LDS partial slot
+  int32_t pad;
+};
+
+// One bath of a DOF tile, copied out of BathDev so the epilogue's operands are one descriptor
+// round trip away.  DOF row0 + r is in the bath iff bit r of bmask; bath-local k = DOF + boff
+// (CH_INV: k from inv).
+struct ChBath {
+  const double* noise;
+  double *S, *Xcur, *Xq, *Yq, *H, *NR;
+  const int32_t* inv;
+  double c;
+  int64_t vs;
+  int32_t nc, ldh, R, NRS, has_q;
+  int32_t bath;      // StepDev bath index, -1: none
+  uint32_t bmask;
+  int32_t boff;
+};
+
+// The bath of an S(t+1) tile: near-field partial slots and ladder level blocks (unused levels
+// point at a zero row with ld 0, so every load is unconditional)
+struct ChSfin {
+  const double* NP;  // parity-0 slot 0 of the bath's near-field partials
+  double* S;
+  const double* lvl[MAXLVL];
+  int32_t lvl_ld[MAXLVL];
+  int64_t vs;
+  int32_t nqn, nc;
 };
 
 struct ChTile {
@@ -142,16 +173,12 @@ struct ChTile {
   double* dst;       // CH_RAW: row 0, column 0 of the tile in parity buffer 0
   int32_t ldd;
   int32_t first;     // CH_DOF: the tile that zeroes the other-parity cache words
-  int8_t ntw[CH_NW]; // tasks of wave w
-  int8_t ob[CH_NOUT + 1];  // output o adds LDS slots [ob[o], ob[o+1]); outputs: Y of tile bath u
-                           // (u < CH_TB), YQ of tile bath u (CH_TB + u), YD (2 CH_TB);
-                           // CH_SFIN / CH_RAW use output 0
-  int8_t pad[8 - (CH_NW + CH_NOUT + 1) % 8];
-  // CH_DOF: the tile's baths tb[u] (-1: none); DOF row0 + r is in bath tb[u] iff bit r of bmask[u];
-  // bath-local k = DOF + boff[u] (CH_INV: k from the bath's inv table)
-  int32_t tb[CH_TB];
-  uint32_t bmask[CH_TB];
-  int32_t boff[CH_TB];
+  int32_t ntw[CH_NW]; // tasks of wave w (32-bit: read with scalar loads)
+  int32_t ob[CH_NOUT + 1];  // output o adds LDS slots [ob[o], ob[o+1]); outputs: Y of tile bath u
+                            // (u < CH_TB), YQ of tile bath u (CH_TB + u), YD (2 CH_TB);
+                            // CH_SFIN / CH_RAW use output 0
+  ChBath tb[CH_TB];  // CH_DOF: the baths meeting the tile
+  ChSfin sf;         // CH_SFIN
   ChTask task[CH_NW][CH_TPW];
 };
 constexpr int32_t CH_INV = -0x40000000;
@@ -161,6 +188,8 @@ constexpr int32_t CH_INV = -0x40000000;
 // current far / mid blocks were computed, so no kernel starts with a dependent load of a clock
 struct StepArgs {
   int64_t t;                 // md.t of this step
+  int32_t dbg;               // GLE_CHAIN_DBG: record this launch's timeline
+  int32_t pad;
   int64_t lvl_off[MAXLVL];   // per level: offset (doubles) of target t+1 in its block buffer
 };
 void launch_contract(int rn, int cu, const CItem* items, int nitems, StepArgs ta, hipStream_t s);
@@ -169,11 +198,13 @@ void launch_reduce(const RItem* items, int nitems, int max_elems, StepArgs ta,
 // stage 0/1/2 = A/B/C.  mode: A: 1 = harmonic id0 potential with md.potforce's cache rule (YD = dyn.q_t
 // present), 0 = potential force at q_t already in Fc; bit 1: write the id1 cache distance.
 // B / C: 1 = harmonic force at q~ (B computes YD = dyn.q~), 0 = host force in Fc.
-void launch_chain(int stage, const ChTile* tiles, int ntiles, const StepDev* sd, StepArgs ta, int mode,
-                  hipStream_t s);
+void launch_chain(int stage, int nw, int drn, size_t lds_bytes, const ChTile* tiles, int ntiles, const StepDev* sd,
+                  StepArgs ta, int mode, hipStream_t s);
 void launch_finalize(const StepDev* sd, int B, int nmd, int nbath, hipStream_t s);
 void launch_philox_normal(double* x, int64_t nfreq, int64_t ncp, int64_t nc, int64_t B,
                           uint64_t seed, uint64_t traj_offset, hipStream_t s);
+void launch_near_fill(const double* H, int64_t ldh, int R, int B, int ncp, double* NR, int64_t vs, int NRS,
+                      int64_t t, hipStream_t s);
 void launch_ring_copy(double* H, int64_t ldh, int R, int B, int nc, int64_t tau0, int nt, double* buf,
                       int dir, hipStream_t s);
 void launch_contract_cplx(int rn, const CItem* items, int nitems, StepArgs ta, hipStream_t s);

@@ -575,6 +575,28 @@ void launch_ring_copy(double* H, int64_t ldh, int R, int B, int nc, int64_t tau0
   ring_copy_kernel<<<(unsigned)blocks, 256, 0, s>>>(H, ldh, R, B, nc, tau0, nt, buf, dir);
 }
 
+// near ring (slot-major [NRS][vs], the chain's compact copy of the newest p): slots of times
+// t, t-1, ..., t-NRS+1 from the history ring
+__global__ void near_fill_kernel(const double* __restrict__ H, int64_t ldh, int R, int B, int ncp,
+                                 double* __restrict__ NR, int64_t vs, int NRS, int64_t t) {
+  const int64_t n = (int64_t)NRS * ncp * B;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = e % B;
+    const int64_t k = (e / B) % ncp;
+    const int64_t s = e / ((int64_t)B * ncp);
+    const int64_t tau = t - s;
+    NR[pmod(tau, NRS) * vs + k * B + b] = H[k * ldh + pmod(tau, R) * B + b];
+  }
+}
+
+void launch_near_fill(const double* H, int64_t ldh, int R, int B, int ncp, double* NR, int64_t vs, int NRS,
+                      int64_t t, hipStream_t s) {
+  const int64_t n = (int64_t)NRS * ncp * B;
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
+  near_fill_kernel<<<(unsigned)blocks, 256, 0, s>>>(H, ldh, R, B, ncp, NR, vs, NRS, t);
+}
+
 }  // namespace gle
 
 namespace gle {
