@@ -105,7 +105,11 @@ struct Level {
   int cstride = 1;             // twiddle-table stride (Pspec / P)
   int sidx = 0;                // background stream
   std::vector<LevelBath> lb;   // per bath
-  Op op[2];                    // direct: per output parity; spectral: op[0] (per-frequency products)
+  Op op[2];                    // direct: per output parity
+  std::vector<CgItem> cg;      // spectral: the batched GEMM of the per-frequency products
+  CgItem* d_cg = nullptr;
+  int cg_rn = 4;
+  double cg_flops = 0, cg_bytes = 0;  // algorithmic, per block
   hipEvent_t ev[2] = {nullptr, nullptr};
   int64_t last_block = INT64_MIN;
   int64_t bg_block[2] = {INT64_MIN, INT64_MIN};  // block launched on the background stream
@@ -1020,9 +1024,9 @@ int freeze(gle_handle* h) {
       for (auto& b : h->baths) {
         if (b.ml <= lv.lag0) continue;
         const int M = (std::min(lv.lag1, b.ml) + lv.P - 1) / lv.P - 2;
-        need += (size_t)(lv.P + 1) * 2 * b.nrt * b.nks * M * 64 * 8;
-        need += (size_t)(lv.P + 1) * 2 * b.ncp * (2 * (M + 4) * B + 1024) * 8;
-        need += (size_t)(lv.P + 1) * 2 * b.nc * B * 8;
+        need += (size_t)(lv.P + 1) * 3 * b.nrt * b.nks * M * 64 * 8;
+        need += (size_t)(lv.P + 1) * 3 * b.ncp * (2 * (M + 4) * B + 1024) * 8;
+        need += (size_t)(lv.P + 1) * 3 * b.nc * B * 8;
       }
     }
     size_t fr = 0, tot = 0;
@@ -1079,9 +1083,9 @@ int freeze(gle_handle* h) {
       L.M = (L.lag1 + lv.P - 1) / lv.P - 2;
       L.Rseg = L.M + 4;
       L.ldseg = 2 * (int64_t)L.Rseg * B + 512;
-      L.khat_fstride = (int64_t)2 * b.nrt * b.nks * L.M * 64;  // Re block then Im block
-      L.seg_fstride = (int64_t)2 * b.ncp * L.ldseg;             // Re rows then Im rows
-      L.yfstride = (int64_t)2 * b.nc * B;
+      L.khat_fstride = (int64_t)3 * b.nrt * b.nks * L.M * 64;  // the three Gauss planes
+      L.seg_fstride = (int64_t)3 * b.ncp * L.ldseg;             // Re + Im, Im, Re rows
+      L.yfstride = (int64_t)3 * b.nc * B;                       // T_0, T_1, T_2
       rc = dalloc_n(h, &L.d_khat, (size_t)(lv.P + 1) * L.khat_fstride);
       if (!rc) rc = dalloc_n(h, &L.d_seg, (size_t)(lv.P + 1) * L.seg_fstride + 4096);
       if (!rc) rc = dalloc_n(h, &L.d_Yspec, (size_t)(lv.P + 1) * L.yfstride + 4096);
@@ -1151,44 +1155,46 @@ int freeze(gle_handle* h) {
   //             (the segment ring holds Xhat of the segments ending at sigma*P)
   for (auto& lv : h->levels) {
     if (lv.spectral) {
-      Op& op = lv.op[0];
-      op.cplx = true;
-      Planner p(h, op, rn_step);
-      int nprod = 0;
-      for (auto& L : lv.lb)
-        if (L.active) nprod += lv.P + 1;
+      // one workgroup per (bath, f, Gauss part g, 64-row group, 16 RN-column tile); items of one
+      // (f, g) are adjacent, so the row groups that share an X window run together
+      lv.cg.clear();
+      lv.cg_rn = (int)std::min<int64_t>(4, (B + 15) / 16);
+      lv.cg_flops = lv.cg_bytes = 0;
+      const int NT = 16 * lv.cg_rn;
       for (size_t j = 0; j < h->baths.size(); ++j) {
         Bath& b = h->baths[j];
         LevelBath& L = lv.lb[j];
         if (!L.active) continue;
-        for (int f = 0; f <= lv.P; ++f) {
-          Gemm g{};
-          g.cplx = true;
-          g.A = L.d_khat + (int64_t)f * L.khat_fstride;
-          g.a_ks = (int64_t)L.M * 64;
-          g.a_rt = (int64_t)b.nks * g.a_ks;
-          g.a_im = (int64_t)b.nrt * b.nks * L.M * 64;
-          g.nrt_total = b.nrt;
-          g.nks_total = b.nks;
-          g.i0 = 0;
-          g.i1 = L.M;
-          g.X = L.d_seg + (int64_t)f * L.seg_fstride;
-          g.x_im = (int64_t)b.ncp * L.ldseg;
-          g.ldx = L.ldseg;
-          g.ring = L.Rseg;
-          g.cs = (int)B;
-          g.tshift = 0;
-          g.tdiv = lv.P;
-          g.M = b.nc;
-          g.Kd = b.nc;
-          g.N = (int)B;
-          g.dst = L.d_Yspec + (int64_t)f * L.yfstride;
-          g.dst_im = (int64_t)b.nc * B;
-          g.ldd = B;
-          p.add(g, std::max(1, 1536 / std::max(1, nprod)), 16);
-        }
+        const int64_t a_rt = (int64_t)L.M * b.nks * 64;
+        const int64_t plane = (int64_t)b.nrt * a_rt;
+        for (int f = 0; f <= lv.P; ++f)
+          for (int g = 0; g < 3; ++g) {
+            for (int rg = 0; 4 * rg < b.nrt; ++rg)
+              for (int c0 = 0; c0 < B; c0 += NT) {
+                CgItem it{};
+                it.A = L.d_khat + (int64_t)f * L.khat_fstride + g * plane + (int64_t)4 * rg * a_rt;
+                it.X = L.d_seg + (int64_t)f * L.seg_fstride + (int64_t)g * b.ncp * L.ldseg;
+                it.out = L.d_Yspec + (int64_t)f * L.yfstride + (int64_t)g * b.nc * B + (int64_t)64 * rg * B + c0;
+                it.a_rt = a_rt;
+                it.ldx = (int32_t)L.ldseg;
+                it.cs = (int32_t)B;
+                it.Rseg = L.Rseg;
+                it.M = L.M;
+                it.nks = b.nks;
+                it.nrt = std::min(4, b.nrt - 4 * rg);
+                it.nrows = std::min(64, b.nc - 64 * rg);
+                it.ncols = (int)std::min<int64_t>(NT, B - c0);
+                it.ldo = (int32_t)B;
+                it.col0 = c0;
+                lv.cg.push_back(it);
+              }
+            // algorithmic work of T_g(f): A read once, X window read once, T written
+            lv.cg_flops += 2.0 * b.nc * ((double)L.M * b.nc) * B;
+            lv.cg_bytes += 8.0 * ((double)b.nc * L.M * b.nc + (double)L.M * b.nc * B + (double)b.nc * B);
+          }
       }
-      rc = p.done();
+      rc = dalloc_n(h, &lv.d_cg, lv.cg.size());
+      if (!rc) rc = upload(h, lv.d_cg, lv.cg.data(), lv.cg.size() * sizeof(CgItem));
       if (rc) return rc;
     } else {
       for (int par = 0; par < 2; ++par) {
@@ -1304,7 +1310,22 @@ int launch_level_block(gle_handle* h, Level& lv, int64_t k, hipStream_t s, bool 
                          L.seg_fstride, L.ldseg, L.Rseg, h->d_cstab, lv.cstride, s))
         return fail(h, GLE_ERR_UNSUP, "segment transform launch failed (P = " + std::to_string(lv.P) + ")");
     }
-    run_op(h, lv.op[0], s, ta, true);
+    // the batched GEMM of the per-frequency products, profiled like run_op (the dominant kernel)
+    hipEvent_t e1 = nullptr;
+    if (h->prof && !lv.cg.empty()) {
+      if (h->ev_used + 2 > h->ev.size()) drain_profile(h);
+      hipEventRecord(h->ev[h->ev_used], s);
+      e1 = h->ev[h->ev_used + 1];
+      h->ev_used += 2;
+    }
+    launch_cgemm(lv.cg_rn, lv.d_cg, (int)lv.cg.size(), T / lv.P, s);
+    if (e1) {
+      hipEventRecord(e1, s);
+      h->prof_n += 1;
+      h->prof_flops += lv.cg_flops;
+      h->prof_bytes += lv.cg_bytes;
+    }
+    (void)ta;
     for (size_t j = 0; j < h->baths.size(); ++j) {
       Bath& b = h->baths[j];
       LevelBath& L = lv.lb[j];
@@ -2125,7 +2146,7 @@ int gle_plan_info(gle_handle* h, int64_t* block_len, int64_t* far_items, int64_t
                   int32_t* far_mode) {
   if (!h) return GLE_ERR_ARG;
   int64_t items = 0;
-  for (auto& lv : h->levels) items += (int64_t)lv.op[0].items.size();
+  for (auto& lv : h->levels) items += (int64_t)(lv.spectral ? lv.cg.size() : lv.op[0].items.size());
   if (block_len) *block_len = h->frozen ? h->P0 : 0;
   if (far_mode) *far_mode = h->frozen ? h->far_mode : h->cfg.far_mode;
   if (far_items) *far_items = items;

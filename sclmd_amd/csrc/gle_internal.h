@@ -52,6 +52,20 @@ struct CItem {
   int64_t a_im, x_im, o_im;
 };
 
+// One workgroup of a spectral level's batched GEMM (gle_kernels.hip cgemm_kernel): 64 rows x 16 RN
+// columns of T_g(f) = sum_m A_g(f, m) X_g(f, sigma - m).
+struct CgItem {
+  const double* A;   // A plane of (f, g) at row tile 4 rg, k-step 0: [rt][m][ks][64]
+  const double* X;   // segment-ring plane of (f, g), row 0
+  double* out;       // T_g(f) at row 64 rg, column col0
+  int64_t a_rt;      // doubles between row tiles of A (M nks 64)
+  int32_t ldx, cs;   // X row stride, columns per ring slot (B)
+  int32_t Rseg, M, nks;
+  int32_t nrt;       // row tiles present (<= 4)
+  int32_t nrows, ncols;  // valid rows (<= 64), columns
+  int32_t ldo, col0;
+};
+
 // Deterministic fixed-order sum of split partial tiles (+ optional far-field addend).
 struct RItem {
   double* dst;
@@ -208,6 +222,7 @@ void launch_near_fill(const double* H, int64_t ldh, int R, int B, int ncp, doubl
 void launch_ring_copy(double* H, int64_t ldh, int R, int B, int nc, int64_t tau0, int nt, double* buf,
                       int dir, hipStream_t s);
 void launch_contract_cplx(int rn, const CItem* items, int nitems, StepArgs ta, hipStream_t s);
+void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStream_t s);
 void launch_khat_pack(const double* Kf, int ml, int nks_k, double* khat, int P, int m0, int M,
                       int nc, int nrt2, int nks2, const double* cstab, int cstride, hipStream_t s);
 int launch_seg_fft(const double* H, int64_t ldh, int R, int B, int nc, int ncp, int P, int64_t T,

@@ -607,28 +607,28 @@ namespace gle {
 // cstab[q] = (cos(pi q / Pmax), sin(pi q / Pmax)), q < 2 Pmax; a level reads it with stride
 // Pmax / P, so e^{-i pi f n / P} = (cs.x, -cs.y) at q = ((f n) mod 2P) * stride.
 //
-//   Khat_m(f) = sum_i' k_m[i'] e^{-i pi f i'/P}, f = 0..P, packed as the real block
-//   [[Re, -Im], [Im, Re]] (2nc x 2nc) in fragment-native order [f][part][rt][ks][m-m0][64], read
-//   straight out of the fragment-native K already on the device (one-time setup).
+//   Khat_m(f) = sum_i' k_m[i'] e^{-i pi f i'/P}, f = 0..P, stored as the three real planes of the
+//   Gauss 3-multiplication  g = 0: Re,  1: Re + Im,  2: Im - Re  in fragment-native order
+//   [f][g][rt][m - m0][ks][64] (a wave streams its row tile's k-steps contiguously), read straight
+//   out of the fragment-native K already on the device (one-time setup).
 __global__ void khat_pack_kernel(const double* __restrict__ Kf, int ml, int nks_k,
                                  double* __restrict__ khat, int P, int m0, int M, int nc, int nrt2,
                                  int nks2, const double2* __restrict__ cstab, int cstride) {
-  const int64_t total = (int64_t)(P + 1) * 2 * nrt2 * nks2 * M * 64;
+  const int64_t total = (int64_t)(P + 1) * nrt2 * M * nks2 * 64;
+  const int64_t plane = (int64_t)nrt2 * M * nks2 * 64;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int lane = (int)(e & 63);
     int64_t r_ = e >> 6;
-    const int mm = (int)(r_ % M);
-    r_ /= M;
     const int ks2 = (int)(r_ % nks2);
     r_ /= nks2;
+    const int mm = (int)(r_ % M);
+    r_ /= M;
     const int rt2 = (int)(r_ % nrt2);
-    r_ /= nrt2;
-    const int part = (int)(r_ & 1);
-    const int f = (int)(r_ >> 1);
+    const int f = (int)(r_ / nrt2);
     const int r = 16 * rt2 + (lane & 15);
     const int k = 4 * ks2 + (lane >> 4);
-    double v = 0.0;
+    double re = 0.0, im = 0.0;
     if (r < nc && k < nc) {
       const int64_t base = (((int64_t)(r >> 4) * nks_k + (k >> 2)) * ml) * 64 + (r & 15) + 16 * (k & 3);
       const int m = mm + m0;
@@ -637,10 +637,14 @@ __global__ void khat_pack_kernel(const double* __restrict__ Kf, int ml, int nks_
         if (i >= ml) break;
         const double kv = Kf[base + (int64_t)i * 64];
         const double2 cs = cstab[((f * ip) % (2 * P)) * cstride];
-        v += part ? -kv * cs.y : kv * cs.x;
+        re += kv * cs.x;
+        im -= kv * cs.y;
       }
     }
-    khat[e] = v;
+    const int64_t o = (int64_t)f * 3 * plane + (((int64_t)rt2 * M + mm) * nks2 + ks2) * 64 + lane;
+    khat[o] = re;
+    khat[o + plane] = re + im;
+    khat[o + 2 * plane] = im - re;
   }
 }
 
@@ -678,10 +682,113 @@ __device__ __forceinline__ void lds_fft(double2* buf, int logn, const double2* _
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Spectral level contraction as a batched real GEMM: for every (bath, frequency f, Gauss part g)
+//   T_g(f)[nc x B] = sum_{m < M} A_g(f, m)[nc x nc] . X_g(f, sigma - m)[nc x B],   sigma = T / P
+// (the Gauss 3-multiplication of the complex per-frequency products: 3 real products, not 4).
+// A workgroup owns 64 rows x 16 RN columns of one T_g(f): each of its 4 waves streams its 16-row
+// tile's A fragments from HBM into registers one chunk ahead; X moves through a double-buffered
+// LDS chunk of CG_KC k-steps shared by the 4 waves.  No split over k: no partials, no reduce.
+constexpr int CG_KC = 8;   // k-steps per LDS chunk
+constexpr int CG_LD = 80;  // LDS row stride (doubles): 64 columns + 16, ds_read_b64 at most 2-way
+
+template <int RN>
+__global__ __launch_bounds__(256, 2) void cgemm_kernel(const CgItem* __restrict__ items, int64_t tseg) {
+  __shared__ double xs[2][4 * CG_KC * CG_LD];
+  constexpr int NT = 16 * RN;
+  constexpr int XPT = 4 * CG_KC * NT / 256;  // X doubles per thread per chunk
+  constexpr int TPR = NT / XPT;              // staging threads per X row
+  const CgItem it = items[blockIdx.x];
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int brow = lane >> 4, bcol = lane & 15;
+  const int S = it.M * it.nks;
+  const int nch = (S + CG_KC - 1) / CG_KC;
+  const bool active = wave < it.nrt;
+  const double* Aw = it.A + (int64_t)wave * it.a_rt + lane;
+  const int xr = tid / TPR, xc = (tid % TPR) * XPT;
+  double xv[XPT], a0[CG_KC], a1[CG_KC];
+  auto load_x = [&](int c) {
+#pragma unroll
+    for (int u = 0; u < XPT; ++u) xv[u] = 0.0;
+    const int s = c * CG_KC + (xr >> 2);
+    if (xr < 4 * CG_KC && s < S) {
+      const int i = s / it.nks, ks = s - i * it.nks;
+      const double* xp =
+          it.X + (int64_t)(4 * ks + (xr & 3)) * it.ldx + pmod(tseg - i, it.Rseg) * it.cs + it.col0 + xc;
+#pragma unroll
+      for (int u = 0; u < XPT; ++u) xv[u] = xp[u];
+    }
+  };
+  auto store_x = [&](int buf) {
+    if (xr < 4 * CG_KC) {
+#pragma unroll
+      for (int u = 0; u < XPT; ++u) xs[buf][xr * CG_LD + xc + u] = xv[u];
+    }
+  };
+  auto load_a = [&](int c, double(&a)[CG_KC]) {
+#pragma unroll
+    for (int u = 0; u < CG_KC; ++u) {
+      const int s = c * CG_KC + u;
+      a[u] = (active && s < S) ? Aw[(int64_t)s * 64] : 0.0;
+    }
+  };
+  d4 acc[RN];
+#pragma unroll
+  for (int n = 0; n < RN; ++n) acc[n] = d4{0.0, 0.0, 0.0, 0.0};
+  load_x(0);
+  load_a(0, a0);
+  store_x(0);
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    const int buf = c & 1;
+    const bool more = c + 1 < nch;
+    if (more) {
+      load_x(c + 1);
+      load_a(c + 1, a1);
+    }
+    if (active) {
+      const double* xb = xs[buf] + brow * CG_LD + bcol;
+#pragma unroll
+      for (int u = 0; u < CG_KC; ++u) {
+        if (c * CG_KC + u < S) {
+#pragma unroll
+          for (int n = 0; n < RN; ++n)
+            acc[n] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[u], xb[4 * u * CG_LD + 16 * n], acc[n], 0, 0, 0);
+        }
+      }
+    }
+    if (more) store_x(buf ^ 1);
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < CG_KC; ++u) a0[u] = a1[u];
+  }
+  if (active) {
+    // f64 MFMA C/D map: col = lane & 15, row = (lane >> 4) + 4 * reg
+#pragma unroll
+    for (int n = 0; n < RN; ++n)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = 16 * wave + brow + 4 * q, col = 16 * n + bcol;
+        if (row < it.nrows && col < it.ncols) it.out[(int64_t)row * it.ldo + col] = acc[n][q];
+      }
+  }
+}
+
+void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStream_t s) {
+  if (nitems <= 0) return;
+  switch (rn) {
+    case 1: cgemm_kernel<1><<<nitems, 256, 0, s>>>(items, tseg); break;
+    case 2: cgemm_kernel<2><<<nitems, 256, 0, s>>>(items, tseg); break;
+    default: cgemm_kernel<4><<<nitems, 256, 0, s>>>(items, tseg); break;
+  }
+}
+
 // Segment spectra of the nseg newest segments sigma = T/P - sidx (grid: sidx x DOF k x 8-trajectory
 // chunk): x[n] = p at time sigma*P - 2P + 2 + n (n < 2P-1), x[2P-1] = 0;
-// Xhat(f) = sum_n x[n] e^{-i pi f n / P}, f = 0..P, written as rows [k] = Re and [ncp + k] = Im of
-// the frequency-f segment ring (mirrored slots).  Two real series per complex FFT.
+// Xhat(f) = sum_n x[n] e^{-i pi f n / P}, f = 0..P, written into the frequency-f segment ring as the
+// Gauss planes  g = 0: Re + Im,  1: Im,  2: Re  (rows [g ncp + k], mirrored slots).  Two real series
+// per complex FFT.
 constexpr int FFT_BC = 8;  // trajectories per block
 __global__ __launch_bounds__(256) void seg_fft_kernel(const double* __restrict__ H, int64_t ldh, int R,
                                                       int B, int nc, int ncp, int P, int logn,
@@ -732,11 +839,13 @@ __global__ __launch_bounds__(256) void seg_fft_kernel(const double* __restrict__
       im = -0.5 * (z.x - zc.x);
     }
     double* sf = seg + (int64_t)f * seg_fstride + b;
-    sf[(int64_t)k * ldseg + slot * B] = re;
-    sf[(int64_t)k * ldseg + (slot + Rseg) * B] = re;
-    const int64_t ir = (int64_t)(ncp + k) * ldseg;
-    sf[ir + slot * B] = im;
-    sf[ir + (slot + Rseg) * B] = im;
+    const double v[3] = {re + im, im, re};
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+      const int64_t ir = (int64_t)(g * ncp + k) * ldseg;
+      sf[ir + slot * B] = v[g];
+      sf[ir + (slot + Rseg) * B] = v[g];
+    }
   }
 }
 
@@ -760,7 +869,8 @@ int launch_seg_fft(const double* H, int64_t ldh, int R, int B, int nc, int ncp, 
 }
 
 // Block output out(kP + 1 + j) = y[j + P - 1] (j < P) of the real inverse transform of the
-// Hermitian spectrum Y(f), f = 0..P (Im Y_0, Im Y_P ignored as by irfft):
+// Hermitian spectrum Y(f), f = 0..P (Im Y_0, Im Y_P ignored as by irfft), assembled from the Gauss
+// products T_g(f):
 //   y[n] = (1/2P) sum_{f<2P} Y(f) e^{+i pi f n / P},  Y(2P - f) = conj Y(f).
 // Grid: DOF k x 8-trajectory chunk; two real outputs per complex inverse FFT.
 __global__ __launch_bounds__(256) void far_ifft_kernel(const double* __restrict__ Y, int64_t yfstride,
@@ -773,7 +883,7 @@ __global__ __launch_bounds__(256) void far_ifft_kernel(const double* __restrict_
   const int bc = blockIdx.x % nbc;
   const int k = blockIdx.x / nbc;
   const int b0 = bc * FFT_BC;
-  const int64_t im_off = (int64_t)nc * B;
+  const int64_t pl = (int64_t)nc * B;
   for (int e = threadIdx.x; e < N * FFT_BC / 2; e += blockDim.x) {
     const int q = e % (FFT_BC / 2);
     const int f = e / (FFT_BC / 2);
@@ -782,14 +892,17 @@ __global__ __launch_bounds__(256) void far_ifft_kernel(const double* __restrict_
     const bool realonly = (fs == 0) || (fs == P);
     const int ba = b0 + 2 * q, bb = ba + 1;
     const double* yf = Y + (int64_t)fs * yfstride + (int64_t)k * B;
+    // Re Y = T_0 - T_1, Im Y = T_0 + T_2 (Gauss products, planes [f][g][nc][B])
     double ar = 0.0, ai = 0.0, br = 0.0, bi = 0.0;
     if (ba < B) {
-      ar = yf[ba];
-      ai = realonly ? 0.0 : yf[im_off + ba];
+      const double t0 = yf[ba];
+      ar = t0 - yf[pl + ba];
+      ai = realonly ? 0.0 : t0 + yf[2 * pl + ba];
     }
     if (bb < B) {
-      br = yf[bb];
-      bi = realonly ? 0.0 : yf[im_off + bb];
+      const double t0 = yf[bb];
+      br = t0 - yf[pl + bb];
+      bi = realonly ? 0.0 : t0 + yf[2 * pl + bb];
     }
     if (cj) {
       ai = -ai;

@@ -29,7 +29,7 @@ for k, v in sorted(d.items(), key=lambda kv: -sum(kv[1]))[:30]:
 
 if "--steps" in sys.argv:
     rows.sort(key=lambda r: r["s"])
-    cs = [r for r in rows if r["n"].startswith("chain_kernel<2>")]
+    cs = [r for r in rows if r["n"].startswith("chain_kernel<2")]
     n = min(100, len(cs) - 1)
     if n > 0:
         a, b = cs[-n - 1]["e"], cs[-1]["e"]
