@@ -82,6 +82,8 @@ def main():
     ap.add_argument("--block-len", type=int, default=0)
     ap.add_argument("--max-block", type=int, default=0)
     ap.add_argument("--far-mode", default="auto", choices=["auto", "direct", "spectral"])
+    ap.add_argument("--gmem", default="device", choices=["device", "host"],
+                    help="memory-kernel construction (phbath.gmem) on the device or with numpy")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
@@ -104,7 +106,7 @@ def main():
     from sclmd_amd import synthetic
 
     t_setup = time.perf_counter()
-    dyn, axyz, baths, meta = synthetic.junction(args.config, seed=1234)
+    dyn, axyz, baths, meta = synthetic.junction(args.config, seed=1234, gmem_device=args.gmem == "device")
     m = MD.md(meta["dt"], meta["nmd"], meta["T"], axyz=axyz, dyn=dyn, ntraj=args.ntraj,
               seed=1000 + rank * args.ntraj, traj_offset=rank * args.ntraj, device=local_rank,
               noise_mode="device", block_len=args.block_len, far_mode=args.far_mode,
@@ -184,11 +186,17 @@ def main():
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            if tj.get("config") == args.config and tj.get("ntraj") == args.ntraj:
+            if (tj.get("config") == args.config and tj.get("ntraj") == args.ntraj
+                    and tj.get("far_mode") == st.plan_info()["far_mode"]):
                 roof["traffic"] = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass
-        roof.update({"kernel": "contract_kernel (far-field memory-kernel contraction)",
+        if st.plan_info()["far_mode"] == "spectral":
+            kname = ("cgemm_kernel (far field: per-frequency Gauss 3-multiplication GEMMs of the "
+                     "spectral ladder levels)")
+        else:
+            kname = "contract_kernel (far field: direct ladder-level memory-kernel contraction)"
+        roof.update({"kernel": kname,
                      "launches": prof["launches"], "avg_launch_ms": avg_ms,
                      "algorithmic_flops_per_launch": fl, "algorithmic_bytes_per_launch": by})
         res["roofline"] = roof
@@ -197,7 +205,7 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         noise = [st.get_noise(i)[0] for i in range(len(baths))]
-        bh = [(b.cids, b.kernel, noise[i]) for i, b in enumerate(baths)]
+        bh = [(b.cids, st.get_kernel(i), noise[i]) for i, b in enumerate(baths)]
         res["cpu_baseline"] = cpu_baseline(bh, m.dyn, meta["nph"], meta["dt"], meta["nmd"], args.cpu_budget)
         res["speedup_vs_cpu_baseline"] = value / res["cpu_baseline"]["value"]
     if rank == 0:

@@ -95,6 +95,22 @@ int gle_device_count(int32_t* count);
 int gle_add_bath(gle_handle* h, int32_t kind, const int64_t* cids, int64_t nc, int64_t ml,
                  const double* kernel, double bias, const double* exim, const double* zeta1,
                  const double* zeta2, int32_t* bath_id);
+/* phbath.gmem (baths.py:412-445) + md.AddBath on the device: the memory kernel is built in HBM,
+ * never crossing PCIe.  gamt (baths.py:19-52) is linear in Gamma through flinterp
+ * (functions.py:117-134), so K_i = sum_g W[i][g] gamma[g] with
+ *   W      [ml][ngw]      = scale * C(t_i, w) . I(w -> gwl): the cosine (eta = 0) or damped
+ *                            (eta != 0) coefficients times the interpolation weights, built by the
+ *                            caller (sclmd_amd.baths.gmem_coefficients)
+ *   gamma  [ngw][nc][nc]  the friction spectrum on gwl (phbath.gamma before the eta update)
+ * Phonon bath, dt factor iff ml > 1 as gle_add_bath. */
+int gle_add_bath_gmem(gle_handle* h, const int64_t* cids, int64_t nc, int64_t ml, const double* W,
+                      int64_t ngw, const double* gamma, int32_t* bath_id);
+/* Copy slices [i0, i0 + n) of a bath's device kernel out: out [n][nc][nc] (bath.kernel). */
+int gle_get_kernel(gle_handle* h, int32_t bath, int64_t i0, int64_t n, double* out);
+/* Standalone gamt on device `device`: out[i][e] = sum_g W[i][g] G[g][e], out [ml][nel],
+ * W [ml][ngw], G [ngw][nel].  Errors: gle_last_error(NULL). */
+int gle_gamt(int32_t device, int64_t ml, int64_t ngw, int64_t nel, const double* W, const double* G,
+             double* out);
 /* md.setDyn (md.py:250-292): harmonic potential force -dyn.q used when no host force is given
  * (md.potforce, md.py:466-467).  dyn [nph][nph] as already processed by setDyn. */
 int gle_set_dyn(gle_handle* h, const double* dyn);

@@ -25,7 +25,7 @@ EXPORTS = [
     "gle_set_history", "gle_get_history", "gle_get_force", "gle_set_noise", "gle_get_noise",
     "gle_noise_factors", "gle_noise_generate", "gle_step_begin", "gle_step_end", "gle_run",
     "gle_sync", "gle_get_current", "gle_get_energy", "gle_current_sums", "gle_profile",
-    "gle_profile_read", "gle_plan_info",
+    "gle_profile_read", "gle_plan_info", "gle_add_bath_gmem", "gle_get_kernel", "gle_gamt",
 ]
 
 
@@ -54,6 +54,10 @@ _SIGS = {
     "gle_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int32)]),
     "gle_add_bath": (ctypes.c_int, [_P, ctypes.c_int32, _I64, ctypes.c_int64, ctypes.c_int64, _D,
                                     ctypes.c_double, _D, _D, _D, ctypes.POINTER(ctypes.c_int32)]),
+    "gle_add_bath_gmem": (ctypes.c_int, [_P, _I64, ctypes.c_int64, ctypes.c_int64, _D, ctypes.c_int64, _D,
+                                         ctypes.POINTER(ctypes.c_int32)]),
+    "gle_get_kernel": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, _D]),
+    "gle_gamt": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _D, _D, _D]),
     "gle_set_dyn": (ctypes.c_int, [_P, _D]),
     "gle_set_constraint": (ctypes.c_int, [_P, _I64, ctypes.c_int64]),
     "gle_set_state": (ctypes.c_int, [_P, _D, _D, ctypes.c_int64]),
@@ -117,6 +121,25 @@ def device_count():
     return int(n.value) if rc == 0 else 0
 
 
+def gamt_device(W, G, device=0):
+    """out[i] = sum_g W[i, g] G[g] on the device (the contraction of gamt, baths.py:19-52).
+    W (ml, ngw); G (ngw, ...) -> (ml, ...)."""
+    lib = load()
+    W = _f64(W)
+    G = np.asarray(G, dtype=np.float64)
+    ml, ngw = W.shape
+    if G.shape[0] != ngw:
+        raise ValueError("gamt_device: W is (%d, %d) but G has %d rows" % (ml, ngw, G.shape[0]))
+    tail = G.shape[1:]
+    nel = int(np.prod(tail)) if tail else 1
+    G2 = _f64(G, (ngw, nel))
+    out = np.empty((ml, nel))
+    rc = lib.gle_gamt(int(device), ml, ngw, nel, _ptr(W), _ptr(G2), _ptr(out))
+    if rc != 0:
+        raise GLEError("gle_gamt failed (%s): %s" % (_ERRNAMES.get(rc, rc), lib.gle_last_error(None).decode()))
+    return out.reshape((ml,) + tail)
+
+
 class Stepper:
     """Owner of one gle_handle: a batch of ntraj trajectories of one system on one device."""
 
@@ -169,6 +192,29 @@ class Stepper:
         self.bath_nc.append(nc)
         self.bath_ml.append(ml)
         return int(bid.value)
+
+    def add_bath_gmem(self, cids, W, gamma):
+        """Phonon bath whose memory kernel K_i = sum_g W[i, g] gamma[g] is built on the device
+        (gle_add_bath_gmem)."""
+        cids = np.ascontiguousarray(np.asarray(cids, dtype=np.int64))
+        nc = len(cids)
+        W = _f64(W)
+        ml, ngw = W.shape
+        gamma = _f64(gamma, (ngw, nc, nc))
+        bid = ctypes.c_int32(-1)
+        self._chk(self.lib.gle_add_bath_gmem(self.h, cids.ctypes.data_as(_I64), nc, ml, _ptr(W), ngw,
+                                             _ptr(gamma), ctypes.byref(bid)), "gle_add_bath_gmem")
+        self.nbath += 1
+        self.bath_nc.append(nc)
+        self.bath_ml.append(ml)
+        return int(bid.value)
+
+    def get_kernel(self, bath, i0=0, n=None):
+        ml, nc = self.bath_ml[bath], self.bath_nc[bath]
+        n = ml - i0 if n is None else n
+        out = np.empty((n, nc, nc))
+        self._chk(self.lib.gle_get_kernel(self.h, int(bath), int(i0), int(n), _ptr(out)), "gle_get_kernel")
+        return out
 
     def set_dyn(self, dyn):
         d = _f64(dyn, (self.nph, self.nph))

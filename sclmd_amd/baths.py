@@ -11,7 +11,7 @@ from concurrent.futures import ThreadPoolExecutor
 import numpy as np
 
 from . import noise as _noise
-from .functions import antisymmetrize, chkShape, flinterp_many, symmetrize
+from .functions import antisymmetrize, chkShape, flinterp_many, interp_weights, symmetrize
 
 
 def gamt(tl, wl, gwl, gam, eta_ad=0):
@@ -33,6 +33,31 @@ def gamt(tl, wl, gwl, gam, eta_ad=0):
              + w / (w + 1j * eta_ad) * np.exp(1j * w * tt - eta_ad * tt))
         k = (np.real(c) @ g2) * (wl[-1] / np.pi / nw)
     return np.real(k).reshape((len(tl),) + shape)
+
+
+def gmem_coefficients(tl, wl, gwl, eta_ad=0):
+    """W (len(tl), len(gwl)) with gamt(tl, wl, gwl, gam, eta_ad) == W . gam (baths.py:19-52).
+
+    flinterp (functions.py:117-134) is linear in the spectrum -- two weights per frequency -- so
+    the reference's (t, w) double loop factors into scale * C(t, w) . I(w -> gwl): the device
+    builds the kernel as ONE contraction over the ngw spectrum nodes (gle_add_bath_gmem)."""
+    tl = np.asarray(tl, dtype=float)
+    wl = np.asarray(wl, dtype=float)
+    gwl = np.asarray(gwl, dtype=float)
+    nw = len(wl)
+    interp = np.zeros((nw, len(gwl)))
+    for k, x in enumerate(wl):
+        i, j, wi, wj = interp_weights(x, gwl)
+        interp[k, i] += wi
+        interp[k, j] += wj
+    if eta_ad == 0:
+        c = np.cos(np.outer(tl, wl)) * (2.0 * wl[-1] / np.pi / nw)
+    else:
+        w = wl[None, :]
+        tt = tl[:, None]
+        c = np.real(w / (w - 1j * eta_ad) * np.exp(-1j * w * tt - eta_ad * tt)
+                    + w / (w + 1j * eta_ad) * np.exp(1j * w * tt - eta_ad * tt)) * (wl[-1] / np.pi / nw)
+    return c @ interp
 
 
 def _eigh_stack(spec):
@@ -229,8 +254,35 @@ class phbath(_BathBase):
             a.append(-np.imag(sig[j]) / wl[j])
         self.gamma = np.array(a)
 
-    def gmem(self):
-        """Memory kernel K_i = gamt(dt*i) for i < ml (baths.py:412-445)."""
+    @property
+    def kernel(self):
+        """The memory kernel [ml][nc][nc].  After gmem(on_device=True) it is built on the device
+        when the bath is added to an md object; reading it here evaluates the same contraction
+        W . gamma on the host (once)."""
+        k = self.__dict__.get("_kernel")
+        rec = self.__dict__.get("_gmem")
+        if k is None and rec is not None:
+            W, G = rec
+            k = (W @ np.asarray(G).reshape(len(G), -1)).reshape((W.shape[0],) + np.shape(G)[1:])
+            self.__dict__["_kernel"] = k
+        return k
+
+    @kernel.setter
+    def kernel(self, value):
+        self.__dict__["_kernel"] = value
+        self.__dict__["_gmem"] = None
+
+    @property
+    def gmem_recipe(self):
+        """(W, gamma) of a device-built kernel (gmem(on_device=True)), else None."""
+        return self.__dict__.get("_gmem")
+
+    def gmem(self, on_device=False):
+        """Memory kernel K_i = gamt(dt*i) for i < ml (baths.py:412-445).
+
+        on_device (extension): keep only the coefficient matrix W of gmem_coefficients and the
+        spectrum; the kernel itself is built in HBM by gle_add_bath_gmem (no host copy of the
+        ml x nc x nc kernel, no PCIe transfer)."""
         if self.ml is None or self.dt is None:
             raise ValueError("phbath.gmem: length of memory kernel not set")
         if self.local:
@@ -238,6 +290,18 @@ class phbath(_BathBase):
             self.kernel = self.gamma
             return
         tl = [self.dt * i for i in range(self.ml)]
+        if on_device:
+            gam = np.asarray(self.gamma, dtype=float)
+            W = gmem_coefficients(tl, self.wl, self.gwl, self.eta_ad)
+            self.kernel = None
+            self.__dict__["_gmem"] = (W, gam)
+            if self.eta_ad != 0:
+                # gamma update of baths.py:429-445: sum_it dt K[it] cos(gwl t_it) = (D . W) . gamma
+                d = np.cos(np.outer(np.asarray(self.gwl, dtype=float), np.asarray(tl))) * self.dt
+                g = (d @ W) @ gam.reshape(len(gam), -1)
+                self.gammaOld = self.gamma
+                self.gamma = np.real(g).reshape(np.shape(self.gammaOld))
+            return
         self.kernel = gamt(tl, self.wl, self.gwl, self.gamma, self.eta_ad)
         if self.eta_ad != 0:
             c = np.cos(np.outer(np.asarray(self.gwl, dtype=float), np.asarray(tl))) * self.dt

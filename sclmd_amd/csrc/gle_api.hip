@@ -1335,7 +1335,8 @@ int launch_level_block(gle_handle* h, Level& lv, int64_t k, hipStream_t s, bool 
         return fail(h, GLE_ERR_UNSUP, "inverse transform launch failed (P = " + std::to_string(lv.P) + ")");
     }
   } else {
-    run_op(h, lv.op[par], s, ta, true);
+    // profiled only when no level is spectral: the roofline then names one kernel class
+    run_op(h, lv.op[par], s, ta, h->far_mode != GLE_FAR_SPECTRAL);
   }
   HIPCHK(h, hipEventRecord(lv.ev[par], s));
   return GLE_OK;
@@ -1635,14 +1636,16 @@ int gle_destroy(gle_handle* h) {
   return GLE_OK;
 }
 
-int gle_add_bath(gle_handle* h, int32_t kind, const int64_t* cids, int64_t nc, int64_t ml,
-                 const double* kernel, double bias, const double* exim, const double* zeta1,
-                 const double* zeta2, int32_t* bath_id) {
-  if (!h) return GLE_ERR_ARG;
+}  // extern "C"
+
+namespace {
+
+// shared argument checks of gle_add_bath / gle_add_bath_gmem; fills the bath's shape fields
+int new_bath(gle_handle* h, int32_t kind, const int64_t* cids, int64_t nc, int64_t ml, Bath& b) {
   if (h->frozen) return fail(h, GLE_ERR_STATE, "baths must be added before the first state/step call");
   if ((int)h->baths.size() >= MAXBATH) return fail(h, GLE_ERR_UNSUP, "too many baths");
   if (kind != GLE_BATH_PHONON && kind != GLE_BATH_ELECTRON) return fail(h, GLE_ERR_ARG, "bad bath kind");
-  if (!cids || nc <= 0 || nc > h->nph || ml <= 0 || !kernel) return fail(h, GLE_ERR_ARG, "bad bath shape");
+  if (!cids || nc <= 0 || nc > h->nph || ml <= 0) return fail(h, GLE_ERR_ARG, "bad bath shape");
   if (kind == GLE_BATH_ELECTRON && ml != 1) return fail(h, GLE_ERR_ARG, "electron bath is time-local (ml == 1, baths.py:97)");
   std::vector<int> seen(h->nph, 0);
   for (int64_t k = 0; k < nc; ++k) {
@@ -1650,7 +1653,6 @@ int gle_add_bath(gle_handle* h, int32_t kind, const int64_t* cids, int64_t nc, i
     if (seen[cids[k]]++) return fail(h, GLE_ERR_ARG, "duplicate DOF in cids");
   }
   hipSetDevice(h->cfg.device);
-  Bath b;
   b.kind = kind;
   b.nc = (int)nc;
   b.ncp = (int)rup(nc, 8);
@@ -1659,6 +1661,62 @@ int gle_add_bath(gle_handle* h, int32_t kind, const int64_t* cids, int64_t nc, i
   b.ml = (int)ml;
   b.c = ml > 1 ? h->dt : 1.0;  // baths.py:454-457 (and :235-241)
   b.cids.assign(cids, cids + nc);
+  return GLE_OK;
+}
+
+// per-bath device buffers and the DOF map; b.d_K and b.K0 are already set
+int commit_bath(gle_handle* h, Bath&& b, int32_t* bath_id) {
+  const int64_t nc = b.nc;
+  const int64_t* cids = b.cids.data();
+  int rc = 0;
+  b.inv.assign(h->nph, -1);
+  for (int64_t k = 0; k < nc; ++k) b.inv[cids[k]] = (int32_t)k;
+  const int64_t B = h->B;
+  const size_t nbuf = (size_t)(b.ncp + 64) * B + 1024;
+  b.vs = (int64_t)nbuf;
+  rc |= dalloc_n(h, &b.d_inv, (size_t)h->nph);
+  if (!rc) rc = upload(h, b.d_inv, b.inv.data(), b.inv.size() * 4);
+  rc |= dalloc_n(h, &b.d_noise, (size_t)h->nmd * nc * B);
+  rc |= dalloc_n(h, &b.d_S, 2 * nbuf);
+  rc |= dalloc_n(h, &b.d_Xcur, 2 * nbuf);
+  rc |= dalloc_n(h, &b.d_Xq, 2 * nbuf);
+  rc |= dalloc_n(h, &b.d_cur, (size_t)h->nmd * B);
+  if (b.has_q) rc |= dalloc_n(h, &b.d_Yq, nbuf);
+  if (rc) return GLE_ERR_NOMEM;
+  h->baths.push_back(std::move(b));
+  if (bath_id) *bath_id = (int32_t)h->baths.size() - 1;
+  return GLE_OK;
+}
+
+// W [ml][ngw] -> W^T zero padded to [rup(ngw, 4)][rup(ml, 16)]
+std::vector<double> transpose_w(const double* W, int64_t ml, int64_t ngw, int64_t* mlp) {
+  *mlp = rup(ml, 16);
+  const int64_t ngwp = rup(ngw, 4);
+  std::vector<double> wt((size_t)ngwp * *mlp, 0.0);
+  for (int64_t i = 0; i < ml; ++i)
+    for (int64_t g = 0; g < ngw; ++g) wt[(size_t)(g * *mlp + i)] = W[i * ngw + g];
+  return wt;
+}
+
+struct DevTmp {  // scratch device buffer freed on scope exit (setup paths)
+  void* p = nullptr;
+  ~DevTmp() {
+    if (p) hipFree(p);
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+int gle_add_bath(gle_handle* h, int32_t kind, const int64_t* cids, int64_t nc, int64_t ml,
+                 const double* kernel, double bias, const double* exim, const double* zeta1,
+                 const double* zeta2, int32_t* bath_id) {
+  if (!h) return GLE_ERR_ARG;
+  if (!kernel) return fail(h, GLE_ERR_ARG, "bad bath shape");
+  Bath b;
+  int rc0 = new_bath(h, kind, cids, nc, ml, b);
+  if (rc0) return rc0;
   b.K.assign(kernel, kernel + ml * nc * nc);
   // electron-bath bias terms, active only if exim, zeta1, zeta2 are all nonzero (baths.py:233)
   auto anynz = [&](const double* m) {
@@ -1688,25 +1746,95 @@ int gle_add_bath(gle_handle* h, int32_t kind, const int64_t* cids, int64_t nc, i
       if (rc) return rc;
     }
   }
-  b.inv.assign(h->nph, -1);
-  for (int64_t k = 0; k < nc; ++k) b.inv[cids[k]] = (int32_t)k;
-  const int64_t B = h->B;
-  const size_t nbuf = (size_t)(b.ncp + 64) * B + 1024;
-  b.vs = (int64_t)nbuf;
-  rc |= dalloc_n(h, &b.d_inv, (size_t)h->nph);
-  if (!rc) rc = upload(h, b.d_inv, b.inv.data(), b.inv.size() * 4);
-  rc |= dalloc_n(h, &b.d_noise, (size_t)h->nmd * nc * B);
-  rc |= dalloc_n(h, &b.d_S, 2 * nbuf);
-  rc |= dalloc_n(h, &b.d_Xcur, 2 * nbuf);
-  rc |= dalloc_n(h, &b.d_Xq, 2 * nbuf);
-  rc |= dalloc_n(h, &b.d_cur, (size_t)h->nmd * B);
-  if (b.has_q) rc |= dalloc_n(h, &b.d_Yq, nbuf);
-  if (rc) return GLE_ERR_NOMEM;
   b.K0.assign(b.K.begin(), b.K.begin() + nc * nc);
   b.K.clear();
   b.K.shrink_to_fit();
-  h->baths.push_back(std::move(b));
-  if (bath_id) *bath_id = (int32_t)h->baths.size() - 1;
+  return commit_bath(h, std::move(b), bath_id);
+}
+
+int gle_add_bath_gmem(gle_handle* h, const int64_t* cids, int64_t nc, int64_t ml, const double* W,
+                      int64_t ngw, const double* gamma, int32_t* bath_id) {
+  if (!h) return GLE_ERR_ARG;
+  if (!W || !gamma || ngw <= 0) return fail(h, GLE_ERR_ARG, "gmem: bad coefficient / spectrum shape");
+  Bath b;
+  int rc = new_bath(h, GLE_BATH_PHONON, cids, nc, ml, b);
+  if (rc) return rc;
+  const int64_t nfrag = (int64_t)b.nrt * b.nks;
+  const int64_t ngwp = rup(ngw, 4);
+  int64_t mlp = 0;
+  std::vector<double> wt = transpose_w(W, ml, ngw, &mlp);
+  DevTmp d_wt, d_gam, d_gf;
+  HIPCHK(h, hipMalloc(&d_wt.p, wt.size() * 8));
+  HIPCHK(h, hipMalloc(&d_gam.p, (size_t)ngw * nc * nc * 8));
+  HIPCHK(h, hipMalloc(&d_gf.p, (size_t)nfrag * ngwp * 64 * 8));
+  HIPCHK(h, hipMemcpyAsync(d_wt.p, wt.data(), wt.size() * 8, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(d_gam.p, gamma, (size_t)ngw * nc * nc * 8, hipMemcpyHostToDevice, h->stream));
+  launch_gamma_pack((const double*)d_gam.p, (int)ngw, (int)ngwp, b.nc, b.nrt, b.nks, (double*)d_gf.p, h->stream);
+  rc = dalloc_n(h, &b.d_K, (size_t)nfrag * ml * 64);
+  if (rc) return rc;
+  if (launch_kgen((const double*)d_wt.p, mlp, (int)ngw, (const double*)d_gf.p, ngwp * 64, 64, b.d_K, ml * 64, 64,
+                  (int)ml, nfrag, 64, h->stream))
+    return fail(h, GLE_ERR_HIP, "gmem: kernel-construction launch failed");
+  // host copy of slice 0 (the chain's K0 rows are packed on the host in plan_chain)
+  std::vector<double> f0((size_t)nfrag * 64);
+  HIPCHK(h, hipMemcpy2DAsync(f0.data(), 64 * 8, b.d_K, (size_t)ml * 64 * 8, 64 * 8, (size_t)nfrag,
+                             hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  b.K0.assign((size_t)nc * nc, 0.0);
+  for (int rt = 0; rt < b.nrt; ++rt)
+    for (int ks = 0; ks < b.nks; ++ks)
+      for (int l = 0; l < 64; ++l) {
+        const int64_t r = 16 * rt + (l & 15), c = 4 * ks + (l >> 4);
+        if (r < nc && c < nc) b.K0[(size_t)(r * nc + c)] = f0[((size_t)rt * b.nks + ks) * 64 + l];
+      }
+  return commit_bath(h, std::move(b), bath_id);
+}
+
+int gle_get_kernel(gle_handle* h, int32_t bath, int64_t i0, int64_t n, double* out) {
+  if (!h || !out) return GLE_ERR_ARG;
+  if (bath < 0 || bath >= (int32_t)h->baths.size()) return fail(h, GLE_ERR_ARG, "bad bath id");
+  const Bath& b = h->baths[bath];
+  if (i0 < 0 || n < 0 || i0 + n > b.ml) return fail(h, GLE_ERR_ARG, "kernel slice range out of [0, ml)");
+  if (n == 0) return GLE_OK;
+  hipSetDevice(h->cfg.device);
+  const int64_t nfrag = (int64_t)b.nrt * b.nks;
+  std::vector<double> f((size_t)nfrag * n * 64);
+  HIPCHK(h, hipMemcpy2DAsync(f.data(), (size_t)n * 64 * 8, b.d_K + i0 * 64, (size_t)b.ml * 64 * 8,
+                             (size_t)n * 64 * 8, (size_t)nfrag, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  const int64_t nc = b.nc;
+  for (int rt = 0; rt < b.nrt; ++rt)
+    for (int ks = 0; ks < b.nks; ++ks)
+      for (int64_t i = 0; i < n; ++i) {
+        const double* src = &f[(((size_t)rt * b.nks + ks) * n + i) * 64];
+        for (int l = 0; l < 64; ++l) {
+          const int64_t r = 16 * rt + (l & 15), c = 4 * ks + (l >> 4);
+          if (r < nc && c < nc) out[(i * nc + r) * nc + c] = src[l];
+        }
+      }
+  return GLE_OK;
+}
+
+int gle_gamt(int32_t device, int64_t ml, int64_t ngw, int64_t nel, const double* W, const double* G,
+             double* out) {
+  if (ml <= 0 || ngw <= 0 || nel <= 0 || !W || !G || !out) return fail(nullptr, GLE_ERR_ARG, "gamt: bad shape");
+  if (hipSetDevice(device) != hipSuccess) return fail(nullptr, GLE_ERR_HIP, "gamt: no such device");
+  int64_t mlp = 0;
+  std::vector<double> wt = transpose_w(W, ml, ngw, &mlp);
+  const int64_t nblk = (nel + 63) / 64;
+  DevTmp d_wt, d_g, d_o;
+  auto ok = [](hipError_t e) { return e == hipSuccess; };
+  if (!ok(hipMalloc(&d_wt.p, wt.size() * 8)) || !ok(hipMalloc(&d_g.p, (size_t)ngw * nel * 8)) ||
+      !ok(hipMalloc(&d_o.p, (size_t)ml * nel * 8)))
+    return fail(nullptr, GLE_ERR_NOMEM, "gamt: device allocation failed");
+  if (!ok(hipMemcpy(d_wt.p, wt.data(), wt.size() * 8, hipMemcpyHostToDevice)) ||
+      !ok(hipMemcpy(d_g.p, G, (size_t)ngw * nel * 8, hipMemcpyHostToDevice)))
+    return fail(nullptr, GLE_ERR_HIP, "gamt: upload failed");
+  if (launch_kgen((const double*)d_wt.p, mlp, (int)ngw, (const double*)d_g.p, 64, nel, (double*)d_o.p, 64, nel,
+                  (int)ml, nblk, (int)(nel - 64 * (nblk - 1)), nullptr))
+    return fail(nullptr, GLE_ERR_HIP, "gamt: launch failed");
+  if (!ok(hipMemcpy(out, d_o.p, (size_t)ml * nel * 8, hipMemcpyDeviceToHost)))
+    return fail(nullptr, GLE_ERR_HIP, "gamt: download failed");
   return GLE_OK;
 }
 

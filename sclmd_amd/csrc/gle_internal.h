@@ -232,5 +232,10 @@ int launch_far_ifft(const double* Y, int64_t yfstride, int nc, int B, int P, dou
                     int64_t ldout, const double* cstab, int cstride, hipStream_t s);
 int launch_fft_noise(const double* a, double* noise, const double* tw, int64_t nmd, int64_t nc,
                      int64_t arows, int64_t B, int is_complex, double scale, hipStream_t s);
+// memory-kernel construction (gle_gmem.hip): out[b o_blk + i o_row + l] = sum_g W[i][g] G[b g_blk + g g_row + l]
+// over 64-lane blocks b < nblk (the last has nvalid_last lanes), WT = W^T zero padded [ngwp][mlp]
+int launch_kgen(const double* WT, int64_t mlp, int ngw, const double* G, int64_t g_blk, int64_t g_row,
+                double* out, int64_t o_blk, int64_t o_row, int ml, int64_t nblk, int nvalid_last, hipStream_t s);
+void launch_gamma_pack(const double* gam, int ngw, int ngwp, int nc, int nrt, int nks, double* gf, hipStream_t s);
 
 }  // namespace gle

@@ -344,6 +344,10 @@ class md:
         st = _native.Stepper(self.nph, self.ntraj, self.nmd, self.dt, dev, self.block_len, self.far_mode,
                              self.max_block)
         for b in self.baths:
+            rec = getattr(b, "gmem_recipe", None)
+            if rec is not None and b.__dict__.get("_kernel") is None:
+                st.add_bath_gmem(b.cids, rec[0], rec[1])   # kernel built in HBM (phbath.gmem)
+                continue
             if b.kernel is None:
                 raise ValueError("md: bath %s has no kernel (call phbath.gmem())" % b)
             if b.kind == "ebath":

@@ -52,10 +52,10 @@ CONFIGS = {
 }
 
 
-def make_phbath(T, dofs, ml, nmd, rng, dt=DT, nw=500, debye=0.2):
+def make_phbath(T, dofs, ml, nmd, rng, dt=DT, nw=500, debye=0.2, gmem_device=False):
     gwl, gam = gamma_spectrum(len(dofs), rng)
     b = phbath(T, dofs, debye=debye, nw=nw, dt=dt, nmd=nmd, ml=ml, mcof=2.0, gamma=gam, gwl=gwl)
-    b.gmem()
+    b.gmem(on_device=gmem_device)
     return b
 
 
@@ -75,9 +75,11 @@ def make_biased_ebath(T, dofs, nmd, rng, dt=DT, bias=1.0):
                  exim=anti(), exip=sym(), zeta1=sym(), zeta2=anti())
 
 
-def junction(config="C3", T=300.0, delta=0.1, seed=1234, ml=None, nmd=None, natom=None, nw=500):
+def junction(config="C3", T=300.0, delta=0.1, seed=1234, ml=None, nmd=None, natom=None, nw=500,
+             gmem_device=False):
     """(dyn, axyz, baths, meta) for a configuration; ml/nmd/natom override the defaults for
-    reduced test sizes.  Bath temperatures T(1 +- delta/2) as in runmd.py:51-55."""
+    reduced test sizes.  Bath temperatures T(1 +- delta/2) as in runmd.py:51-55.  gmem_device:
+    phonon-bath kernels are built on the device (phbath.gmem(on_device=True))."""
     na, ranges, ml0, nmd0, erange = CONFIGS[config]
     natom = natom or na
     scale = natom / na
@@ -90,7 +92,7 @@ def junction(config="C3", T=300.0, delta=0.1, seed=1234, ml=None, nmd=None, nato
     for (a0, a1), Tb in zip(ranges, temps):
         a0, a1 = int(round(a0 * scale)), int(round(a1 * scale))
         dofs = list(range(3 * a0, 3 * a1))
-        baths.append(make_phbath(Tb, dofs, ml, nmd, rng, nw=nw))
+        baths.append(make_phbath(Tb, dofs, ml, nmd, rng, nw=nw, gmem_device=gmem_device))
     if erange is not None:
         a0, a1 = int(round(erange[0] * scale)), int(round(erange[1] * scale))
         baths.append(make_biased_ebath(T, list(range(3 * a0, 3 * a1)), nmd, rng))

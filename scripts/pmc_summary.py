@@ -13,27 +13,38 @@ import json
 import os
 
 
-def per_launch(path, kernel, grid=None):
-    vals = []
-    for r in csv.DictReader(open(path)):
-        if kernel in r["Kernel_Name"] and (grid is None or r["Grid_Size"] == grid):
-            vals.append(float(r["Counter_Value"]))
-    return vals
+def per_launch(path, kernel, last=0):
+    """Counter value per dispatch of `kernel`, in dispatch order; last > 0 keeps only the final
+    `last` dispatches (the bench's timed region: nothing of that kernel runs after it)."""
+    rows = [r for r in csv.DictReader(open(path)) if kernel in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r.get("Dispatch_Id", r.get("Correlation_Id", 0))))
+    vals = [float(r["Counter_Value"]) for r in rows]
+    return vals[-last:] if last > 0 else vals
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("pmcdir")
     ap.add_argument("out")
-    ap.add_argument("--kernel", default="contract_kernel<16")
+    ap.add_argument("--kernel", default="cgemm_kernel")
     ap.add_argument("--config", default="C3")
     ap.add_argument("--ntraj", type=int, default=64)
+    ap.add_argument("--far-mode", default="spectral")
+    ap.add_argument("--last", type=int, default=-1,
+                    help="dispatches of the timed region (default: the bench JSON's roofline.launches)")
     a = ap.parse_args()
-    f = per_launch(os.path.join(a.pmcdir, "FETCH_SIZE", "run_counter_collection.csv"), a.kernel)
-    w = per_launch(os.path.join(a.pmcdir, "WRITE_SIZE", "run_counter_collection.csv"), a.kernel)
+    last = a.last
+    if last < 0:
+        try:
+            last = int(json.load(open(os.path.join(a.pmcdir, "FETCH_SIZE.json")))["roofline"]["launches"])
+        except (OSError, ValueError, KeyError):
+            last = 0
+    f = per_launch(os.path.join(a.pmcdir, "FETCH_SIZE", "run_counter_collection.csv"), a.kernel, last)
+    w = per_launch(os.path.join(a.pmcdir, "WRITE_SIZE", "run_counter_collection.csv"), a.kernel, last)
     fetch = sum(f) / len(f) * 1024.0
     write = sum(w) / len(w) * 1024.0
-    res = {"config": a.config, "ntraj": a.ntraj, "kernel": a.kernel, "launches": [len(f), len(w)],
+    res = {"config": a.config, "ntraj": a.ntraj, "far_mode": a.far_mode, "kernel": a.kernel,
+           "launches": [len(f), len(w)],
            "fetch_size_bytes_raw": fetch, "write_size_bytes": write,
            "hbm_bytes_per_launch": 2.0 * fetch + write,
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "

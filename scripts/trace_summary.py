@@ -27,6 +27,14 @@ for k, v in sorted(d.items(), key=lambda kv: -sum(kv[1]))[:30]:
     print("%-40s grid %6d x %4d  n %5d  med %9.1f us  min %9.1f  total %10.1f us (%4.1f%%)"
           % (k[0], k[1], k[2], len(v), v[len(v) // 2], v[0], sum(v), 100 * sum(v) / tot))
 
+if "--last" in sys.argv:
+    # average duration of the last N dispatches of a kernel (the bench's timed region)
+    i = sys.argv.index("--last")
+    kn, n = sys.argv[i + 1], int(sys.argv[i + 2])
+    ks = sorted([r for r in rows if kn in r["n"]], key=lambda r: r["s"])[-n:]
+    if ks:
+        print("\nlast %d dispatches of %s: avg %.2f us" % (len(ks), kn, sum(r["e"] - r["s"] for r in ks) / len(ks) / 1e3))
+
 if "--steps" in sys.argv:
     rows.sort(key=lambda r: r["s"])
     cs = [r for r in rows if r["n"].startswith("chain_kernel<2")]

@@ -65,6 +65,31 @@ def test_gamt_and_gmem():
     assert b.ml == 1 and np.array_equal(b.kernel, g["kernel_debye"])
 
 
+def test_gmem_coefficients_factor_gamt():
+    """The device kernel build contracts W = scale C(t, w) . I(w -> gwl) with Gamma
+    (gle_add_bath_gmem); W . Gamma must equal the reference gamt (golden, both eta branches), and
+    phbath.gmem(on_device=True) must leave the same kernel / updated gamma as the host path."""
+    from sclmd_amd import baths as B
+
+    g = load_golden("gamt")
+    ml, nw, dt = int(g["ml"]), int(g["nw"]), float(g["dt"])
+    for tag, eta in (("eta0", 0.0), ("eta1", 0.02)):
+        b = B.phbath(300.0, list(range(4)), debye=0.2, nw=nw, dt=dt, nmd=64, ml=ml,
+                     gamma=g["gam"].copy(), gwl=g["gwl"], eta_ad=eta)
+        W = B.gmem_coefficients([dt * i for i in range(ml)], b.wl, g["gwl"], eta)
+        assert W.shape == (ml, len(g["gwl"]))
+        assert rel(np.einsum("ig,gab->iab", W, g["gam"]), g["kernel_" + tag]) < 1e-12
+        b.gmem(on_device=True)
+        assert b.gmem_recipe is not None and b.__dict__["_kernel"] is None
+        assert rel(b.gamma, g["gamma_after_" + tag]) < 1e-12
+        assert rel(b.kernel, g["kernel_" + tag]) < 1e-12      # lazy host evaluation of W . gamma
+    W = B.gmem_coefficients(g["gamt_tl"], g["gamt_wl"], g["gwl"])
+    assert rel(np.einsum("ig,gab->iab", W, g["gam"]), g["gamt_direct"]) < 1e-12
+    # assigning a kernel drops the device recipe (the explicit kernel wins)
+    b.kernel = g["kernel_eta0"]
+    assert b.gmem_recipe is None
+
+
 def test_ebath_conventions():
     from sclmd_amd.baths import ebath
 
