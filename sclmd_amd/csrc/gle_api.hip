@@ -142,6 +142,9 @@ struct gle_handle {
   unsigned long long* d_dbg = nullptr;  // GLE_CHAIN_DBG stamps
   double* d_zero = nullptr;            // zero row (chain S(t+1) tiles' unused level slots)
   bool dbg_no_ladder = false;  // GLE_DBG_NO_LADDER: skip the ladder blocks (timing experiments only)
+  int bg_grid = 0;             // GLE_BG_GRID: cap of the far-field GEMM grid (grid-stride over items)
+  int dbg_skip = 0;            // GLE_DBG_SKIP bits (timing experiments only, wrong results):
+                               // 1 cgemm, 2 seg_fft, 4 far_ifft, 8 direct level ops
   int dbg_ntile = 0;
   int64_t dbg_t = -1;
   double* d_tw = nullptr;
@@ -1159,6 +1162,18 @@ int freeze(gle_handle* h) {
       // (f, g) are adjacent, so the row groups that share an X window run together
       lv.cg.clear();
       lv.cg_rn = (int)std::min<int64_t>(4, (B + 15) / 16);
+      {
+        // small levels: narrower column tiles (A read once per 32 instead of 64 columns) so the
+        // launch has at least two workgroups per CU to hide the HBM latency of the A stream
+        int64_t n4 = 0;
+        for (size_t j = 0; j < h->baths.size(); ++j)
+          if (lv.lb[j].active)
+            n4 += (int64_t)(lv.P + 1) * 3 * ((h->baths[j].nrt + 3) / 4) * ((B + 16 * lv.cg_rn - 1) / (16 * lv.cg_rn));
+        int ncu = 256;
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, h->cfg.device) == hipSuccess) ncu = prop.multiProcessorCount;
+        if (lv.cg_rn == 4 && n4 < 2 * ncu) lv.cg_rn = 2;
+      }
       lv.cg_flops = lv.cg_bytes = 0;
       const int NT = 16 * lv.cg_rn;
       for (size_t j = 0; j < h->baths.size(); ++j) {
@@ -1306,6 +1321,7 @@ int launch_level_block(gle_handle* h, Level& lv, int64_t k, hipStream_t s, bool 
       Bath& b = h->baths[j];
       LevelBath& L = lv.lb[j];
       if (!L.active) continue;
+      if (!priming && (h->dbg_skip & 2)) continue;
       if (launch_seg_fft(b.d_H, b.ldh, b.R, (int)h->B, b.nc, b.ncp, lv.P, T, priming ? L.M : 1, L.d_seg,
                          L.seg_fstride, L.ldseg, L.Rseg, h->d_cstab, lv.cstride, s))
         return fail(h, GLE_ERR_UNSUP, "segment transform launch failed (P = " + std::to_string(lv.P) + ")");
@@ -1318,7 +1334,7 @@ int launch_level_block(gle_handle* h, Level& lv, int64_t k, hipStream_t s, bool 
       e1 = h->ev[h->ev_used + 1];
       h->ev_used += 2;
     }
-    launch_cgemm(lv.cg_rn, lv.d_cg, (int)lv.cg.size(), T / lv.P, s);
+    if (priming || !(h->dbg_skip & 1)) launch_cgemm(lv.cg_rn, lv.d_cg, (int)lv.cg.size(), T / lv.P, s, priming ? 0 : h->bg_grid);
     if (e1) {
       hipEventRecord(e1, s);
       h->prof_n += 1;
@@ -1330,13 +1346,14 @@ int launch_level_block(gle_handle* h, Level& lv, int64_t k, hipStream_t s, bool 
       Bath& b = h->baths[j];
       LevelBath& L = lv.lb[j];
       if (!L.active) continue;
+      if (!priming && (h->dbg_skip & 4)) continue;
       if (launch_far_ifft(L.d_Yspec, L.yfstride, b.nc, (int)h->B, lv.P, L.d_out + (int64_t)par * lv.P * h->B,
                           (int64_t)2 * lv.P * h->B, h->d_cstab, lv.cstride, s))
         return fail(h, GLE_ERR_UNSUP, "inverse transform launch failed (P = " + std::to_string(lv.P) + ")");
     }
   } else {
     // profiled only when no level is spectral: the roofline then names one kernel class
-    run_op(h, lv.op[par], s, ta, h->far_mode != GLE_FAR_SPECTRAL);
+    if (priming || !(h->dbg_skip & 8)) run_op(h, lv.op[par], s, ta, h->far_mode != GLE_FAR_SPECTRAL);
   }
   HIPCHK(h, hipEventRecord(lv.ev[par], s));
   return GLE_OK;
@@ -1503,6 +1520,8 @@ int gle_create(const gle_config* cfg, gle_handle** out) {
   h->dt = cfg->dt;
   h->nphp = rup(h->nph, 8);
   h->dbg_no_ladder = getenv("GLE_DBG_NO_LADDER") != nullptr;
+  if (const char* e = getenv("GLE_DBG_SKIP")) h->dbg_skip = atoi(e);
+  if (const char* e = getenv("GLE_BG_GRID")) h->bg_grid = std::max(0, atoi(e));
   // main stream (the latency-bound per-step chain) at the highest priority, background streams
   // (ladder blocks) at the lowest
   {

@@ -41,10 +41,26 @@ __device__ __forceinline__ int64_t cmod(int64_t a, int64_t m) {
   return r < 0 ? r + m : r;
 }
 
-// k-steps a wave keeps in flight per batch (16-wave workgroups have 128 registers per lane)
+// k-steps a wave keeps in flight per batch (16-wave workgroups have 128 registers per lane).
+// The batch sets the kernel's register count: 8/4/2 k-steps with 4 waves per SIMD (128 VGPRs)
+// keeps every tile of a stage resident at once, even beside the background ladder kernels; a
+// deeper batch (24/12/8: 190 VGPRs, 2 waves per SIMD) left a third of stage A's tiles waiting for
+// a slot and measured 900k vs 1.04M traj-steps/s at C3.
+#ifndef CH_U1
+#define CH_U1 8
+#endif
+#ifndef CH_U2
+#define CH_U2 4
+#endif
+#ifndef CH_U4
+#define CH_U4 2
+#endif
+#ifndef CH_WPE
+#define CH_WPE 4
+#endif
 template <int RN, int NW>
 struct Batch {
-  static constexpr int U = NW >= 16 ? (RN == 1 ? 16 : (RN == 2 ? 6 : 3)) : (RN == 1 ? 24 : (RN == 2 ? 12 : 8));
+  static constexpr int U = NW >= 16 ? (RN == 1 ? 16 : (RN == 2 ? 6 : 3)) : (RN == 1 ? CH_U1 : (RN == 2 ? CH_U2 : CH_U4));
 };
 
 // GLE_CHAIN_DBG timeline: stamp 0 entry, 1 descriptor read, 2 products done, 3 end (100 MHz)
@@ -595,7 +611,7 @@ __device__ __forceinline__ void raw(const ChTile* __restrict__ T, const StepDev*
 }
 
 template <int STAGE, int NW, int DRN>
-__global__ __launch_bounds__(NW * 64) void chain_kernel(const ChTile* __restrict__ tiles, const StepDev* sd,
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(DRN == 1 && NW <= 8 ? CH_WPE : 1, 8))) void chain_kernel(const ChTile* __restrict__ tiles, const StepDev* sd,
                                                         StepArgs ta, int mode) {
   extern __shared__ double lds[];
   // The tile descriptor and the step descriptor's header are copied into LDS with one round of

@@ -657,12 +657,13 @@ void launch_khat_pack(const double* Kf, int ml, int nks_k, double* khat, int P, 
 // In-place radix-2 FFT of NS complex series of length N = 2^logn held bit-reversed in LDS
 // (buf[s * N + i]); sign -1 = forward, +1 = inverse (unscaled).
 template <int NS>
-__device__ __forceinline__ void lds_fft(double2* buf, int logn, const double2* __restrict__ cstab,
-                                        int cstride_n, double sign) {
+__device__ __forceinline__ void lds_fft(double2* buf, int logn, const double2* tw, double sign) {
+  // tw: the N/2 twiddles e^{-2 pi i j / N}, j < N/2, staged in LDS by the caller (a twiddle load
+  // from global memory in every stage would put logn dependent L2 round trips on the path)
   const int N = 1 << logn, h = N >> 1;
   for (int st = 1; st <= logn; ++st) {
     const int half = 1 << (st - 1);
-    const int tstride = (N >> st) * cstride_n;  // twiddle e^{-2 pi i jj / 2^st} = table[jj * (N/2^st) * 2 * stride / 2]
+    const int tstride = N >> st;  // e^{-2 pi i jj / 2^st} = tw[jj * N / 2^st]
     for (int j = threadIdx.x; j < NS * h; j += blockDim.x) {
       const int sidx = j / h, jb = j - sidx * h;
       const int g = jb >> (st - 1);
@@ -670,7 +671,7 @@ __device__ __forceinline__ void lds_fft(double2* buf, int logn, const double2* _
       double2* bs = buf + sidx * N;
       const int i0 = (g << st) + jj;
       const int i1 = i0 + half;
-      const double2 c = cstab[jj * tstride];
+      const double2 c = tw[jj * tstride];
       const double wx = c.x, wy = sign * c.y;  // e^{sign i 2 pi jj / 2^st}
       const double2 x0 = bs[i0];
       const double2 x1 = bs[i1];
@@ -680,6 +681,11 @@ __device__ __forceinline__ void lds_fft(double2* buf, int logn, const double2* _
     }
     __syncthreads();
   }
+}
+
+// twiddles of a length-N transform into LDS: tw[j] = cstab[j * cstride], j < N/2
+__device__ __forceinline__ void stage_twiddles(double2* tw, int N, const double2* __restrict__ cstab, int cstride) {
+  for (int j = threadIdx.x; j < N / 2; j += blockDim.x) tw[j] = cstab[(int64_t)j * cstride];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -692,77 +698,94 @@ __device__ __forceinline__ void lds_fft(double2* buf, int logn, const double2* _
 constexpr int CG_KC = 8;   // k-steps per LDS chunk
 constexpr int CG_LD = 80;  // LDS row stride (doubles): 64 columns + 16, ds_read_b64 at most 2-way
 
+typedef const __attribute__((address_space(1))) double gdbl;
+
 template <int RN>
-__global__ __launch_bounds__(256, 2) void cgemm_kernel(const CgItem* __restrict__ items, int64_t tseg) {
-  __shared__ double xs[2][4 * CG_KC * CG_LD];
+__device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, double (&xs)[2][4 * CG_KC * CG_LD]) {
   constexpr int NT = 16 * RN;
   constexpr int XPT = 4 * CG_KC * NT / 256;  // X doubles per thread per chunk
   constexpr int TPR = NT / XPT;              // staging threads per X row
-  const CgItem it = items[blockIdx.x];
+  static_assert(4 * CG_KC * TPR == 256, "one X row per TPR threads, every thread stages");
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
   const int brow = lane >> 4, bcol = lane & 15;
   const int S = it.M * it.nks;
   const int nch = (S + CG_KC - 1) / CG_KC;
   const bool active = wave < it.nrt;
-  const double* Aw = it.A + (int64_t)wave * it.a_rt + lane;
+  // global address space: flat loads would also count on lgkmcnt, and every LDS-read wait before an
+  // MFMA would then drain the HBM prefetches in flight
+  gdbl* Aw = (gdbl*)(it.A + (int64_t)(active ? wave : 0) * it.a_rt + lane);
   const int xr = tid / TPR, xc = (tid % TPR) * XPT;
-  double xv[XPT], a0[CG_KC], a1[CG_KC];
-  auto load_x = [&](int c) {
-#pragma unroll
-    for (int u = 0; u < XPT; ++u) xv[u] = 0.0;
-    const int s = c * CG_KC + (xr >> 2);
-    if (xr < 4 * CG_KC && s < S) {
-      const int i = s / it.nks, ks = s - i * it.nks;
-      const double* xp =
-          it.X + (int64_t)(4 * ks + (xr & 3)) * it.ldx + pmod(tseg - i, it.Rseg) * it.cs + it.col0 + xc;
-#pragma unroll
-      for (int u = 0; u < XPT; ++u) xv[u] = xp[u];
-    }
-  };
-  auto store_x = [&](int buf) {
-    if (xr < 4 * CG_KC) {
-#pragma unroll
-      for (int u = 0; u < XPT; ++u) xs[buf][xr * CG_LD + xc + u] = xv[u];
-    }
-  };
-  auto load_a = [&](int c, double(&a)[CG_KC]) {
-#pragma unroll
-    for (int u = 0; u < CG_KC; ++u) {
-      const int s = c * CG_KC + u;
-      a[u] = (active && s < S) ? Aw[(int64_t)s * 64] : 0.0;
-    }
-  };
+  const int tbase = (int)pmod(tseg, it.Rseg);  // ring slot of segment tseg (32-bit from here on)
+  // Prefetch depth: A fragments (HBM, the streamed operand) 2 chunks ahead of the MFMAs; X
+  // (segment ring, L2/MALL) into registers one chunk ahead, then into the other LDS buffer.  One
+  // chunk (8 k-steps, 8 RN MFMAs per wave) is too short to cover an HBM round trip on its own.
+  // Loads are branch-free (clamped address, zero by multiplication): a branch around a load makes
+  // the waitcnt pass drain every load in flight.
+  double xv[XPT], a0[CG_KC], a1[CG_KC], a2[CG_KC];
   d4 acc[RN];
 #pragma unroll
   for (int n = 0; n < RN; ++n) acc[n] = d4{0.0, 0.0, 0.0, 0.0};
-  load_x(0);
-  load_a(0, a0);
-  store_x(0);
+#define CG_LOAD_X(c, XV)                                                                              \
+  do {                                                                                                \
+    const int s0_ = (c) * CG_KC + (xr >> 2);                                                          \
+    const int sc_ = s0_ < S ? s0_ : S - 1;                                                            \
+    const int i_ = (int)((unsigned)sc_ / (unsigned)it.nks), ks_ = sc_ - i_ * it.nks;                  \
+    int slot_ = tbase - i_;                                                                           \
+    slot_ += slot_ < 0 ? it.Rseg : 0; /* i < M < Rseg */                                              \
+    gdbl* xp_ = (gdbl*)(it.X + (int64_t)(4 * ks_ + (xr & 3)) * it.ldx + (int64_t)slot_ * it.cs +      \
+                        it.col0 + xc);                                                                \
+    _Pragma("unroll") for (int u = 0; u < XPT; ++u) XV[u] = xp_[u];                                   \
+  } while (0)
+  /* rows past S are stored as zeros (the multiply waits for the load only here, at the store) */
+#define CG_STORE_X(c, buf, XV)                                                                        \
+  do {                                                                                                \
+    const double m_ = (c) * CG_KC + (xr >> 2) < S ? 1.0 : 0.0;                                        \
+    _Pragma("unroll") for (int u = 0; u < XPT; ++u) xs[buf][xr * CG_LD + xc + u] = XV[u] * m_;        \
+  } while (0)
+#define CG_LOAD_A(c, AV)                                                                              \
+  do {                                                                                                \
+    _Pragma("unroll") for (int u = 0; u < CG_KC; ++u) {                                               \
+      const int s0_ = (c) * CG_KC + u;                                                                \
+      AV[u] = Aw[(int64_t)(s0_ < S ? s0_ : S - 1) * 64]; /* masked at the MFMA */                 \
+    }                                                                                                 \
+  } while (0)
+  // chunk c: MFMAs on A chunk c (registers) and X chunk c (LDS buffer c&1); chunk c+2's A goes
+  // into the registers chunk c-1 used, chunk c+1's X into the other LDS buffer.  The A register
+  // roles rotate with period 3, spelled out so every role is static.
+#define CG_STEP(c, ACUR, ANEXT)                                                                       \
+  do {                                                                                                \
+    const int c_ = (c);                                                                               \
+    /* X first: vmcnt retires in order, so the X store at the end of the step then waits for X  */ \
+    /* (and older loads) only, while chunk c+2's A stays in flight                              */ \
+    /* unconditional (clamped) loads: paths that skip a load confuse the waitcnt pass          */ \
+    CG_LOAD_X(c_ + 1, xv);                                                                            \
+    CG_LOAD_A(c_ + 2, ANEXT);                                                                         \
+    const double* xb_ = xs[c_ & 1] + brow * CG_LD + bcol;                                             \
+    _Pragma("unroll") for (int u = 0; u < CG_KC; ++u) {                                               \
+      const double a_ = ACUR[u] * ((active && c_ * CG_KC + u < S) ? 1.0 : 0.0);                       \
+      _Pragma("unroll") for (int n = 0; n < RN; ++n) acc[n] =                                         \
+          __builtin_amdgcn_mfma_f64_16x16x4f64(a_, xb_[4 * u * CG_LD + 16 * n], acc[n], 0, 0, 0);     \
+    }                                                                                                 \
+    CG_STORE_X(c_ + 1, (c_ & 1) ^ 1, xv);                                                             \
+    __syncthreads();                                                                                  \
+  } while (0)
+  CG_LOAD_A(0, a0);
+  CG_LOAD_A(1, a1);
+  CG_LOAD_X(0, xv);
+  CG_STORE_X(0, 0, xv);
   __syncthreads();
-  for (int c = 0; c < nch; ++c) {
-    const int buf = c & 1;
-    const bool more = c + 1 < nch;
-    if (more) {
-      load_x(c + 1);
-      load_a(c + 1, a1);
-    }
-    if (active) {
-      const double* xb = xs[buf] + brow * CG_LD + bcol;
-#pragma unroll
-      for (int u = 0; u < CG_KC; ++u) {
-        if (c * CG_KC + u < S) {
-#pragma unroll
-          for (int n = 0; n < RN; ++n)
-            acc[n] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[u], xb[4 * u * CG_LD + 16 * n], acc[n], 0, 0, 0);
-        }
-      }
-    }
-    if (more) store_x(buf ^ 1);
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < CG_KC; ++u) a0[u] = a1[u];
+  for (int c = 0; c < nch; c += 3) {
+    CG_STEP(c, a0, a2);
+    if (c + 1 >= nch) break;
+    CG_STEP(c + 1, a1, a0);
+    if (c + 2 >= nch) break;
+    CG_STEP(c + 2, a2, a1);
   }
+#undef CG_STEP
+#undef CG_LOAD_A
+#undef CG_STORE_X
+#undef CG_LOAD_X
   if (active) {
     // f64 MFMA C/D map: col = lane & 15, row = (lane >> 4) + 4 * reg
 #pragma unroll
@@ -775,12 +798,22 @@ __global__ __launch_bounds__(256, 2) void cgemm_kernel(const CgItem* __restrict_
   }
 }
 
-void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStream_t s) {
+template <int RN>
+__global__ __launch_bounds__(256, 2) void cgemm_kernel(const CgItem* __restrict__ items, int nitems, int64_t tseg) {
+  __shared__ double xs[2][4 * CG_KC * CG_LD];
+  for (int item = blockIdx.x; item < nitems; item += gridDim.x) {
+    const CgItem it = items[item];
+    cgemm_item<RN>(it, tseg, xs);
+    __syncthreads();
+  }
+}
+void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStream_t s, int max_grid) {
   if (nitems <= 0) return;
+  const int grid = (max_grid > 0 && max_grid < nitems) ? max_grid : nitems;
   switch (rn) {
-    case 1: cgemm_kernel<1><<<nitems, 256, 0, s>>>(items, tseg); break;
-    case 2: cgemm_kernel<2><<<nitems, 256, 0, s>>>(items, tseg); break;
-    default: cgemm_kernel<4><<<nitems, 256, 0, s>>>(items, tseg); break;
+    case 1: cgemm_kernel<1><<<grid, 256, 0, s>>>(items, nitems, tseg); break;
+    case 2: cgemm_kernel<2><<<grid, 256, 0, s>>>(items, nitems, tseg); break;
+    default: cgemm_kernel<4><<<grid, 256, 0, s>>>(items, nitems, tseg); break;
   }
 }
 
@@ -789,25 +822,28 @@ void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStre
 // Xhat(f) = sum_n x[n] e^{-i pi f n / P}, f = 0..P, written into the frequency-f segment ring as the
 // Gauss planes  g = 0: Re + Im,  1: Im,  2: Re  (rows [g ncp + k], mirrored slots).  Two real series
 // per complex FFT.
-constexpr int FFT_BC = 8;  // trajectories per block
+// BC trajectories per block: 64 for the small transforms (one block per DOF, 512 B rows, every
+// thread busy in every butterfly stage), fewer for long transforms (LDS: BC/2 series of 2P points)
+template <int BC>
 __global__ __launch_bounds__(256) void seg_fft_kernel(const double* __restrict__ H, int64_t ldh, int R,
                                                       int B, int nc, int ncp, int P, int logn,
                                                       int64_t T, double* __restrict__ seg,
                                                       int64_t seg_fstride, int64_t ldseg, int Rseg,
                                                       const double2* __restrict__ cstab, int cstride) {
-  extern __shared__ double2 fbuf[];
+  extern __shared__ double2 fbuf[];  // BC/2 series of N points, then N/2 twiddles
   const int N = 2 * P;
-  const int nbc = (B + FFT_BC - 1) / FFT_BC;
+  stage_twiddles(fbuf + (BC / 2) * N, N, cstab, cstride);
+  const int nbc = (B + BC - 1) / BC;
   const int bc = blockIdx.x % nbc;
   const int k = (blockIdx.x / nbc) % nc;
   const int sidx = blockIdx.x / (nbc * nc);
   const int64_t sigma = T / P - sidx;
   const int64_t t0 = sigma * P - 2 * P + 2;
-  const int b0 = bc * FFT_BC;
+  const int b0 = bc * BC;
   const double* hk = H + (int64_t)k * ldh;
-  for (int e = threadIdx.x; e < N * FFT_BC / 2; e += blockDim.x) {
-    const int q = e % (FFT_BC / 2);
-    const int n = e / (FFT_BC / 2);
+  for (int e = threadIdx.x; e < N * BC / 2; e += blockDim.x) {
+    const int q = e % (BC / 2);
+    const int n = e / (BC / 2);
     double xr = 0.0, xi = 0.0;
     if (n < N - 1) {
       const double* hs = hk + pmod(t0 + n, R) * B;
@@ -819,11 +855,11 @@ __global__ __launch_bounds__(256) void seg_fft_kernel(const double* __restrict__
     fbuf[q * N + rev] = make_double2(xr, xi);
   }
   __syncthreads();
-  lds_fft<FFT_BC / 2>(fbuf, logn, cstab, cstride, -1.0);
+  lds_fft<BC / 2>(fbuf, logn, fbuf + (BC / 2) * N, -1.0);
   const int64_t slot = pmod(sigma, Rseg);
-  for (int e = threadIdx.x; e < (P + 1) * FFT_BC; e += blockDim.x) {
-    const int bl = e % FFT_BC;
-    const int f = e / FFT_BC;
+  for (int e = threadIdx.x; e < (P + 1) * BC; e += blockDim.x) {
+    const int bl = e % BC;
+    const int f = e / BC;
     const int b = b0 + bl;
     if (b >= B) continue;
     const int q = bl >> 1;
@@ -849,23 +885,42 @@ __global__ __launch_bounds__(256) void seg_fft_kernel(const double* __restrict__
   }
 }
 
+// trajectories per FFT block: the largest of 64/32/16/8 (not above B rounded to 8) whose LDS
+// (BC/2 complex series of 2P points) stays within 64 KiB
+static int fft_bc(int B, int P) {
+  int bc = 64;
+  while (bc > 8 && (bc > ((B + 7) / 8) * 8 || (size_t)(bc / 2) * 2 * P * 16 > 64 * 1024)) bc /= 2;
+  return bc;
+}
+
+template <int BC>
+static int seg_fft_launch(const double* H, int64_t ldh, int R, int B, int nc, int ncp, int P, int logn, int64_t T,
+                          int nseg, double* seg, int64_t seg_fstride, int64_t ldseg, int Rseg,
+                          const double* cstab, int cstride, hipStream_t s) {
+  const size_t shmem = ((size_t)(BC / 2) * 2 * P + P) * sizeof(double2);
+  if (shmem > 160 * 1024) return -2;
+  if (hipFuncSetAttribute((const void*)seg_fft_kernel<BC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)shmem) != hipSuccess)
+    return -3;
+  const int nbc = (B + BC - 1) / BC;
+  const int64_t blocks = (int64_t)nseg * nc * nbc;
+  seg_fft_kernel<BC><<<(unsigned)blocks, 256, shmem, s>>>(H, ldh, R, B, nc, ncp, P, logn, T, seg, seg_fstride,
+                                                           ldseg, Rseg, (const double2*)cstab, cstride);
+  return 0;
+}
+
 int launch_seg_fft(const double* H, int64_t ldh, int R, int B, int nc, int ncp, int P, int64_t T,
                    int nseg, double* seg, int64_t seg_fstride, int64_t ldseg, int Rseg,
                    const double* cstab, int cstride, hipStream_t s) {
   int logn = 0;
   while ((1 << logn) < 2 * P) ++logn;
   if ((1 << logn) != 2 * P) return -1;
-  const size_t shmem = (size_t)(FFT_BC / 2) * 2 * P * sizeof(double2);
-  if (shmem > 160 * 1024) return -2;
-  if (hipFuncSetAttribute((const void*)seg_fft_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)shmem) != hipSuccess)
-    return -3;
-  const int nbc = (B + FFT_BC - 1) / FFT_BC;
-  const int64_t blocks = (int64_t)nseg * nc * nbc;
-  seg_fft_kernel<<<(unsigned)blocks, 256, shmem, s>>>(H, ldh, R, B, nc, ncp, P, logn, T, seg,
-                                                      seg_fstride, ldseg, Rseg,
-                                                      (const double2*)cstab, cstride);
-  return 0;
+  switch (fft_bc(B, P)) {
+    case 64: return seg_fft_launch<64>(H, ldh, R, B, nc, ncp, P, logn, T, nseg, seg, seg_fstride, ldseg, Rseg, cstab, cstride, s);
+    case 32: return seg_fft_launch<32>(H, ldh, R, B, nc, ncp, P, logn, T, nseg, seg, seg_fstride, ldseg, Rseg, cstab, cstride, s);
+    case 16: return seg_fft_launch<16>(H, ldh, R, B, nc, ncp, P, logn, T, nseg, seg, seg_fstride, ldseg, Rseg, cstab, cstride, s);
+    default: return seg_fft_launch<8>(H, ldh, R, B, nc, ncp, P, logn, T, nseg, seg, seg_fstride, ldseg, Rseg, cstab, cstride, s);
+  }
 }
 
 // Block output out(kP + 1 + j) = y[j + P - 1] (j < P) of the real inverse transform of the
@@ -873,20 +928,22 @@ int launch_seg_fft(const double* H, int64_t ldh, int R, int B, int nc, int ncp, 
 // products T_g(f):
 //   y[n] = (1/2P) sum_{f<2P} Y(f) e^{+i pi f n / P},  Y(2P - f) = conj Y(f).
 // Grid: DOF k x 8-trajectory chunk; two real outputs per complex inverse FFT.
+template <int BC>
 __global__ __launch_bounds__(256) void far_ifft_kernel(const double* __restrict__ Y, int64_t yfstride,
                                                        int nc, int B, int P, int logn,
                                                        double* __restrict__ out, int64_t ldout,
                                                        const double2* __restrict__ cstab, int cstride) {
-  extern __shared__ double2 fbuf[];
+  extern __shared__ double2 fbuf[];  // BC/2 series of N points, then N/2 twiddles
   const int N = 2 * P;
-  const int nbc = (B + FFT_BC - 1) / FFT_BC;
+  stage_twiddles(fbuf + (BC / 2) * N, N, cstab, cstride);
+  const int nbc = (B + BC - 1) / BC;
   const int bc = blockIdx.x % nbc;
   const int k = blockIdx.x / nbc;
-  const int b0 = bc * FFT_BC;
+  const int b0 = bc * BC;
   const int64_t pl = (int64_t)nc * B;
-  for (int e = threadIdx.x; e < N * FFT_BC / 2; e += blockDim.x) {
-    const int q = e % (FFT_BC / 2);
-    const int f = e / (FFT_BC / 2);
+  for (int e = threadIdx.x; e < N * BC / 2; e += blockDim.x) {
+    const int q = e % (BC / 2);
+    const int f = e / (BC / 2);
     const bool cj = f > P;
     const int fs = cj ? N - f : f;
     const bool realonly = (fs == 0) || (fs == P);
@@ -913,11 +970,11 @@ __global__ __launch_bounds__(256) void far_ifft_kernel(const double* __restrict_
     fbuf[q * N + rev] = make_double2(ar - bi, ai + br);
   }
   __syncthreads();
-  lds_fft<FFT_BC / 2>(fbuf, logn, cstab, cstride, 1.0);
+  lds_fft<BC / 2>(fbuf, logn, fbuf + (BC / 2) * N, 1.0);
   const double scale = 1.0 / N;
-  for (int e = threadIdx.x; e < P * FFT_BC; e += blockDim.x) {
-    const int bl = e % FFT_BC;
-    const int j = e / FFT_BC;
+  for (int e = threadIdx.x; e < P * BC; e += blockDim.x) {
+    const int bl = e % BC;
+    const int j = e / BC;
     const int b = b0 + bl;
     if (b >= B) continue;
     const double2 z = fbuf[(bl >> 1) * N + j + P - 1];
@@ -925,20 +982,31 @@ __global__ __launch_bounds__(256) void far_ifft_kernel(const double* __restrict_
   }
 }
 
+template <int BC>
+static int far_ifft_launch(const double* Y, int64_t yfstride, int nc, int B, int P, int logn, double* out,
+                           int64_t ldout, const double* cstab, int cstride, hipStream_t s) {
+  const size_t shmem = ((size_t)(BC / 2) * 2 * P + P) * sizeof(double2);
+  if (shmem > 160 * 1024) return -2;
+  if (hipFuncSetAttribute((const void*)far_ifft_kernel<BC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)shmem) != hipSuccess)
+    return -3;
+  const int nbc = (B + BC - 1) / BC;
+  far_ifft_kernel<BC><<<(unsigned)(nc * nbc), 256, shmem, s>>>(Y, yfstride, nc, B, P, logn, out, ldout,
+                                                              (const double2*)cstab, cstride);
+  return 0;
+}
+
 int launch_far_ifft(const double* Y, int64_t yfstride, int nc, int B, int P, double* out,
                     int64_t ldout, const double* cstab, int cstride, hipStream_t s) {
   int logn = 0;
   while ((1 << logn) < 2 * P) ++logn;
   if ((1 << logn) != 2 * P) return -1;
-  const size_t shmem = (size_t)(FFT_BC / 2) * 2 * P * sizeof(double2);
-  if (shmem > 160 * 1024) return -2;
-  if (hipFuncSetAttribute((const void*)far_ifft_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)shmem) != hipSuccess)
-    return -3;
-  const int nbc = (B + FFT_BC - 1) / FFT_BC;
-  far_ifft_kernel<<<(unsigned)(nc * nbc), 256, shmem, s>>>(Y, yfstride, nc, B, P, logn, out, ldout,
-                                                          (const double2*)cstab, cstride);
-  return 0;
+  switch (fft_bc(B, P)) {
+    case 64: return far_ifft_launch<64>(Y, yfstride, nc, B, P, logn, out, ldout, cstab, cstride, s);
+    case 32: return far_ifft_launch<32>(Y, yfstride, nc, B, P, logn, out, ldout, cstab, cstride, s);
+    case 16: return far_ifft_launch<16>(Y, yfstride, nc, B, P, logn, out, ldout, cstab, cstride, s);
+    default: return far_ifft_launch<8>(Y, yfstride, nc, B, P, logn, out, ldout, cstab, cstride, s);
+  }
 }
 
 }  // namespace gle
