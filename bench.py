@@ -75,8 +75,10 @@ def cpu_baseline(baths_host, dyn, nph, dt, nmd, budget_s=15.0, max_steps=200):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    # 512 timed steps = two periods of the largest ladder level (P = 256 at C3), so every level's
+    # blocks are in the window in proportion (a 200-step window under-samples the big levels)
+    ap.add_argument("--steps", type=int, default=512)
+    ap.add_argument("--warmup", type=int, default=64)
     ap.add_argument("--ntraj", type=int, default=64, help="trajectories per GPU")
     ap.add_argument("--config", default="C3")
     ap.add_argument("--block-len", type=int, default=0)
@@ -133,9 +135,11 @@ def main():
     st.sync()
     t0 = time.perf_counter()
     m.steps(args.steps)
+    t_enq = time.perf_counter() - t0
     st.sync()
     barrier()
     el = time.perf_counter() - t0
+    log("[bench] rank %d host enqueue %.3f ms of %.3f ms timed" % (rank, t_enq * 1e3, el * 1e3))
     prof = st.profile_read()
     st.profile(False)
     # one reduce of the time-averaged current statistics (the ensemble output)

@@ -113,6 +113,14 @@ struct Level {
   hipEvent_t ev[2] = {nullptr, nullptr};
   int64_t last_block = INT64_MIN;
   int64_t bg_block[2] = {INT64_MIN, INT64_MIN};  // block launched on the background stream
+  // a block is issued in pieces spread over the P / P0 first-level boundaries of its window, so a
+  // long block never sits in front of the next small-level block on the in-order stream:
+  // spectral: [segment transform] [cgemm item chunk]... [inverse transform + event]
+  int ncg_chunk = 1;
+  int npiece = 1;
+  int64_t pend_block = INT64_MIN;  // block whose pieces are still being issued
+  int64_t pend_t0 = 0;
+  int next_piece = 0;
 };
 
 }  // namespace
@@ -1097,6 +1105,7 @@ int freeze(gle_handle* h) {
                        lv.cstride, h->stream);
       HIPCHK(h, hipStreamSynchronize(h->stream));
     }
+    // background stream per level group (a first level on a stream of its own measured slower)
     lv.sidx = lv.P <= 8 * P0 ? 0 : (lv.P <= 64 * P0 ? 1 : 2);
     for (int q = 0; q < 2; ++q)
       HIPCHK(h, hipEventCreateWithFlags(&lv.ev[q], hipEventDisableTiming | hipEventReleaseToDevice));
@@ -1211,6 +1220,16 @@ int freeze(gle_handle* h) {
       rc = dalloc_n(h, &lv.d_cg, lv.cg.size());
       if (!rc) rc = upload(h, lv.d_cg, lv.cg.data(), lv.cg.size() * sizeof(CgItem));
       if (rc) return rc;
+      {
+        // cgemm chunks of >= 2 workgroups per CU, at most one chunk per first-level boundary
+        int ncu = 256;
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, h->cfg.device) == hipSuccess) ncu = prop.multiProcessorCount;
+        const int nslot = std::max(1, lv.P / h->P0);
+        lv.ncg_chunk = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)lv.cg.size() / (2 * ncu), nslot));
+        if (const char* e = getenv("GLE_NO_PIECES")) lv.ncg_chunk = atoi(e) > 0 ? 1 : lv.ncg_chunk;
+        lv.npiece = lv.ncg_chunk + 2;
+      }
     } else {
       for (int par = 0; par < 2; ++par) {
         Planner p(h, lv.op[par], rn_for((int64_t)lv.P * B));
@@ -1310,53 +1329,66 @@ int freeze(gle_handle* h) {
   return GLE_OK;
 }
 
-// Block k of level lv on stream s.  Spectral: the newest segment spectrum is transformed first
-// (all M the block reads when priming).
-int launch_level_block(gle_handle* h, Level& lv, int64_t k, hipStream_t s, bool priming) {
+// Pieces [j0, j1) of block k of level lv on stream s (see Level::npiece); the last piece records
+// the block's event.  Spectral: the newest segment spectrum is transformed first (all M when
+// priming), then the cgemm item chunks, then the inverse transform.
+int launch_level_pieces(gle_handle* h, Level& lv, int64_t k, hipStream_t s, bool priming, int j0, int j1) {
   const int64_t T = (k - 1) * (int64_t)lv.P;
   const StepArgs ta = step_args(h, T);
   const int par = (int)(k & 1);
-  if (lv.spectral) {
-    for (size_t j = 0; j < h->baths.size(); ++j) {
-      Bath& b = h->baths[j];
-      LevelBath& L = lv.lb[j];
-      if (!L.active) continue;
-      if (!priming && (h->dbg_skip & 2)) continue;
-      if (launch_seg_fft(b.d_H, b.ldh, b.R, (int)h->B, b.nc, b.ncp, lv.P, T, priming ? L.M : 1, L.d_seg,
-                         L.seg_fstride, L.ldseg, L.Rseg, h->d_cstab, lv.cstride, s))
-        return fail(h, GLE_ERR_UNSUP, "segment transform launch failed (P = " + std::to_string(lv.P) + ")");
+  for (int j = j0; j < j1; ++j) {
+    if (!lv.spectral) {
+      // profiled only when no level is spectral: the roofline then names one kernel class
+      if (priming || !(h->dbg_skip & 8)) run_op(h, lv.op[par], s, ta, h->far_mode != GLE_FAR_SPECTRAL);
+      continue;
     }
-    // the batched GEMM of the per-frequency products, profiled like run_op (the dominant kernel)
-    hipEvent_t e1 = nullptr;
-    if (h->prof && !lv.cg.empty()) {
-      if (h->ev_used + 2 > h->ev.size()) drain_profile(h);
-      hipEventRecord(h->ev[h->ev_used], s);
-      e1 = h->ev[h->ev_used + 1];
-      h->ev_used += 2;
+    if (j == 0) {
+      for (size_t b = 0; b < h->baths.size(); ++b) {
+        Bath& bb = h->baths[b];
+        LevelBath& L = lv.lb[b];
+        if (!L.active || (!priming && (h->dbg_skip & 2))) continue;
+        if (launch_seg_fft(bb.d_H, bb.ldh, bb.R, (int)h->B, bb.nc, bb.ncp, lv.P, T, priming ? L.M : 1, L.d_seg,
+                           L.seg_fstride, L.ldseg, L.Rseg, h->d_cstab, lv.cstride, s))
+          return fail(h, GLE_ERR_UNSUP, "segment transform launch failed (P = " + std::to_string(lv.P) + ")");
+      }
+    } else if (j <= lv.ncg_chunk) {
+      // one chunk of the batched GEMM of the per-frequency products, profiled like run_op
+      const int64_t n = (int64_t)lv.cg.size();
+      const int64_t c0 = n * (j - 1) / lv.ncg_chunk, c1 = n * j / lv.ncg_chunk;
+      if (c1 <= c0) continue;
+      hipEvent_t e1 = nullptr;
+      if (h->prof) {
+        if (h->ev_used + 2 > h->ev.size()) drain_profile(h);
+        hipEventRecord(h->ev[h->ev_used], s);
+        e1 = h->ev[h->ev_used + 1];
+        h->ev_used += 2;
+      }
+      if (priming || !(h->dbg_skip & 1))
+        launch_cgemm(lv.cg_rn, lv.d_cg + c0, (int)(c1 - c0), T / lv.P, s, priming ? 0 : h->bg_grid);
+      if (e1) {
+        hipEventRecord(e1, s);
+        const double frac = (double)(c1 - c0) / (double)n;
+        h->prof_n += 1;
+        h->prof_flops += lv.cg_flops * frac;
+        h->prof_bytes += lv.cg_bytes * frac;
+      }
+    } else {
+      for (size_t b = 0; b < h->baths.size(); ++b) {
+        Bath& bb = h->baths[b];
+        LevelBath& L = lv.lb[b];
+        if (!L.active || (!priming && (h->dbg_skip & 4))) continue;
+        if (launch_far_ifft(L.d_Yspec, L.yfstride, bb.nc, (int)h->B, lv.P, L.d_out + (int64_t)par * lv.P * h->B,
+                            (int64_t)2 * lv.P * h->B, h->d_cstab, lv.cstride, s))
+          return fail(h, GLE_ERR_UNSUP, "inverse transform launch failed (P = " + std::to_string(lv.P) + ")");
+      }
     }
-    if (priming || !(h->dbg_skip & 1)) launch_cgemm(lv.cg_rn, lv.d_cg, (int)lv.cg.size(), T / lv.P, s, priming ? 0 : h->bg_grid);
-    if (e1) {
-      hipEventRecord(e1, s);
-      h->prof_n += 1;
-      h->prof_flops += lv.cg_flops;
-      h->prof_bytes += lv.cg_bytes;
-    }
-    (void)ta;
-    for (size_t j = 0; j < h->baths.size(); ++j) {
-      Bath& b = h->baths[j];
-      LevelBath& L = lv.lb[j];
-      if (!L.active) continue;
-      if (!priming && (h->dbg_skip & 4)) continue;
-      if (launch_far_ifft(L.d_Yspec, L.yfstride, b.nc, (int)h->B, lv.P, L.d_out + (int64_t)par * lv.P * h->B,
-                          (int64_t)2 * lv.P * h->B, h->d_cstab, lv.cstride, s))
-        return fail(h, GLE_ERR_UNSUP, "inverse transform launch failed (P = " + std::to_string(lv.P) + ")");
-    }
-  } else {
-    // profiled only when no level is spectral: the roofline then names one kernel class
-    if (priming || !(h->dbg_skip & 8)) run_op(h, lv.op[par], s, ta, h->far_mode != GLE_FAR_SPECTRAL);
   }
-  HIPCHK(h, hipEventRecord(lv.ev[par], s));
+  if (j1 >= lv.npiece) HIPCHK(h, hipEventRecord(lv.ev[par], s));
   return GLE_OK;
+}
+
+int launch_level_block(gle_handle* h, Level& lv, int64_t k, hipStream_t s, bool priming) {
+  return launch_level_pieces(h, lv, k, s, priming, 0, lv.npiece);
 }
 
 // After set_state / set_history: S(t) from the whole history, and the two level blocks that cover
@@ -1380,6 +1412,7 @@ int prime(gle_handle* h) {
     if (rc) return rc;
     lv.last_block = k0 + 1;
     lv.bg_block[0] = lv.bg_block[1] = INT64_MIN;
+    lv.pend_block = INT64_MIN;
   }
   // near-field partials of target t+1 (lags >= 2: p up to t-1), as the chain of step t-1 leaves them
   for (auto& b : h->baths)
@@ -1405,24 +1438,43 @@ int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
   const int64_t t = h->t;
   // ladder: at each block boundary T = kP, start block k+1 (targets T+P+1..T+2P, data up to T) on
   // the level's background stream once step T-1 has closed; consume block k from this step on
+  // The block's pieces are issued over the first-level boundaries T, T+P0, ..., T+P-P0 (levels in
+  // increasing P, so each boundary's small-level block is queued before the big levels' pieces).
   bool bg_waited[gle_handle::NBG] = {};
-  for (auto& lv : h->levels) {
-    if (t % lv.P != 0 || h->dbg_no_ladder) continue;
-    const int64_t k = t / lv.P;
-    if (k + 1 > lv.last_block) {
+  if (!h->dbg_no_ladder && t % h->P0 == 0) {
+    for (auto& lv : h->levels) {
       hipStream_t bs = h->bg[lv.sidx];
-      if (!bg_waited[lv.sidx]) {
-        HIPCHK(h, hipStreamWaitEvent(bs, h->ev_step, 0));
-        bg_waited[lv.sidx] = true;
+      const int64_t k = floordiv(t, lv.P);
+      if (t % lv.P == 0 && k + 1 > lv.last_block) {
+        if (lv.pend_block != INT64_MIN) {  // (cannot happen: the last piece is due at T + P - P0)
+          rc = launch_level_pieces(h, lv, lv.pend_block, bs, false, lv.next_piece, lv.npiece);
+          if (rc) return rc;
+        }
+        if (!bg_waited[lv.sidx]) {
+          HIPCHK(h, hipStreamWaitEvent(bs, h->ev_step, 0));
+          bg_waited[lv.sidx] = true;
+        }
+        lv.pend_block = k + 1;
+        lv.pend_t0 = t;
+        lv.next_piece = 0;
+        lv.last_block = k + 1;
+        lv.bg_block[(k + 1) & 1] = k + 1;
       }
-      rc = launch_level_block(h, lv, k + 1, bs, false);
-      if (rc) return rc;
-      lv.last_block = k + 1;
-      lv.bg_block[(k + 1) & 1] = k + 1;
-    }
-    if (lv.bg_block[k & 1] == k) {
-      HIPCHK(h, hipStreamWaitEvent(h->stream, lv.ev[k & 1], 0));
-      lv.bg_block[k & 1] = INT64_MIN;
+      if (lv.pend_block != INT64_MIN) {
+        const int nslot = std::max(1, lv.P / h->P0);
+        const int slot = (int)((t - lv.pend_t0) / h->P0);
+        const int j1 = slot + 1 >= nslot ? lv.npiece : (int)(((int64_t)(slot + 1) * lv.npiece + nslot - 1) / nslot);
+        if (j1 > lv.next_piece) {
+          rc = launch_level_pieces(h, lv, lv.pend_block, bs, false, lv.next_piece, j1);
+          if (rc) return rc;
+          lv.next_piece = j1;
+        }
+        if (lv.next_piece >= lv.npiece) lv.pend_block = INT64_MIN;
+      }
+      if (t % lv.P == 0 && lv.bg_block[k & 1] == k) {
+        HIPCHK(h, hipStreamWaitEvent(h->stream, lv.ev[k & 1], 0));
+        lv.bg_block[k & 1] = INT64_MIN;
+      }
     }
   }
   const bool need_pot = (fpot_host_T == nullptr) && !h->pot_cache_exact;

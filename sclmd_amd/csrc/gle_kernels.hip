@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <vector>
 #include <cstdio>
 
 #include "gle_internal.h"
@@ -879,17 +880,34 @@ __global__ __launch_bounds__(256) void seg_fft_kernel(const double* __restrict__
 #pragma unroll
     for (int g = 0; g < 3; ++g) {
       const int64_t ir = (int64_t)(g * ncp + k) * ldseg;
-      sf[ir + slot * B] = v[g];
-      sf[ir + (slot + Rseg) * B] = v[g];
+      sf[ir + slot * B] = v[g];  // (cgemm addresses ring slots modulo Rseg: no mirrored copy)
     }
   }
+}
+
+// raise a kernel's dynamic-LDS limit once per (kernel, device): a per-launch attribute call costs
+// host time on the step's critical path at block boundaries
+static bool lds_attr_once(const void* fn) {
+  constexpr int MAXDEV = 64;
+  struct Entry {
+    const void* fn;
+    int dev;
+  };
+  static thread_local std::vector<Entry> done;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev >= MAXDEV) return false;
+  for (const Entry& e : done)
+    if (e.fn == fn && e.dev == dev) return true;
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess) return false;
+  done.push_back({fn, dev});
+  return true;
 }
 
 // trajectories per FFT block: the largest of 64/32/16/8 (not above B rounded to 8) whose LDS
 // (BC/2 complex series of 2P points) stays within 64 KiB
 static int fft_bc(int B, int P) {
   int bc = 64;
-  while (bc > 8 && (bc > ((B + 7) / 8) * 8 || (size_t)(bc / 2) * 2 * P * 16 > 64 * 1024)) bc /= 2;
+  while (bc > 8 && (bc > ((B + 7) / 8) * 8 || ((size_t)(bc / 2) * 2 * P + P) * 16 > 64 * 1024)) bc /= 2;
   return bc;
 }
 
@@ -899,9 +917,9 @@ static int seg_fft_launch(const double* H, int64_t ldh, int R, int B, int nc, in
                           const double* cstab, int cstride, hipStream_t s) {
   const size_t shmem = ((size_t)(BC / 2) * 2 * P + P) * sizeof(double2);
   if (shmem > 160 * 1024) return -2;
-  if (hipFuncSetAttribute((const void*)seg_fft_kernel<BC>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)shmem) != hipSuccess)
-    return -3;
+  // raise the dynamic-LDS limit once per instantiation (a per-launch attribute call costs host
+  // time on the step's critical path at block boundaries)
+  if (!lds_attr_once((const void*)seg_fft_kernel<BC>)) return -3;
   const int nbc = (B + BC - 1) / BC;
   const int64_t blocks = (int64_t)nseg * nc * nbc;
   seg_fft_kernel<BC><<<(unsigned)blocks, 256, shmem, s>>>(H, ldh, R, B, nc, ncp, P, logn, T, seg, seg_fstride,
@@ -987,9 +1005,9 @@ static int far_ifft_launch(const double* Y, int64_t yfstride, int nc, int B, int
                            int64_t ldout, const double* cstab, int cstride, hipStream_t s) {
   const size_t shmem = ((size_t)(BC / 2) * 2 * P + P) * sizeof(double2);
   if (shmem > 160 * 1024) return -2;
-  if (hipFuncSetAttribute((const void*)far_ifft_kernel<BC>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)shmem) != hipSuccess)
-    return -3;
+  // raise the dynamic-LDS limit once per instantiation (a per-launch attribute call costs host
+  // time on the step's critical path at block boundaries)
+  if (!lds_attr_once((const void*)far_ifft_kernel<BC>)) return -3;
   const int nbc = (B + BC - 1) / BC;
   far_ifft_kernel<BC><<<(unsigned)(nc * nbc), 256, shmem, s>>>(Y, yfstride, nc, B, P, logn, out, ldout,
                                                               (const double2*)cstab, cstride);

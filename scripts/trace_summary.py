@@ -69,3 +69,13 @@ if "--steps" in sys.argv:
         gaps.sort()
         if gaps:
             print("  chain launch gaps: med %.2f us  p90 %.2f us" % (gaps[len(gaps) // 2], gaps[int(len(gaps) * 0.9)]))
+
+if "--gaps" in sys.argv:
+    # idle time on the main stream between consecutive chain launches over the last 100 steps
+    rows.sort(key=lambda r: r["s"])
+    ch = [r for r in rows if r["n"].startswith("chain_kernel")][-301:]
+    gaps = [(b["s"] - a["e"]) / 1e3 for a, b in zip(ch, ch[1:])]
+    if gaps:
+        print("\nchain gaps over %d launches: total %.1f us = %.2f us/step; largest %s"
+              % (len(gaps), sum(gaps), sum(gaps) / (len(gaps) / 3.0),
+                 [round(x, 1) for x in sorted(gaps)[-8:]]))
