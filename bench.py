@@ -86,6 +86,11 @@ def main():
     ap.add_argument("--far-mode", default="auto", choices=["auto", "direct", "spectral"])
     ap.add_argument("--gmem", default="device", choices=["device", "host"],
                     help="memory-kernel construction (phbath.gmem) on the device or with numpy")
+    ap.add_argument("--noise", default="device", choices=["device", "white"],
+                    help="device: coloured noise from the bath spectra (factorised on the host, drawn "
+                         "and filtered on the device); white: seeded N(0, 1e-3^2) realisations assigned "
+                         "to bath.noise (throughput runs of configurations whose noise factors do not "
+                         "fit next to the spectral kernels, e.g. C5; the step does the same work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
@@ -113,13 +118,21 @@ def main():
               seed=1000 + rank * args.ntraj, traj_offset=rank * args.ntraj, device=local_rank,
               noise_mode="device", block_len=args.block_len, far_mode=args.far_mode,
               max_block=args.max_block, verbose=False)
+    log("[bench] rank %d system built (%.1fs)" % (rank, time.perf_counter() - t_setup))
     for b in baths:
         m.AddBath(b)
     m.initialise()
     m.ResetHis()
-    for i in range(len(baths)):
-        m.gen_noise(i, 0)
-    st = m._st
+    log("[bench] rank %d state initialised (%.1fs)" % (rank, time.perf_counter() - t_setup))
+    if args.noise == "white":
+        rng = np.random.default_rng(4321 + rank)
+        for b in baths:
+            b.noise = rng.standard_normal((args.ntraj, meta["nmd"], b.nc)) * 1e-3
+    else:
+        for i in range(len(baths)):
+            m.gen_noise(i, 0)
+    st = m._ensure_device()
+    m.steps(0)  # uploads assigned noise
     st.sync()
     setup_s = time.perf_counter() - t_setup
     log("[bench] rank %d setup %.1fs plan %s" % (rank, setup_s, st.plan_info()))
@@ -164,8 +177,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (seeded chain junction, gmem kernels, device Philox coloured noise)",
-        "config": {"workload": "%s: %d-atom chain junction, %d phonon baths nc=%s, ml=%d, nmd=%d, "
+        "data": "synthetic (seeded chain junction, device gmem kernels, %s)" % (
+            "device Philox coloured noise" if args.noise == "device" else "injected white noise, throughput only"),
+        "config": {"workload": "%s: %d-atom chain junction, %d baths nc=%s, ml=%d, nmd=%d, "
                                "%d traj/GPU" % (args.config, meta["natom"], len(baths), meta["nc"],
                                                 meta["ml"], meta["nmd"], args.ntraj),
                    "ntraj_per_gpu": args.ntraj, "ntraj_total": world * args.ntraj,

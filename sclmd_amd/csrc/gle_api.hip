@@ -1036,13 +1036,16 @@ int freeze(gle_handle* h) {
         if (b.ml <= lv.lag0) continue;
         const int M = (std::min(lv.lag1, b.ml) + lv.P - 1) / lv.P - 2;
         need += (size_t)(lv.P + 1) * 3 * b.nrt * b.nks * M * 64 * 8;
-        need += (size_t)(lv.P + 1) * 3 * b.ncp * (2 * (M + 4) * B + 1024) * 8;
+        need += (size_t)(lv.P + 1) * 3 * b.ncp * ((M + 4) * B + 512) * 8;
         need += (size_t)(lv.P + 1) * 3 * b.nc * B * 8;
       }
     }
+    // the spectral buffers are the last big allocations of the plan (the kernels, noise and history
+    // rings are already resident): keep a reserve for the remaining per-level buffers and the chain
     size_t fr = 0, tot = 0;
     hipMemGetInfo(&fr, &tot);
-    if (need > fr / 2) {
+    const size_t reserve = std::max<size_t>((size_t)8 << 30, tot / 32);
+    if (need + reserve > fr) {
       if (mode == GLE_FAR_SPECTRAL)
         return fail(h, GLE_ERR_NOMEM, "spectral levels need " + std::to_string(need >> 20) + " MiB");
       for (auto& lv : h->levels) lv.spectral = false;
@@ -1093,7 +1096,7 @@ int freeze(gle_handle* h) {
       if (!lv.spectral) continue;
       L.M = (L.lag1 + lv.P - 1) / lv.P - 2;
       L.Rseg = L.M + 4;
-      L.ldseg = 2 * (int64_t)L.Rseg * B + 512;
+      L.ldseg = (int64_t)L.Rseg * B + 512;  // ring slots addressed modulo Rseg (no mirrored copy)
       L.khat_fstride = (int64_t)3 * b.nrt * b.nks * L.M * 64;  // the three Gauss planes
       L.seg_fstride = (int64_t)3 * b.ncp * L.ldseg;             // Re + Im, Im, Re rows
       L.yfstride = (int64_t)3 * b.nc * B;                       // T_0, T_1, T_2
