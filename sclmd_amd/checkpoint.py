@@ -1,0 +1,51 @@
+"""MD{j}.nc checkpoint files of md.Run (sclmd/md.py:684-764 dump, :506-567 resume, :768-783 helpers).
+
+The reference writes them with netCDF4 (HDF5-based NETCDF4 format, zlib).  netCDF4 is not installed
+here, so the files are written in the NetCDF classic (64-bit offset) format with scipy.io -- the same
+dimension names, variable names, shapes and float64 data, readable by netCDF4.Dataset and by
+ReadNetCDFVar below.  Deviations (documented in md.dump): no zlib compression; with ntraj > 1 every
+per-trajectory variable gains a leading 'traj' dimension; with several ranks each rank writes its
+own shard to MD{j}.r{rank}.nc.
+"""
+import os
+
+import numpy as np
+from scipy.io import netcdf_file
+
+
+def Write2NetCDFFile(ncfile, var, varLabel, dimensions, units=None, description=None):
+    """Create a float64 variable and fill it (md.py:768-775)."""
+    v = np.asarray(var, dtype=np.float64)
+    tmp = ncfile.createVariable(varLabel, "d", tuple(dimensions))
+    if len(dimensions) and ncfile.dimensions.get(dimensions[0]) is None:
+        tmp[: v.shape[0]] = v  # record (unlimited) dimension
+    else:
+        tmp[:] = v
+    if units:
+        tmp.units = units
+    if description:
+        tmp.description = description
+
+
+def ReadNetCDFVar(file, var):
+    """Copy of one variable of an MD{j}.nc file (md.py:778-783)."""
+    with netcdf_file(file, "r", mmap=False) as f:
+        return np.array(f.variables[var].data, dtype=np.float64)
+
+
+def has_var(file, var):
+    with netcdf_file(file, "r", mmap=False) as f:
+        return var in f.variables
+
+
+def open_for_write(path, title="Output from md.py"):
+    tmp = path + ".tmp"
+    f = netcdf_file(tmp, "w", version=2)
+    f.title = title
+    return f, tmp
+
+
+def commit(f, tmp, path):
+    """Close and atomically move into place (a crash never leaves a half-written checkpoint)."""
+    f.close()
+    os.replace(tmp, path)

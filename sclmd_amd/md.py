@@ -508,24 +508,165 @@ class md:
 
         return ensemble.rank(self.comm) == 0
 
+    # ------------------------------------------------------------------------------ checkpoints
+    def _ncname(self, j):
+        from . import ensemble
+
+        w = ensemble.world_size(self.comm)
+        return "MD%d.nc" % j if w == 1 else "MD%d.r%d.nc" % (j, ensemble.rank(self.comm))
+
+    @property
+    def phis(self):
+        """Velocity history, newest first: (ml, nph), or (ntraj, ml, nph) (md.py:345-346, 386-387).
+        The device keeps the history of the bath-coupled DOFs only (the only ones the friction
+        reads); the columns of other DOFs, and rows past a bath's own ml, read as zeros."""
+        st = self._ensure_device()
+        out = np.zeros((self.ntraj, self.ml, self.nph))
+        for i, b in enumerate(self.baths):
+            h = st.get_history(i)                      # (ntraj, ml_b, nc_b)
+            out[:, : h.shape[1], np.asarray(b.cids)] = h
+        return out[0] if self.ntraj == 1 else out
+
+    @property
+    def qhis(self):
+        """Position history (md.py:346, 387).  Only its newest row (the current q) ever enters a
+        force (ebath bias, baths.py:245-247), so the device keeps none: zeros of the reference's
+        shape."""
+        shp = (self.ml, self.nph) if self.ntraj == 1 else (self.ntraj, self.ml, self.nph)
+        return np.zeros(shp)
+
+    def _load_phis(self, phis):
+        st = self._ensure_device()
+        ph = np.asarray(phis, dtype=float)
+        if ph.ndim == 2:
+            ph = np.broadcast_to(ph, (self.ntraj,) + ph.shape)
+        for i, b in enumerate(self.baths):
+            ml_b = st.bath_ml[i]
+            h = np.zeros((self.ntraj, ml_b, len(b.cids)))
+            n = min(ml_b, ph.shape[1])
+            h[:, :n, :] = ph[:, :n, :][:, :, np.asarray(b.cids)]
+            st.set_history(i, h)
+        self._reset_his = False
+
+    def dump(self, ipie, id):
+        """Write MD{id}.nc (md.py:684-764): energy, p, q, t, ipie, phis, qhis, and with saveall the
+        noise series (and ps/qs with savep/saveq), with savep the power spectrum.  Deviations: NetCDF
+        classic format (netCDF4 is not installed; see sclmd_amd.checkpoint); fhis{i} (the per-step
+        bath forces) is not recorded on the device and is not written."""
+        from . import checkpoint as C
+
+        multi = self.ntraj > 1
+        tr = ("traj",) if multi else ()
+        f, tmp = C.open_for_write(self._ncname(id))
+        f.createDimension("nnmd", None)  # the record dimension (the classic format wants it first)
+        f.createDimension("nph", self.nph)
+        f.createDimension("one", 1)
+        f.createDimension("two", 2)
+        f.createDimension("mem", self.ml)
+        f.createDimension("nmd", self.nmd)
+        if multi:
+            f.createDimension("traj", self.ntraj)
+        if self.atomlist is not None:
+            f.createDimension("atomlist", len(self.atomlist))
+        for i, b in enumerate(self.baths):
+            f.createDimension("n" + str(i), b.nc)
+        if self.saveall:
+            for i, b in enumerate(self.baths):
+                nz = np.asarray(b.noise)
+                if multi:  # (ntraj, nmd, nc) -> (nmd, ntraj, nc): the record dimension comes first
+                    f.createDimension("traj" + str(i), nz.shape[0])
+                    C.Write2NetCDFFile(f, np.transpose(nz, (1, 0, 2)), "noise" + str(i),
+                                       ("nnmd", "traj" + str(i), "n" + str(i)), units="")
+                else:
+                    C.Write2NetCDFFile(f, nz, "noise" + str(i), ("nnmd", "n" + str(i)), units="")
+            if self.savep:
+                C.Write2NetCDFFile(f, self.ps, "ps", ("nnmd", "nph"), units="")
+            if self.saveq:
+                C.Write2NetCDFFile(f, self.qs, "qs", ("nnmd", "nph"), units="")
+        if self.savep:
+            C.Write2NetCDFFile(f, self.power, "power", ("nnmd", "two"), units="")
+            if self.atomlist is not None:
+                C.Write2NetCDFFile(f, self.poweratomlist, "poweratomlist", ("atomlist", "nnmd", "two"), units="")
+        e = np.asarray(self.etot)
+        C.Write2NetCDFFile(f, e.T if multi else e, "energy", ("nnmd",) + tr, units="")
+        C.Write2NetCDFFile(f, self.p, "p", tr + ("nph",), units="")
+        C.Write2NetCDFFile(f, self.q, "q", tr + ("nph",), units="")
+        C.Write2NetCDFFile(f, [self.t], "t", ("one",), units="")
+        C.Write2NetCDFFile(f, [ipie], "ipie", ("one",), units="")
+        C.Write2NetCDFFile(f, self.phis, "phis", tr + ("mem", "nph"), units="")
+        C.Write2NetCDFFile(f, self.qhis, "qhis", tr + ("mem", "nph"), units="")
+        C.commit(f, tmp, self._ncname(id))
+
+    def _resume(self, j):
+        """The reference's per-run file logic (md.py:506-567).  Returns the last finished piece
+        (-1 for a new run) or None when run j is already complete."""
+        from .checkpoint import ReadNetCDFVar
+
+        fn, fnm = self._ncname(j), self._ncname(j - 1)
+        if os.path.isfile(fn):
+            self._log("find file: " + fn)
+            ipie = int(ReadNetCDFVar(fn, "ipie")[0])
+            if ipie + 1 < self.npie:
+                self._log("unfinished run: reading resume information")
+                if not (self.saveall and self.saveq and self.savep):
+                    raise RuntimeError("md.Run: saveall, savep and saveq must be set to continue an "
+                                       "unfinished run (the reference exits here, md.py:531-533)")
+                self.p = ReadNetCDFVar(fn, "p")
+                self.q = ReadNetCDFVar(fn, "q")
+                self.t = int(ReadNetCDFVar(fn, "t")[0])
+                self._load_phis(ReadNetCDFVar(fn, "phis"))
+                self.power = ReadNetCDFVar(fn, "power")
+                if self.atomlist is not None:
+                    self.poweratomlist = ReadNetCDFVar(fn, "poweratomlist")
+                self.qs = ReadNetCDFVar(fn, "qs")
+                self.ps = ReadNetCDFVar(fn, "ps")
+                for i, b in enumerate(self.baths):
+                    nz = ReadNetCDFVar(fn, "noise" + str(i))
+                    b.noise = np.transpose(nz, (1, 0, 2)) if nz.ndim == 3 else nz
+                return ipie
+            if ipie + 1 == self.npie:
+                self._log("finished run")
+                if self.savep:
+                    self.power = ReadNetCDFVar(fn, "power")
+                    if self.atomlist is not None:
+                        self.poweratomlist = ReadNetCDFVar(fn, "poweratomlist")
+                self.t = int(ReadNetCDFVar(fn, "t")[0])
+                return None
+            raise RuntimeError("md.Run: ipie error in %s (ipie = %d)" % (fn, ipie))
+        if os.path.isfile(fnm):
+            self._log("reading history from previous run")
+            self.p = ReadNetCDFVar(fnm, "p")
+            self.q = ReadNetCDFVar(fnm, "q")
+            self.t = int(ReadNetCDFVar(fnm, "t")[0])
+            ph = ReadNetCDFVar(fnm, "phis")
+            if ph.shape[-2:] == (self.ml, self.nph):
+                self._load_phis(ph)
+        elif j != 0:
+            raise RuntimeError("md.Run: no previous nc file exists (%s)" % fnm)
+        for i in range(len(self.baths)):
+            self.gen_noise(i, j)
+        self.ResetSavepq()
+        return -1
+
     def Run(self):
         """Independent runs nstart..nstop-1 (md.py:493-682): fresh noise per run, state and history
-        carried over, per-run time-averaged heat current written to kappa.{T}.bath{i}.run{j}.dat.
-        NetCDF checkpoint/resume (md.dump, md.py:684-764) is not implemented: runs always start
-        fresh."""
+        carried over, per-run time-averaged heat current written to kappa.{T}.bath{i}.run{j}.dat,
+        MD{j}.nc written after every piece and read back to resume an unfinished run or to continue
+        from the previous run (md.py:506-567)."""
         self.initialise()
         self.ResetHis()
         self.info()
         self._ensure_device()
         for j in range(self.nstart, self.nstop):
             self._log("\nMD run: " + str(j))
-            for i in range(len(self.baths)):
-                self.gen_noise(i, j)
-            self.ResetSavepq()
+            ipie = self._resume(j)
+            if ipie is None:
+                continue
             traj = None
             if self.nstep is not None and self._is_root():
                 traj = open("trajectories." + str(self.T) + ".run" + str(j) + ".ani", "w")
-            for _ in range(self.npie):
+            piece = ipie
+            for piece in range(ipie + 1, self.npie):
                 nsteps = int(self.nmd / self.npie)
                 if self.nstep is None:
                     self.steps(nsteps)
@@ -535,6 +676,7 @@ class md:
                         tt = self.t - 1
                         if traj is not None and (tt == 0 or tt % self.nstep == 0):
                             self._write_frame(traj, tt)
+                self.dump(piece, j)
             if traj is not None:
                 traj.close()
             if self.cf:
@@ -542,6 +684,7 @@ class md:
                 self.cflist = []
             if self.savep:
                 self._power(j)
+            self.dump(piece, j)
             cur = self._st.get_current()                      # (nbath, ntraj, nmd)
             sums = self._reduce(self._st.current_sums())      # (nbath, 3) over all ranks
             kap = sums[:, 0] / sums[:, 2] * U.curcof
@@ -554,6 +697,9 @@ class md:
                         fk.write("%i %f    %f \n" % (j, self.T, kap[ii]))
                 if self.saveq:
                     self._avestructure(j)
+                if self.rmnc and os.path.exists(self._ncname(j - 1)):  # md.py:676-679
+                    self._log("Remove " + self._ncname(j - 1))
+                    os.remove(self._ncname(j - 1))
 
     def _write_frame(self, fh, tt):
         q = self.q if self.ntraj == 1 else self.q[0]

@@ -1,0 +1,127 @@
+"""GPU tests of md.Run's MD{j}.nc checkpoints (md.dump, md.py:684-764) and resume logic
+(md.py:506-567): continuing from the previous run's file and resuming an unfinished run reproduce
+the uninterrupted run.
+
+Tolerance 1e-10 relative (a resumed run re-derives the memory sum from the stored history with the
+priming contraction instead of the ladder blocks: rounding only)."""
+import os
+import shutil
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
+
+
+def _md(nstart, nstop, npie=2, save=True):
+    from sclmd_amd import md as MD
+    from sclmd_amd import synthetic
+
+    dyn, axyz, baths, meta = synthetic.junction("C3", seed=5, natom=10, ml=16, nmd=64, nw=60)
+    m = MD.md(meta["dt"], meta["nmd"], meta["T"], axyz=axyz, dyn=dyn, nstart=nstart, nstop=nstop,
+              npie=npie, seed=11, noise_mode="device", verbose=False)
+    for b in baths:
+        m.AddBath(b)
+    m.AddConstr([range(0, 3)])
+    if save:
+        m.CalPowerSpec()
+        m.CalAveStruct()
+        m.SaveAll()
+    return m
+
+
+def _final(m):
+    return np.array(m.p), np.array(m.q), int(m.t), np.array(m.kappa_runs)
+
+
+@pytest.fixture
+def uninterrupted(tmp_path_factory):
+    d = tmp_path_factory.mktemp("full")
+    cwd = os.getcwd()
+    os.chdir(d)
+    try:
+        m = _md(0, 2)
+        m.Run()
+        res = _final(m)
+        m.close()
+    finally:
+        os.chdir(cwd)
+    return d, res
+
+
+def test_dump_files(uninterrupted):
+    from sclmd_amd.checkpoint import ReadNetCDFVar, has_var
+
+    d, (p, q, t, kap) = uninterrupted
+    fn = str(d / "MD1.nc")
+    for v in ("energy", "p", "q", "t", "ipie", "phis", "qhis", "power", "noise0", "noise1", "ps", "qs"):
+        assert has_var(fn, v), v
+    assert int(ReadNetCDFVar(fn, "ipie")[0]) == 1 and int(ReadNetCDFVar(fn, "t")[0]) == t == 128
+    assert rel(ReadNetCDFVar(fn, "p"), p) == 0.0 and rel(ReadNetCDFVar(fn, "q"), q) == 0.0
+    assert ReadNetCDFVar(fn, "phis").shape == (16, 30) and ReadNetCDFVar(fn, "noise0").shape == (64, 9)
+
+
+def test_continue_from_previous_run(uninterrupted, tmp_path, monkeypatch):
+    d, (p, q, t, kap) = uninterrupted
+    shutil.copy(d / "MD0.nc", tmp_path / "MD0.nc")
+    monkeypatch.chdir(tmp_path)
+    m = _md(1, 2)
+    m.Run()
+    p2, q2, t2, kap2 = _final(m)
+    m.close()
+    assert t2 == t
+    assert rel(q2, q) < 1e-10 and rel(p2, p) < 1e-10
+    assert rel(kap2[-1], kap[-1]) < 1e-9
+
+
+def test_resume_unfinished_run(uninterrupted, tmp_path, monkeypatch):
+    from sclmd_amd import md as MD
+
+    d, (p, q, t, kap) = uninterrupted
+    monkeypatch.chdir(tmp_path)
+    # interrupted process: run 0 complete, run 1 stops after its first piece (ipie = 0 on disk)
+    real_dump = MD.md.dump
+
+    class Stop(Exception):
+        pass
+
+    def dump_then_stop(self, ipie, id):
+        real_dump(self, ipie, id)
+        if id == 1 and ipie == 0:
+            raise Stop()
+
+    monkeypatch.setattr(MD.md, "dump", dump_then_stop)
+    m = _md(0, 2)
+    with pytest.raises(Stop):
+        m.Run()
+    m.close()
+    monkeypatch.setattr(MD.md, "dump", real_dump)
+    from sclmd_amd.checkpoint import ReadNetCDFVar
+
+    assert int(ReadNetCDFVar("MD1.nc", "ipie")[0]) == 0
+    # new process: run 0 is found finished, run 1 resumes at its second piece
+    m = _md(0, 2)
+    m.Run()
+    p2, q2, t2, _ = _final(m)
+    m.close()
+    assert t2 == t
+    assert rel(q2, q) < 1e-10 and rel(p2, p) < 1e-10
+
+
+def test_unfinished_run_needs_saveall(uninterrupted, tmp_path, monkeypatch):
+    from sclmd_amd.checkpoint import ReadNetCDFVar  # noqa: F401
+
+    d, _ = uninterrupted
+    monkeypatch.chdir(tmp_path)
+    m = _md(0, 1, save=False)
+    m.Run()                       # writes MD0.nc with ipie = 1 (finished, npie = 2)
+    m.close()
+    m = _md(0, 1, npie=4, save=False)   # same file read as unfinished (ipie + 1 < npie)
+    with pytest.raises(RuntimeError, match="saveall"):
+        m.Run()
+    m.close()

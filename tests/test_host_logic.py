@@ -163,3 +163,27 @@ def test_synthetic_junction_shapes():
     assert np.allclose(dyn, dyn.T) and np.linalg.eigvalsh(dyn).min() > 0
     dyn, axyz, baths, meta = synthetic.junction("C5", ml=8, nmd=32, natom=30, nw=50)
     assert len(baths) == 3 and baths[2].kind == "ebath" and baths[2].biased()
+
+
+def test_checkpoint_netcdf_roundtrip(tmp_path):
+    """MD{j}.nc helpers (md.py:768-783): record (unlimited) and fixed dimensions, float64 exact,
+    atomic replace."""
+    from sclmd_amd import checkpoint as C
+
+    fn = str(tmp_path / "MD0.nc")
+    rng = np.random.default_rng(0)
+    ps, phis = rng.normal(size=(8, 5)), rng.normal(size=(3, 5))
+    f, tmp = C.open_for_write(fn)
+    f.createDimension("nnmd", None)
+    f.createDimension("nph", 5)
+    f.createDimension("one", 1)
+    f.createDimension("mem", 3)
+    C.Write2NetCDFFile(f, ps, "ps", ("nnmd", "nph"), units="")
+    C.Write2NetCDFFile(f, phis, "phis", ("mem", "nph"), units="")
+    C.Write2NetCDFFile(f, [42], "t", ("one",), units="")
+    assert not os.path.exists(fn)
+    C.commit(f, tmp, fn)
+    assert os.path.exists(fn) and not os.path.exists(tmp)
+    assert np.array_equal(C.ReadNetCDFVar(fn, "ps"), ps)
+    assert np.array_equal(C.ReadNetCDFVar(fn, "phis"), phis)
+    assert C.ReadNetCDFVar(fn, "t")[0] == 42 and C.has_var(fn, "ps") and not C.has_var(fn, "qs")
