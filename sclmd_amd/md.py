@@ -537,6 +537,7 @@ class md:
 
     def _load_phis(self, phis):
         st = self._ensure_device()
+        self._push_state()  # history slots are relative to the device's t: set p, q, t first
         ph = np.asarray(phis, dtype=float)
         if ph.ndim == 2:
             ph = np.broadcast_to(ph, (self.ntraj,) + ph.shape)
