@@ -118,6 +118,7 @@ struct Level {
   // spectral: [segment transform] [cgemm item chunk]... [inverse transform + event]
   int ncg_chunk = 1;
   int npiece = 1;
+  int64_t ev_seq[2] = {0, 0};      // enqueue order of ev[] (merged main-stream waits)
   int64_t pend_block = INT64_MIN;  // block whose pieces are still being issued
   int64_t pend_t0 = 0;
   int next_piece = 0;
@@ -151,6 +152,9 @@ struct gle_handle {
   double* d_zero = nullptr;            // zero row (chain S(t+1) tiles' unused level slots)
   bool dbg_no_ladder = false;  // GLE_DBG_NO_LADDER: skip the ladder blocks (timing experiments only)
   int bg_grid = 0;             // GLE_BG_GRID: cap of the far-field GEMM grid (grid-stride over items)
+  int piece_slack = 1;         // GLE_PIECE_SLACK: boundaries left between a block's last piece and its use
+  bool merge_waits = true;     // GLE_MERGE_WAITS=0: one main-stream wait per level
+  int64_t ev_seq_counter = 0;
   int dbg_skip = 0;            // GLE_DBG_SKIP bits (timing experiments only, wrong results):
                                // 1 cgemm, 2 seg_fft, 4 far_ifft, 8 direct level ops
   int dbg_ntile = 0;
@@ -1386,7 +1390,10 @@ int launch_level_pieces(gle_handle* h, Level& lv, int64_t k, hipStream_t s, bool
       }
     }
   }
-  if (j1 >= lv.npiece) HIPCHK(h, hipEventRecord(lv.ev[par], s));
+  if (j1 >= lv.npiece) {
+    HIPCHK(h, hipEventRecord(lv.ev[par], s));
+    lv.ev_seq[par] = ++h->ev_seq_counter;
+  }
   return GLE_OK;
 }
 
@@ -1444,6 +1451,8 @@ int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
   // The block's pieces are issued over the first-level boundaries T, T+P0, ..., T+P-P0 (levels in
   // increasing P, so each boundary's small-level block is queued before the big levels' pieces).
   bool bg_waited[gle_handle::NBG] = {};
+  hipEvent_t wait_ev[gle_handle::NBG] = {};
+  int64_t wait_seq[gle_handle::NBG] = {};
   if (!h->dbg_no_ladder && t % h->P0 == 0) {
     for (auto& lv : h->levels) {
       hipStream_t bs = h->bg[lv.sidx];
@@ -1464,7 +1473,9 @@ int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
         lv.bg_block[(k + 1) & 1] = k + 1;
       }
       if (lv.pend_block != INT64_MIN) {
-        const int nslot = std::max(1, lv.P / h->P0);
+        // the pieces go out over the first nslot - slack boundaries: the last one then has at least
+        // `slack` first-level blocks of time to drain before the main stream needs the block
+        const int nslot = std::max(1, lv.P / h->P0 - h->piece_slack);
         const int slot = (int)((t - lv.pend_t0) / h->P0);
         const int j1 = slot + 1 >= nslot ? lv.npiece : (int)(((int64_t)(slot + 1) * lv.npiece + nslot - 1) / nslot);
         if (j1 > lv.next_piece) {
@@ -1475,10 +1486,21 @@ int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
         if (lv.next_piece >= lv.npiece) lv.pend_block = INT64_MIN;
       }
       if (t % lv.P == 0 && lv.bg_block[k & 1] == k) {
-        HIPCHK(h, hipStreamWaitEvent(h->stream, lv.ev[k & 1], 0));
+        // per background stream, waiting for the block enqueued last implies the earlier ones
+        // (in-order streams): one barrier packet per stream instead of one per level
+        if (h->merge_waits) {
+          if (!wait_ev[lv.sidx] || lv.ev_seq[k & 1] > wait_seq[lv.sidx]) {
+            wait_ev[lv.sidx] = lv.ev[k & 1];
+            wait_seq[lv.sidx] = lv.ev_seq[k & 1];
+          }
+        } else {
+          HIPCHK(h, hipStreamWaitEvent(h->stream, lv.ev[k & 1], 0));
+        }
         lv.bg_block[k & 1] = INT64_MIN;
       }
     }
+    for (int i = 0; i < gle_handle::NBG; ++i)
+      if (wait_ev[i]) HIPCHK(h, hipStreamWaitEvent(h->stream, wait_ev[i], 0));
   }
   const bool need_pot = (fpot_host_T == nullptr) && !h->pot_cache_exact;
   const StepArgs ta = step_args(h);
@@ -1577,6 +1599,8 @@ int gle_create(const gle_config* cfg, gle_handle** out) {
   h->dbg_no_ladder = getenv("GLE_DBG_NO_LADDER") != nullptr;
   if (const char* e = getenv("GLE_DBG_SKIP")) h->dbg_skip = atoi(e);
   if (const char* e = getenv("GLE_BG_GRID")) h->bg_grid = std::max(0, atoi(e));
+  if (const char* e = getenv("GLE_PIECE_SLACK")) h->piece_slack = std::max(0, atoi(e));
+  if (const char* e = getenv("GLE_MERGE_WAITS")) h->merge_waits = atoi(e) != 0;
   // main stream (the latency-bound per-step chain) at the highest priority, background streams
   // (ladder blocks) at the lowest
   {
