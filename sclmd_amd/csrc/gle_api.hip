@@ -109,6 +109,7 @@ struct Level {
   std::vector<CgItem> cg;      // spectral: the batched GEMM of the per-frequency products
   CgItem* d_cg = nullptr;
   int cg_rn = 4;
+  int cg_split = 1;            // split-K halves per product (small levels: 2 workgroups per CU)
   double cg_flops = 0, cg_bytes = 0;  // algorithmic, per block
   hipEvent_t ev[2] = {nullptr, nullptr};
   int64_t last_block = INT64_MIN;
@@ -1088,6 +1089,25 @@ int freeze(gle_handle* h) {
   }
   for (auto& lv : h->levels) {
     lv.cstride = lv.spectral ? Pspec / lv.P : 1;
+    lv.cg_rn = (int)std::min<int64_t>(4, (B + 15) / 16);
+    lv.cg_split = 1;
+    if (lv.spectral) {
+      // small levels: split the k range of every product in two (partial planes added by the
+      // inverse transform) so the launch has >= 2 workgroups per CU to hide the HBM latency of the
+      // K̂ stream, which is still read once (GLE_CG_NARROW: 32-column tiles instead, reading it
+      // once per 32 columns)
+      int64_t n4 = 0;
+      for (auto& b : h->baths)
+        if (b.ml > lv.lag0)
+          n4 += (int64_t)(lv.P + 1) * 3 * ((b.nrt + 3) / 4) * ((B + 16 * lv.cg_rn - 1) / (16 * lv.cg_rn));
+      int ncu = 256;
+      hipDeviceProp_t prop;
+      if (hipGetDeviceProperties(&prop, h->cfg.device) == hipSuccess) ncu = prop.multiProcessorCount;
+      if (n4 < 2 * ncu) {
+        if (getenv("GLE_CG_NARROW")) lv.cg_rn = 2;
+        else lv.cg_split = 2;
+      }
+    }
     lv.lb.assign(h->baths.size(), LevelBath{});
     for (size_t j = 0; j < h->baths.size(); ++j) {
       Bath& b = h->baths[j];
@@ -1106,7 +1126,7 @@ int freeze(gle_handle* h) {
       L.yfstride = (int64_t)3 * b.nc * B;                       // T_0, T_1, T_2
       rc = dalloc_n(h, &L.d_khat, (size_t)(lv.P + 1) * L.khat_fstride);
       if (!rc) rc = dalloc_n(h, &L.d_seg, (size_t)(lv.P + 1) * L.seg_fstride + 4096);
-      if (!rc) rc = dalloc_n(h, &L.d_Yspec, (size_t)(lv.P + 1) * L.yfstride + 4096);
+      if (!rc) rc = dalloc_n(h, &L.d_Yspec, (size_t)lv.cg_split * (lv.P + 1) * L.yfstride + 4096);
       if (rc) return rc;
       launch_khat_pack(b.d_K, b.ml, b.nks, L.d_khat, lv.P, 2, L.M, b.nc, b.nrt, b.nks, h->d_cstab,
                        lv.cstride, h->stream);
@@ -1176,20 +1196,7 @@ int freeze(gle_handle* h) {
     if (lv.spectral) {
       // one workgroup per (bath, f, Gauss part g, 64-row group, 16 RN-column tile); items of one
       // (f, g) are adjacent, so the row groups that share an X window run together
-      lv.cg.clear();
-      lv.cg_rn = (int)std::min<int64_t>(4, (B + 15) / 16);
-      {
-        // small levels: narrower column tiles (A read once per 32 instead of 64 columns) so the
-        // launch has at least two workgroups per CU to hide the HBM latency of the A stream
-        int64_t n4 = 0;
-        for (size_t j = 0; j < h->baths.size(); ++j)
-          if (lv.lb[j].active)
-            n4 += (int64_t)(lv.P + 1) * 3 * ((h->baths[j].nrt + 3) / 4) * ((B + 16 * lv.cg_rn - 1) / (16 * lv.cg_rn));
-        int ncu = 256;
-        hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, h->cfg.device) == hipSuccess) ncu = prop.multiProcessorCount;
-        if (lv.cg_rn == 4 && n4 < 2 * ncu) lv.cg_rn = 2;
-      }
+      lv.cg.clear();  // cg_rn / cg_split were chosen with the level's buffers
       lv.cg_flops = lv.cg_bytes = 0;
       const int NT = 16 * lv.cg_rn;
       for (size_t j = 0; j < h->baths.size(); ++j) {
@@ -1201,11 +1208,16 @@ int freeze(gle_handle* h) {
         for (int f = 0; f <= lv.P; ++f)
           for (int g = 0; g < 3; ++g) {
             for (int rg = 0; 4 * rg < b.nrt; ++rg)
-              for (int c0 = 0; c0 < B; c0 += NT) {
+              for (int c0 = 0; c0 < B; c0 += NT)
+                for (int hk = 0; hk < lv.cg_split; ++hk) {
                 CgItem it{};
+                const int S = L.M * b.nks;
+                it.s0 = S * hk / lv.cg_split;
+                it.ns = S * (hk + 1) / lv.cg_split - it.s0;
                 it.A = L.d_khat + (int64_t)f * L.khat_fstride + g * plane + (int64_t)4 * rg * a_rt;
                 it.X = L.d_seg + (int64_t)f * L.seg_fstride + (int64_t)g * b.ncp * L.ldseg;
-                it.out = L.d_Yspec + (int64_t)f * L.yfstride + (int64_t)g * b.nc * B + (int64_t)64 * rg * B + c0;
+                it.out = L.d_Yspec + (int64_t)hk * (lv.P + 1) * L.yfstride + (int64_t)f * L.yfstride +
+                         (int64_t)g * b.nc * B + (int64_t)64 * rg * B + c0;
                 it.a_rt = a_rt;
                 it.ldx = (int32_t)L.ldseg;
                 it.cs = (int32_t)B;
@@ -1384,7 +1396,8 @@ int launch_level_pieces(gle_handle* h, Level& lv, int64_t k, hipStream_t s, bool
         Bath& bb = h->baths[b];
         LevelBath& L = lv.lb[b];
         if (!L.active || (!priming && (h->dbg_skip & 4))) continue;
-        if (launch_far_ifft(L.d_Yspec, L.yfstride, bb.nc, (int)h->B, lv.P, L.d_out + (int64_t)par * lv.P * h->B,
+        if (launch_far_ifft(L.d_Yspec, L.yfstride, lv.cg_split > 1 ? (int64_t)(lv.P + 1) * L.yfstride : 0, bb.nc,
+                            (int)h->B, lv.P, L.d_out + (int64_t)par * lv.P * h->B,
                             (int64_t)2 * lv.P * h->B, h->d_cstab, lv.cstride, s))
           return fail(h, GLE_ERR_UNSUP, "inverse transform launch failed (P = " + std::to_string(lv.P) + ")");
       }

@@ -64,6 +64,7 @@ struct CgItem {
   int32_t nrt;       // row tiles present (<= 4)
   int32_t nrows, ncols;  // valid rows (<= 64), columns
   int32_t ldo, col0;
+  int32_t s0, ns;    // k-step range [s0, s0 + ns) of this item (split-K halves write separate planes)
 };
 
 // Deterministic fixed-order sum of split partial tiles (+ optional far-field addend).
@@ -228,7 +229,7 @@ void launch_khat_pack(const double* Kf, int ml, int nks_k, double* khat, int P, 
 int launch_seg_fft(const double* H, int64_t ldh, int R, int B, int nc, int ncp, int P, int64_t T,
                    int nseg, double* seg, int64_t seg_fstride, int64_t ldseg, int Rseg,
                    const double* cstab, int cstride, hipStream_t s);
-int launch_far_ifft(const double* Y, int64_t yfstride, int nc, int B, int P, double* out,
+int launch_far_ifft(const double* Y, int64_t yfstride, int64_t ysplit, int nc, int B, int P, double* out,
                     int64_t ldout, const double* cstab, int cstride, hipStream_t s);
 int launch_fft_noise(const double* a, double* noise, const double* tw, int64_t nmd, int64_t nc,
                      int64_t arows, int64_t B, int is_complex, double scale, hipStream_t s);

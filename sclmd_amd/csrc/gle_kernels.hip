@@ -710,12 +710,12 @@ __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, doubl
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
   const int brow = lane >> 4, bcol = lane & 15;
-  const int S = it.M * it.nks;
+  const int S = it.ns;  // k-steps of this item: [it.s0, it.s0 + S) of the M nks of T_g(f)
   const int nch = (S + CG_KC - 1) / CG_KC;
   const bool active = wave < it.nrt;
   // global address space: flat loads would also count on lgkmcnt, and every LDS-read wait before an
   // MFMA would then drain the HBM prefetches in flight
-  gdbl* Aw = (gdbl*)(it.A + (int64_t)(active ? wave : 0) * it.a_rt + lane);
+  gdbl* Aw = (gdbl*)(it.A + (int64_t)(active ? wave : 0) * it.a_rt + (int64_t)it.s0 * 64 + lane);
   const int xr = tid / TPR, xc = (tid % TPR) * XPT;
   const int tbase = (int)pmod(tseg, it.Rseg);  // ring slot of segment tseg (32-bit from here on)
   // Prefetch depth: A fragments (HBM, the streamed operand) 2 chunks ahead of the MFMAs; X
@@ -730,7 +730,7 @@ __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, doubl
 #define CG_LOAD_X(c, XV)                                                                              \
   do {                                                                                                \
     const int s0_ = (c) * CG_KC + (xr >> 2);                                                          \
-    const int sc_ = s0_ < S ? s0_ : S - 1;                                                            \
+    const int sc_ = it.s0 + (s0_ < S ? s0_ : S - 1);                                                  \
     const int i_ = (int)((unsigned)sc_ / (unsigned)it.nks), ks_ = sc_ - i_ * it.nks;                  \
     int slot_ = tbase - i_;                                                                           \
     slot_ += slot_ < 0 ? it.Rseg : 0; /* i < M < Rseg */                                              \
@@ -948,7 +948,7 @@ int launch_seg_fft(const double* H, int64_t ldh, int R, int B, int nc, int ncp, 
 // Grid: DOF k x 8-trajectory chunk; two real outputs per complex inverse FFT.
 template <int BC>
 __global__ __launch_bounds__(256) void far_ifft_kernel(const double* __restrict__ Y, int64_t yfstride,
-                                                       int nc, int B, int P, int logn,
+                                                       int64_t ysplit, int nc, int B, int P, int logn,
                                                        double* __restrict__ out, int64_t ldout,
                                                        const double2* __restrict__ cstab, int cstride) {
   extern __shared__ double2 fbuf[];  // BC/2 series of N points, then N/2 twiddles
@@ -969,15 +969,17 @@ __global__ __launch_bounds__(256) void far_ifft_kernel(const double* __restrict_
     const double* yf = Y + (int64_t)fs * yfstride + (int64_t)k * B;
     // Re Y = T_0 - T_1, Im Y = T_0 + T_2 (Gauss products, planes [f][g][nc][B])
     double ar = 0.0, ai = 0.0, br = 0.0, bi = 0.0;
+    // split-K levels: the two k-halves of every product, added in fixed order (deterministic)
+    auto tg = [&](int g, int b) { return ysplit ? yf[g * pl + b] + yf[ysplit + g * pl + b] : yf[g * pl + b]; };
     if (ba < B) {
-      const double t0 = yf[ba];
-      ar = t0 - yf[pl + ba];
-      ai = realonly ? 0.0 : t0 + yf[2 * pl + ba];
+      const double t0 = tg(0, ba);
+      ar = t0 - tg(1, ba);
+      ai = realonly ? 0.0 : t0 + tg(2, ba);
     }
     if (bb < B) {
-      const double t0 = yf[bb];
-      br = t0 - yf[pl + bb];
-      bi = realonly ? 0.0 : t0 + yf[2 * pl + bb];
+      const double t0 = tg(0, bb);
+      br = t0 - tg(1, bb);
+      bi = realonly ? 0.0 : t0 + tg(2, bb);
     }
     if (cj) {
       ai = -ai;
@@ -1001,29 +1003,29 @@ __global__ __launch_bounds__(256) void far_ifft_kernel(const double* __restrict_
 }
 
 template <int BC>
-static int far_ifft_launch(const double* Y, int64_t yfstride, int nc, int B, int P, int logn, double* out,
-                           int64_t ldout, const double* cstab, int cstride, hipStream_t s) {
+static int far_ifft_launch(const double* Y, int64_t yfstride, int64_t ysplit, int nc, int B, int P, int logn,
+                           double* out, int64_t ldout, const double* cstab, int cstride, hipStream_t s) {
   const size_t shmem = ((size_t)(BC / 2) * 2 * P + P) * sizeof(double2);
   if (shmem > 160 * 1024) return -2;
   // raise the dynamic-LDS limit once per instantiation (a per-launch attribute call costs host
   // time on the step's critical path at block boundaries)
   if (!lds_attr_once((const void*)far_ifft_kernel<BC>)) return -3;
   const int nbc = (B + BC - 1) / BC;
-  far_ifft_kernel<BC><<<(unsigned)(nc * nbc), 256, shmem, s>>>(Y, yfstride, nc, B, P, logn, out, ldout,
+  far_ifft_kernel<BC><<<(unsigned)(nc * nbc), 256, shmem, s>>>(Y, yfstride, ysplit, nc, B, P, logn, out, ldout,
                                                               (const double2*)cstab, cstride);
   return 0;
 }
 
-int launch_far_ifft(const double* Y, int64_t yfstride, int nc, int B, int P, double* out,
+int launch_far_ifft(const double* Y, int64_t yfstride, int64_t ysplit, int nc, int B, int P, double* out,
                     int64_t ldout, const double* cstab, int cstride, hipStream_t s) {
   int logn = 0;
   while ((1 << logn) < 2 * P) ++logn;
   if ((1 << logn) != 2 * P) return -1;
   switch (fft_bc(B, P)) {
-    case 64: return far_ifft_launch<64>(Y, yfstride, nc, B, P, logn, out, ldout, cstab, cstride, s);
-    case 32: return far_ifft_launch<32>(Y, yfstride, nc, B, P, logn, out, ldout, cstab, cstride, s);
-    case 16: return far_ifft_launch<16>(Y, yfstride, nc, B, P, logn, out, ldout, cstab, cstride, s);
-    default: return far_ifft_launch<8>(Y, yfstride, nc, B, P, logn, out, ldout, cstab, cstride, s);
+    case 64: return far_ifft_launch<64>(Y, yfstride, ysplit, nc, B, P, logn, out, ldout, cstab, cstride, s);
+    case 32: return far_ifft_launch<32>(Y, yfstride, ysplit, nc, B, P, logn, out, ldout, cstab, cstride, s);
+    case 16: return far_ifft_launch<16>(Y, yfstride, ysplit, nc, B, P, logn, out, ldout, cstab, cstride, s);
+    default: return far_ifft_launch<8>(Y, yfstride, ysplit, nc, B, P, logn, out, ldout, cstab, cstride, s);
   }
 }
 
