@@ -91,6 +91,11 @@ def main():
                          "and filtered on the device); white: seeded N(0, 1e-3^2) realisations assigned "
                          "to bath.noise (throughput runs of configurations whose noise factors do not "
                          "fit next to the spectral kernels, e.g. C5; the step does the same work)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
+                         "rehearse the multi-rank path, e.g. with --same-device on a one-GPU box)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="every rank on device 0 (rehearsal of the N > 1 control flow on one GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
@@ -106,8 +111,10 @@ def main():
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if args.same_device:
+            local_rank = 0
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        dist.init_process_group(args.dist_backend)
 
     from sclmd_amd import md as MD
     from sclmd_amd import synthetic
@@ -160,7 +167,7 @@ def main():
     if dist is not None:
         import torch
 
-        tt = torch.tensor([el], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([el], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
 
