@@ -65,9 +65,15 @@ struct Bath {
   double* d_Kn = nullptr;  // compact fragment copy of the per-step slices [0, nn): [rt][ks][i][64]
   int nn = 1;
   double* d_Kq = nullptr;
+  // fused B+C stage: bath-local Fc copy, V = n1 - c S1, packed K0^2, K0 Kq and K0 P dyn (runs per
+  // DOF tile)
+  double *d_Xf = nullptr, *d_V = nullptr, *d_K0sqd = nullptr, *d_KKqd = nullptr, *d_KDd = nullptr;
+  std::vector<std::vector<std::pair<int, int>>> kd_rng;
+  std::vector<int64_t> kd_tofs;
   // K0 / Kq rows in DOF order for the chain's DOF tiles: tile rt at [tofs[rt]][ks][64]
   double *d_K0d = nullptr, *d_Kqd = nullptr;
   std::vector<int64_t> tofs;
+  int64_t tofs_n = 0;
   int32_t* d_inv = nullptr;
   double *d_noise = nullptr, *d_S = nullptr, *d_Yq = nullptr;
   double *d_Xcur = nullptr, *d_Xq = nullptr, *d_H = nullptr, *d_cur = nullptr;
@@ -169,6 +175,8 @@ struct gle_handle {
   bool host_force_step = false;
   Op op_prime;
   Chain chA[2], chB[2], chC, chNear;  // [with dyn.q]; chNear: all near-field partial tiles (priming)
+  Chain chBC;                          // stages B + C fused (harmonic force, disjoint baths)
+  bool fuse_bc = false;
   int ch_nw[3] = {4, 8, 4};            // chain workgroup waves per stage
   int ch_drn = 1;                      // DOF-tile 16-column MFMA tiles
   int P0 = 1;          // first level block; near field = lags [1, 2 P0)
@@ -678,7 +686,21 @@ int plan_chain(gle_handle* h) {
   h->ch_drn = drn;
   const int ncol1 = (int)((B + 16 * drn - 1) / (16 * drn));
   // K0 / Kq rows in DOF order: DOF tile rt of bath j at tofs[rt], [ks][64] fragments
+  auto pack_dof_b = [&](const Bath& b, const std::vector<double>& M) {
+    std::vector<double> f((size_t)b.tofs_n, 0.0);
+    for (int rt = 0; rt < ntile; ++rt) {
+      if (b.tofs[rt] < 0) continue;
+      for (int ks = 0; ks < b.nks; ++ks)
+        for (int l = 0; l < 64; ++l) {
+          const int64_t d = 16 * rt + (l & 15), kc = 4 * ks + (l >> 4);
+          if (d >= h->nph || kc >= b.nc || b.inv[d] < 0) continue;
+          f[(size_t)(b.tofs[rt] + ks * 64 + l)] = M[(size_t)b.inv[d] * b.nc + kc];
+        }
+    }
+    return f;
+  };
   for (auto& b : h->baths) {
+    auto pack_dof = [&](const std::vector<double>& M) { return pack_dof_b(b, M); };
     b.tofs.assign(ntile, -1);
     int64_t n = 0;
     for (int rt = 0; rt < ntile; ++rt) {
@@ -689,19 +711,7 @@ int plan_chain(gle_handle* h) {
         n += (int64_t)b.nks * 64;
       }
     }
-    auto pack_dof = [&](const std::vector<double>& M) {
-      std::vector<double> f((size_t)n, 0.0);
-      for (int rt = 0; rt < ntile; ++rt) {
-        if (b.tofs[rt] < 0) continue;
-        for (int ks = 0; ks < b.nks; ++ks)
-          for (int l = 0; l < 64; ++l) {
-            const int64_t d = 16 * rt + (l & 15), kc = 4 * ks + (l >> 4);
-            if (d >= h->nph || kc >= b.nc || b.inv[d] < 0) continue;
-            f[(size_t)(b.tofs[rt] + ks * 64 + l)] = M[(size_t)b.inv[d] * b.nc + kc];
-          }
-      }
-      return f;
-    };
+    b.tofs_n = n;
     std::vector<double> f = pack_dof(b.K0);
     int rc = dalloc_n(h, &b.d_K0d, f.size());
     if (!rc) rc = upload(h, b.d_K0d, f.data(), f.size() * 8);
@@ -762,6 +772,113 @@ int plan_chain(gle_handle* h) {
     if (!rc) rc = upload(h, h->d_dynd, f.data(), f.size() * 8);
     if (rc) return rc;
   }
+  // fused B+C stage (dof_BC in gle_chain.hip): harmonic force and pairwise disjoint baths
+  {
+    bool disjoint = true;
+    std::vector<int> owner(h->nph, -1);
+    for (int j = 0; j < nb && disjoint; ++j)
+      for (int64_t d : h->baths[j].cids) {
+        if (owner[d] >= 0) disjoint = false;
+        owner[d] = j;
+      }
+    const char* e = getenv("GLE_FUSE_BC");
+    h->fuse_bc = h->has_dyn && disjoint && nb > 0 && !(e && atoi(e) == 0);
+  }
+  if (h->fuse_bc) {
+    for (auto& b : h->baths) {
+      const int64_t nc = b.nc, nph = h->nph;
+      int rc = dalloc_n(h, &b.d_Xf, (size_t)b.vs);
+      if (!rc) rc = dalloc_n(h, &b.d_V, (size_t)b.vs);
+      if (rc) return rc;
+      // K0^2 and K0 Kq (nc x nc), K0 P dyn (nc x nph): host fp64, row-streaming triple loops
+      std::vector<double> sq((size_t)nc * nc, 0.0);
+      for (int64_t r = 0; r < nc; ++r)
+        for (int64_t k = 0; k < nc; ++k) {
+          const double a = b.K0[(size_t)(r * nc + k)];
+          if (a == 0.0) continue;
+          const double* src = &b.K0[(size_t)(k * nc)];
+          double* dst = &sq[(size_t)(r * nc)];
+          for (int64_t c2 = 0; c2 < nc; ++c2) dst[c2] += a * src[c2];
+        }
+      std::vector<double> f = pack_dof_b(b, sq);
+      rc = dalloc_n(h, &b.d_K0sqd, f.size());
+      if (!rc) rc = upload(h, b.d_K0sqd, f.data(), f.size() * 8);
+      if (rc) return rc;
+      if (b.has_q) {
+        std::vector<double> kq((size_t)nc * nc, 0.0);
+        for (int64_t r = 0; r < nc; ++r)
+          for (int64_t k = 0; k < nc; ++k) {
+            const double a = b.K0[(size_t)(r * nc + k)];
+            if (a == 0.0) continue;
+            for (int64_t c2 = 0; c2 < nc; ++c2) kq[(size_t)(r * nc + c2)] += a * b.Kq[(size_t)(k * nc + c2)];
+          }
+        f = pack_dof_b(b, kq);
+        rc = dalloc_n(h, &b.d_KKqd, f.size());
+        if (!rc) rc = upload(h, b.d_KKqd, f.data(), f.size() * 8);
+        if (rc) return rc;
+      }
+      std::vector<double> kd((size_t)nc * nph, 0.0);
+      for (int64_t k = 0; k < nc; ++k) {
+        const double* drow = &h->dyn_h[(size_t)(b.cids[k] * nph)];
+        std::vector<int64_t> nzc;
+        for (int64_t c2 = 0; c2 < nph; ++c2)
+          if (drow[c2] != 0.0) nzc.push_back(c2);
+        for (int64_t r = 0; r < nc; ++r) {
+          const double a = b.K0[(size_t)(r * nc + k)];
+          if (a == 0.0) continue;
+          for (int64_t c2 : nzc) kd[(size_t)(r * nph + c2)] += a * drow[c2];
+        }
+      }
+      // DOF-tile fragments of K0 P dyn: per tile at most two runs of nonzero 16x4 blocks
+      const int nksd = (int)(h->nphp / 4);
+      b.kd_rng.assign(ntile, {});
+      b.kd_tofs.assign(ntile, 0);
+      int64_t n = 0;
+      for (int rt = 0; rt < ntile; ++rt) {
+        std::vector<std::pair<int, int>> rg;
+        for (int ks = 0; ks < nksd; ++ks) {
+          bool nz = false;
+          for (int r = 0; r < 16 && !nz; ++r) {
+            const int64_t d = 16 * rt + r;
+            if (d >= nph || b.inv[d] < 0) continue;
+            for (int64_t c2 = 4 * ks; c2 < 4 * ks + 4 && c2 < nph; ++c2) nz |= kd[(size_t)(b.inv[d] * nph + c2)] != 0.0;
+          }
+          if (!nz) continue;
+          if (!rg.empty() && rg.back().first + rg.back().second == ks) ++rg.back().second;
+          else rg.push_back({ks, 1});
+        }
+        while (rg.size() > 2) {
+          size_t bi = 0;
+          int bg = INT32_MAX;
+          for (size_t i = 0; i + 1 < rg.size(); ++i) {
+            const int gap = rg[i + 1].first - (rg[i].first + rg[i].second);
+            if (gap < bg) {
+              bg = gap;
+              bi = i;
+            }
+          }
+          rg[bi].second = rg[bi + 1].first + rg[bi + 1].second - rg[bi].first;
+          rg.erase(rg.begin() + bi + 1);
+        }
+        b.kd_tofs[rt] = n;
+        for (auto& r : rg) n += (int64_t)r.second * 64;
+        b.kd_rng[rt] = rg;
+      }
+      std::vector<double> fk((size_t)std::max<int64_t>(n, 64), 0.0);
+      for (int rt = 0; rt < ntile; ++rt) {
+        int64_t o = b.kd_tofs[rt];
+        for (auto& r : b.kd_rng[rt])
+          for (int ks = r.first; ks < r.first + r.second; ++ks, o += 64)
+            for (int l = 0; l < 64; ++l) {
+              const int64_t d = 16 * rt + (l & 15), c2 = 4 * ks + (l >> 4);
+              if (d < nph && c2 < nph && b.inv[d] >= 0) fk[(size_t)(o + l)] = kd[(size_t)(b.inv[d] * nph + c2)];
+            }
+      }
+      rc = dalloc_n(h, &b.d_KDd, fk.size());
+      if (!rc) rc = upload(h, b.d_KDd, fk.data(), fk.size() * 8);
+      if (rc) return rc;
+    }
+  }
   // zero row for the S(t+1) tiles' unused level slots (read at column offsets up to 2 P B + B)
   {
     int Pt = 1;
@@ -806,6 +923,7 @@ int plan_chain(gle_handle* h) {
     std::vector<Seg> segs;
     std::vector<Seg> qsegs;
     int nu = 0;
+    int ubath[CH_TB] = {-1, -1, -1};
     for (int u = 0; u < CH_TB; ++u) T.tb[u].bath = -1;
     for (int j = 0; j < nb; ++j) {
       Bath& b = h->baths[j];
@@ -842,6 +960,9 @@ int plan_chain(gle_handle* h) {
       cb.bath = j;
       cb.bmask = m;
       cb.boff = affine ? off : CH_INV;
+      cb.Xf = h->fuse_bc ? b.d_Xf : nullptr;
+      cb.V = h->fuse_bc ? b.d_V : nullptr;
+      ubath[u] = j;
       Seg y{u, b.d_K0d + b.tofs[rt], 64, nullptr, (int)B, 0, 0, b.nks, 0};
       if (stage == 0) {
         y.X = b.d_NR;
@@ -851,16 +972,48 @@ int plan_chain(gle_handle* h) {
         y.X = b.d_Xcur + (stage == 2 ? b.vs : 0);
       }
       segs.push_back(y);
-      if (b.has_q && stage < 2)
-        qsegs.push_back(Seg{CH_TB + u, b.d_Kqd + b.tofs[rt], 64, b.d_Xq + (stage == 1 ? b.vs : 0), (int)B, 0, 0, b.nks, 0});
+      if (b.has_q && stage != 2)
+        qsegs.push_back(Seg{CH_TB + u, b.d_Kqd + b.tofs[rt], 64, b.d_Xq + (stage == 0 ? 0 : b.vs), (int)B, 0, 0,
+                            b.nks, 0});
     }
     segs.insert(segs.end(), qsegs.begin(), qsegs.end());
-    if (withD && h->has_dyn && stage < 2) {
+    if (withD && h->has_dyn && stage != 2) {
       int64_t o = h->dyn_tofs[rt];
       for (auto& r : h->dyn_rng[rt]) {
         segs.push_back(Seg{2 * CH_TB, h->d_dynd + o, 64, (stage == 0 ? h->d_Q : h->d_Qt) + (int64_t)4 * r.first * B,
                            (int)B, 0, 0, r.second, 0});
         o += (int64_t)r.second * 64;
+      }
+    }
+    if (stage == 3) {  // fused B+C: the composite products (outputs in increasing order)
+      for (int u = 0; u < nu; ++u) {
+        const Bath& b = h->baths[ubath[u]];
+        segs.push_back(Seg{CH_OYB + u, b.d_K0sqd + b.tofs[rt], 64, b.d_Xcur, (int)B, 0, 0, b.nks, 0});
+      }
+      for (int u = 0; u < nu; ++u) {
+        const Bath& b = h->baths[ubath[u]];
+        if (b.ml >= 2)  // V = n1 - c S1 from the S(t+1) tiles
+          segs.push_back(Seg{CH_OYC + u, b.d_K0d + b.tofs[rt], 64, b.d_V, (int)B, 0, 0, b.nks, 0});
+        else            // no memory sum: V = noise(t+1), read from the noise ring
+          segs.push_back(Seg{CH_OYC + u, b.d_K0d + b.tofs[rt], 64, b.d_noise, (int)B, (int)h->nmd, 1, b.nks,
+                             (int)(b.nc * B)});
+      }
+      for (int u = 0; u < nu; ++u) {
+        const Bath& b = h->baths[ubath[u]];
+        int64_t o = b.kd_tofs[rt];
+        for (auto& r : b.kd_rng[rt]) {
+          segs.push_back(Seg{CH_OYD + u, b.d_KDd + o, 64, h->d_Qt + (int64_t)4 * r.first * B, (int)B, 0, 0, r.second, 0});
+          o += (int64_t)r.second * 64;
+        }
+      }
+      for (int u = 0; u < nu; ++u) {
+        const Bath& b = h->baths[ubath[u]];
+        segs.push_back(Seg{CH_OYE + u, b.d_K0d + b.tofs[rt], 64, b.d_Xf, (int)B, 0, 0, b.nks, 0});
+      }
+      for (int u = 0; u < nu; ++u) {
+        const Bath& b = h->baths[ubath[u]];
+        if (b.has_q)
+          segs.push_back(Seg{CH_OYF + u, b.d_KKqd + b.tofs[rt], 64, b.d_Xq + b.vs, (int)B, 0, 0, b.nks, 0});
       }
     }
     int64_t W = 0;
@@ -888,6 +1041,10 @@ int plan_chain(gle_handle* h) {
   h->chNear.tiles.clear();
   h->chNear.nw = 4;
   h->chNear.lds = 0;
+  h->chBC.tiles.clear();
+  h->chBC.flops = 0;
+  h->chBC.nw = h->ch_nw[1];
+  h->chBC.lds = (size_t)256 * drn * 8;
   for (int rt = 0; rt < ntile; ++rt)
     for (int ct = 0; ct < ncol1; ++ct) {
       int rc = 0;
@@ -896,6 +1053,7 @@ int plan_chain(gle_handle* h) {
         if (!rc) rc = dof_tile(1, v == 1, rt, ct, h->chB[v]);
       }
       if (!rc) rc = dof_tile(2, false, rt, ct, h->chC);
+      if (!rc && h->fuse_bc) rc = dof_tile(3, true, rt, ct, h->chBC);
       if (rc) return rc;
     }
   // S(t+1) tiles (chain A): K_1.p_t + near-field partials + levels, per bath row tile
@@ -918,6 +1076,9 @@ int plan_chain(gle_handle* h) {
         sf.vs = b.vs;
         sf.nqn = b.nqn;
         sf.nc = b.nc;
+        sf.noise = h->fuse_bc ? b.d_noise : nullptr;
+        sf.V = h->fuse_bc ? b.d_V : nullptr;
+        sf.c = b.c;
         for (int l = 0; l < MAXLVL; ++l) {
           const bool act = l < (int)h->levels.size() && h->levels[l].lb[j].active;
           sf.lvl[l] = act ? h->levels[l].lb[j].d_out : h->d_zero;
@@ -960,7 +1121,7 @@ int plan_chain(gle_handle* h) {
           // near-field tiles go to the stages named in GLE_NEAR_IN (default A and C), round robin
           const int ns = (int)strlen(near_in);
           const char st = near_in[q % std::max(1, ns)];
-          Chain* pair[2] = {nullptr, nullptr};
+          Chain* pair[3] = {nullptr, nullptr, nullptr};
           if (st == 'A') {
             pair[0] = &h->chA[0];
             pair[1] = &h->chA[1];
@@ -970,6 +1131,7 @@ int plan_chain(gle_handle* h) {
           } else {
             pair[0] = &h->chC;
           }
+          if (st != 'A' && h->fuse_bc) pair[2] = &h->chBC;  // the fused launch replaces B and C
           for (Chain* c : pair) {
             if (!c) continue;
             ChTile Tc = T;
@@ -984,7 +1146,7 @@ int plan_chain(gle_handle* h) {
         }
     }
   }
-  for (Chain* c : {&h->chA[0], &h->chA[1], &h->chB[0], &h->chB[1], &h->chC, &h->chNear}) {
+  for (Chain* c : {&h->chA[0], &h->chA[1], &h->chB[0], &h->chB[1], &h->chC, &h->chNear, &h->chBC}) {
     int rc = upload_chain(h, *c);
     if (rc) return rc;
   }
@@ -1534,8 +1696,12 @@ int step_end_impl(gle_handle* h, const double* fpot_host_T) {
     if (!h->has_dyn) return fail(h, GLE_ERR_STATE, "no potential force at q~");
     if (h->host_force_step) return fail(h, GLE_ERR_STATE, "step begun with a host force must end with one");
   }
-  run_chain(h, 1, h->chB[mode1], ta, mode1, h->levels.empty());
-  run_chain(h, 2, h->chC, ta, mode1, h->levels.empty());
+  if (h->fuse_bc && mode1 == 1) {
+    run_chain(h, 3, h->chBC, ta, mode1, h->levels.empty());
+  } else {
+    run_chain(h, 1, h->chB[mode1], ta, mode1, h->levels.empty());
+    run_chain(h, 2, h->chC, ta, mode1, h->levels.empty());
+  }
   // the next step is a block boundary: the background blocks started there wait for this step
   if (!h->levels.empty() && (h->t + 1) % h->P0 == 0) HIPCHK(h, hipEventRecord(h->ev_step, h->stream));
   h->t += 1;

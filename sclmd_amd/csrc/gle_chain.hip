@@ -65,6 +65,7 @@ struct Batch {
 
 // GLE_CHAIN_DBG timeline: stamp 0 entry, 1 descriptor read, 2 products done, 3 end (100 MHz)
 __device__ __forceinline__ void stamp(const StepDev* __restrict__ sd, int stage, int k, const StepArgs& ta) {
+  if (stage > 2) stage = 2;  // the fused B+C stage records into stage C's rows
   if (ta.dbg && threadIdx.x == 0 && (int)blockIdx.x < sd->dbg_ntile)
     G(sd->dbg)[((int64_t)stage * sd->dbg_ntile + blockIdx.x) * 4 + k] = __builtin_amdgcn_s_memrealtime();
 }
@@ -283,6 +284,10 @@ __device__ __forceinline__ void dof_A(const ChTile* __restrict__ T, const StepDe
         G(sd->Q0)[E[x].i] = q[x];
       }
     }
+    // fused B+C: the cached force on the bath rows, the X of K0.Fc (the id1 cache-hit case)
+#pragma unroll
+    for (int u = 0; u < CH_TB; ++u)
+      if (kk[x][u] >= 0 && T->tb[u].Xf) G(T->tb[u].Xf)[(int64_t)kk[x][u] * B + E[x].b] = f;
 #pragma unroll
     for (int u = 0; u < CH_TB; ++u) {
       cur[x][u] = 0.0;
@@ -544,6 +549,150 @@ __device__ __forceinline__ void dof_C(const ChTile* __restrict__ T, const StepDe
   }
 }
 
+// stages B + C fused (md.py:401-408 in one launch; harmonic force, pairwise disjoint baths).  With
+// G = Fpot(q~) + sum_u (n1 - c S1 - Kq q~) and F1(x) = G - sum_u c K0 x on the bath rows:
+//   p1 = p_half + dt F1(p_half) / 2
+//   K0 p1 = K0 p_half + dt/2 (K0 G_u - c K0^2 p_half),  K0 G_u = K0 Fpot_u + K0 V - (K0 Kq) q~
+//   K0 Fpot_u = K0 Fc (potforce cache hit) or -(K0 P dyn) q~ (miss), V = n1 - c S1 (stage A)
+//   p2 = p_half + dt F1(p1) / 2,  F1(p1) = G - sum_u c K0 p1
+// so every product reads only stage A's outputs: one dependent launch instead of two.  K0 p1 is
+// re-associated (rounding only).
+template <int NW, int DRN>
+__device__ __forceinline__ void dof_BC(const ChTile* __restrict__ T, const StepDev* __restrict__ sd,
+                                       const StepArgs& ta, int mode, double* lds) {
+  using Geo = DofGeo<NW, DRN>;
+  constexpr int EPT = Geo::EPT;
+  const int B = sd->B;
+  const int64_t t = ta.t;
+  const int t1 = (int)((t + 1) % sd->nmd);
+  const int par = (int)(t & 1), par1 = par ^ 1;
+  const double dt = sd->dt;
+  const bool harm = mode != 0;
+  Elem E[EPT];
+  double ph[EPT], qt[EPT], fc[EPT], q0[EPT];
+  unsigned long long w1[EPT];
+  int cons[EPT];
+  int kk[EPT][CH_TB];
+  double nz[EPT][CH_TB], sv[EPT][CH_TB];
+#pragma unroll
+  for (int x = 0; x < EPT; ++x) {
+    E[x] = elem_of<NW, DRN>(T, sd, x);
+    ph[x] = qt[x] = fc[x] = q0[x] = 0.0;
+    w1[x] = 0;
+    cons[x] = 0;
+    if (E[x].ok) {
+      ph[x] = G(sd->Ph)[E[x].i];
+      qt[x] = G(sd->Qt)[E[x].i];
+      fc[x] = G(sd->Fc)[E[x].i];
+      cons[x] = G(sd->cmask)[E[x].d];
+      if (harm) {
+        q0[x] = G(sd->Q0)[E[x].i];
+        w1[x] = *G(pmax_word(sd, 1, par, E[x].b));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < CH_TB; ++u) {
+      kk[x][u] = -1;
+      nz[x][u] = sv[x][u] = 0.0;
+      const ChBath& bd = T->tb[u];
+      kk[x][u] = bath_row(bd, E[x]);
+      if (kk[x][u] >= 0) {
+        nz[x][u] = G(bd.noise)[((int64_t)t1 * bd.nc + kk[x][u]) * B + E[x].b];
+        sv[x][u] = G(bd.S)[(int64_t)par1 * bd.vs + (int64_t)kk[x][u] * B + E[x].b];
+      }
+    }
+  }
+  run_products<NW>(T, t, lds);
+  __syncthreads();
+  // the words this launch reads (w1) are read above: only now may the first tile reset them
+  if (T->first && threadIdx.x < Geo::NT && T->c0 + (int)threadIdx.x < B) {
+    *G(pmax_word(sd, 1, par1, T->c0 + threadIdx.x)) = 0ull;
+    if (harm) G(sd->qvalid)[T->c0 + threadIdx.x] = 1;
+  }
+  stamp(sd, 3, 2, ta);
+  double dq[EPT];
+#pragma unroll
+  for (int x = 0; x < EPT; ++x) {
+    const int e = threadIdx.x + x * NW * 64;
+    const bool hit1 = harm ? word_hit(w1[x]) : true;
+    double fpot = fc[x];  // potforce(q~)
+    if (!hit1 && E[x].in) {
+      fpot = -1.0 * out_sum(T, lds, 2 * CH_TB, e, Geo::NE);
+      if (E[x].ok) {  // md.potforce miss at q~: evaluate and cache (md.py:472-473)
+        G(sd->Fc)[E[x].i] = fpot;
+        G(sd->Q0)[E[x].i] = qt[x];
+      }
+    }
+    double g = fpot;
+#pragma unroll
+    for (int u = 0; u < CH_TB; ++u)
+      if (kk[x][u] >= 0) {
+        const ChBath& bd = T->tb[u];
+        g += nz[x][u] - bd.c * sv[x][u];
+        if (bd.has_q) g -= out_sum(T, lds, CH_TB + u, e, Geo::NE);
+      }
+    double f1 = g;  // F1(p_half) (md.py:401)
+#pragma unroll
+    for (int u = 0; u < CH_TB; ++u)
+      if (kk[x][u] >= 0) f1 -= T->tb[u].c * out_sum(T, lds, u, e, Geo::NE);
+    double f2 = g;  // F1(p1) (md.py:403)
+#pragma unroll
+    for (int u = 0; u < CH_TB; ++u)
+      if (kk[x][u] >= 0) {
+        const ChBath& bd = T->tb[u];
+        const double ya = out_sum(T, lds, u, e, Geo::NE);
+        double kg = (hit1 ? out_sum(T, lds, CH_OYE + u, e, Geo::NE) : -out_sum(T, lds, CH_OYD + u, e, Geo::NE)) +
+                    out_sum(T, lds, CH_OYC + u, e, Geo::NE);
+        if (bd.has_q) kg -= out_sum(T, lds, CH_OYF + u, e, Geo::NE);
+        const double k0p1 = ya + dt * (kg - bd.c * out_sum(T, lds, CH_OYB + u, e, Geo::NE)) / 2.0;
+        f2 -= bd.c * k0p1;
+      }
+    (void)f1;
+    double p2 = ph[x] + dt * f2 / 2.0;  // md.py:404
+    double qn = qt[x];
+    if (cons[x] != 0) {  // ApplyConstraint (md.py:407-408, 782-794)
+      p2 = 0.0;
+      qn = 0.0;
+    }
+    if (E[x].ok) {
+      G(sd->P)[E[x].i] = p2;
+      G(sd->Q)[E[x].i] = qn;
+      G(sd->Flast)[E[x].i] = f2;
+    }
+#pragma unroll
+    for (int u = 0; u < CH_TB; ++u) {
+      if (kk[x][u] >= 0) {
+        const ChBath& bd = T->tb[u];
+        const int64_t kb = (int64_t)kk[x][u] * B + E[x].b;
+        const int64_t slot = cmod(t + 1, bd.R);
+        __attribute__((address_space(1))) double* hh = G(bd.H + (int64_t)kk[x][u] * bd.ldh + E[x].b);
+        hh[slot * B] = p2;
+        hh[(slot + bd.R) * B] = p2;
+        G(bd.NR)[cmod(t + 1, bd.NRS) * bd.vs + kb] = p2;
+        if (bd.has_q) G(bd.Xq)[kb] = qn;
+      }
+    }
+    dq[x] = E[x].ok ? fabs(qn - (hit1 ? q0[x] : qt[x])) : 0.0;
+  }
+  if (harm) {  // cache distance of q_{t+1} for the next step's id0 call
+    __syncthreads();
+#pragma unroll
+    for (int x = 0; x < EPT; ++x) {
+      const int e = threadIdx.x + x * NW * 64;
+      if (E[x].in) lds[e] = dq[x];
+    }
+    __syncthreads();
+    const int c = threadIdx.x;
+    const int b = T->c0 + c;
+    if (c < Geo::NT && b < B) {
+      bool nan;
+      const double m = col_red<NW, DRN>(lds, 0, c, true, nan);
+      const unsigned long long bits = nan ? 0x7FF8000000000000ull : (unsigned long long)__double_as_longlong(m);
+      atomicMax(pmax_word(sd, 0, par1, b), bits);
+    }
+  }
+}
+
 // S(t+1) of bath rows [row0, row0+16) x 16 rn columns: K_1.p_t (the products) + near-field
 // partials + levels
 template <int NW, int DRN>
@@ -588,7 +737,15 @@ __device__ __forceinline__ void sfin(const ChTile* __restrict__ T, const StepDev
 #pragma unroll
   for (int x = 0; x < EPT; ++x) {
     const int e = threadIdx.x + x * NW * 64;
-    if (ok[x]) G(sf.S)[(int64_t)par1 * sf.vs + kb[x]] = out_sum(T, lds, 0, e, NE) + pre[x];
+    if (ok[x]) {
+      const double s1 = out_sum(T, lds, 0, e, NE) + pre[x];
+      G(sf.S)[(int64_t)par1 * sf.vs + kb[x]] = s1;
+      if (sf.V) {  // fused B+C: V = noise(t+1) - c S(t+1), the bath part of F1 that K0 acts on
+        const int t1 = (int)((t + 1) % sd->nmd);
+        const int k = (int)(kb[x] / B), b = (int)(kb[x] - (int64_t)k * B);
+        G(sf.V)[kb[x]] = G(sf.noise)[((int64_t)t1 * sf.nc + k) * B + b] - sf.c * s1;
+      }
+    }
   }
 }
 
@@ -638,7 +795,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(DRN == 
   if (kind == CH_DOF) {
     if (STAGE == 0) dof_A<NW, DRN>(T, sd, ta, mode, lds);
     else if (STAGE == 1) dof_B<NW, DRN>(T, sd, ta, mode, lds);
-    else dof_C<NW, DRN>(T, sd, ta, mode, lds);
+    else if (STAGE == 2) dof_C<NW, DRN>(T, sd, ta, mode, lds);
+    else dof_BC<NW, DRN>(T, sd, ta, mode, lds);
   } else if (kind == CH_SFIN) {
     sfin<NW, DRN>(T, sd, ta, lds, STAGE);
   } else {
@@ -669,7 +827,8 @@ void launch_chain(int stage, int nw, int drn, size_t lds_bytes, const ChTile* ti
   if (ntiles <= 0) return;
   if (stage == 0) launch_st<0>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
   else if (stage == 1) launch_st<1>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
-  else launch_st<2>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
+  else if (stage == 2) launch_st<2>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
+  else launch_st<3>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
 }
 
 }  // namespace gle

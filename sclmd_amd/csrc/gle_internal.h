@@ -132,7 +132,15 @@ struct StepDev {
 constexpr int CH_NW = 16;       // waves per chain workgroup (max)
 constexpr int CH_TPW = 3;       // tasks per wave
 constexpr int CH_TB = 3;        // baths a DOF tile may intersect
-constexpr int CH_NOUT = 2 * CH_TB + 1;
+// DOF-tile outputs: Y = K0.x of tile bath u (u), YQ = Kq.q (CH_TB + u), YD = dyn.q (2 CH_TB); the
+// fused velocity-iteration stage (STAGE 3) adds per tile bath u: K0^2.p_half (CH_OYB + u),
+// K0.V (CH_OYC + u), (K0 P dyn).q~ (CH_OYD + u), K0.Fc (CH_OYE + u), (K0 Kq).q~ (CH_OYF + u)
+constexpr int CH_OYB = 2 * CH_TB + 1;
+constexpr int CH_OYC = CH_OYB + CH_TB;
+constexpr int CH_OYD = CH_OYC + CH_TB;
+constexpr int CH_OYE = CH_OYD + CH_TB;
+constexpr int CH_OYF = CH_OYE + CH_TB;
+constexpr int CH_NOUT = CH_OYF + CH_TB;
 constexpr int CH_LDS_PER_WAVE = 1024;  // doubles of LDS partial slots per wave
 constexpr int CH_NPMAX = 16;    // near-field partial slots read by one SFIN element
 enum { CH_DOF = 0, CH_SFIN = 1, CH_RAW = 2 };
@@ -156,6 +164,8 @@ struct ChTask {
 struct ChBath {
   const double* noise;
   double *S, *Xcur, *Xq, *Yq, *H, *NR;
+  double* Xf;        // fused B+C: bath-local copy of the cached potential force after stage A
+  double* V;         // fused B+C: noise(t+1) - c S(t+1), bath-local (written by the S(t+1) tiles)
   const int32_t* inv;
   double c;
   int64_t vs;
@@ -170,6 +180,9 @@ struct ChBath {
 struct ChSfin {
   const double* NP;  // parity-0 slot 0 of the bath's near-field partials
   double* S;
+  const double* noise;  // fused B+C: V = noise(t+1) - c S(t+1) into V (nullptr: not fused)
+  double* V;
+  double c;
   const double* lvl[MAXLVL];
   int32_t lvl_ld[MAXLVL];
   int64_t vs;
