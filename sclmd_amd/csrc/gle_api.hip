@@ -1407,7 +1407,11 @@ int freeze(gle_handle* h) {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, h->cfg.device) == hipSuccess) ncu = prop.multiProcessorCount;
         const int nslot = std::max(1, lv.P / h->P0);
-        lv.ncg_chunk = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)lv.cg.size() / (2 * ncu), nslot));
+        double per_cu = 2.0;  // GLE_CG_PER_CU: workgroups per CU per chunk (experiment switch)
+        if (const char* e = getenv("GLE_CG_PER_CU")) per_cu = std::max(0.25, atof(e));
+        const double want = (double)lv.cg.size() / (per_cu * ncu);
+        const int64_t nch = getenv("GLE_CG_CEIL") ? (int64_t)std::ceil(want - 1e-9) : (int64_t)want;
+        lv.ncg_chunk = (int)std::max<int64_t>(1, std::min<int64_t>(nch, nslot));
         if (const char* e = getenv("GLE_NO_PIECES")) lv.ncg_chunk = atoi(e) > 0 ? 1 : lv.ncg_chunk;
         lv.npiece = lv.ncg_chunk + 2;
       }
