@@ -1957,7 +1957,9 @@ int commit_bath(gle_handle* h, Bath&& b, int32_t* bath_id) {
   b.vs = (int64_t)nbuf;
   rc |= dalloc_n(h, &b.d_inv, (size_t)h->nph);
   if (!rc) rc = upload(h, b.d_inv, b.inv.data(), b.inv.size() * 4);
-  rc |= dalloc_n(h, &b.d_noise, (size_t)h->nmd * nc * B);
+  // zero tail of (ncp - nc) rows: the fused stage reads noise(t+1) as an MFMA operand of ncp rows
+  // (K0 columns past nc are zero), which runs past the last time slot by ncp - nc rows
+  rc |= dalloc_n(h, &b.d_noise, ((size_t)h->nmd * nc + (b.ncp - nc)) * B + 64);
   rc |= dalloc_n(h, &b.d_S, 2 * nbuf);
   rc |= dalloc_n(h, &b.d_Xcur, 2 * nbuf);
   rc |= dalloc_n(h, &b.d_Xq, 2 * nbuf);
