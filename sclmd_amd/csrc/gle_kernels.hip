@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <vector>
 #include <cstdio>
+#include <cstdlib>
 
 #include "gle_internal.h"
 
@@ -799,22 +800,40 @@ __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, doubl
   }
 }
 
+// xcd != 0 (one pass, grid a multiple of 8): blocks b, b + 8, ... run on one XCD (round-robin
+// dispatch), so XCD b % 8 gets the contiguous item range [(b % 8) per, (b % 8 + 1) per): the row
+// groups of one (f, g) product, which read the same X window, then share that XCD's L2 instead of
+// each fetching the window into a different XCD.
 template <int RN>
-__global__ __launch_bounds__(256, 2) void cgemm_kernel(const CgItem* __restrict__ items, int nitems, int64_t tseg) {
+__global__ __launch_bounds__(256, 2) void cgemm_kernel(const CgItem* __restrict__ items, int nitems, int64_t tseg,
+                                                       int xcd) {
   __shared__ double xs[2][4 * CG_KC * CG_LD];
+  if (xcd) {
+    const int per = gridDim.x >> 3;
+    const int item = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    if (item < nitems) cgemm_item<RN>(items[item], tseg, xs);
+    return;
+  }
   for (int item = blockIdx.x; item < nitems; item += gridDim.x) {
     const CgItem it = items[item];
     cgemm_item<RN>(it, tseg, xs);
     __syncthreads();
   }
 }
+static int g_cg_xcd = -1;  // GLE_CG_XCD=0 switches the XCD grouping off (experiment switch)
 void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStream_t s, int max_grid) {
   if (nitems <= 0) return;
-  const int grid = (max_grid > 0 && max_grid < nitems) ? max_grid : nitems;
+  if (g_cg_xcd < 0) {
+    const char* e = getenv("GLE_CG_XCD");
+    g_cg_xcd = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  const bool capped = max_grid > 0 && max_grid < nitems;
+  const int xcd = (!capped && g_cg_xcd) ? 1 : 0;
+  const int grid = capped ? max_grid : (xcd ? (nitems + 7) / 8 * 8 : nitems);
   switch (rn) {
-    case 1: cgemm_kernel<1><<<grid, 256, 0, s>>>(items, nitems, tseg); break;
-    case 2: cgemm_kernel<2><<<grid, 256, 0, s>>>(items, nitems, tseg); break;
-    default: cgemm_kernel<4><<<grid, 256, 0, s>>>(items, nitems, tseg); break;
+    case 1: cgemm_kernel<1><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd); break;
+    case 2: cgemm_kernel<2><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd); break;
+    default: cgemm_kernel<4><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd); break;
   }
 }
 
