@@ -102,3 +102,37 @@ def test_vv_batched_trajectories(case, far_mode):
         assert relerr(q[b], sim.q) < RTOL_TRAJ
         assert relerr(p[b], sim.p) < RTOL_TRAJ
     st.close()
+
+
+@pytest.mark.parametrize("case", ["vv_biased", "vv_mixed"])
+def test_vv_wide_batch_across_noise_periods(case):
+    """64 trajectories (several chain column tiles) run across two ends of the noise ring -- the
+    last time slot is where an operand read past the ring once faulted -- checked against the
+    oracle on a few trajectories."""
+    g = load_golden(case)
+    B, nmd = 64, int(g["nmd"])
+    rng = np.random.default_rng(11)
+    st = stepper_from_golden(g, B)
+    p0 = g["p0"][None] * (1 + 0.1 * rng.normal(size=(B, 1)))
+    q0 = g["q0"][None] * (1 + 0.1 * rng.normal(size=(B, 1)))
+    st.set_state(p0, q0, 0)
+    noises = []
+    for i in range(int(g["nbath"])):
+        st.set_history(i, None)
+        nz = g["b%d_noise" % i][None] * (1 + rng.normal(size=(B, 1, 1)))
+        noises.append(nz)
+        st.set_noise(i, nz)
+    nsteps = 2 * nmd + 3
+    st.run(nsteps)
+    p, q, t = st.get_state()
+    assert t == nsteps
+    for b in (0, 17, 63):
+        sim = oracle_from_golden(g)
+        sim.p, sim.q = p0[b].copy(), q0[b].copy()
+        for i, bath in enumerate(sim.baths):
+            bath.noise = noises[i][b]
+        for _ in range(nsteps):
+            sim.step()
+        assert relerr(q[b], sim.q) < RTOL_TRAJ
+        assert relerr(p[b], sim.p) < RTOL_TRAJ
+    st.close()
