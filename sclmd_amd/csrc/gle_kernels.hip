@@ -702,17 +702,17 @@ constexpr int CG_LD = 80;  // LDS row stride (doubles): 64 columns + 16, ds_read
 
 typedef const __attribute__((address_space(1))) double gdbl;
 
-template <int RN>
-__device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, double (&xs)[2][4 * CG_KC * CG_LD]) {
+template <int RN, int KC>
+__device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, double (&xs)[2][4 * KC * CG_LD]) {
   constexpr int NT = 16 * RN;
-  constexpr int XPT = 4 * CG_KC * NT / 256;  // X doubles per thread per chunk
+  constexpr int XPT = 4 * KC * NT / 256;  // X doubles per thread per chunk
   constexpr int TPR = NT / XPT;              // staging threads per X row
-  static_assert(4 * CG_KC * TPR == 256, "one X row per TPR threads, every thread stages");
+  static_assert(4 * KC * TPR == 256, "one X row per TPR threads, every thread stages");
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
   const int brow = lane >> 4, bcol = lane & 15;
   const int S = it.ns;  // k-steps of this item: [it.s0, it.s0 + S) of the M nks of T_g(f)
-  const int nch = (S + CG_KC - 1) / CG_KC;
+  const int nch = (S + KC - 1) / KC;
   const bool active = wave < it.nrt;
   // global address space: flat loads would also count on lgkmcnt, and every LDS-read wait before an
   // MFMA would then drain the HBM prefetches in flight
@@ -724,13 +724,13 @@ __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, doubl
   // chunk (8 k-steps, 8 RN MFMAs per wave) is too short to cover an HBM round trip on its own.
   // Loads are branch-free (clamped address, zero by multiplication): a branch around a load makes
   // the waitcnt pass drain every load in flight.
-  double xv[XPT], a0[CG_KC], a1[CG_KC], a2[CG_KC];
+  double xv[XPT], a0[KC], a1[KC], a2[KC];
   d4 acc[RN];
 #pragma unroll
   for (int n = 0; n < RN; ++n) acc[n] = d4{0.0, 0.0, 0.0, 0.0};
 #define CG_LOAD_X(c, XV)                                                                              \
   do {                                                                                                \
-    const int s0_ = (c) * CG_KC + (xr >> 2);                                                          \
+    const int s0_ = (c) * KC + (xr >> 2);                                                          \
     const int sc_ = it.s0 + (s0_ < S ? s0_ : S - 1);                                                  \
     const int i_ = (int)((unsigned)sc_ / (unsigned)it.nks), ks_ = sc_ - i_ * it.nks;                  \
     int slot_ = tbase - i_;                                                                           \
@@ -742,13 +742,13 @@ __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, doubl
   /* rows past S are stored as zeros (the multiply waits for the load only here, at the store) */
 #define CG_STORE_X(c, buf, XV)                                                                        \
   do {                                                                                                \
-    const double m_ = (c) * CG_KC + (xr >> 2) < S ? 1.0 : 0.0;                                        \
+    const double m_ = (c) * KC + (xr >> 2) < S ? 1.0 : 0.0;                                        \
     _Pragma("unroll") for (int u = 0; u < XPT; ++u) xs[buf][xr * CG_LD + xc + u] = XV[u] * m_;        \
   } while (0)
 #define CG_LOAD_A(c, AV)                                                                              \
   do {                                                                                                \
-    _Pragma("unroll") for (int u = 0; u < CG_KC; ++u) {                                               \
-      const int s0_ = (c) * CG_KC + u;                                                                \
+    _Pragma("unroll") for (int u = 0; u < KC; ++u) {                                               \
+      const int s0_ = (c) * KC + u;                                                                \
       AV[u] = Aw[(int64_t)(s0_ < S ? s0_ : S - 1) * 64]; /* masked at the MFMA */                 \
     }                                                                                                 \
   } while (0)
@@ -764,8 +764,8 @@ __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, doubl
     CG_LOAD_X(c_ + 1, xv);                                                                            \
     CG_LOAD_A(c_ + 2, ANEXT);                                                                         \
     const double* xb_ = xs[c_ & 1] + brow * CG_LD + bcol;                                             \
-    _Pragma("unroll") for (int u = 0; u < CG_KC; ++u) {                                               \
-      const double a_ = ACUR[u] * ((active && c_ * CG_KC + u < S) ? 1.0 : 0.0);                       \
+    _Pragma("unroll") for (int u = 0; u < KC; ++u) {                                               \
+      const double a_ = ACUR[u] * ((active && c_ * KC + u < S) ? 1.0 : 0.0);                       \
       _Pragma("unroll") for (int n = 0; n < RN; ++n) acc[n] =                                         \
           __builtin_amdgcn_mfma_f64_16x16x4f64(a_, xb_[4 * u * CG_LD + 16 * n], acc[n], 0, 0, 0);     \
     }                                                                                                 \
@@ -804,36 +804,47 @@ __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, doubl
 // dispatch), so XCD b % 8 gets the contiguous item range [(b % 8) per, (b % 8 + 1) per): the row
 // groups of one (f, g) product, which read the same X window, then share that XCD's L2 instead of
 // each fetching the window into a different XCD.
-template <int RN>
-__global__ __launch_bounds__(256, 2) void cgemm_kernel(const CgItem* __restrict__ items, int nitems, int64_t tseg,
+template <int RN, int KC>
+__global__ __launch_bounds__(256, KC <= 4 ? 3 : 2) void cgemm_kernel(const CgItem* __restrict__ items, int nitems, int64_t tseg,
                                                        int xcd) {
-  __shared__ double xs[2][4 * CG_KC * CG_LD];
+  __shared__ double xs[2][4 * KC * CG_LD];
   if (xcd) {
     const int per = gridDim.x >> 3;
     const int item = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
-    if (item < nitems) cgemm_item<RN>(items[item], tseg, xs);
+    if (item < nitems) cgemm_item<RN, KC>(items[item], tseg, xs);
     return;
   }
   for (int item = blockIdx.x; item < nitems; item += gridDim.x) {
     const CgItem it = items[item];
-    cgemm_item<RN>(it, tseg, xs);
+    cgemm_item<RN, KC>(it, tseg, xs);
     __syncthreads();
   }
 }
 static int g_cg_xcd = -1;  // GLE_CG_XCD=0 switches the XCD grouping off (experiment switch)
+static int g_cg_kc = 0;    // k-steps per LDS chunk: 4 (159 VGPRs, 3 waves/SIMD; 23.9 vs 21.6 TF/s in situ), GLE_CG_KC=8: 8
 void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStream_t s, int max_grid) {
   if (nitems <= 0) return;
   if (g_cg_xcd < 0) {
     const char* e = getenv("GLE_CG_XCD");
     g_cg_xcd = (e && atoi(e) == 0) ? 0 : 1;
+    const char* k = getenv("GLE_CG_KC");
+    g_cg_kc = (k && atoi(k) == 8) ? 8 : 4;
   }
   const bool capped = max_grid > 0 && max_grid < nitems;
   const int xcd = (!capped && g_cg_xcd) ? 1 : 0;
   const int grid = capped ? max_grid : (xcd ? (nitems + 7) / 8 * 8 : nitems);
+  if (g_cg_kc == 4) {
+    switch (rn) {
+      case 1: cgemm_kernel<1, 4><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd); break;
+      case 2: cgemm_kernel<2, 4><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd); break;
+      default: cgemm_kernel<4, 4><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd); break;
+    }
+    return;
+  }
   switch (rn) {
-    case 1: cgemm_kernel<1><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd); break;
-    case 2: cgemm_kernel<2><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd); break;
-    default: cgemm_kernel<4><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd); break;
+    case 1: cgemm_kernel<1, CG_KC><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd); break;
+    case 2: cgemm_kernel<2, CG_KC><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd); break;
+    default: cgemm_kernel<4, CG_KC><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd); break;
   }
 }
 

@@ -267,7 +267,19 @@ class md:
         self.dyn = mdot(self.U, np.diag(np.array(av)), np.transpose(self.U))
 
     def AddPotential(self, pint):
-        self.pforce = pint
+        """Host force driver (md.py:481), or a list of drivers, one per trajectory of this rank's
+        ensemble.  With a list, the trajectories' driver calls of a force phase run concurrently on
+        a thread pool (LAMMPS / SIESTA / DeePMD release the GIL inside their engines), so an
+        ensemble's host force phase costs about one driver call instead of ntraj of them.  A single
+        driver instance is called for the trajectories one after another."""
+        if isinstance(pint, (list, tuple)):
+            if len(pint) != self.ntraj:
+                raise ValueError("AddPotential: %d drivers for %d trajectories" % (len(pint), self.ntraj))
+            self.pforces = list(pint)
+            self.pforce = self.pforces[0]
+        else:
+            self.pforces = None
+            self.pforce = pint
 
     def CompareForce(self, forcedriver):
         self.cf = 1
@@ -430,15 +442,35 @@ class md:
         return f
 
     def _host_forces(self, qs, cache):
+        """Per-trajectory md.potforce with its sameq cache (md.py:437-474, 767-779)."""
         out = np.empty_like(qs)
+        miss = []
         for b in range(self.ntraj):
             q0, f0 = cache[b]
             if len(q0) == len(qs[b]) and np.max(np.abs(qs[b] - q0)) < 10e-10:
                 out[b] = f0
             else:
-                f = np.asarray(self.pforce.force(qs[b].copy()), dtype=float)
-                cache[b] = (qs[b].copy(), f)
+                miss.append(b)
+        drivers = getattr(self, "pforces", None)
+        if drivers is not None and len(miss) > 1:
+            if getattr(self, "_pool", None) is None:
+                from concurrent.futures import ThreadPoolExecutor
+
+                nw = min(self.ntraj, int(os.environ.get("SCLMD_FORCE_WORKERS", os.cpu_count() or 1)))
+                self._pool = ThreadPoolExecutor(max_workers=max(1, nw))
+            qc = {b: qs[b].copy() for b in miss}
+            futs = {b: self._pool.submit(drivers[b].force, qc[b]) for b in miss}
+            for b in miss:  # collected in trajectory order: the cache update is deterministic
+                f = np.asarray(futs[b].result(), dtype=float)
+                cache[b] = (qc[b], f)
                 out[b] = f
+            return out
+        for b in miss:
+            drv = drivers[b] if drivers is not None else self.pforce
+            q = qs[b].copy()
+            f = np.asarray(drv.force(q), dtype=float)
+            cache[b] = (q, f)
+            out[b] = f
         return out
 
     # ------------------------------------------------------------------------------ stepping
@@ -735,6 +767,9 @@ class md:
                         "   " + str(ave[ip * 3 + 2]) + "\n")
 
     def close(self):
+        if getattr(self, "_pool", None) is not None:
+            self._pool.shutdown(wait=True)
+            self._pool = None
         if self._st is not None:
             self._pull()
             self._st.close()

@@ -324,3 +324,48 @@ def test_ladder_long_kernel_vs_oracle(far_mode, block_len, max_block):
         for b_ in (j, j + 2, B - 2 + j):
             assert rel(qg[b_], sim.q) < 1e-9 and rel(pg[b_], sim.p) < 1e-9, (b_, rel(qg[b_], sim.q))
     st.close()
+
+
+@pytest.mark.parametrize("case", ["vv_mixed", "vv_biased"])
+def test_host_driver_ensemble_per_trajectory_drivers(case):
+    """An ensemble whose host forces come from one driver per trajectory (called concurrently):
+    every trajectory follows the device-harmonic trajectory of the same initial state and noise."""
+    from sclmd_amd import md as MD
+    from sclmd_amd import synthetic
+    from sclmd_amd.baths import ebath, phbath
+    from sclmd_amd.drivers import HarmonicDriver
+
+    g = load_golden(case)
+    B = 3
+    dt, nmd = float(g["dt"]), int(g["nmd"])
+    axyz = synthetic.axyz_chain(int(g["natom"]))
+    rng = np.random.default_rng(9)
+    p0 = g["p0"][None] * (1 + 0.1 * rng.normal(size=(B, 1)))
+    q0 = g["q0"][None] * (1 + 0.1 * rng.normal(size=(B, 1)))
+    out = []
+    for use_driver in (True, False):
+        m = MD.md(dt, nmd, float(g["T"]), axyz=axyz, dyn=None if use_driver else g["dyn_md"], ntraj=B,
+                  verbose=False)
+        for i in range(int(g["nbath"])):
+            cids = g["b%d_cids" % i]
+            if str(g["b%d_kind" % i]) == "ebath":
+                b = ebath(cids, 300.0, dt, nmd, bias=float(g["b%d_bias" % i]), efric=g["b%d_efric" % i],
+                          exim=g["b%d_exim" % i], zeta1=g["b%d_zeta1" % i], zeta2=g["b%d_zeta2" % i])
+            else:
+                b = phbath(300.0, cids, 0.2, 10, dt, nmd, ml=int(g["b%d_ml" % i]))
+                b.kernel = g["b%d_kernel" % i]
+                b.ml = int(g["b%d_ml" % i])
+            b.noise = g["b%d_noise" % i]
+            m.AddBath(b)
+        c = constr_from(g)
+        if c:
+            m.AddConstr(c)
+        if use_driver:
+            m.AddPotential([HarmonicDriver(g["dyn_md"], axyz) for _ in range(B)])
+        m.p, m.q, m.t = p0.copy(), q0.copy(), 0
+        m.ResetHis()
+        for _ in range(int(g["nsteps"])):
+            m.vv(0)
+        out.append((np.array(m.p), np.array(m.q)))
+        m.close()
+    assert rel(out[0][1], out[1][1]) < 1e-10 and rel(out[0][0], out[1][0]) < 1e-10
