@@ -122,7 +122,7 @@ def main():
     t_setup = time.perf_counter()
     dyn, axyz, baths, meta = synthetic.junction(args.config, seed=1234, gmem_device=args.gmem == "device")
     m = MD.md(meta["dt"], meta["nmd"], meta["T"], axyz=axyz, dyn=dyn, ntraj=args.ntraj,
-              seed=1000 + rank * args.ntraj, traj_offset=rank * args.ntraj, device=local_rank,
+              seed=1000, traj_offset=rank * args.ntraj, device=local_rank,
               noise_mode="device", block_len=args.block_len, far_mode=args.far_mode,
               max_block=args.max_block, verbose=False)
     log("[bench] rank %d system built (%.1fs)" % (rank, time.perf_counter() - t_setup))

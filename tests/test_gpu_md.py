@@ -369,3 +369,36 @@ def test_host_driver_ensemble_per_trajectory_drivers(case):
         out.append((np.array(m.p), np.array(m.q)))
         m.close()
     assert rel(out[0][1], out[1][1]) < 1e-10 and rel(out[0][0], out[1][0]) < 1e-10
+
+
+def test_ensemble_sharding_invariance(tmp_path, monkeypatch):
+    """The multi-GPU ensemble by construction: trajectory g's initial state and device noise are keyed
+    by its global index (seed + traj_offset + b), so one 16-trajectory md equals two 8-trajectory
+    shards with traj_offset 0 and 8 -- what ranks 0 and 1 hold -- up to the summation order of the
+    batched kernels (1e-9 relative on p, q and the heat currents)."""
+    from sclmd_amd import md as MD
+    from sclmd_amd import synthetic
+
+    monkeypatch.chdir(tmp_path)
+
+    def run(ntraj, offset):
+        dyn, axyz, baths, meta = synthetic.junction("C3", seed=5, natom=12, ml=64, nmd=256, nw=80)
+        m = MD.md(meta["dt"], meta["nmd"], meta["T"], axyz=axyz, dyn=dyn, ntraj=ntraj, seed=77,
+                  traj_offset=offset, noise_mode="device", verbose=False)
+        for b in baths:
+            m.AddBath(b)
+        m.initialise()
+        m.ResetHis()
+        for i in range(len(baths)):
+            m.gen_noise(i, 0)
+        m.steps(300)
+        p, q, _ = m._st.get_state()
+        cur = m._st.get_current()
+        m.close()
+        return p, q, cur
+
+    p, q, cur = run(16, 0)
+    p0, q0, c0 = run(8, 0)
+    p1, q1, c1 = run(8, 8)
+    assert rel(np.concatenate([p0, p1]), p) < 1e-9 and rel(np.concatenate([q0, q1]), q) < 1e-9
+    assert rel(np.concatenate([c0, c1], axis=1), cur) < 1e-9
