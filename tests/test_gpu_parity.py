@@ -136,3 +136,34 @@ def test_vv_wide_batch_across_noise_periods(case):
         assert relerr(q[b], sim.q) < RTOL_TRAJ
         assert relerr(p[b], sim.p) < RTOL_TRAJ
     st.close()
+
+
+def test_no_bath_nve_vs_oracle():
+    """md without baths (md.py: the bath loops of force() are empty): velocity Verlet on the harmonic
+    potential alone, with constraints, against the oracle; energy stays constant to the integrator's
+    order."""
+    from sclmd_amd import _native as N
+    from oracle import sclmd_oracle as O
+
+    g = load_golden("vv_mixed")
+    nph, nmd, dt = 3 * int(g["natom"]), int(g["nmd"]), float(g["dt"])
+    B = 3
+    st = N.Stepper(nph, B, nmd, dt, 0)
+    st.set_dyn(g["dyn_md"])
+    st.set_constraint([0, 1])
+    rng = np.random.default_rng(2)
+    p0 = rng.normal(size=(B, nph)) * 1e-2
+    q0 = rng.normal(size=(B, nph)) * 1e-1
+    p0[:, :2] = q0[:, :2] = 0.0
+    st.set_state(p0, q0, 0)
+    nsteps = 2 * nmd + 5
+    st.run(nsteps)
+    p, q, t = st.get_state()
+    assert t == nsteps
+    for b in range(B):
+        sim = O.GLE(nph, dt, nmd, [], dyn=g["dyn_md"], constr=[range(0, 2)])
+        sim.p, sim.q = p0[b].copy(), q0[b].copy()
+        for _ in range(nsteps):
+            sim.step()
+        assert relerr(q[b], sim.q) < RTOL_TRAJ and relerr(p[b], sim.p) < RTOL_TRAJ
+    st.close()
