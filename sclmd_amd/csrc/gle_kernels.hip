@@ -702,7 +702,7 @@ constexpr int CG_LD = 80;  // LDS row stride (doubles): 64 columns + 16, ds_read
 
 typedef const __attribute__((address_space(1))) double gdbl;
 
-template <int RN, int KC>
+template <int RN, int KC, int DBG = 0>
 __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, double (&xs)[2][4 * KC * CG_LD]) {
   constexpr int NT = 16 * RN;
   constexpr int XPT = 4 * KC * NT / 256;  // X doubles per thread per chunk
@@ -749,7 +749,7 @@ __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, doubl
   do {                                                                                                \
     _Pragma("unroll") for (int u = 0; u < KC; ++u) {                                               \
       const int s0_ = (c) * KC + u;                                                                \
-      AV[u] = Aw[(int64_t)(s0_ < S ? s0_ : S - 1) * 64]; /* masked at the MFMA */                 \
+      AV[u] = (DBG & 1) ? 1e-3 * (s0_ + 1) : Aw[(int64_t)(s0_ < S ? s0_ : S - 1) * 64]; /* masked */ \
     }                                                                                                 \
   } while (0)
   // chunk c: MFMAs on A chunk c (registers) and X chunk c (LDS buffer c&1); chunk c+2's A goes
@@ -761,16 +761,19 @@ __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, doubl
     /* X first: vmcnt retires in order, so the X store at the end of the step then waits for X  */ \
     /* (and older loads) only, while chunk c+2's A stays in flight                              */ \
     /* unconditional (clamped) loads: paths that skip a load confuse the waitcnt pass          */ \
-    CG_LOAD_X(c_ + 1, xv);                                                                            \
+    if (!(DBG & 4)) CG_LOAD_X(c_ + 1, xv);                                                            \
     CG_LOAD_A(c_ + 2, ANEXT);                                                                         \
     const double* xb_ = xs[c_ & 1] + brow * CG_LD + bcol;                                             \
     _Pragma("unroll") for (int u = 0; u < KC; ++u) {                                               \
       const double a_ = ACUR[u] * ((active && c_ * KC + u < S) ? 1.0 : 0.0);                       \
       _Pragma("unroll") for (int n = 0; n < RN; ++n) acc[n] =                                         \
-          __builtin_amdgcn_mfma_f64_16x16x4f64(a_, xb_[4 * u * CG_LD + 16 * n], acc[n], 0, 0, 0);     \
+          __builtin_amdgcn_mfma_f64_16x16x4f64(a_, (DBG & 2) ? a_ * (n + 1) : xb_[4 * u * CG_LD + 16 * n], \
+                                               acc[n], 0, 0, 0);                                      \
     }                                                                                                 \
-    CG_STORE_X(c_ + 1, (c_ & 1) ^ 1, xv);                                                             \
-    __syncthreads();                                                                                  \
+    if (!(DBG & 4)) {                                                                                 \
+      CG_STORE_X(c_ + 1, (c_ & 1) ^ 1, xv);                                                           \
+      __syncthreads();                                                                                \
+    }                                                                                                 \
   } while (0)
   CG_LOAD_A(0, a0);
   CG_LOAD_A(1, a1);
@@ -804,23 +807,24 @@ __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, doubl
 // dispatch), so XCD b % 8 gets the contiguous item range [(b % 8) per, (b % 8 + 1) per): the row
 // groups of one (f, g) product, which read the same X window, then share that XCD's L2 instead of
 // each fetching the window into a different XCD.
-template <int RN, int KC>
+template <int RN, int KC, int DBG = 0>
 __global__ __launch_bounds__(256, KC <= 4 ? 3 : 2) void cgemm_kernel(const CgItem* __restrict__ items, int nitems, int64_t tseg,
                                                        int xcd) {
   __shared__ double xs[2][4 * KC * CG_LD];
   if (xcd) {
     const int per = gridDim.x >> 3;
     const int item = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
-    if (item < nitems) cgemm_item<RN, KC>(items[item], tseg, xs);
+    if (item < nitems) cgemm_item<RN, KC, DBG>(items[item], tseg, xs);
     return;
   }
   for (int item = blockIdx.x; item < nitems; item += gridDim.x) {
     const CgItem it = items[item];
-    cgemm_item<RN, KC>(it, tseg, xs);
+    cgemm_item<RN, KC, DBG>(it, tseg, xs);
     __syncthreads();
   }
 }
 static int g_cg_xcd = -1;  // GLE_CG_XCD=0 switches the XCD grouping off (experiment switch)
+static int g_cg_dbg = 0;
 static int g_cg_kc = 0;    // k-steps per LDS chunk: 4 (159 VGPRs, 3 waves/SIMD; 23.9 vs 21.6 TF/s in situ), GLE_CG_KC=8: 8
 void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStream_t s, int max_grid) {
   if (nitems <= 0) return;
@@ -829,10 +833,21 @@ void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStre
     g_cg_xcd = (e && atoi(e) == 0) ? 0 : 1;
     const char* k = getenv("GLE_CG_KC");
     g_cg_kc = (k && atoi(k) == 8) ? 8 : 4;
+    // 1: no K-hat loads, 2: no LDS operand reads, 4: no X staging / barrier; 3, 7: combinations
+    const char* d = getenv("GLE_CG_DBG");
+    g_cg_dbg = d ? std::max(0, std::min(7, atoi(d))) : 0;
   }
   const bool capped = max_grid > 0 && max_grid < nitems;
   const int xcd = (!capped && g_cg_xcd) ? 1 : 0;
   const int grid = capped ? max_grid : (xcd ? (nitems + 7) / 8 * 8 : nitems);
+  if (g_cg_dbg && rn == 4 && g_cg_kc == 4) {  // GLE_CG_DBG timing experiments (results invalid)
+    if (g_cg_dbg == 1) cgemm_kernel<4, 4, 1><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd);
+    else if (g_cg_dbg == 2) cgemm_kernel<4, 4, 2><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd);
+    else if (g_cg_dbg == 3) cgemm_kernel<4, 4, 3><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd);
+    else if (g_cg_dbg == 4) cgemm_kernel<4, 4, 4><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd);
+    else cgemm_kernel<4, 4, 7><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd);
+    return;
+  }
   if (g_cg_kc == 4) {
     switch (rn) {
       case 1: cgemm_kernel<1, 4><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd); break;
