@@ -837,29 +837,37 @@ void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStre
     const char* d = getenv("GLE_CG_DBG");
     g_cg_dbg = d ? std::max(0, std::min(7, atoi(d))) : 0;
   }
+  // GLE_CG_LDS_PAD (bytes, experiment switch): unused dynamic LDS per workgroup, capping how many
+  // far-field workgroups a CU holds so the per-step chain's workgroups find room beside them
+  static int lds_pad = -1;
+  if (lds_pad < 0) {
+    const char* e = getenv("GLE_CG_LDS_PAD");
+    lds_pad = e ? std::max(0, std::min(96 * 1024, atoi(e))) : 0;
+  }
+  const size_t shm = (size_t)lds_pad;
   const bool capped = max_grid > 0 && max_grid < nitems;
   const int xcd = (!capped && g_cg_xcd) ? 1 : 0;
   const int grid = capped ? max_grid : (xcd ? (nitems + 7) / 8 * 8 : nitems);
   if (g_cg_dbg && rn == 4 && g_cg_kc == 4) {  // GLE_CG_DBG timing experiments (results invalid)
-    if (g_cg_dbg == 1) cgemm_kernel<4, 4, 1><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd);
-    else if (g_cg_dbg == 2) cgemm_kernel<4, 4, 2><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd);
-    else if (g_cg_dbg == 3) cgemm_kernel<4, 4, 3><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd);
-    else if (g_cg_dbg == 4) cgemm_kernel<4, 4, 4><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd);
-    else cgemm_kernel<4, 4, 7><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd);
+    if (g_cg_dbg == 1) cgemm_kernel<4, 4, 1><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd);
+    else if (g_cg_dbg == 2) cgemm_kernel<4, 4, 2><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd);
+    else if (g_cg_dbg == 3) cgemm_kernel<4, 4, 3><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd);
+    else if (g_cg_dbg == 4) cgemm_kernel<4, 4, 4><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd);
+    else cgemm_kernel<4, 4, 7><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd);
     return;
   }
   if (g_cg_kc == 4) {
     switch (rn) {
-      case 1: cgemm_kernel<1, 4><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd); break;
-      case 2: cgemm_kernel<2, 4><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd); break;
-      default: cgemm_kernel<4, 4><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd); break;
+      case 1: cgemm_kernel<1, 4><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd); break;
+      case 2: cgemm_kernel<2, 4><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd); break;
+      default: cgemm_kernel<4, 4><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd); break;
     }
     return;
   }
   switch (rn) {
-    case 1: cgemm_kernel<1, CG_KC><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd); break;
-    case 2: cgemm_kernel<2, CG_KC><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd); break;
-    default: cgemm_kernel<4, CG_KC><<<grid, 256, 0, s>>>(items, nitems, tseg, xcd); break;
+    case 1: cgemm_kernel<1, CG_KC><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd); break;
+    case 2: cgemm_kernel<2, CG_KC><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd); break;
+    default: cgemm_kernel<4, CG_KC><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd); break;
   }
 }
 
