@@ -1369,6 +1369,10 @@ int freeze(gle_handle* h) {
         const int64_t plane = (int64_t)b.nrt * a_rt;
         for (int f = 0; f <= lv.P; ++f)
           for (int g = 0; g < 3; ++g) {
+            // f = 0 and f = P: K-hat and X-hat are real, so Re Y = T_0 - T_1 = T_0 (X plane 1 = Im = 0)
+            // and Im Y is dropped (far_ifft realonly): planes 1 and 2 are not needed, their T
+            // planes stay zero
+            if ((f == 0 || f == lv.P) && g != 0) continue;
             for (int rg = 0; 4 * rg < b.nrt; ++rg)
               for (int c0 = 0; c0 < B; c0 += NT)
                 for (int hk = 0; hk < lv.cg_split; ++hk) {
