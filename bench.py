@@ -5,7 +5,10 @@ Workload (BASELINE.json metric, configs[2] = SURVEY.md C3): 300-atom chain junct
 baths with nc = 300 coupled DOF each, 1024-step memory kernel, nmd = 4096, fp64, 64 independent
 trajectories per GPU (weak scaling: C4 = 8 x 64).  A "step" is one md.vv of every trajectory on
 this GPU.  Setup (memory-kernel construction, noise factorisation and generation, H2D) is outside
-the timed region.
+the timed region.  Before the warm-up an untimed fill (2 x the largest ladder block) brings the
+memory-sum ladder to its steady state, so any window of K steps carries K / P blocks of every
+level (reported as ladder_window).  Other lines: --config C2 --ntraj 1 (the north-star 1-trajectory
+comparison), --config C5 --ntraj 32.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU, RCCL reduce)
@@ -46,10 +49,36 @@ def cpu_info():
     return model
 
 
-def cpu_baseline(baths_host, dyn, nph, dt, nmd, budget_s=15.0, max_steps=200):
+def blas_info():
+    try:
+        from threadpoolctl import threadpool_info
+
+        for d in threadpool_info():
+            if d.get("user_api") == "blas":
+                return "%s %s (%s, %d threads)" % (d.get("internal_api"), d.get("version"),
+                                                   d.get("architecture"), d.get("num_threads", 0))
+    except Exception:  # pragma: no cover - informational only
+        pass
+    return "unknown BLAS"
+
+
+def blas_threads():
+    try:
+        from threadpoolctl import threadpool_info
+
+        for d in threadpool_info():
+            if d.get("user_api") == "blas":
+                return int(d.get("num_threads", 1))
+    except Exception:  # pragma: no cover
+        pass
+    return 1
+
+
+def cpu_baseline(baths_host, dyn, nph, dt, nmd, budget_s=20.0, nsample=5):
     """Time the oracle's reference-shaped step (3 memory passes/step, per-slice matvecs,
     shift-copied history) for ONE trajectory -- the reference runs trajectories one after another
-    (md.py:506), so its ensemble throughput equals this single-trajectory rate."""
+    (md.py:506), so its ensemble throughput equals this single-trajectory rate.  Median of
+    `nsample` samples of about budget_s / nsample seconds each, after one warm-up step."""
     from oracle import sclmd_oracle as O
 
     bs = [O.Bath("ph", c, k, n, dt, nmd) for (c, k, n) in baths_host]
@@ -58,29 +87,45 @@ def cpu_baseline(baths_host, dyn, nph, dt, nmd, budget_s=15.0, max_steps=200):
     sim.p = rng.normal(size=nph) * 1e-3
     sim.q = rng.normal(size=nph) * 1e-3
     sim.step()  # warm-up
-    n, t0 = 0, time.perf_counter()
-    while n < max_steps:
-        sim.step()
-        n += 1
-        if time.perf_counter() - t0 > budget_s:
-            break
-    el = time.perf_counter() - t0
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.environ.get("OPENBLAS_NUM_THREADS", os.cpu_count() or 1)))
-    return {"value": n / el, "unit": "traj-steps/s", "cores": min(threads, os.cpu_count() or 1),
+    rates, nsteps = [], 0
+    for _ in range(nsample):
+        n, t0 = 0, time.perf_counter()
+        while True:
+            sim.step()
+            n += 1
+            if time.perf_counter() - t0 > budget_s / nsample:
+                break
+        rates.append(n / (time.perf_counter() - t0))
+        nsteps += n
+    return {"value": float(np.median(rates)), "unit": "traj-steps/s", "cores": blas_threads(),
             "kind": "port",
-            "sample": "%d md.vv steps of 1 trajectory of the same C3 junction (oracle restatement of "
-                      "sclmd md.vv/phbath.bforce, numpy+OpenBLAS, %s)" % (n, cpu_info())}
+            "sample": "median of %d samples (%d md.vv steps in all) of 1 trajectory of the same junction "
+                      "(oracle restatement of sclmd md.vv/phbath.bforce, reference algorithm shape), "
+                      "numpy %s + %s, %s" % (nsample, nsteps, np.__version__, blas_info(), cpu_info()),
+            "samples": [float(r) for r in rates]}
+
+
+METRIC = "GLE steps/sec/GPU, 300-atom junction, 1024-step kernel, 64-traj ensemble"
+
+
+def refuse_experiment_env():
+    """The release library reads no environment; refuse anything that could select the experiment
+    build or its switches (some of them skip work and give wrong results)."""
+    bad = sorted(k for k in os.environ if k.startswith("GLE_"))
+    lib = os.environ.get("SCLMD_AMD_LIB", "")
+    if bad or ("_exp" in os.path.basename(lib)):
+        raise SystemExit("bench.py: refusing to run with experiment settings %s%s" % (
+            bad, (" SCLMD_AMD_LIB=" + lib) if lib else ""))
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # 512 timed steps = two periods of the largest ladder level (P = 256 at C3), so every level's
-    # blocks are in the window in proportion (a 200-step window under-samples the big levels)
+    # 512 timed steps = two periods of the largest ladder level (P = 256 at C3)
     ap.add_argument("--steps", type=int, default=512)
     ap.add_argument("--warmup", type=int, default=64)
     ap.add_argument("--ntraj", type=int, default=64, help="trajectories per GPU")
-    ap.add_argument("--config", default="C3")
+    ap.add_argument("--config", default="C3", choices=["C2", "C3", "C5"])
     ap.add_argument("--block-len", type=int, default=0)
     ap.add_argument("--max-block", type=int, default=0)
     ap.add_argument("--far-mode", default="auto", choices=["auto", "direct", "spectral"])
@@ -89,18 +134,22 @@ def main():
     ap.add_argument("--noise", default="device", choices=["device", "white"],
                     help="device: coloured noise from the bath spectra (factorised on the host, drawn "
                          "and filtered on the device); white: seeded N(0, 1e-3^2) realisations assigned "
-                         "to bath.noise (throughput runs of configurations whose noise factors do not "
-                         "fit next to the spectral kernels, e.g. C5; the step does the same work)")
+                         "to bath.noise (throughput runs only; the step does the same work)")
+    ap.add_argument("--fill", type=int, default=-1,
+                    help="untimed steps before the warm-up that bring the memory-sum ladder to its steady "
+                         "state (history older than the largest level's window); -1 = 2 x the largest "
+                         "block length")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
                          "rehearse the multi-rank path, e.g. with --same-device on a one-GPU box)")
     ap.add_argument("--same-device", action="store_true",
                     help="every rank on device 0 (rehearsal of the N > 1 control flow on one GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="PMC-derived HBM bytes per dominant-kernel launch (from a rocprofv3 --pmc pass)")
     args = ap.parse_args()
+    refuse_experiment_env()
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -142,12 +191,20 @@ def main():
     m.steps(0)  # uploads assigned noise
     st.sync()
     setup_s = time.perf_counter() - t_setup
-    log("[bench] rank %d setup %.1fs plan %s" % (rank, setup_s, st.plan_info()))
+    plan = st.plan_info()
+    log("[bench] rank %d setup %.1fs plan %s" % (rank, setup_s, plan))
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
+    levels = st.profile_levels()
+    ptop = max([P for P, _ in levels] + [1])
+    fill = 2 * ptop if args.fill < 0 else args.fill
+    t_fill = time.perf_counter()
+    m.steps(fill)
+    st.sync()
+    log("[bench] rank %d ladder fill %d steps (%.2fs)" % (rank, fill, time.perf_counter() - t_fill))
     m.steps(args.warmup)
     st.sync()
     st.profile(True)
@@ -161,6 +218,7 @@ def main():
     el = time.perf_counter() - t0
     log("[bench] rank %d host enqueue %.3f ms of %.3f ms timed" % (rank, t_enq * 1e3, el * 1e3))
     prof = st.profile_read()
+    window_levels = st.profile_levels()
     st.profile(False)
     # one reduce of the time-averaged current statistics (the ensemble output)
     sums = m._reduce(st.current_sums())
@@ -172,14 +230,15 @@ def main():
         el = float(tt.item())
 
     value = world * args.ntraj * args.steps / el
+    ms_per_step = el / args.steps * 1e3
     res = {
-        "metric": "GLE steps/sec/GPU, 300-atom junction, 1024-step kernel, 64-traj ensemble",
+        "metric": METRIC,
         "value": value,
         "unit": "traj-steps/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": el / args.steps * 1e3,
+        "ms_per_step": ms_per_step,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -190,10 +249,23 @@ def main():
                                "%d traj/GPU" % (args.config, meta["natom"], len(baths), meta["nc"],
                                                 meta["ml"], meta["nmd"], args.ntraj),
                    "ntraj_per_gpu": args.ntraj, "ntraj_total": world * args.ntraj,
-                   "block_len": st.plan_info()["block_len"], "far_mode": st.plan_info()["far_mode"],
+                   "block_len": plan["block_len"], "far_mode": plan["far_mode"],
                    "parallelism": "ensemble-dp%d" % world},
         "value_per_gpu": value / world,
         "setup_s": setup_s,
+        "fill_steps": fill,
+        # per ladder level: blocks issued in the timed window vs the steady-state share K / P
+        "ladder_window": [{"P": P, "blocks": round(bl, 3), "steady": round(args.steps / P, 3)}
+                          for P, bl in window_levels],
+    }
+    # whole-step roofline: the algorithm's own work per step (SURVEY.md 8d conventions, gle_step_work)
+    fl_step, by_step = st.step_work()
+    res["step_roofline"] = {
+        "flops_per_step": fl_step, "bytes_per_step": by_step,
+        "achieved_tflops": fl_step / (ms_per_step * 1e-3) / 1e12,
+        "frac_mfma": fl_step / (ms_per_step * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS,
+        "achieved_gbs": by_step / (ms_per_step * 1e-3) / 1e9,
+        "frac_hbm": by_step / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
     }
     if prof["launches"] > 0:
         avg_ms = prof["ms"] / prof["launches"]
@@ -212,11 +284,11 @@ def main():
             with open(args.traffic_json) as f:
                 tj = json.load(f)
             if (tj.get("config") == args.config and tj.get("ntraj") == args.ntraj
-                    and tj.get("far_mode") == st.plan_info()["far_mode"]):
+                    and tj.get("far_mode") == plan["far_mode"]):
                 roof["traffic"] = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass
-        if st.plan_info()["far_mode"] == "spectral":
+        if plan["far_mode"] == "spectral":
             kname = ("cgemm_kernel (far field: per-frequency Gauss 3-multiplication GEMMs of the "
                      "spectral ladder levels)")
         else:

@@ -21,7 +21,7 @@
  * bad shapes, e.g. baths.py:115-116, md.py:171-176: here errors are reported, never exit.)
  *
  * Threading: a handle is bound to one HIP device and one stream and is not thread-safe.
- * Multi-GPU = one handle per process/device (torch.distributed + RCCL reduce in the shim).
+ * Multi-GPU = one handle per process/device; the ensemble reduce is gle_reduce_current over RCCL.
  */
 #ifndef HIPGLE_H
 #define HIPGLE_H
@@ -172,6 +172,20 @@ int gle_get_energy(gle_handle* h, double* etot);
  * out: [nbath][3] */
 int gle_current_sums(gle_handle* h, double* out);
 
+/* ---- ensemble reduce ------------------------------------------------ */
+/* The per-run heat-current statistics of the whole ensemble: out [nbath][3] = the sum over every
+ * rank's gle_current_sums, by one RCCL all-reduce (sum, fp64) over xGMI on the handle's stream.
+ * comm: an RCCL communicator (ncclComm_t, e.g. from gle_comm_init) with one rank per handle, or
+ * NULL for this handle's trajectories alone.  Collective: every rank of comm must call it. */
+int gle_reduce_current(gle_handle* h, void* comm, double* out);
+/* RCCL communicator helpers for C callers without their own RCCL setup: rank 0 makes the id
+ * (GLE_COMM_ID_BYTES opaque bytes), the caller distributes it (MPI, sockets, torch.distributed),
+ * every rank then calls gle_comm_init with its own rank and HIP device. */
+#define GLE_COMM_ID_BYTES 128
+int gle_comm_unique_id(char* id);
+int gle_comm_init(int32_t nranks, int32_t rank, int32_t device, const char* id, void** comm);
+int gle_comm_destroy(void* comm);
+
 /* ---- measurement ---------------------------------------------------------------------- */
 /* Record HIP events around every launch of the memory-kernel contraction (the dominant kernel)
  * on the handle's stream. */
@@ -184,6 +198,14 @@ int gle_profile_read(gle_handle* h, int64_t* nlaunch, double* total_ms, double* 
  * device memory in use, far-field mode actually chosen. */
 int gle_plan_info(gle_handle* h, int64_t* block_len, int64_t* far_items, int64_t* device_bytes,
                   int32_t* far_mode);
+/* Memory-sum ladder levels: *nlevel = number of levels; for the first nmax levels the block length
+ * P[l] and the blocks of that level issued since profiling was enabled (a block issued in pieces
+ * counts its pieces' share).  Over a window of K steps a level in steady state issues K / P. */
+int gle_profile_levels(gle_handle* h, int32_t nmax, int32_t* nlevel, int32_t* P, double* blocks);
+/* Algorithmic work of one steady-state harmonic step of the plan, all trajectories on this device:
+ * flops and bytes (every matrix entry read once, every product counted once, no padding; ladder
+ * blocks averaged over their period).  Requires a plan (after gle_set_state). */
+int gle_step_work(gle_handle* h, double* flops, double* bytes);
 
 #ifdef __cplusplus
 }

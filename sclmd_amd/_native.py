@@ -26,6 +26,8 @@ EXPORTS = [
     "gle_noise_factors", "gle_noise_generate", "gle_step_begin", "gle_step_end", "gle_run",
     "gle_sync", "gle_get_current", "gle_get_energy", "gle_current_sums", "gle_profile",
     "gle_profile_read", "gle_plan_info", "gle_add_bath_gmem", "gle_get_kernel", "gle_gamt",
+    "gle_profile_levels", "gle_step_work", "gle_reduce_current", "gle_comm_unique_id", "gle_comm_init",
+    "gle_comm_destroy",
 ]
 
 
@@ -79,6 +81,14 @@ _SIGS = {
     "gle_profile": (ctypes.c_int, [_P, ctypes.c_int32]),
     "gle_profile_read": (ctypes.c_int, [_P, _I64, _D, _D, _D]),
     "gle_plan_info": (ctypes.c_int, [_P, _I64, _I64, _I64, ctypes.POINTER(ctypes.c_int32)]),
+    "gle_profile_levels": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32),
+                                          ctypes.POINTER(ctypes.c_int32), _D]),
+    "gle_step_work": (ctypes.c_int, [_P, _D, _D]),
+    "gle_reduce_current": (ctypes.c_int, [_P, _P, _D]),
+    "gle_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
+    "gle_comm_init": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p,
+                                     ctypes.POINTER(_P)]),
+    "gle_comm_destroy": (ctypes.c_int, [_P]),
 }
 
 _lib = None
@@ -138,6 +148,39 @@ def gamt_device(W, G, device=0):
     if rc != 0:
         raise GLEError("gle_gamt failed (%s): %s" % (_ERRNAMES.get(rc, rc), lib.gle_last_error(None).decode()))
     return out.reshape((ml,) + tail)
+
+
+COMM_ID_BYTES = 128
+
+
+def comm_unique_id():
+    """RCCL unique id (bytes) for gle_comm_init; made by one rank, shared by the caller."""
+    lib = load()
+    buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+    rc = lib.gle_comm_unique_id(buf)
+    if rc != 0:
+        raise GLEError("gle_comm_unique_id failed: %s" % lib.gle_last_error(None).decode())
+    return buf.raw
+
+
+class Comm:
+    """RCCL communicator of the C-ABI (gle_comm_init): one rank per process and device."""
+
+    def __init__(self, nranks, rank, device, uid):
+        self.lib = load()
+        if len(uid) != COMM_ID_BYTES:
+            raise ValueError("unique id must be %d bytes" % COMM_ID_BYTES)
+        c = _P()
+        rc = self.lib.gle_comm_init(int(nranks), int(rank), int(device), uid, ctypes.byref(c))
+        if rc != 0:
+            raise GLEError("gle_comm_init failed (%s): %s" % (_ERRNAMES.get(rc, rc),
+                                                              self.lib.gle_last_error(None).decode()))
+        self.c = c
+
+    def close(self):
+        if getattr(self, "c", None):
+            self.lib.gle_comm_destroy(self.c)
+            self.c = None
 
 
 class Stepper:
@@ -309,6 +352,14 @@ class Stepper:
         self._chk(self.lib.gle_current_sums(self.h, _ptr(out)), "gle_current_sums")
         return out
 
+    def reduce_current(self, comm=None):
+        """Ensemble current statistics [nbath][3] summed over the ranks of an RCCL Comm (None: this
+        handle only) -- gle_reduce_current."""
+        out = np.empty((self.nbath, 3))
+        self._chk(self.lib.gle_reduce_current(self.h, None if comm is None else comm.c, _ptr(out)),
+                  "gle_reduce_current")
+        return out
+
     def profile(self, enable=True):
         self._chk(self.lib.gle_profile(self.h, 1 if enable else 0), "gle_profile")
 
@@ -327,3 +378,19 @@ class Stepper:
         names = {v: k for k, v in FAR_MODES.items()}
         return {"block_len": int(a.value), "far_items": int(b.value), "device_bytes": int(c.value),
                 "far_mode": names.get(int(m.value), int(m.value))}
+
+    def profile_levels(self):
+        """[(P, blocks issued since profiling was enabled)] per ladder level."""
+        n = ctypes.c_int32(0)
+        self._chk(self.lib.gle_profile_levels(self.h, 0, ctypes.byref(n), None, None), "gle_profile_levels")
+        P = (ctypes.c_int32 * max(1, n.value))()
+        bl = np.zeros(max(1, n.value))
+        self._chk(self.lib.gle_profile_levels(self.h, n.value, ctypes.byref(n), P, _ptr(bl)),
+                  "gle_profile_levels")
+        return [(int(P[i]), float(bl[i])) for i in range(n.value)]
+
+    def step_work(self):
+        """Algorithmic (flops, bytes) of one steady-state step of the plan (gle_step_work)."""
+        fl, by = ctypes.c_double(0), ctypes.c_double(0)
+        self._chk(self.lib.gle_step_work(self.h, ctypes.byref(fl), ctypes.byref(by)), "gle_step_work")
+        return fl.value, by.value

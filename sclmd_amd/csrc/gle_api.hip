@@ -18,6 +18,8 @@
 #include <string>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "../../include/hipgle.h"
 #include "gle_internal.h"
 
@@ -197,6 +199,7 @@ struct gle_handle {
   size_t ev_used = 0;
   int64_t prof_n = 0;
   double prof_ms = 0, prof_flops = 0, prof_bytes = 0;
+  double prof_blocks[MAXLVL] = {};  // ladder blocks issued per level since profiling was enabled
 };
 
 namespace {
@@ -674,13 +677,13 @@ int plan_chain(gle_handle* h) {
   const int64_t B = h->B;
   const int nb = (int)h->baths.size();
   const int ntile = h->ndblk;
-  if (const char* e = getenv("GLE_CHAIN_NW")) {
+  if (const char* e = gle_env("GLE_CHAIN_NW")) {
     int v[3] = {4, 8, 4};
     sscanf(e, "%d,%d,%d", &v[0], &v[1], &v[2]);
     for (int i = 0; i < 3; ++i) h->ch_nw[i] = v[i] >= 16 ? 16 : (v[i] >= 8 ? 8 : 4);
   }
-  if (const char* e = getenv("GLE_CHAIN_DRN")) h->ch_drn = atoi(e) >= 2 ? 2 : 1;
-  const char* near_in = getenv("GLE_NEAR_IN");
+  if (const char* e = gle_env("GLE_CHAIN_DRN")) h->ch_drn = atoi(e) >= 2 ? 2 : 1;
+  const char* near_in = gle_env("GLE_NEAR_IN");
   if (!near_in) near_in = "AC";
   const int drn = (int)std::min<int64_t>(h->ch_drn, (B + 15) / 16);
   h->ch_drn = drn;
@@ -781,7 +784,7 @@ int plan_chain(gle_handle* h) {
         if (owner[d] >= 0) disjoint = false;
         owner[d] = j;
       }
-    const char* e = getenv("GLE_FUSE_BC");
+    const char* e = gle_env("GLE_FUSE_BC");
     h->fuse_bc = h->has_dyn && disjoint && nb > 0 && !(e && atoi(e) == 0);
   }
   if (h->fuse_bc) {
@@ -890,7 +893,7 @@ int plan_chain(gle_handle* h) {
   const int rn_raw = (int)std::min<int64_t>(4, (B + 15) / 16);
   const int nt_raw = 16 * rn_raw;
   const int ncolr = (int)((B + nt_raw - 1) / nt_raw);
-  const char* env = getenv("GLE_NEAR_KS");
+  const char* env = gle_env("GLE_NEAR_KS");
   const int raw_ks = env ? std::max(4, atoi(env)) : 24;
   for (auto& b : h->baths) {
     b.NRS = std::max(2, b.nn + 1);
@@ -1266,7 +1269,7 @@ int freeze(gle_handle* h) {
       hipDeviceProp_t prop;
       if (hipGetDeviceProperties(&prop, h->cfg.device) == hipSuccess) ncu = prop.multiProcessorCount;
       if (n4 < 2 * ncu) {
-        if (getenv("GLE_CG_NARROW")) lv.cg_rn = 2;
+        if (gle_env("GLE_CG_NARROW")) lv.cg_rn = 2;
         else lv.cg_split = 2;
       }
     }
@@ -1412,11 +1415,11 @@ int freeze(gle_handle* h) {
         if (hipGetDeviceProperties(&prop, h->cfg.device) == hipSuccess) ncu = prop.multiProcessorCount;
         const int nslot = std::max(1, lv.P / h->P0);
         double per_cu = 2.0;  // GLE_CG_PER_CU: workgroups per CU per chunk (experiment switch)
-        if (const char* e = getenv("GLE_CG_PER_CU")) per_cu = std::max(0.25, atof(e));
+        if (const char* e = gle_env("GLE_CG_PER_CU")) per_cu = std::max(0.25, atof(e));
         const double want = (double)lv.cg.size() / (per_cu * ncu);
-        const int64_t nch = getenv("GLE_CG_CEIL") ? (int64_t)std::ceil(want - 1e-9) : (int64_t)want;
+        const int64_t nch = gle_env("GLE_CG_CEIL") ? (int64_t)std::ceil(want - 1e-9) : (int64_t)want;
         lv.ncg_chunk = (int)std::max<int64_t>(1, std::min<int64_t>(nch, nslot));
-        if (const char* e = getenv("GLE_NO_PIECES")) lv.ncg_chunk = atoi(e) > 0 ? 1 : lv.ncg_chunk;
+        if (const char* e = gle_env("GLE_NO_PIECES")) lv.ncg_chunk = atoi(e) > 0 ? 1 : lv.ncg_chunk;
         lv.npiece = lv.ncg_chunk + 2;
       }
     } else {
@@ -1470,7 +1473,7 @@ int freeze(gle_handle* h) {
   sd.part = h->d_part;
   sd.cmask = h->d_cmask;
   sd.ndblk = h->ndblk;
-  if (const char* dbg = getenv("GLE_CHAIN_DBG")) {
+  if (const char* dbg = gle_env("GLE_CHAIN_DBG")) {
     size_t n = 0;
     for (Chain* c : {&h->chA[1], &h->chB[1], &h->chC}) n = std::max(n, c->tiles.size());
     sd.dbg_ntile = (int32_t)n;
@@ -1525,10 +1528,12 @@ int launch_level_pieces(gle_handle* h, Level& lv, int64_t k, hipStream_t s, bool
   const int64_t T = (k - 1) * (int64_t)lv.P;
   const StepArgs ta = step_args(h, T);
   const int par = (int)(k & 1);
+  const int li = (int)(&lv - h->levels.data());
   for (int j = j0; j < j1; ++j) {
     if (!lv.spectral) {
       // profiled only when no level is spectral: the roofline then names one kernel class
       if (priming || !(h->dbg_skip & 8)) run_op(h, lv.op[par], s, ta, h->far_mode != GLE_FAR_SPECTRAL);
+      if (h->prof && !priming) h->prof_blocks[li] += 1.0;
       continue;
     }
     if (j == 0) {
@@ -1554,6 +1559,7 @@ int launch_level_pieces(gle_handle* h, Level& lv, int64_t k, hipStream_t s, bool
       }
       if (priming || !(h->dbg_skip & 1))
         launch_cgemm(lv.cg_rn, lv.d_cg + c0, (int)(c1 - c0), T / lv.P, s, priming ? 0 : h->bg_grid);
+      if (h->prof && !priming) h->prof_blocks[li] += (double)(c1 - c0) / (double)n;
       if (e1) {
         hipEventRecord(e1, s);
         const double frac = (double)(c1 - c0) / (double)n;
@@ -1584,8 +1590,12 @@ int launch_level_block(gle_handle* h, Level& lv, int64_t k, hipStream_t s, bool 
   return launch_level_pieces(h, lv, k, s, priming, 0, lv.npiece);
 }
 
-// After set_state / set_history: S(t) from the whole history, and the two level blocks that cover
-// targets t+1 .. (the next block boundary) + P, all on the main stream.
+// After set_state / set_history: S(t) from the whole history and, per level, block k0 = floor(t/P)
+// (targets up to the next block boundary) on the main stream.  Block k0 + 1 enters the level's
+// piece schedule at once, as if it had been started at the boundary k0 P: its pieces go out on
+// the background stream over the first-level boundaries up to (k0 + 1) P (the ones already passed
+// at the first step), so every window of steps after a prime carries the steady-state share of
+// far-field work.
 int prime(gle_handle* h) {
   join_bg(h);  // blocks still in flight read the ring and write the buffers recomputed here
   const StepArgs ta = step_args(h);
@@ -1601,18 +1611,25 @@ int prime(gle_handle* h) {
   for (auto& lv : h->levels) {
     const int64_t k0 = floordiv(h->t, lv.P);
     int rc = launch_level_block(h, lv, k0, h->stream, true);
-    if (!rc) rc = launch_level_block(h, lv, k0 + 1, h->stream, false);
     if (rc) return rc;
     lv.last_block = k0 + 1;
     lv.bg_block[0] = lv.bg_block[1] = INT64_MIN;
-    lv.pend_block = INT64_MIN;
+    lv.bg_block[(k0 + 1) & 1] = k0 + 1;  // the main stream waits for it at (k0 + 1) P
+    lv.pend_block = k0 + 1;
+    lv.pend_t0 = k0 * (int64_t)lv.P;
+    lv.next_piece = 0;
   }
   // near-field partials of target t+1 (lags >= 2: p up to t-1), as the chain of step t-1 leaves them
   for (auto& b : h->baths)
     launch_near_fill(b.d_H, b.ldh, b.R, (int)h->B, b.ncp, b.d_NR, b.vs, b.NRS, h->t, h->stream);
   launch_chain(1, h->chNear.nw, h->ch_drn, h->chNear.lds, h->chNear.d, (int)h->chNear.tiles.size(), h->d_sd,
                step_args(h, h->t - 1), 0, h->stream);
-  if (!h->levels.empty()) HIPCHK(h, hipEventRecord(h->ev_step, h->stream));
+  if (!h->levels.empty()) {
+    // the pending blocks' pieces read what this prime wrote (segment spectra, ring)
+    HIPCHK(h, hipEventRecord(h->ev_step, h->stream));
+    for (int i = 0; i < gle_handle::NBG; ++i)
+      if (h->bg[i]) HIPCHK(h, hipStreamWaitEvent(h->bg[i], h->ev_step, 0));
+  }
   h->need_prime = false;
   return GLE_OK;
 }
@@ -1783,11 +1800,11 @@ int gle_create(const gle_config* cfg, gle_handle** out) {
   h->nmd = cfg->nmd;
   h->dt = cfg->dt;
   h->nphp = rup(h->nph, 8);
-  h->dbg_no_ladder = getenv("GLE_DBG_NO_LADDER") != nullptr;
-  if (const char* e = getenv("GLE_DBG_SKIP")) h->dbg_skip = atoi(e);
-  if (const char* e = getenv("GLE_BG_GRID")) h->bg_grid = std::max(0, atoi(e));
-  if (const char* e = getenv("GLE_PIECE_SLACK")) h->piece_slack = std::max(0, atoi(e));
-  if (const char* e = getenv("GLE_MERGE_WAITS")) h->merge_waits = atoi(e) != 0;
+  h->dbg_no_ladder = gle_env("GLE_DBG_NO_LADDER") != nullptr;
+  if (const char* e = gle_env("GLE_DBG_SKIP")) h->dbg_skip = atoi(e);
+  if (const char* e = gle_env("GLE_BG_GRID")) h->bg_grid = std::max(0, atoi(e));
+  if (const char* e = gle_env("GLE_PIECE_SLACK")) h->piece_slack = std::max(0, atoi(e));
+  if (const char* e = gle_env("GLE_MERGE_WAITS")) h->merge_waits = atoi(e) != 0;
   // main stream (the latency-bound per-step chain) at the highest priority, background streams
   // (ladder blocks) at the lowest
   {
@@ -1797,7 +1814,7 @@ int gle_create(const gle_config* cfg, gle_handle** out) {
     // GLE_BG_RESERVE=R: the background streams stay off CU mask bits [0, R), which the per-step
     // chain then finds free at every launch
     int reserve = 0;
-    if (const char* r = getenv("GLE_BG_RESERVE")) reserve = std::max(0, atoi(r));
+    if (const char* r = gle_env("GLE_BG_RESERVE")) reserve = std::max(0, atoi(r));
     std::vector<uint32_t> cumask;
     if (reserve > 0) {
       hipDeviceProp_t prop;
@@ -2542,6 +2559,7 @@ int gle_profile(gle_handle* h, int32_t enable) {
   h->ev_used = 0;
   h->prof_n = 0;
   h->prof_ms = h->prof_flops = h->prof_bytes = 0;
+  for (double& b : h->prof_blocks) b = 0.0;
   return GLE_OK;
 }
 
@@ -2557,6 +2575,79 @@ int gle_profile_read(gle_handle* h, int64_t* nlaunch, double* total_ms, double* 
   return GLE_OK;
 }
 
+int gle_profile_levels(gle_handle* h, int32_t nmax, int32_t* nlevel, int32_t* P, double* blocks) {
+  if (!h || nmax < 0) return GLE_ERR_ARG;
+  const int n = (int)h->levels.size();
+  if (nlevel) *nlevel = n;
+  for (int l = 0; l < n && l < nmax; ++l) {
+    if (P) P[l] = h->levels[l].P;
+    if (blocks) blocks[l] = h->prof_blocks[l];
+  }
+  return GLE_OK;
+}
+
+// Algorithmic work of one steady-state harmonic step of the plan, all trajectories (SURVEY.md 8d
+// conventions: every matrix entry read once, every product counted once, no padding):
+//   chain  K0.p_t, K_1.p_t + near lags [2, nn) (S(t+1)), the velocity stage's products (fused:
+//          K0.p_half, K0^2.p_half, K0.V, K0.Fpot or (K0 P dyn).q~, dyn.q~; else K0.p_half, K0.p1,
+//          dyn.q~) and the bias products;
+//   ladder per level (block work) / P: spectral = Gauss GEMMs + segment / inverse transforms
+//          (5 N log2 N per complex length-N transform, two real series each), direct = contraction.
+int gle_step_work(gle_handle* h, double* flops, double* bytes) {
+  if (!h) return GLE_ERR_ARG;
+  if (!h->frozen) return fail(h, GLE_ERR_STATE, "no plan yet (call gle_set_state first)");
+  const double B = (double)h->B;
+  double fl = 0.0, by = 0.0;
+  double dyn_nnz = 0.0;
+  for (double v : h->dyn_h) dyn_nnz += v != 0.0 ? 1.0 : 0.0;
+  for (const Bath& b : h->baths) {
+    const double nc2 = (double)b.nc * b.nc;
+    double kd_nnz = 0.0;  // entries of K0 P dyn in its nonzero 16 x 4 blocks (fused stage)
+    for (size_t rt = 0; rt < b.kd_rng.size(); ++rt) {
+      int rows = 0;
+      for (int r = 0; r < 16 && 16 * (int64_t)rt + r < h->nph; ++r) rows += b.inv[16 * rt + r] >= 0 ? 1 : 0;
+      for (const auto& r : b.kd_rng[rt]) kd_nnz += 4.0 * r.second * rows;
+    }
+    double nprod = 1.0;                              // K0.p_t (stage A)
+    if (b.ml > 1) nprod += (double)(b.nn - 1);       // K_1 + near lags [2, nn)
+    nprod += h->fuse_bc ? 3.0 : 2.0;                 // K0.p_half, K0^2.p_half / K0.V | K0.p1
+    if (b.has_q) nprod += h->fuse_bc ? 3.0 : 2.0;    // Kq.q_t, Kq.q~ (+ K0 Kq.q~)
+    fl += 2.0 * nc2 * B * nprod;
+    by += 8.0 * nc2 * ((double)b.nn + (h->fuse_bc ? 1.0 : 0.0) + (b.has_q ? 2.0 : 0.0));
+    if (h->fuse_bc) {
+      fl += 2.0 * kd_nnz * B;  // (K0 P dyn).q~ on a potential-cache miss (every harmonic step)
+      by += 8.0 * kd_nnz;
+    }
+    by += 8.0 * 12.0 * b.nc * B;  // bath-local vectors: noise rows, S, V, gathers, ring pushes
+  }
+  fl += 2.0 * dyn_nnz * B;  // dyn.q~ (the potential force at q~)
+  by += 8.0 * dyn_nnz + 8.0 * 12.0 * (double)h->nph * B;  // dyn, state vectors (p, q, p_half, q~, F, caches)
+  for (const Level& lv : h->levels) {
+    const double P = (double)lv.P;
+    if (lv.spectral) {
+      const double N = 2.0 * P;
+      double nser = 0.0;  // complex transforms per block (two real series each), per direction
+      for (size_t j = 0; j < h->baths.size(); ++j)
+        if (lv.lb[j].active) nser += (double)h->baths[j].nc * B / 2.0;
+      const double fft = 2.0 * nser * 5.0 * N * std::log2(N);
+      double fby = 0.0;
+      for (size_t j = 0; j < h->baths.size(); ++j)
+        if (lv.lb[j].active) {
+          const double ncb = (double)h->baths[j].nc * B;
+          fby += 8.0 * ncb * (N + 3.0 * (P + 1.0)) + 8.0 * ncb * (3.0 * (P + 1.0) * lv.cg_split + P);
+        }
+      fl += (lv.cg_flops + fft) / P;
+      by += (lv.cg_bytes + fby) / P;
+    } else {
+      fl += lv.op[0].flops / P;
+      by += lv.op[0].bytes / P;
+    }
+  }
+  if (flops) *flops = fl;
+  if (bytes) *bytes = by;
+  return GLE_OK;
+}
+
 int gle_plan_info(gle_handle* h, int64_t* block_len, int64_t* far_items, int64_t* device_bytes,
                   int32_t* far_mode) {
   if (!h) return GLE_ERR_ARG;
@@ -2566,6 +2657,59 @@ int gle_plan_info(gle_handle* h, int64_t* block_len, int64_t* far_items, int64_t
   if (far_mode) *far_mode = h->frozen ? h->far_mode : h->cfg.far_mode;
   if (far_items) *far_items = items;
   if (device_bytes) *device_bytes = (int64_t)h->dev_bytes;
+  return GLE_OK;
+}
+
+// ---- ensemble reduce over RCCL (SURVEY.md 8b gle_reduce_current, 8e) ----------------------
+static_assert(GLE_COMM_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "RCCL unique-id size");
+
+int gle_comm_unique_id(char* id) {
+  if (!id) return fail(nullptr, GLE_ERR_ARG, "null id buffer");
+  ncclUniqueId u;
+  const ncclResult_t r = ncclGetUniqueId(&u);
+  if (r != ncclSuccess) return fail(nullptr, GLE_ERR_HIP, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+  memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+  return GLE_OK;
+}
+
+int gle_comm_init(int32_t nranks, int32_t rank, int32_t device, const char* id, void** comm) {
+  if (!id || !comm || nranks < 1 || rank < 0 || rank >= nranks) return fail(nullptr, GLE_ERR_ARG, "bad communicator arguments");
+  *comm = nullptr;
+  if (hipSetDevice(device) != hipSuccess) return fail(nullptr, GLE_ERR_HIP, "gle_comm_init: no such device");
+  ncclUniqueId u;
+  memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+  ncclComm_t c = nullptr;
+  const ncclResult_t r = ncclCommInitRank(&c, nranks, u, rank);
+  if (r != ncclSuccess) return fail(nullptr, GLE_ERR_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  *comm = (void*)c;
+  return GLE_OK;
+}
+
+int gle_comm_destroy(void* comm) {
+  if (!comm) return GLE_OK;
+  const ncclResult_t r = ncclCommDestroy((ncclComm_t)comm);
+  if (r != ncclSuccess) return fail(nullptr, GLE_ERR_HIP, std::string("ncclCommDestroy: ") + ncclGetErrorString(r));
+  return GLE_OK;
+}
+
+int gle_reduce_current(gle_handle* h, void* comm, double* out) {
+  if (!h || !out) return GLE_ERR_ARG;
+  const size_t n = 3 * h->baths.size();
+  if (n == 0) return GLE_OK;
+  int rc = gle_current_sums(h, out);  // this handle's [sum mean, sum mean^2, ntraj] per bath
+  if (rc || !comm) return rc;
+  hipSetDevice(h->cfg.device);
+  double* d = nullptr;
+  HIPCHK(h, hipMalloc((void**)&d, n * 8));
+  hipError_t e = hipMemcpyAsync(d, out, n * 8, hipMemcpyHostToDevice, h->stream);
+  ncclResult_t r = ncclSuccess;
+  if (e == hipSuccess) r = ncclAllReduce(d, d, n, ncclDouble, ncclSum, (ncclComm_t)comm, h->stream);
+  if (e == hipSuccess && r == ncclSuccess) e = hipMemcpyAsync(out, d, n * 8, hipMemcpyDeviceToHost, h->stream);
+  const hipError_t es = hipStreamSynchronize(h->stream);
+  hipFree(d);
+  if (r != ncclSuccess) return fail(h, GLE_ERR_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+  if (e != hipSuccess || es != hipSuccess)
+    return fail(h, GLE_ERR_HIP, std::string("reduce copies: ") + hipGetErrorString(e != hipSuccess ? e : es));
   return GLE_OK;
 }
 

@@ -13,8 +13,21 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 namespace gle {
+
+// Experiment switches (GLE_* environment variables: plan variants, timing-only variants that skip
+// work and give wrong results, timelines) exist only in a -DGLE_EXPERIMENTS build
+// (`make experiments`).  The release library reads no environment at all.
+inline const char* gle_env(const char* name) {
+#ifdef GLE_EXPERIMENTS
+  return std::getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
 
 constexpr int WG = 256;            // threads per workgroup of the contraction kernel (4 waves)
 constexpr int KC = 2;              // k-steps (4 rows each) staged per LDS stage

@@ -829,25 +829,26 @@ static int g_cg_kc = 0;    // k-steps per LDS chunk: 4 (159 VGPRs, 3 waves/SIMD;
 void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStream_t s, int max_grid) {
   if (nitems <= 0) return;
   if (g_cg_xcd < 0) {
-    const char* e = getenv("GLE_CG_XCD");
+    const char* e = gle_env("GLE_CG_XCD");
     g_cg_xcd = (e && atoi(e) == 0) ? 0 : 1;
-    const char* k = getenv("GLE_CG_KC");
+    const char* k = gle_env("GLE_CG_KC");
     g_cg_kc = (k && atoi(k) == 8) ? 8 : 4;
     // 1: no K-hat loads, 2: no LDS operand reads, 4: no X staging / barrier; 3, 7: combinations
-    const char* d = getenv("GLE_CG_DBG");
+    const char* d = gle_env("GLE_CG_DBG");
     g_cg_dbg = d ? std::max(0, std::min(7, atoi(d))) : 0;
   }
   // GLE_CG_LDS_PAD (bytes, experiment switch): unused dynamic LDS per workgroup, capping how many
   // far-field workgroups a CU holds so the per-step chain's workgroups find room beside them
   static int lds_pad = -1;
   if (lds_pad < 0) {
-    const char* e = getenv("GLE_CG_LDS_PAD");
+    const char* e = gle_env("GLE_CG_LDS_PAD");
     lds_pad = e ? std::max(0, std::min(96 * 1024, atoi(e))) : 0;
   }
   const size_t shm = (size_t)lds_pad;
   const bool capped = max_grid > 0 && max_grid < nitems;
   const int xcd = (!capped && g_cg_xcd) ? 1 : 0;
   const int grid = capped ? max_grid : (xcd ? (nitems + 7) / 8 * 8 : nitems);
+#ifdef GLE_EXPERIMENTS
   if (g_cg_dbg && rn == 4 && g_cg_kc == 4) {  // GLE_CG_DBG timing experiments (results invalid)
     if (g_cg_dbg == 1) cgemm_kernel<4, 4, 1><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd);
     else if (g_cg_dbg == 2) cgemm_kernel<4, 4, 2><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd);
@@ -856,6 +857,7 @@ void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStre
     else cgemm_kernel<4, 4, 7><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd);
     return;
   }
+#endif
   if (g_cg_kc == 4) {
     switch (rn) {
       case 1: cgemm_kernel<1, 4><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd); break;

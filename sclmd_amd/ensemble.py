@@ -36,9 +36,12 @@ def shard(ntraj_total, rank_, world):
     return offset, count
 
 
-def allreduce_sums(sums, group=None):
+def allreduce_sums(sums, group=None, device=None):
     """Sum the per-rank [sum_b mean_t cur, sum_b (mean_t cur)^2, ntraj] rows over all ranks with a
-    single collective (fp64).  A no-op without an initialised process group."""
+    single collective (fp64).  A no-op without an initialised process group.  device: the HIP
+    device of this rank's stepper; with the nccl backend (RCCL) the tensor goes there and it
+    becomes torch's current device (a script that never called torch.cuda.set_device would
+    otherwise put every rank's all-reduce on device 0)."""
     d = _dist()
     sums = np.asarray(sums, dtype=np.float64)
     if d is None:
@@ -46,7 +49,12 @@ def allreduce_sums(sums, group=None):
     import torch
 
     backend = d.get_backend(group)
-    dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+    if backend == "nccl":
+        if device is not None and torch.cuda.current_device() != int(device):
+            torch.cuda.set_device(int(device))
+        dev = torch.device("cuda", torch.cuda.current_device())
+    else:
+        dev = torch.device("cpu")
     t = torch.from_numpy(np.ascontiguousarray(sums)).to(dev)
     d.all_reduce(t, op=d.ReduceOp.SUM, group=group)
     return t.cpu().numpy()

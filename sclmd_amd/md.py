@@ -350,9 +350,7 @@ class md:
             return self._st
         if self.nph is None:
             raise ValueError("md: the number of degrees of freedom is not set (axyz/dyn)")
-        dev = self.device
-        if dev is None:
-            dev = int(os.environ.get("LOCAL_RANK", "0")) if _native.device_count() > 1 else 0
+        dev = self._device_ordinal()
         st = _native.Stepper(self.nph, self.ntraj, self.nmd, self.dt, dev, self.block_len, self.far_mode,
                              self.max_block)
         for b in self.baths:
@@ -533,7 +531,12 @@ class md:
     def _reduce(self, sums):
         from . import ensemble
 
-        return ensemble.allreduce_sums(sums, self.comm)
+        return ensemble.allreduce_sums(sums, self.comm, device=self._device_ordinal())
+
+    def _device_ordinal(self):
+        if self.device is not None:
+            return int(self.device)
+        return int(os.environ.get("LOCAL_RANK", "0")) if _native.device_count() > 1 else 0
 
     def _is_root(self):
         from . import ensemble
@@ -606,6 +609,8 @@ class md:
         if self.saveall:
             for i, b in enumerate(self.baths):
                 nz = np.asarray(b.noise)
+                if multi and nz.ndim == 2:  # one host-injected realisation shared by every trajectory
+                    nz = np.broadcast_to(nz, (self.ntraj,) + nz.shape)
                 if multi:  # (ntraj, nmd, nc) -> (nmd, ntraj, nc): the record dimension comes first
                     f.createDimension("traj" + str(i), nz.shape[0])
                     C.Write2NetCDFFile(f, np.transpose(nz, (1, 0, 2)), "noise" + str(i),
@@ -730,9 +735,10 @@ class md:
                         fk.write("%i %f    %f \n" % (j, self.T, kap[ii]))
                 if self.saveq:
                     self._avestructure(j)
-                if self.rmnc and os.path.exists(self._ncname(j - 1)):  # md.py:676-679
-                    self._log("Remove " + self._ncname(j - 1))
-                    os.remove(self._ncname(j - 1))
+            # every rank removes its own shard of the previous run's file (md.py:676-679)
+            if self.rmnc and os.path.exists(self._ncname(j - 1)):
+                self._log("Remove " + self._ncname(j - 1))
+                os.remove(self._ncname(j - 1))
 
     def _write_frame(self, fh, tt):
         q = self.q if self.ntraj == 1 else self.q[0]
