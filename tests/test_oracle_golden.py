@@ -136,3 +136,63 @@ def test_tools_tables():
     np.testing.assert_allclose([m, s], g["tc_2"], rtol=1e-6)
     m, s = O.conductance(kb, 0.1, float(g["T"]), 1, 3)
     np.testing.assert_allclose([m, s], g["tc_3"], rtol=1e-6)
+
+
+@pytest.mark.parametrize("case", vv_cases())
+def test_batch_oracle_matches_reference_trajectory(case):
+    """GLEBatch (one memory-tail product per step, trajectories in columns) reproduces the
+    reference-generated vv trajectories (ntr = 1) like GLE does."""
+    from oracle import sclmd_oracle as O
+
+    g = load_golden(case)
+    sim = oracle_from_golden(g)
+    bt = O.GLEBatch(sim.nph, sim.dt, sim.nmd, sim.baths, g["dyn_md"], ntr=1, constr=sim.constr)
+    bt.p, bt.q = g["p0"].copy()[:, None], g["q0"].copy()[:, None]
+    nmd, cur = int(g["nmd"]), []
+    for _ in range(int(g["nsteps"])):
+        t = bt.t
+        bt.step()
+        cur.append([c[0, t % nmd] for c in bt.cur])
+    assert close(bt.q[:, 0], g["q"][-1], 1e-12) and close(bt.p[:, 0], g["p"][-1], 1e-12)
+    assert close(cur, g["cur"], 1e-11)
+
+
+def test_batch_oracle_matches_reference_shaped_oracle_long_memory():
+    """GLEBatch vs GLE with a 64-slice kernel, a nonzero history, an unaligned start, a biased
+    electron bath and constraints: three distinct trajectories, 150 steps (1e-12)."""
+    from oracle import sclmd_oracle as O
+    from sclmd_amd import synthetic
+
+    rng = np.random.default_rng(3)
+    dyn, _, baths, meta = synthetic.junction("C5", natom=12, ml=64, nmd=128, nw=60, seed=4)
+    nph, dt, nmd = meta["nph"], meta["dt"], meta["nmd"]
+    ntr, t0, nst = 3, 11, 150
+    p = rng.normal(size=(nph, ntr)) * 1e-3
+    q = rng.normal(size=(nph, ntr)) * 1e-3
+    hist = [rng.normal(size=(ntr, b.ml, b.nc)) * 1e-3 for b in baths]
+    noise = [rng.normal(size=(ntr, nmd, b.nc)) * 1e-3 for b in baths]
+    constr = [range(0, 3)]
+
+    def obath(b, nz):
+        if b.kind == "ebath":
+            return O.Bath("e", b.cids, b.kernel, nz, dt, nmd, bias=b.bias, exim=b.exim, zeta1=b.zeta1,
+                          zeta2=b.zeta2)
+        return O.Bath("ph", b.cids, b.kernel, nz, dt, nmd)
+
+    bt = O.GLEBatch(nph, dt, nmd, [obath(b, noise[i]) for i, b in enumerate(baths)], dyn, ntr=ntr, constr=constr)
+    bt.p, bt.q, bt.t = p.copy(), q.copy(), t0
+    for i in range(len(baths)):
+        bt.set_history(i, hist[i])
+    for _ in range(nst):
+        bt.step()
+    assert any(ob.biased() for ob in bt.baths)
+    for j in range(ntr):
+        sim = O.GLE(nph, dt, nmd, [obath(b, noise[i][j]) for i, b in enumerate(baths)], dyn=dyn, constr=constr)
+        sim.p, sim.q, sim.t = p[:, j].copy(), q[:, j].copy(), t0
+        for i, b in enumerate(baths):
+            sim.phis[: b.ml, b.cids] = hist[i][j]
+        for _ in range(nst):
+            sim.step()
+        assert close(bt.q[:, j], sim.q, 1e-12) and close(bt.p[:, j], sim.p, 1e-12)
+        for i, ob in enumerate(sim.baths):
+            assert close(bt.cur[i][j], ob.cur, 1e-11)
