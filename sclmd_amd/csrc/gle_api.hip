@@ -69,7 +69,9 @@ struct Bath {
   double* d_Kq = nullptr;
   // fused B+C stage: bath-local Fc copy, V = n1 - c S1, packed K0^2, K0 Kq and K0 P dyn (runs per
   // DOF tile)
+  // (fused stage: d_K0sqd = M1 = K0 - a K0^2, d_hK0d = h K0, d_KKqd = -h K0 Kq, d_KDd = -h K0 P dyn)
   double *d_Xf = nullptr, *d_V = nullptr, *d_K0sqd = nullptr, *d_KKqd = nullptr, *d_KDd = nullptr;
+  double* d_hK0d = nullptr;
   std::vector<std::vector<std::pair<int, int>>> kd_rng;
   std::vector<int64_t> kd_tofs;
   // K0 / Kq rows in DOF order for the chain's DOF tiles: tile rt at [tofs[rt]][ks][64]
@@ -593,7 +595,8 @@ struct Seg {
   int a_ks;
   const double* X;
   int ldx, ring, tshift, nks;
-  int sst;  // ring: doubles between slots
+  int sst;       // ring: doubles between slots
+  int cond = 0;  // 0 / CH_HIT / CH_MISS (ChTask::cond)
 };
 
 // Split the k-steps [g_begin, g_end) of the concatenated segments evenly over the CH_NW waves of
@@ -646,6 +649,7 @@ int fill_tasks(gle_handle* h, ChTile& T, const std::vector<Seg>& segs, int nout,
         tk.sst = sg.sst;
         tk.nks = (int32_t)(s1 - s0);
         tk.slot = cur_slot;
+        tk.cond = sg.cond;
         *flops += 2048.0 * T.rn * (double)(s1 - s0);
       }
       pos += sg.nks;
@@ -793,7 +797,9 @@ int plan_chain(gle_handle* h) {
       int rc = dalloc_n(h, &b.d_Xf, (size_t)b.vs);
       if (!rc) rc = dalloc_n(h, &b.d_V, (size_t)b.vs);
       if (rc) return rc;
-      // K0^2 and K0 Kq (nc x nc), K0 P dyn (nc x nph): host fp64, row-streaming triple loops
+      // M1 = K0 - a K0^2 (a = c dt/2), h K0 and -h K0 Kq (h = dt/2) (nc x nc), -h K0 P dyn (nc x nph):
+      // host fp64, row-streaming triple loops.  K0.p1 = M1.p_half + h K0.(V + Fpot_b) - h (K0 Kq).q~
+      const double hh = h->dt / 2.0, aa = b.c * h->dt / 2.0;
       std::vector<double> sq((size_t)nc * nc, 0.0);
       for (int64_t r = 0; r < nc; ++r)
         for (int64_t k = 0; k < nc; ++k) {
@@ -803,10 +809,19 @@ int plan_chain(gle_handle* h) {
           double* dst = &sq[(size_t)(r * nc)];
           for (int64_t c2 = 0; c2 < nc; ++c2) dst[c2] += a * src[c2];
         }
+      for (size_t e = 0; e < sq.size(); ++e) sq[e] = b.K0[e] - aa * sq[e];
       std::vector<double> f = pack_dof_b(b, sq);
-      rc = dalloc_n(h, &b.d_K0sqd, f.size());
+      rc = dalloc_n(h, &b.d_K0sqd, f.size());  // M1
       if (!rc) rc = upload(h, b.d_K0sqd, f.data(), f.size() * 8);
       if (rc) return rc;
+      {
+        std::vector<double> hk((size_t)nc * nc);
+        for (size_t e = 0; e < hk.size(); ++e) hk[e] = hh * b.K0[e];
+        f = pack_dof_b(b, hk);
+        rc = dalloc_n(h, &b.d_hK0d, f.size());
+        if (!rc) rc = upload(h, b.d_hK0d, f.data(), f.size() * 8);
+        if (rc) return rc;
+      }
       if (b.has_q) {
         std::vector<double> kq((size_t)nc * nc, 0.0);
         for (int64_t r = 0; r < nc; ++r)
@@ -815,6 +830,7 @@ int plan_chain(gle_handle* h) {
             if (a == 0.0) continue;
             for (int64_t c2 = 0; c2 < nc; ++c2) kq[(size_t)(r * nc + c2)] += a * b.Kq[(size_t)(k * nc + c2)];
           }
+        for (double& v : kq) v *= -hh;
         f = pack_dof_b(b, kq);
         rc = dalloc_n(h, &b.d_KKqd, f.size());
         if (!rc) rc = upload(h, b.d_KKqd, f.data(), f.size() * 8);
@@ -874,7 +890,7 @@ int plan_chain(gle_handle* h) {
           for (int ks = r.first; ks < r.first + r.second; ++ks, o += 64)
             for (int l = 0; l < 64; ++l) {
               const int64_t d = 16 * rt + (l & 15), c2 = 4 * ks + (l >> 4);
-              if (d < nph && c2 < nph && b.inv[d] >= 0) fk[(size_t)(o + l)] = kd[(size_t)(b.inv[d] * nph + c2)];
+              if (d < nph && c2 < nph && b.inv[d] >= 0) fk[(size_t)(o + l)] = -hh * kd[(size_t)(b.inv[d] * nph + c2)];
             }
       }
       rc = dalloc_n(h, &b.d_KDd, fk.size());
@@ -974,7 +990,7 @@ int plan_chain(gle_handle* h) {
       } else {
         y.X = b.d_Xcur + (stage == 2 ? b.vs : 0);
       }
-      segs.push_back(y);
+      if (stage != 3) segs.push_back(y);  // the fused stage needs K0.p1 only (CH_OYB + CH_OYD / CH_OYE)
       if (b.has_q && stage != 2)
         qsegs.push_back(Seg{CH_TB + u, b.d_Kqd + b.tofs[rt], 64, b.d_Xq + (stage == 0 ? 0 : b.vs), (int)B, 0, 0,
                             b.nks, 0});
@@ -989,34 +1005,35 @@ int plan_chain(gle_handle* h) {
       }
     }
     if (stage == 3) {  // fused B+C: the composite products (outputs in increasing order)
-      for (int u = 0; u < nu; ++u) {
+      // the potential force at q~ enters through dyn.q~ only on a cache miss (md.py:449-473)
+      for (auto& sg : segs)
+        if (sg.o == 2 * CH_TB) sg.cond = CH_MISS;
+      for (int u = 0; u < nu; ++u) {  // OYB: M1.p_half + h K0.V - h (K0 Kq).q~
         const Bath& b = h->baths[ubath[u]];
         segs.push_back(Seg{CH_OYB + u, b.d_K0sqd + b.tofs[rt], 64, b.d_Xcur, (int)B, 0, 0, b.nks, 0});
-      }
-      for (int u = 0; u < nu; ++u) {
-        const Bath& b = h->baths[ubath[u]];
         if (b.ml >= 2)  // V = n1 - c S1 from the S(t+1) tiles
-          segs.push_back(Seg{CH_OYC + u, b.d_K0d + b.tofs[rt], 64, b.d_V, (int)B, 0, 0, b.nks, 0});
+          segs.push_back(Seg{CH_OYB + u, b.d_hK0d + b.tofs[rt], 64, b.d_V, (int)B, 0, 0, b.nks, 0});
         else            // no memory sum: V = noise(t+1), read from the noise ring
-          segs.push_back(Seg{CH_OYC + u, b.d_K0d + b.tofs[rt], 64, b.d_noise, (int)B, (int)h->nmd, 1, b.nks,
+          segs.push_back(Seg{CH_OYB + u, b.d_hK0d + b.tofs[rt], 64, b.d_noise, (int)B, (int)h->nmd, 1, b.nks,
                              (int)(b.nc * B)});
+        if (b.has_q)
+          segs.push_back(Seg{CH_OYB + u, b.d_KKqd + b.tofs[rt], 64, b.d_Xq + b.vs, (int)B, 0, 0, b.nks, 0});
       }
-      for (int u = 0; u < nu; ++u) {
+      for (int u = 0; u < nu; ++u) {  // OYD: -h (K0 P dyn).q~   (cache miss at q~)
         const Bath& b = h->baths[ubath[u]];
         int64_t o = b.kd_tofs[rt];
         for (auto& r : b.kd_rng[rt]) {
-          segs.push_back(Seg{CH_OYD + u, b.d_KDd + o, 64, h->d_Qt + (int64_t)4 * r.first * B, (int)B, 0, 0, r.second, 0});
+          Seg sg{CH_OYD + u, b.d_KDd + o, 64, h->d_Qt + (int64_t)4 * r.first * B, (int)B, 0, 0, r.second, 0};
+          sg.cond = CH_MISS;
+          segs.push_back(sg);
           o += (int64_t)r.second * 64;
         }
       }
-      for (int u = 0; u < nu; ++u) {
+      for (int u = 0; u < nu; ++u) {  // OYE: h K0.Fc   (cache hit at q~)
         const Bath& b = h->baths[ubath[u]];
-        segs.push_back(Seg{CH_OYE + u, b.d_K0d + b.tofs[rt], 64, b.d_Xf, (int)B, 0, 0, b.nks, 0});
-      }
-      for (int u = 0; u < nu; ++u) {
-        const Bath& b = h->baths[ubath[u]];
-        if (b.has_q)
-          segs.push_back(Seg{CH_OYF + u, b.d_KKqd + b.tofs[rt], 64, b.d_Xq + b.vs, (int)B, 0, 0, b.nks, 0});
+        Seg sg{CH_OYE + u, b.d_hK0d + b.tofs[rt], 64, b.d_Xf, (int)B, 0, 0, b.nks, 0};
+        sg.cond = CH_HIT;
+        segs.push_back(sg);
       }
     }
     int64_t W = 0;

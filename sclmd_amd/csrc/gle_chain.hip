@@ -58,6 +58,10 @@ __device__ __forceinline__ int64_t cmod(int64_t a, int64_t m) {
 #ifndef CH_WPE
 #define CH_WPE 4
 #endif
+// CH_DB: double-buffered operand batches (the next batch of a task in flight during this one's MFMAs)
+#ifndef CH_DB
+#define CH_DB 0
+#endif
 template <int RN, int NW>
 struct Batch {
   static constexpr int U = NW >= 16 ? (RN == 1 ? 16 : (RN == 2 ? 6 : 3)) : (RN == 1 ? CH_U1 : (RN == 2 ? CH_U2 : CH_U4));
@@ -71,10 +75,14 @@ __device__ __forceinline__ void stamp(const StepDev* __restrict__ sd, int stage,
 }
 
 // The wave's tasks: acc += A_s . X rows 4s..4s+3 over each task's k-steps; a task run ends in its
-// LDS slot (16 x 16 RN doubles, row-major).
+// LDS slot (16 x 16 RN doubles, row-major).  A task's k-steps are loaded in batches of U,
+// double-buffered: the loads of batch j+1 are in flight while the MFMAs of batch j run, so a wave
+// waits for about one memory round trip per task (<= CH_TPW) plus its MFMA chain instead of one
+// round trip per batch.  skip: bit 0 drops the tasks of cond CH_HIT (no trajectory of the tile
+// takes the potential-cache hit branch), bit 1 those of cond CH_MISS; their slots read as zeros.
 template <int RN, int NW>
 __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave, int lane, int64_t t,
-                                         double* lds) {
+                                         double* lds, int skip) {
   constexpr int U = Batch<RN, NW>::U;
   constexpr int NT = 16 * RN;
   const int nt = T->ntw[wave];
@@ -83,62 +91,79 @@ __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave,
 #pragma unroll
   for (int n = 0; n < RN; ++n) acc[n] = d4{0.0, 0.0, 0.0, 0.0};
   int cur = -1;
+  auto flush = [&]() {
+#pragma unroll
+    for (int n = 0; n < RN; ++n)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        lds[cur * 16 * NT + (brow + 4 * q) * NT + 16 * n + bcol] = acc[n][q];
+        acc[n][q] = 0.0;
+      }
+  };
   for (int i = 0; i < CH_TPW; ++i) {
     if (i >= nt) break;
     const ChTask tk = T->task[wave][i];
+    const bool off = (tk.cond == CH_HIT && (skip & 1)) || (tk.cond == CH_MISS && (skip & 2));
     if (tk.slot != cur) {
-      if (cur >= 0) {
-#pragma unroll
-        for (int n = 0; n < RN; ++n)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            lds[cur * 16 * NT + (brow + 4 * q) * NT + 16 * n + bcol] = acc[n][q];
-            acc[n][q] = 0.0;
-          }
-      }
+      if (cur >= 0) flush();
       cur = tk.slot;
     }
+    if (off) continue;  // contributes nothing: a slot of skipped tasks only is flushed as zeros
     int64_t col = T->c0;
     if (tk.ring) col += cmod(t + tk.tshift, tk.ring) * (int64_t)tk.sst;
     gdouble* A = (gdouble*)(tk.A + lane);
     gdouble* X = (gdouble*)(tk.X + col + (int64_t)brow * tk.ldx + bcol);
     const int64_t xs = 4 * (int64_t)tk.ldx;
-    for (int s0 = 0; s0 < tk.nks; s0 += U) {
-      double a[U], b[U][RN];
+    const int nks = tk.nks, aks = tk.a_ks;
+    double a0[U], b0[U][RN], a1[U], b1[U][RN];
+    auto fetch = [&](int s0, double (&a)[U], double (&b)[U][RN]) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int s = s0 + u;
-        if (s < tk.nks) {
-          a[u] = A[(int64_t)s * tk.a_ks];
+        if (s < nks) {
+          a[u] = A[(int64_t)s * aks];
 #pragma unroll
           for (int n = 0; n < RN; ++n) b[u][n] = X[(int64_t)s * xs + 16 * n];
         }
       }
+    };
+    auto compute = [&](int s0, double (&a)[U], double (&b)[U][RN]) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (s0 + u < tk.nks) {
+      for (int u = 0; u < U; ++u)
+        if (s0 + u < nks) {
 #pragma unroll
           for (int n = 0; n < RN; ++n) acc[n] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b[u][n], acc[n], 0, 0, 0);
         }
-      }
+    };
+#if CH_DB
+    fetch(0, a0, b0);
+    for (int s0 = 0; s0 < nks; s0 += 2 * U) {
+      if (s0 + U < nks) fetch(s0 + U, a1, b1);
+      compute(s0, a0, b0);
+      if (s0 + U >= nks) break;
+      if (s0 + 2 * U < nks) fetch(s0 + 2 * U, a0, b0);
+      compute(s0 + U, a1, b1);
     }
+#else
+    (void)a1;
+    (void)b1;
+    for (int s0 = 0; s0 < nks; s0 += U) {
+      fetch(s0, a0, b0);
+      compute(s0, a0, b0);
+    }
+#endif
   }
-  if (cur >= 0) {
-#pragma unroll
-    for (int n = 0; n < RN; ++n)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) lds[cur * 16 * NT + (brow + 4 * q) * NT + 16 * n + bcol] = acc[n][q];
-  }
+  if (cur >= 0) flush();
 }
 
 template <int NW>
-__device__ __forceinline__ void run_products(const ChTile* __restrict__ T, int64_t t, double* lds) {
+__device__ __forceinline__ void run_products(const ChTile* __restrict__ T, int64_t t, double* lds, int skip = 0) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   switch (T->rn) {
-    case 1: products<1, NW>(T, wave, lane, t, lds); break;
-    case 2: products<2, NW>(T, wave, lane, t, lds); break;
-    default: products<4, NW>(T, wave, lane, t, lds); break;
+    case 1: products<1, NW>(T, wave, lane, t, lds, skip); break;
+    case 2: products<2, NW>(T, wave, lane, t, lds, skip); break;
+    default: products<4, NW>(T, wave, lane, t, lds, skip); break;
   }
 }
 
@@ -550,13 +575,15 @@ __device__ __forceinline__ void dof_C(const ChTile* __restrict__ T, const StepDe
 }
 
 // stages B + C fused (md.py:401-408 in one launch; harmonic force, pairwise disjoint baths).  With
-// G = Fpot(q~) + sum_u (n1 - c S1 - Kq q~) and F1(x) = G - sum_u c K0 x on the bath rows:
-//   p1 = p_half + dt F1(p_half) / 2
-//   K0 p1 = K0 p_half + dt/2 (K0 G_u - c K0^2 p_half),  K0 G_u = K0 Fpot_u + K0 V - (K0 Kq) q~
-//   K0 Fpot_u = K0 Fc (potforce cache hit) or -(K0 P dyn) q~ (miss), V = n1 - c S1 (stage A)
-//   p2 = p_half + dt F1(p1) / 2,  F1(p1) = G - sum_u c K0 p1
-// so every product reads only stage A's outputs: one dependent launch instead of two.  K0 p1 is
-// re-associated (rounding only).
+// g = Fpot(q~) + sum_u (V - Kq q~), V = n1 - c S1 (the bath part of F1 that does not depend on the
+// velocity argument) and F1(x) = g - sum_u c K0 x on the bath rows:
+//   p1 = p_half + h F1(p_half),  h = dt/2
+//   K0 p1 = M1 p_half + h K0 (V + Fpot_b) - h (K0 Kq) q~,   M1 = K0 - (c h) K0^2
+//   K0 Fpot_b = K0 Fc (potential cache hit at q~) or -(K0 P dyn) q~ (miss)
+//   p2 = p_half + h F1(p1) = p_half + h (g - c K0 p1)
+// so every product reads only stage A's outputs: one dependent launch instead of two, and three
+// nc x nc products per bath row instead of the six of B + C.  K0 p1 is re-associated (rounding
+// only).  Products of the branch no trajectory of the tile takes are skipped.
 template <int NW, int DRN>
 __device__ __forceinline__ void dof_BC(const ChTile* __restrict__ T, const StepDev* __restrict__ sd,
                                        const StepArgs& ta, int mode, double* lds) {
@@ -570,15 +597,16 @@ __device__ __forceinline__ void dof_BC(const ChTile* __restrict__ T, const StepD
   const bool harm = mode != 0;
   Elem E[EPT];
   double ph[EPT], qt[EPT], fc[EPT], q0[EPT];
-  unsigned long long w1[EPT];
+  bool hit1[EPT];
   int cons[EPT];
   int kk[EPT][CH_TB];
   double nz[EPT][CH_TB], sv[EPT][CH_TB];
+  int anyhit = 0, anymiss = 0;
 #pragma unroll
   for (int x = 0; x < EPT; ++x) {
     E[x] = elem_of<NW, DRN>(T, sd, x);
     ph[x] = qt[x] = fc[x] = q0[x] = 0.0;
-    w1[x] = 0;
+    hit1[x] = true;
     cons[x] = 0;
     if (E[x].ok) {
       ph[x] = G(sd->Ph)[E[x].i];
@@ -587,8 +615,10 @@ __device__ __forceinline__ void dof_BC(const ChTile* __restrict__ T, const StepD
       cons[x] = G(sd->cmask)[E[x].d];
       if (harm) {
         q0[x] = G(sd->Q0)[E[x].i];
-        w1[x] = *G(pmax_word(sd, 1, par, E[x].b));
+        hit1[x] = word_hit(*G(pmax_word(sd, 1, par, E[x].b)));
       }
+      anyhit |= hit1[x] ? 1 : 0;
+      anymiss |= hit1[x] ? 0 : 1;
     }
 #pragma unroll
     for (int u = 0; u < CH_TB; ++u) {
@@ -602,7 +632,10 @@ __device__ __forceinline__ void dof_BC(const ChTile* __restrict__ T, const StepD
       }
     }
   }
-  run_products<NW>(T, t, lds);
+  // which potential-cache branches at q~ any trajectory of the tile takes (workgroup-uniform)
+  anyhit = __syncthreads_or(anyhit);
+  anymiss = __syncthreads_or(anymiss);
+  run_products<NW>(T, t, lds, (anyhit ? 0 : 1) | (anymiss ? 0 : 2));
   __syncthreads();
   // the words this launch reads (w1) are read above: only now may the first tile reset them
   if (T->first && threadIdx.x < Geo::NT && T->c0 + (int)threadIdx.x < B) {
@@ -614,40 +647,25 @@ __device__ __forceinline__ void dof_BC(const ChTile* __restrict__ T, const StepD
 #pragma unroll
   for (int x = 0; x < EPT; ++x) {
     const int e = threadIdx.x + x * NW * 64;
-    const bool hit1 = harm ? word_hit(w1[x]) : true;
     double fpot = fc[x];  // potforce(q~)
-    if (!hit1 && E[x].in) {
+    if (!hit1[x] && E[x].in) {
       fpot = -1.0 * out_sum(T, lds, 2 * CH_TB, e, Geo::NE);
       if (E[x].ok) {  // md.potforce miss at q~: evaluate and cache (md.py:472-473)
         G(sd->Fc)[E[x].i] = fpot;
         G(sd->Q0)[E[x].i] = qt[x];
       }
     }
-    double g = fpot;
+    double f2 = fpot;  // F1(p1) (md.py:403) = g - sum_u c K0 p1
 #pragma unroll
     for (int u = 0; u < CH_TB; ++u)
       if (kk[x][u] >= 0) {
         const ChBath& bd = T->tb[u];
-        g += nz[x][u] - bd.c * sv[x][u];
-        if (bd.has_q) g -= out_sum(T, lds, CH_TB + u, e, Geo::NE);
-      }
-    double f1 = g;  // F1(p_half) (md.py:401)
-#pragma unroll
-    for (int u = 0; u < CH_TB; ++u)
-      if (kk[x][u] >= 0) f1 -= T->tb[u].c * out_sum(T, lds, u, e, Geo::NE);
-    double f2 = g;  // F1(p1) (md.py:403)
-#pragma unroll
-    for (int u = 0; u < CH_TB; ++u)
-      if (kk[x][u] >= 0) {
-        const ChBath& bd = T->tb[u];
-        const double ya = out_sum(T, lds, u, e, Geo::NE);
-        double kg = (hit1 ? out_sum(T, lds, CH_OYE + u, e, Geo::NE) : -out_sum(T, lds, CH_OYD + u, e, Geo::NE)) +
-                    out_sum(T, lds, CH_OYC + u, e, Geo::NE);
-        if (bd.has_q) kg -= out_sum(T, lds, CH_OYF + u, e, Geo::NE);
-        const double k0p1 = ya + dt * (kg - bd.c * out_sum(T, lds, CH_OYB + u, e, Geo::NE)) / 2.0;
+        f2 += nz[x][u] - bd.c * sv[x][u];
+        if (bd.has_q) f2 -= out_sum(T, lds, CH_TB + u, e, Geo::NE);
+        const double k0p1 = out_sum(T, lds, CH_OYB + u, e, Geo::NE) +
+                            (hit1[x] ? out_sum(T, lds, CH_OYE + u, e, Geo::NE) : out_sum(T, lds, CH_OYD + u, e, Geo::NE));
         f2 -= bd.c * k0p1;
       }
-    (void)f1;
     double p2 = ph[x] + dt * f2 / 2.0;  // md.py:404
     double qn = qt[x];
     if (cons[x] != 0) {  // ApplyConstraint (md.py:407-408, 782-794)
@@ -672,7 +690,7 @@ __device__ __forceinline__ void dof_BC(const ChTile* __restrict__ T, const StepD
         if (bd.has_q) G(bd.Xq)[kb] = qn;
       }
     }
-    dq[x] = E[x].ok ? fabs(qn - (hit1 ? q0[x] : qt[x])) : 0.0;
+    dq[x] = E[x].ok ? fabs(qn - (hit1[x] ? q0[x] : qt[x])) : 0.0;
   }
   if (harm) {  // cache distance of q_{t+1} for the next step's id0 call
     __syncthreads();

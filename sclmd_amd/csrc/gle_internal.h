@@ -146,8 +146,11 @@ constexpr int CH_NW = 16;       // waves per chain workgroup (max)
 constexpr int CH_TPW = 3;       // tasks per wave
 constexpr int CH_TB = 3;        // baths a DOF tile may intersect
 // DOF-tile outputs: Y = K0.x of tile bath u (u), YQ = Kq.q (CH_TB + u), YD = dyn.q (2 CH_TB); the
-// fused velocity-iteration stage (STAGE 3) adds per tile bath u: K0^2.p_half (CH_OYB + u),
-// K0.V (CH_OYC + u), (K0 P dyn).q~ (CH_OYD + u), K0.Fc (CH_OYE + u), (K0 Kq).q~ (CH_OYF + u)
+// fused velocity-iteration stage (STAGE 3) uses per tile bath u (h = dt/2, a = c dt/2):
+//   CH_OYB + u   M1.p_half + h K0.V - h (K0 Kq).q~        M1 = K0 - a K0^2   (always)
+//   CH_OYD + u   -h (K0 P dyn).q~                                           (potential-cache miss)
+//   CH_OYE + u   h K0.Fc                                                    (potential-cache hit)
+// so K0.p1 = OYB + (hit ? OYE : OYD); CH_OYC / CH_OYF are unused
 constexpr int CH_OYB = 2 * CH_TB + 1;
 constexpr int CH_OYC = CH_OYB + CH_TB;
 constexpr int CH_OYD = CH_OYC + CH_TB;
@@ -168,8 +171,11 @@ struct ChTask {
   int32_t tshift;    // ring: slot pmod(t + tshift, ring)
   int32_t sst;       // ring: doubles between slots
   int32_t slot;      // LDS partial slot
-  int32_t pad;
+  int32_t cond;      // 0: always; CH_HIT / CH_MISS: only when some trajectory of the tile takes the
+                     // potential-cache hit / miss branch at q~ (the fused velocity stage)
 };
+constexpr int32_t CH_HIT = 1;
+constexpr int32_t CH_MISS = 2;
 
 // One bath of a DOF tile, copied out of BathDev so the epilogue's operands are one descriptor
 // round trip away.  DOF row0 + r is in the bath iff bit r of bmask; bath-local k = DOF + boff
