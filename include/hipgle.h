@@ -172,6 +172,32 @@ int gle_get_energy(gle_handle* h, double* etot);
  * out: [nbath][3] */
 int gle_current_sums(gle_handle* h, double* out);
 
+/* ---- per-step recordings (md.savep / saveq / SaveAll, md.py:374-379, 398, 604-653) ---------- */
+#define GLE_REC_P 1     /* md.ps: p_t of every step of the run, slot t mod nmd            */
+#define GLE_REC_Q 2     /* md.qs: q_t likewise                                              */
+#define GLE_REC_F 4     /* md.fhis[i]: bath i's id0 force of every step (bath rows)        */
+#define GLE_REC_HIST 8  /* md.phis / md.qhis on every DOF: rings of the last ml p_t / q_t  */
+/* Record the selected quantities from the next step on, on the device (stage A of each step writes
+ * them; nothing crosses PCIe per step); 0 stops recording.  Buffers start zeroed. */
+int gle_record(gle_handle* h, int32_t flags);
+/* Zero the selected recordings (md.ResetSavepq at a new run, md.py:571-574). */
+int gle_record_zero(gle_handle* h, int32_t flags);
+/* what = GLE_REC_P / GLE_REC_Q: out [ntraj][nmd][nph] (md.ps / md.qs); GLE_REC_F: out
+ * [ntraj][nmd][nc] of bath `bath` (md.fhis restricted to the bath's cids, md.py:398). */
+int gle_get_record(gle_handle* h, int32_t what, int32_t bath, double* out);
+/* md.phis / md.qhis on every DOF, newest first: [ntraj][ml][nph] (rows of times before the
+ * recording started read as zeros); *ml = the ring length (max over baths of ml). */
+int gle_get_record_history(gle_handle* h, double* phis, double* qhis, int64_t* ml);
+/* Restore recordings (a resumed run, md.py:513-534): in has gle_get_record's / _history's layout. */
+int gle_set_record(gle_handle* h, int32_t what, int32_t bath, const double* in);
+int gle_set_record_history(gle_handle* h, const double* phis, const double* qhis);
+/* Velocity power spectra of the recorded ps (functions.powerspecp, functions.py:221-236, and
+ * md.GetPower's per-section spectra, md.py:351-360) for ngroup DOF groups (group g = the next
+ * group_len[g] entries of dofs): out [ngroup][ntraj][nmd] = sum_{k in group} |DFT_t ps[:, k]|^2
+ * per frequency index; the reference's power is dt / nmd times this. */
+int gle_power_spectrum(gle_handle* h, int32_t ngroup, const int64_t* group_len, const int64_t* dofs,
+                       double* out);
+
 /* ---- ensemble reduce ------------------------------------------------ */
 /* The per-run heat-current statistics of the whole ensemble: out [nbath][3] = the sum over every
  * rank's gle_current_sums, by one RCCL all-reduce (sum, fp64) over xGMI on the handle's stream.

@@ -27,8 +27,11 @@ EXPORTS = [
     "gle_sync", "gle_get_current", "gle_get_energy", "gle_current_sums", "gle_profile",
     "gle_profile_read", "gle_plan_info", "gle_add_bath_gmem", "gle_get_kernel", "gle_gamt",
     "gle_profile_levels", "gle_step_work", "gle_reduce_current", "gle_comm_unique_id", "gle_comm_init",
-    "gle_comm_destroy",
+    "gle_comm_destroy", "gle_record", "gle_record_zero", "gle_get_record", "gle_get_record_history",
+    "gle_power_spectrum", "gle_set_record", "gle_set_record_history",
 ]
+
+REC_P, REC_Q, REC_F, REC_HIST = 1, 2, 4, 8
 
 
 class GLEError(RuntimeError):
@@ -89,6 +92,13 @@ _SIGS = {
     "gle_comm_init": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p,
                                      ctypes.POINTER(_P)]),
     "gle_comm_destroy": (ctypes.c_int, [_P]),
+    "gle_record": (ctypes.c_int, [_P, ctypes.c_int32]),
+    "gle_record_zero": (ctypes.c_int, [_P, ctypes.c_int32]),
+    "gle_get_record": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, _D]),
+    "gle_get_record_history": (ctypes.c_int, [_P, _D, _D, _I64]),
+    "gle_power_spectrum": (ctypes.c_int, [_P, ctypes.c_int32, _I64, _I64, _D]),
+    "gle_set_record": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, _D]),
+    "gle_set_record_history": (ctypes.c_int, [_P, _D, _D]),
 }
 
 _lib = None
@@ -350,6 +360,54 @@ class Stepper:
     def current_sums(self):
         out = np.empty((self.nbath, 3))
         self._chk(self.lib.gle_current_sums(self.h, _ptr(out)), "gle_current_sums")
+        return out
+
+    # --------------------------------------------------------------------------- recordings
+    def record(self, flags):
+        """Record REC_P / REC_Q / REC_F / REC_HIST on the device from the next step on (gle_record)."""
+        self._chk(self.lib.gle_record(self.h, int(flags)), "gle_record")
+
+    def record_zero(self, flags):
+        self._chk(self.lib.gle_record_zero(self.h, int(flags)), "gle_record_zero")
+
+    def get_record(self, what, bath=0):
+        """REC_P / REC_Q: (ntraj, nmd, nph); REC_F: (ntraj, nmd, nc) of `bath`."""
+        cols = self.bath_nc[bath] if what == REC_F else self.nph
+        out = np.empty((self.ntraj, self.nmd, cols))
+        self._chk(self.lib.gle_get_record(self.h, int(what), int(bath), _ptr(out)), "gle_get_record")
+        return out
+
+    def get_record_history(self):
+        """(phis, qhis) on every DOF, newest first: (ntraj, ml, nph) each."""
+        ml = ctypes.c_int64(0)
+        self._chk(self.lib.gle_get_record_history(self.h, None, None, ctypes.byref(ml)), "gle_get_record_history")
+        ph = np.empty((self.ntraj, ml.value, self.nph))
+        qh = np.empty((self.ntraj, ml.value, self.nph))
+        self._chk(self.lib.gle_get_record_history(self.h, _ptr(ph), _ptr(qh), ctypes.byref(ml)),
+                  "gle_get_record_history")
+        return ph, qh
+
+    def set_record(self, what, arr, bath=0):
+        cols = self.bath_nc[bath] if what == REC_F else self.nph
+        a = _f64(np.broadcast_to(np.asarray(arr, dtype=np.float64), (self.ntraj, self.nmd, cols)))
+        self._chk(self.lib.gle_set_record(self.h, int(what), int(bath), _ptr(a)), "gle_set_record")
+
+    def set_record_history(self, phis=None, qhis=None):
+        ml = ctypes.c_int64(0)
+        self._chk(self.lib.gle_get_record_history(self.h, None, None, ctypes.byref(ml)), "gle_get_record_history")
+        shp = (self.ntraj, ml.value, self.nph)
+        ph = None if phis is None else _f64(np.broadcast_to(np.asarray(phis, dtype=np.float64), shp))
+        qh = None if qhis is None else _f64(np.broadcast_to(np.asarray(qhis, dtype=np.float64), shp))
+        self._chk(self.lib.gle_set_record_history(self.h, _ptr(ph), _ptr(qh)), "gle_set_record_history")
+
+    def power_spectrum(self, groups):
+        """sum_{k in group} |DFT_t ps[:, k]|^2 for each DOF group: (ngroup, ntraj, nmd)."""
+        lens = np.ascontiguousarray([len(g) for g in groups], dtype=np.int64)
+        dofs = np.ascontiguousarray(np.concatenate([np.asarray(g, dtype=np.int64) for g in groups]) if len(groups)
+                                    else np.zeros(0, dtype=np.int64), dtype=np.int64)
+        out = np.empty((len(groups), self.ntraj, self.nmd))
+        self._chk(self.lib.gle_power_spectrum(self.h, len(groups), lens.ctypes.data_as(_I64),
+                                              dofs.ctypes.data_as(_I64), _ptr(out)), "gle_power_spectrum")
         return out
 
     def reduce_current(self, comm=None):

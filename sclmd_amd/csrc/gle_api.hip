@@ -202,6 +202,12 @@ struct gle_handle {
   int64_t prof_n = 0;
   double prof_ms = 0, prof_flops = 0, prof_bytes = 0;
   double prof_blocks[MAXLVL] = {};  // ladder blocks issued per level since profiling was enabled
+  // per-step recording (gle_record): flags, buffers, host copy of the device step descriptor
+  StepDev sdh{};
+  int32_t rec_flags = 0;
+  double *d_rec_p = nullptr, *d_rec_q = nullptr, *d_rec_hp = nullptr, *d_rec_hq = nullptr;
+  double* d_rec_f[MAXBATH] = {};
+  int rec_ml = 1;
 };
 
 namespace {
@@ -658,7 +664,7 @@ int fill_tasks(gle_handle* h, ChTile& T, const std::vector<Seg>& segs, int nout,
     g0 = g1;
   }
   c.lds = std::max(c.lds, (size_t)slot * 256 * T.rn * 8);
-  if (c.lds > 64 * 1024) return fail(h, GLE_ERR_UNSUP, "chain plan: LDS slots");
+  if (c.lds > 150 * 1024) return fail(h, GLE_ERR_UNSUP, "chain plan: LDS slots");
   int run = 0;
   for (int o = 0; o < nout; ++o) {
     if (nsl[o] && first[o] != run) return fail(h, GLE_ERR_UNSUP, "chain plan: slot order");
@@ -670,8 +676,65 @@ int fill_tasks(gle_handle* h, ChTile& T, const std::vector<Seg>& segs, int nout,
   return GLE_OK;
 }
 
+// XCD-aware tile order.  Workgroups are dispatched round-robin over the 8 XCDs (block b on XCD
+// b mod 8, observed, not guaranteed: speed only, never correctness), each with its own L2.  Tiles
+// that read the same matrix rows (the column tiles of one DOF row tile; the near-field and S(t+1)
+// tiles of one bath row tile) are given one XCD, groups balanced by work (largest first onto the
+// least-loaded XCD), so each XCD's L2 holds ~1/8 of the chain's ~17 MB of matrices instead of
+// every XCD streaming all of them from the MALL each step.  Short XCD lists are padded with empty
+// tiles so that position p of the launch is on XCD p mod 8.
+void xcd_order(gle_handle* h, Chain& c) {
+  constexpr int NX = 8;
+  if (c.tiles.size() < 2 * NX) return;
+  if (const char* e = gle_env("GLE_XCD_ORDER"))
+    if (atoi(e) == 0) return;
+  std::vector<std::pair<int64_t, std::vector<size_t>>> groups;  // (key, tiles)
+  std::vector<double> gwork;
+  for (size_t i = 0; i < c.tiles.size(); ++i) {
+    const ChTile& T = c.tiles[i];
+    const int64_t key = T.kind == CH_DOF ? (int64_t)(T.row0 / 16) : ((int64_t)(T.tile + 1) << 32) + T.row0 / 16;
+    double w = 1.0;
+    for (int wv = 0; wv < CH_NW; ++wv)
+      for (int k = 0; k < T.ntw[wv] && k < CH_TPW; ++k) w += (double)T.task[wv][k].nks * T.rn;
+    size_t g = 0;
+    for (; g < groups.size(); ++g)
+      if (groups[g].first == key) break;
+    if (g == groups.size()) {
+      groups.push_back({key, {}});
+      gwork.push_back(0.0);
+    }
+    groups[g].second.push_back(i);
+    gwork[g] += w;
+  }
+  std::vector<size_t> ord(groups.size());
+  for (size_t g = 0; g < ord.size(); ++g) ord[g] = g;
+  std::stable_sort(ord.begin(), ord.end(), [&](size_t a, size_t b) { return gwork[a] > gwork[b]; });
+  std::vector<std::vector<size_t>> lists(NX);
+  std::vector<double> load(NX, 0.0);
+  for (size_t g : ord) {
+    int x = 0;
+    for (int y = 1; y < NX; ++y)
+      if (load[y] < load[x] || (load[y] == load[x] && lists[y].size() < lists[x].size())) x = y;
+    load[x] += gwork[g];
+    for (size_t i : groups[g].second) lists[x].push_back(i);
+  }
+  size_t n = 0;
+  for (auto& l : lists) n = std::max(n, l.size());
+  ChTile empty{};
+  empty.kind = CH_RAW;  // no tasks, no rows: products and stores are empty
+  empty.rn = 1;
+  empty.dst = h->d_zero;
+  empty.ldd = 1;
+  std::vector<ChTile> out;
+  out.reserve(n * NX);
+  for (size_t m = 0; m < n; ++m)
+    for (int x = 0; x < NX; ++x) out.push_back(m < lists[x].size() ? c.tiles[lists[x][m]] : empty);
+  c.tiles.swap(out);
+}
+
 int upload_chain(gle_handle* h, Chain& c) {
   if (c.tiles.empty()) return GLE_OK;
+  xcd_order(h, c);
   int rc = dalloc_n(h, &c.d, c.tiles.size());
   if (!rc) rc = upload(h, c.d, c.tiles.data(), c.tiles.size() * sizeof(ChTile));
   return rc;
@@ -943,7 +1006,11 @@ int plan_chain(gle_handle* h) {
     std::vector<Seg> qsegs;
     int nu = 0;
     int ubath[CH_TB] = {-1, -1, -1};
-    for (int u = 0; u < CH_TB; ++u) T.tb[u].bath = -1;
+    for (int u = 0; u < CH_TB; ++u) {  // unused slots: valid zero rows (the chain loads them unmasked)
+      ChBath& cb = T.tb[u];
+      cb.bath = -1;
+      cb.noise = cb.S = cb.Yq = h->d_zero;
+    }
     for (int j = 0; j < nb; ++j) {
       Bath& b = h->baths[j];
       uint32_t m = 0;
@@ -965,7 +1032,7 @@ int plan_chain(gle_handle* h) {
       cb.S = b.d_S;
       cb.Xcur = b.d_Xcur;
       cb.Xq = b.d_Xq;
-      cb.Yq = b.d_Yq;
+      cb.Yq = b.d_Yq ? b.d_Yq : h->d_zero;  // read at row 0 only unless has_q
       cb.H = b.d_H;
       cb.NR = b.d_NR;
       cb.inv = b.d_inv;
@@ -1171,6 +1238,35 @@ int plan_chain(gle_handle* h) {
     if (rc) return rc;
   }
   return GLE_OK;
+}
+
+// Allocate the buffers of the enabled recordings (zeroed on first use), point the step descriptor
+// at them (nullptr: off) and upload it.
+int apply_record(gle_handle* h) {
+  const int64_t B = h->B, nph = h->nph, nmd = h->nmd;
+  int mlmax = 1;
+  for (auto& b : h->baths) mlmax = std::max(mlmax, b.ml);
+  h->rec_ml = mlmax;
+  const int f = h->rec_flags;
+  int rc = 0;
+  if ((f & GLE_REC_P) && !h->d_rec_p) rc = dalloc_n(h, &h->d_rec_p, (size_t)nmd * nph * B);
+  if (!rc && (f & GLE_REC_Q) && !h->d_rec_q) rc = dalloc_n(h, &h->d_rec_q, (size_t)nmd * nph * B);
+  if (!rc && (f & GLE_REC_HIST) && !h->d_rec_hp) {
+    rc = dalloc_n(h, &h->d_rec_hp, (size_t)mlmax * nph * B);
+    if (!rc) rc = dalloc_n(h, &h->d_rec_hq, (size_t)mlmax * nph * B);
+  }
+  for (size_t j = 0; j < h->baths.size() && !rc; ++j)
+    if ((f & GLE_REC_F) && !h->d_rec_f[j]) rc = dalloc_n(h, &h->d_rec_f[j], (size_t)nmd * h->baths[j].nc * B);
+  if (rc) return rc;
+  StepDev& sd = h->sdh;
+  sd.rec_p = (f & GLE_REC_P) ? h->d_rec_p : nullptr;
+  sd.rec_q = (f & GLE_REC_Q) ? h->d_rec_q : nullptr;
+  sd.rec_hp = (f & GLE_REC_HIST) ? h->d_rec_hp : nullptr;
+  sd.rec_hq = (f & GLE_REC_HIST) ? h->d_rec_hq : nullptr;
+  for (int j = 0; j < MAXBATH; ++j) sd.rec_f[j] = (f & GLE_REC_F) ? h->d_rec_f[j] : nullptr;
+  sd.rec_ml = mlmax;
+  HIPCHK(h, hipStreamSynchronize(h->stream));  // launches in flight read the old descriptor
+  return upload(h, h->d_sd, &sd, sizeof(sd));
 }
 
 int freeze(gle_handle* h) {
@@ -1532,10 +1628,9 @@ int freeze(gle_handle* h) {
   }
   rc = dalloc_n(h, &h->d_sd, 1);
   if (rc) return rc;
-  rc = upload(h, h->d_sd, &sd, sizeof(sd));
-  if (rc) return rc;
+  h->sdh = sd;
   h->frozen = true;
-  return GLE_OK;
+  return apply_record(h);  // uploads the step descriptor
 }
 
 // Pieces [j0, j1) of block k of level lv on stream s (see Level::npiece); the last piece records
@@ -2662,6 +2757,157 @@ int gle_step_work(gle_handle* h, double* flops, double* bytes) {
   }
   if (flops) *flops = fl;
   if (bytes) *bytes = by;
+  return GLE_OK;
+}
+
+int gle_record(gle_handle* h, int32_t flags) {
+  if (!h) return GLE_ERR_ARG;
+  if (flags & ~(GLE_REC_P | GLE_REC_Q | GLE_REC_F | GLE_REC_HIST)) return fail(h, GLE_ERR_ARG, "bad record flags");
+  hipSetDevice(h->cfg.device);
+  h->rec_flags = flags;
+  if (!h->frozen) return GLE_OK;  // applied when the plan is built
+  return apply_record(h);
+}
+
+int gle_record_zero(gle_handle* h, int32_t flags) {
+  if (!h) return GLE_ERR_ARG;
+  hipSetDevice(h->cfg.device);
+  const size_t n = (size_t)h->nmd * h->nph * h->B * 8;
+  if ((flags & GLE_REC_P) && h->d_rec_p) HIPCHK(h, hipMemsetAsync(h->d_rec_p, 0, n, h->stream));
+  if ((flags & GLE_REC_Q) && h->d_rec_q) HIPCHK(h, hipMemsetAsync(h->d_rec_q, 0, n, h->stream));
+  if ((flags & GLE_REC_HIST) && h->d_rec_hp) {
+    const size_t nh = (size_t)h->rec_ml * h->nph * h->B * 8;
+    HIPCHK(h, hipMemsetAsync(h->d_rec_hp, 0, nh, h->stream));
+    HIPCHK(h, hipMemsetAsync(h->d_rec_hq, 0, nh, h->stream));
+  }
+  for (size_t j = 0; j < h->baths.size(); ++j)
+    if ((flags & GLE_REC_F) && h->d_rec_f[j])
+      HIPCHK(h, hipMemsetAsync(h->d_rec_f[j], 0, (size_t)h->nmd * h->baths[j].nc * h->B * 8, h->stream));
+  return GLE_OK;
+}
+
+int gle_get_record(gle_handle* h, int32_t what, int32_t bath, double* out) {
+  if (!h || !out) return GLE_ERR_ARG;
+  hipSetDevice(h->cfg.device);
+  const int64_t B = h->B, nmd = h->nmd;
+  const double* src = nullptr;
+  int64_t rows = 0, cols = 0;
+  if (what == GLE_REC_P || what == GLE_REC_Q) {
+    src = what == GLE_REC_P ? h->d_rec_p : h->d_rec_q;
+    rows = nmd;
+    cols = h->nph;
+  } else if (what == GLE_REC_F) {
+    int rc = check_bath(h, bath);
+    if (rc) return rc;
+    src = h->d_rec_f[bath];
+    rows = nmd;
+    cols = h->baths[bath].nc;
+  } else {
+    return fail(h, GLE_ERR_ARG, "gle_get_record: what must be GLE_REC_P, GLE_REC_Q or GLE_REC_F");
+  }
+  if (!src) return fail(h, GLE_ERR_STATE, "that quantity was never recorded (gle_record)");
+  std::vector<double> buf((size_t)rows * cols * B);
+  int rc = download(h, buf.data(), src, buf.size() * 8);
+  if (rc) return rc;
+  for (int64_t b = 0; b < B; ++b)
+    for (int64_t r = 0; r < rows; ++r)
+      for (int64_t c = 0; c < cols; ++c) out[((size_t)b * rows + r) * cols + c] = buf[((size_t)r * cols + c) * B + b];
+  return GLE_OK;
+}
+
+int gle_get_record_history(gle_handle* h, double* phis, double* qhis, int64_t* ml) {
+  if (!h) return GLE_ERR_ARG;
+  if (ml) *ml = h->rec_ml;
+  if (!phis && !qhis) return GLE_OK;
+  if (!h->d_rec_hp) return fail(h, GLE_ERR_STATE, "histories were never recorded (gle_record GLE_REC_HIST)");
+  hipSetDevice(h->cfg.device);
+  const int64_t B = h->B, n = h->nph, R = h->rec_ml;
+  std::vector<double> buf((size_t)R * n * B);
+  for (int k = 0; k < 2; ++k) {
+    double* out = k == 0 ? phis : qhis;
+    if (!out) continue;
+    int rc = download(h, buf.data(), k == 0 ? h->d_rec_hp : h->d_rec_hq, buf.size() * 8);
+    if (rc) return rc;
+    // row i (newest first) = time t-1-i = ring slot (t-1-i) mod R
+    for (int64_t i = 0; i < R; ++i) {
+      const int64_t slot = ((h->t - 1 - i) % R + R) % R;
+      for (int64_t b = 0; b < B; ++b)
+        for (int64_t d = 0; d < n; ++d) out[((size_t)b * R + i) * n + d] = buf[((size_t)slot * n + d) * B + b];
+    }
+  }
+  return GLE_OK;
+}
+
+int gle_set_record(gle_handle* h, int32_t what, int32_t bath, const double* in) {
+  if (!h || !in) return GLE_ERR_ARG;
+  hipSetDevice(h->cfg.device);
+  const int64_t B = h->B, nmd = h->nmd;
+  double* dst = nullptr;
+  int64_t cols = 0;
+  if (what == GLE_REC_P || what == GLE_REC_Q) {
+    dst = what == GLE_REC_P ? h->d_rec_p : h->d_rec_q;
+    cols = h->nph;
+  } else if (what == GLE_REC_F) {
+    int rc = check_bath(h, bath);
+    if (rc) return rc;
+    dst = h->d_rec_f[bath];
+    cols = h->baths[bath].nc;
+  } else {
+    return fail(h, GLE_ERR_ARG, "gle_set_record: what must be GLE_REC_P, GLE_REC_Q or GLE_REC_F");
+  }
+  if (!dst) return fail(h, GLE_ERR_STATE, "enable the recording first (gle_record)");
+  std::vector<double> buf((size_t)nmd * cols * B);
+  for (int64_t b = 0; b < B; ++b)
+    for (int64_t r = 0; r < nmd; ++r)
+      for (int64_t c = 0; c < cols; ++c) buf[((size_t)r * cols + c) * B + b] = in[((size_t)b * nmd + r) * cols + c];
+  return upload(h, dst, buf.data(), buf.size() * 8);
+}
+
+int gle_set_record_history(gle_handle* h, const double* phis, const double* qhis) {
+  if (!h) return GLE_ERR_ARG;
+  if (!h->d_rec_hp) return fail(h, GLE_ERR_STATE, "enable GLE_REC_HIST first (gle_record)");
+  hipSetDevice(h->cfg.device);
+  const int64_t B = h->B, n = h->nph, R = h->rec_ml;
+  std::vector<double> buf((size_t)R * n * B);
+  for (int k = 0; k < 2; ++k) {
+    const double* in = k == 0 ? phis : qhis;
+    if (!in) continue;
+    for (int64_t i = 0; i < R; ++i) {
+      const int64_t slot = ((h->t - 1 - i) % R + R) % R;
+      for (int64_t b = 0; b < B; ++b)
+        for (int64_t d = 0; d < n; ++d) buf[((size_t)slot * n + d) * B + b] = in[((size_t)b * R + i) * n + d];
+    }
+    int rc = upload(h, k == 0 ? h->d_rec_hp : h->d_rec_hq, buf.data(), buf.size() * 8);
+    if (rc) return rc;
+  }
+  return GLE_OK;
+}
+
+int gle_power_spectrum(gle_handle* h, int32_t ngroup, const int64_t* group_len, const int64_t* dofs, double* out) {
+  if (!h || ngroup < 1 || !group_len || !dofs || !out) return GLE_ERR_ARG;
+  if (!h->d_rec_p) return fail(h, GLE_ERR_STATE, "gle_power_spectrum needs the recorded velocities (gle_record GLE_REC_P)");
+  hipSetDevice(h->cfg.device);
+  std::vector<int64_t> off(ngroup + 1, 0);
+  for (int g = 0; g < ngroup; ++g) {
+    if (group_len[g] < 0) return fail(h, GLE_ERR_ARG, "negative group length");
+    off[g + 1] = off[g] + group_len[g];
+  }
+  for (int64_t i = 0; i < off[ngroup]; ++i)
+    if (dofs[i] < 0 || dofs[i] >= h->nph) return fail(h, GLE_ERR_ARG, "power spectrum DOF out of range");
+  DevTmp d_off, d_dofs, d_out;
+  HIPCHK(h, hipMalloc(&d_off.p, off.size() * 8));
+  HIPCHK(h, hipMalloc(&d_dofs.p, std::max<int64_t>(1, off[ngroup]) * 8));
+  const size_t no = (size_t)ngroup * h->B * h->nmd;
+  HIPCHK(h, hipMalloc(&d_out.p, no * 8));
+  HIPCHK(h, hipMemcpyAsync(d_off.p, off.data(), off.size() * 8, hipMemcpyHostToDevice, h->stream));
+  if (off[ngroup] > 0)
+    HIPCHK(h, hipMemcpyAsync(d_dofs.p, dofs, off[ngroup] * 8, hipMemcpyHostToDevice, h->stream));
+  sync_bg(h);
+  if (launch_power(h->d_rec_p, h->nph, (int)h->B, h->nmd, ngroup, (const int64_t*)d_off.p, (const int64_t*)d_dofs.p,
+                   h->d_tw, (double*)d_out.p, h->stream))
+    return fail(h, GLE_ERR_UNSUP, "device power spectrum needs nmd a power of two <= 8192");
+  HIPCHK(h, hipMemcpyAsync(out, d_out.p, no * 8, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
   return GLE_OK;
 }
 

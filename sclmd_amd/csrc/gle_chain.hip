@@ -115,33 +115,34 @@ __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave,
     gdouble* X = (gdouble*)(tk.X + col + (int64_t)brow * tk.ldx + bcol);
     const int64_t xs = 4 * (int64_t)tk.ldx;
     const int nks = tk.nks, aks = tk.a_ks;
+    // Loads are branch-free (index clamped to the task's last k-step) and MFMAs past the end
+    // multiply a zero A operand: a load under a branch makes the waitcnt pass drain every load in
+    // flight at the join, which turned each batch into one round trip per k-step.
     double a0[U], b0[U][RN], a1[U], b1[U][RN];
     auto fetch = [&](int s0, double (&a)[U], double (&b)[U][RN]) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int s = s0 + u;
-        if (s < nks) {
-          a[u] = A[(int64_t)s * aks];
+        const int s = min(s0 + u, nks - 1);
+        a[u] = A[(int64_t)s * aks];
 #pragma unroll
-          for (int n = 0; n < RN; ++n) b[u][n] = X[(int64_t)s * xs + 16 * n];
-        }
+        for (int n = 0; n < RN; ++n) b[u][n] = X[(int64_t)s * xs + 16 * n];
       }
     };
     auto compute = [&](int s0, double (&a)[U], double (&b)[U][RN]) {
 #pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (s0 + u < nks) {
+      for (int u = 0; u < U; ++u) {
+        const double av = s0 + u < nks ? a[u] : 0.0;
 #pragma unroll
-          for (int n = 0; n < RN; ++n) acc[n] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b[u][n], acc[n], 0, 0, 0);
-        }
+        for (int n = 0; n < RN; ++n) acc[n] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b[u][n], acc[n], 0, 0, 0);
+      }
     };
 #if CH_DB
     fetch(0, a0, b0);
     for (int s0 = 0; s0 < nks; s0 += 2 * U) {
-      if (s0 + U < nks) fetch(s0 + U, a1, b1);
+      fetch(min(s0 + U, nks - 1), a1, b1);
       compute(s0, a0, b0);
       if (s0 + U >= nks) break;
-      if (s0 + 2 * U < nks) fetch(s0 + 2 * U, a0, b0);
+      fetch(min(s0 + 2 * U, nks - 1), a0, b0);
       compute(s0 + U, a1, b1);
     }
 #else
@@ -216,10 +217,21 @@ __device__ __forceinline__ Elem elem_of(const ChTile* __restrict__ T, const Step
   return E;
 }
 
-// bath-local row of the element's DOF in tile bath bd, or -1
+// bath-local row of the element's DOF in tile bath bd, or -1 (the inv load, for tiles whose bath
+// rows are not an affine image of their DOFs, is under a tile-uniform branch only)
 __device__ __forceinline__ int bath_row(const ChBath& bd, const Elem& E) {
-  if (bd.bath < 0 || !E.ok || !((bd.bmask >> E.r) & 1u)) return -1;
-  return bd.boff == CH_INV ? G(bd.inv)[E.d] : E.d + bd.boff;
+  const bool in = bd.bath >= 0 && E.ok && ((bd.bmask >> E.r) & 1u);
+  int k;
+  if (bd.boff == CH_INV) k = G(bd.inv)[in ? E.d : 0];
+  else k = E.d + bd.boff;
+  return in ? k : -1;
+}
+
+// Prologue loads are unconditional (clamped indices; unused tile-bath slots point at a zero row)
+// and their values are masked afterwards: a load under a divergent branch makes the waitcnt pass
+// drain every load in flight at the join, so the loads would not overlap the products.
+__device__ __forceinline__ int64_t bath_idx(const Elem& E, int k, int B) {
+  return k >= 0 ? (int64_t)k * B + E.b : 0;
 }
 
 // Per-trajectory reductions over the tile's 16 rows, one LDS pass: quantity q of element e at
@@ -263,31 +275,21 @@ __device__ __forceinline__ void dof_A(const ChTile* __restrict__ T, const StepDe
 #pragma unroll
   for (int x = 0; x < EPT; ++x) {
     E[x] = elem_of<NW, DRN>(T, sd, x);
-    p[x] = q[x] = fc[x] = q0[x] = 0.0;
-    w0[x] = 0;
-    qv[x] = 0;
-    if (E[x].ok) {
-      p[x] = G(sd->P)[E[x].i];
-      q[x] = G(sd->Q)[E[x].i];
-      fc[x] = G(sd->Fc)[E[x].i];
-      if (harm || diff1) q0[x] = G(sd->Q0)[E[x].i];
-      if (harm) {
-        qv[x] = G(sd->qvalid)[E[x].b];
-        w0[x] = *G(pmax_word(sd, 0, par, E[x].b));
-      }
-    }
+    const int64_t ii = E[x].ok ? E[x].i : 0;
+    const int bb = E[x].ok ? E[x].b : 0;
+    p[x] = G(sd->P)[ii];
+    q[x] = G(sd->Q)[ii];
+    fc[x] = G(sd->Fc)[ii];
+    q0[x] = G(sd->Q0)[ii];
+    qv[x] = G(sd->qvalid)[bb];
+    w0[x] = *G(pmax_word(sd, 0, par, bb));
 #pragma unroll
     for (int u = 0; u < CH_TB; ++u) {
-      kk[x][u] = -1;
-      nz[x][u] = sv[x][u] = 0.0;
-      {
-        const ChBath& bd = T->tb[u];
-        kk[x][u] = bath_row(bd, E[x]);
-        if (kk[x][u] >= 0) {
-          nz[x][u] = G(bd.noise)[((int64_t)tn * bd.nc + kk[x][u]) * B + E[x].b];
-          sv[x][u] = G(bd.S)[(int64_t)par * bd.vs + (int64_t)kk[x][u] * B + E[x].b];
-        }
-      }
+      const ChBath& bd = T->tb[u];
+      kk[x][u] = bath_row(bd, E[x]);
+      const int64_t kb = bath_idx(E[x], kk[x][u], B);
+      nz[x][u] = G(bd.noise)[(int64_t)tn * bd.nc * B + kb];
+      sv[x][u] = G(bd.S)[(int64_t)par * bd.vs + kb];
     }
   }
   if (T->first && threadIdx.x < Geo::NT && T->c0 + (int)threadIdx.x < B)
@@ -322,6 +324,8 @@ __device__ __forceinline__ void dof_A(const ChTile* __restrict__ T, const StepDe
         if (bd.has_q) fb -= out_sum(T, lds, CH_TB + u, e, Geo::NE);
         f += fb;                 // pf = pf + fbaths[i]  (md.py:432-434)
         cur[x][u] = fb * p[x];   // cur[t] = fbaths[i].p (md.py:397)
+        if (double* rf = sd->rec_f[bd.bath])  // fhis[i][t] = fbaths[i] (md.py:398), bath rows
+          G(rf)[((int64_t)tn * bd.nc + kk[x][u]) * B + E[x].b] = fb;
       }
     }
     const double ph = p[x] + f * dt / 2.0;               // md.py:391
@@ -329,6 +333,15 @@ __device__ __forceinline__ void dof_A(const ChTile* __restrict__ T, const StepDe
     if (E[x].ok) {
       G(sd->Ph)[E[x].i] = ph;
       G(sd->Qt)[E[x].i] = qt;
+      // recordings (pointers are launch-uniform): ps / qs at slot t mod nmd, histories at t mod ml
+      const int64_t rs = (int64_t)tn * sd->nph * B + E[x].i;
+      if (sd->rec_p) G(sd->rec_p)[rs] = p[x];
+      if (sd->rec_q) G(sd->rec_q)[rs] = q[x];
+      if (sd->rec_hp) {
+        const int64_t hs = (int64_t)(t % sd->rec_ml) * sd->nph * B + E[x].i;
+        G(sd->rec_hp)[hs] = p[x];
+        G(sd->rec_hq)[hs] = q[x];
+      }
     }
 #pragma unroll
     for (int u = 0; u < CH_TB; ++u) {
@@ -398,26 +411,18 @@ __device__ __forceinline__ void dof_B(const ChTile* __restrict__ T, const StepDe
 #pragma unroll
   for (int x = 0; x < EPT; ++x) {
     E[x] = elem_of<NW, DRN>(T, sd, x);
-    ph[x] = qt[x] = fc[x] = 0.0;
-    w1[x] = 0;
-    if (E[x].ok) {
-      ph[x] = G(sd->Ph)[E[x].i];
-      qt[x] = G(sd->Qt)[E[x].i];
-      fc[x] = G(sd->Fc)[E[x].i];
-      if (harm) w1[x] = *G(pmax_word(sd, 1, par, E[x].b));
-    }
+    const int64_t ii = E[x].ok ? E[x].i : 0;
+    ph[x] = G(sd->Ph)[ii];
+    qt[x] = G(sd->Qt)[ii];
+    fc[x] = G(sd->Fc)[ii];
+    w1[x] = *G(pmax_word(sd, 1, par, E[x].ok ? E[x].b : 0));
 #pragma unroll
     for (int u = 0; u < CH_TB; ++u) {
-      kk[x][u] = -1;
-      nz[x][u] = sv[x][u] = 0.0;
-      {
-        const ChBath& bd = T->tb[u];
-        kk[x][u] = bath_row(bd, E[x]);
-        if (kk[x][u] >= 0) {
-          nz[x][u] = G(bd.noise)[((int64_t)t1 * bd.nc + kk[x][u]) * B + E[x].b];
-          sv[x][u] = G(bd.S)[(int64_t)par1 * bd.vs + (int64_t)kk[x][u] * B + E[x].b];
-        }
-      }
+      const ChBath& bd = T->tb[u];
+      kk[x][u] = bath_row(bd, E[x]);
+      const int64_t kb = bath_idx(E[x], kk[x][u], B);
+      nz[x][u] = G(bd.noise)[(int64_t)t1 * bd.nc * B + kb];
+      sv[x][u] = G(bd.S)[(int64_t)par1 * bd.vs + kb];
     }
   }
   run_products<NW>(T, t, lds);
@@ -483,29 +488,20 @@ __device__ __forceinline__ void dof_C(const ChTile* __restrict__ T, const StepDe
 #pragma unroll
   for (int x = 0; x < EPT; ++x) {
     E[x] = elem_of<NW, DRN>(T, sd, x);
-    ph[x] = qt[x] = fc[x] = q0[x] = 0.0;
-    cons[x] = 0;
-    if (E[x].ok) {
-      ph[x] = G(sd->Ph)[E[x].i];
-      qt[x] = G(sd->Qt)[E[x].i];
-      fc[x] = G(sd->Fc)[E[x].i];
-      cons[x] = G(sd->cmask)[E[x].d];
-      if (harm) q0[x] = G(sd->Q0)[E[x].i];
-    }
+    const int64_t ii = E[x].ok ? E[x].i : 0;
+    ph[x] = G(sd->Ph)[ii];
+    qt[x] = G(sd->Qt)[ii];
+    fc[x] = G(sd->Fc)[ii];
+    cons[x] = G(sd->cmask)[E[x].ok ? E[x].d : 0];
+    q0[x] = G(sd->Q0)[ii];
 #pragma unroll
     for (int u = 0; u < CH_TB; ++u) {
-      kk[x][u] = -1;
-      nz[x][u] = sv[x][u] = yq[x][u] = 0.0;
-      {
-        const ChBath& bd = T->tb[u];
-        kk[x][u] = bath_row(bd, E[x]);
-        if (kk[x][u] >= 0) {
-          const int64_t kb = (int64_t)kk[x][u] * B + E[x].b;
-          nz[x][u] = G(bd.noise)[((int64_t)t1 * bd.nc + kk[x][u]) * B + E[x].b];
-          sv[x][u] = G(bd.S)[(int64_t)par1 * bd.vs + kb];
-          if (bd.has_q) yq[x][u] = G(bd.Yq)[kb];
-        }
-      }
+      const ChBath& bd = T->tb[u];
+      kk[x][u] = bath_row(bd, E[x]);
+      const int64_t kb = bath_idx(E[x], kk[x][u], B);
+      nz[x][u] = G(bd.noise)[(int64_t)t1 * bd.nc * B + kb];
+      sv[x][u] = G(bd.S)[(int64_t)par1 * bd.vs + kb];
+      yq[x][u] = G(bd.Yq)[bd.has_q ? kb : 0];
     }
   }
   if (T->first && threadIdx.x < Geo::NT && T->c0 + (int)threadIdx.x < B) {
@@ -605,31 +601,23 @@ __device__ __forceinline__ void dof_BC(const ChTile* __restrict__ T, const StepD
 #pragma unroll
   for (int x = 0; x < EPT; ++x) {
     E[x] = elem_of<NW, DRN>(T, sd, x);
-    ph[x] = qt[x] = fc[x] = q0[x] = 0.0;
-    hit1[x] = true;
-    cons[x] = 0;
-    if (E[x].ok) {
-      ph[x] = G(sd->Ph)[E[x].i];
-      qt[x] = G(sd->Qt)[E[x].i];
-      fc[x] = G(sd->Fc)[E[x].i];
-      cons[x] = G(sd->cmask)[E[x].d];
-      if (harm) {
-        q0[x] = G(sd->Q0)[E[x].i];
-        hit1[x] = word_hit(*G(pmax_word(sd, 1, par, E[x].b)));
-      }
-      anyhit |= hit1[x] ? 1 : 0;
-      anymiss |= hit1[x] ? 0 : 1;
-    }
+    const int64_t ii = E[x].ok ? E[x].i : 0;
+    ph[x] = G(sd->Ph)[ii];
+    qt[x] = G(sd->Qt)[ii];
+    fc[x] = G(sd->Fc)[ii];
+    cons[x] = G(sd->cmask)[E[x].ok ? E[x].d : 0];
+    q0[x] = G(sd->Q0)[ii];
+    const unsigned long long w1 = *G(pmax_word(sd, 1, par, E[x].ok ? E[x].b : 0));
+    hit1[x] = harm ? word_hit(w1) : true;
+    anyhit |= (E[x].ok && hit1[x]) ? 1 : 0;
+    anymiss |= (E[x].ok && !hit1[x]) ? 1 : 0;
 #pragma unroll
     for (int u = 0; u < CH_TB; ++u) {
-      kk[x][u] = -1;
-      nz[x][u] = sv[x][u] = 0.0;
       const ChBath& bd = T->tb[u];
       kk[x][u] = bath_row(bd, E[x]);
-      if (kk[x][u] >= 0) {
-        nz[x][u] = G(bd.noise)[((int64_t)t1 * bd.nc + kk[x][u]) * B + E[x].b];
-        sv[x][u] = G(bd.S)[(int64_t)par1 * bd.vs + (int64_t)kk[x][u] * B + E[x].b];
-      }
+      const int64_t kb = bath_idx(E[x], kk[x][u], B);
+      nz[x][u] = G(bd.noise)[(int64_t)t1 * bd.nc * B + kb];
+      sv[x][u] = G(bd.S)[(int64_t)par1 * bd.vs + kb];
     }
   }
   // which potential-cache branches at q~ any trajectory of the tile takes (workgroup-uniform)
@@ -823,11 +811,30 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(DRN == 
   stamp(sd, STAGE, 3, ta);
 }
 
+// dynamic LDS above the 64 KiB default needs the kernel's limit raised (once per kernel and device)
+template <class K>
+bool lds_limit(K* fn, size_t lds) {
+  if (lds <= 64 * 1024) return true;
+  static thread_local int done_dev = -1;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  if (done_dev == dev) return true;
+  if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+    return false;
+  done_dev = dev;
+  return true;
+}
+
 template <int STAGE, int NW>
 void launch_nd(int drn, size_t lds, const ChTile* tiles, int ntiles, const StepDev* sd, StepArgs ta, int mode,
                hipStream_t s) {
-  if (drn == 2) chain_kernel<STAGE, NW, 2><<<ntiles, NW * 64, lds, s>>>(tiles, sd, ta, mode);
-  else chain_kernel<STAGE, NW, 1><<<ntiles, NW * 64, lds, s>>>(tiles, sd, ta, mode);
+  if (drn == 2) {
+    lds_limit(chain_kernel<STAGE, NW, 2>, lds);
+    chain_kernel<STAGE, NW, 2><<<ntiles, NW * 64, lds, s>>>(tiles, sd, ta, mode);
+  } else {
+    lds_limit(chain_kernel<STAGE, NW, 1>, lds);
+    chain_kernel<STAGE, NW, 1><<<ntiles, NW * 64, lds, s>>>(tiles, sd, ta, mode);
+  }
 }
 
 template <int STAGE>

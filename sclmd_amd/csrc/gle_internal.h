@@ -129,6 +129,13 @@ struct StepDev {
   int32_t dbg_ntile;      // stamp slots per stage
   unsigned long long* dbg;   // GLE_CHAIN_DBG: [3 stages][dbg_ntile][4] s_memrealtime stamps, or nullptr
   int64_t dbg_t;          // step whose launches record stamps
+  // per-step recording (gle_record; nullptr: off), written by stage A at step t for slot t mod nmd:
+  double* rec_p;          // md.ps  [nmd][nph][B] (md.py:374-375)
+  double* rec_q;          // md.qs  [nmd][nph][B] (md.py:376-377)
+  double* rec_hp;         // md.phis / md.qhis as rings of rec_ml slots [rec_ml][nph][B] (slot t mod
+  double* rec_hq;         //   rec_ml holds p_t / q_t, md.py:386-387)
+  double* rec_f[MAXBATH]; // md.fhis[i] bath-local [nmd][nc][B] (md.py:398)
+  int32_t rec_ml, rec_pad;
   BathDev bath[MAXBATH];
 };
 
@@ -263,6 +270,9 @@ int launch_seg_fft(const double* H, int64_t ldh, int R, int B, int nc, int ncp, 
                    const double* cstab, int cstride, hipStream_t s);
 int launch_far_ifft(const double* Y, int64_t yfstride, int64_t ysplit, int nc, int B, int P, double* out,
                     int64_t ldout, const double* cstab, int cstride, hipStream_t s);
+// velocity power spectra of recorded series (functions.powerspecp): out [ngroup][B][nmd]
+int launch_power(const double* ps, int64_t nph, int B, int64_t nmd, int ngroup, const int64_t* goff,
+                 const int64_t* dofs, const double* tw, double* out, hipStream_t s);
 int launch_fft_noise(const double* a, double* noise, const double* tw, int64_t nmd, int64_t nc,
                      int64_t arows, int64_t B, int is_complex, double scale, hipStream_t s);
 // memory-kernel construction (gle_gmem.hip): out[b o_blk + i o_row + l] = sum_g W[i][g] G[b g_blk + g g_row + l]

@@ -542,6 +542,82 @@ int launch_fft_noise(const double* a, double* noise, const double* tw, int64_t n
   return 0;
 }
 
+// Velocity power spectrum of recorded series (functions.powerspecp, functions.py:221-236): per DOF
+// group g and trajectory b, out[g][b][f] = sum_{k in group} |DFT_t(ps[t][k][b])(f)|^2 (the
+// reference's |Fourier1D|^2 = dt^2 |DFT|^2 over dt nmd is applied by the caller).  One block per
+// (g, b): the group's DOFs go two at a time through one complex radix-2 FFT in LDS (Z = x1 + i x2,
+// |X1(f)|^2 + |X2(f)|^2 = (|Z(f)|^2 + |Z(N-f)|^2) / 2), accumulated per thread in registers over
+// the frequencies it owns, in fixed DOF order (deterministic).
+template <int NS>
+__device__ __forceinline__ void lds_fft(double2* buf, int logn, const double2* tw, double sign);
+
+template <int FPT>
+__global__ __launch_bounds__(256) void power_kernel(const double* __restrict__ ps, int64_t nph, int B, int logn,
+                                                    const int64_t* __restrict__ goff, const int64_t* __restrict__ dofs,
+                                                    const double2* __restrict__ tw_g, int tw_lds,
+                                                    double* __restrict__ out) {
+  extern __shared__ double2 pbuf[];  // N points (+ N/2 twiddles when tw_lds)
+  const int N = 1 << logn;
+  const int g = blockIdx.x / B, b = blockIdx.x % B;
+  const double2* tw = tw_g;
+  if (tw_lds) {
+    for (int j = threadIdx.x; j < N / 2; j += blockDim.x) pbuf[N + j] = tw_g[j];
+    tw = pbuf + N;
+  }
+  double acc[FPT];
+#pragma unroll
+  for (int j = 0; j < FPT; ++j) acc[j] = 0.0;
+  const int64_t k0 = goff[g], k1 = goff[g + 1];
+  const int64_t rowst = nph * B;
+  for (int64_t kk = k0; kk < k1; kk += 2) {
+    const int64_t d1 = dofs[kk];
+    const bool two = kk + 1 < k1;
+    const int64_t d2 = two ? dofs[kk + 1] : d1;
+    __syncthreads();  // previous pair's reads of pbuf are done
+    for (int t = threadIdx.x; t < N; t += blockDim.x) {
+      const double x1 = ps[(int64_t)t * rowst + d1 * B + b];
+      const double x2 = two ? ps[(int64_t)t * rowst + d2 * B + b] : 0.0;
+      const unsigned rev = __brev((unsigned)t) >> (32 - logn);
+      pbuf[rev] = make_double2(x1, x2);
+    }
+    __syncthreads();
+    // (d_tw holds e^{-2 pi i j/N}: with sign -1 this is the inverse-direction transform, whose
+    // |.|^2 pair sums equal the forward ones for real series)
+    lds_fft<1>(pbuf, logn, tw, -1.0);  // ends with a barrier
+#pragma unroll
+    for (int j = 0; j < FPT; ++j) {
+      const int f = threadIdx.x + 256 * j;
+      if (f < N) {
+        const double2 z = pbuf[f], zc = pbuf[(N - f) & (N - 1)];
+        acc[j] += 0.5 * (z.x * z.x + z.y * z.y + zc.x * zc.x + zc.y * zc.y);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < FPT; ++j) {
+    const int f = threadIdx.x + 256 * j;
+    if (f < N) out[((int64_t)g * B + b) * N + f] = acc[j];
+  }
+}
+
+int launch_power(const double* ps, int64_t nph, int B, int64_t nmd, int ngroup, const int64_t* goff,
+                 const int64_t* dofs, const double* tw, double* out, hipStream_t s) {
+  int logn = 0;
+  while ((1ll << logn) < nmd) ++logn;
+  if ((1ll << logn) != nmd || nmd > 8192 || nmd < 2) return -1;
+  const int tw_lds = nmd <= 4096 ? 1 : 0;
+  const size_t shm = (size_t)nmd * sizeof(double2) + (tw_lds ? (size_t)nmd / 2 * sizeof(double2) : 0);
+  const dim3 grid((unsigned)(ngroup * B));
+  if (nmd <= 1024) {
+    if (hipFuncSetAttribute((const void*)power_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess) return -3;
+    power_kernel<4><<<grid, 256, shm, s>>>(ps, nph, B, logn, goff, dofs, (const double2*)tw, tw_lds, out);
+  } else {
+    if (hipFuncSetAttribute((const void*)power_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess) return -3;
+    power_kernel<32><<<grid, 256, shm, s>>>(ps, nph, B, logn, goff, dofs, (const double2*)tw, tw_lds, out);
+  }
+  return 0;
+}
+
 }  // namespace gle
 
 namespace gle {
@@ -702,6 +778,18 @@ constexpr int CG_LD = 80;  // LDS row stride (doubles): 64 columns + 16, ds_read
 
 typedef const __attribute__((address_space(1))) double gdbl;
 
+// The far-field operand K-hat (GBs, each fragment read once per block) streams through with
+// non-temporal loads, so it does not evict the per-step chain's matrices (~2 MB per XCD with the
+// XCD-aware chain tile order) from the L2s.  CG_NT=0: default cache policy.
+#ifndef CG_NT
+#define CG_NT 1
+#endif
+#if CG_NT
+#define CG_ALOAD(p) __builtin_nontemporal_load(p)
+#else
+#define CG_ALOAD(p) (*(p))
+#endif
+
 template <int RN, int KC, int DBG = 0>
 __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, double (&xs)[2][4 * KC * CG_LD]) {
   constexpr int NT = 16 * RN;
@@ -749,7 +837,7 @@ __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, doubl
   do {                                                                                                \
     _Pragma("unroll") for (int u = 0; u < KC; ++u) {                                               \
       const int s0_ = (c) * KC + u;                                                                \
-      AV[u] = (DBG & 1) ? 1e-3 * (s0_ + 1) : Aw[(int64_t)(s0_ < S ? s0_ : S - 1) * 64]; /* masked */ \
+      AV[u] = (DBG & 1) ? 1e-3 * (s0_ + 1) : CG_ALOAD(&Aw[(int64_t)(s0_ < S ? s0_ : S - 1) * 64]); /* masked */ \
     }                                                                                                 \
   } while (0)
   // chunk c: MFMAs on A chunk c (registers) and X chunk c (LDS buffer c&1); chunk c+2's A goes

@@ -16,7 +16,7 @@ import numpy as np
 
 from . import _native
 from . import units as U
-from .functions import bose, chkShape, mdot, powerspecp, symmetrize
+from .functions import bose, chkShape, mdot, symmetrize
 
 
 def sameq(q1, q2):
@@ -174,10 +174,77 @@ class md:
         self._log("Trajectories on this device:" + str(self.ntraj))
 
     def ResetSavepq(self):
-        if self.savep and self.nmd is not None and self.nph is not None:
-            self.ps = np.zeros((self.nmd, self.nph))
-        if self.saveq and self.nmd is not None and self.nph is not None:
-            self.qs = np.zeros((self.nmd, self.nph))
+        """Zero the recorded p / q series of the run (md.py:571-574 at a new run).  The series are
+        recorded on the device by the step itself (gle_record), for every trajectory."""
+        if self._st is not None:
+            self._st.record_zero(_native.REC_P | _native.REC_Q)
+
+    # ------------------------------------------------------------------------------ recordings
+    def _rec_flags(self):
+        f = 0
+        if self.savep:
+            f |= _native.REC_P
+        if self.saveq:
+            f |= _native.REC_Q
+        if self.saveall:
+            f |= _native.REC_F
+        if getattr(self, "_in_run", False):
+            f |= _native.REC_HIST  # md.phis / md.qhis on every DOF for the MD{j}.nc checkpoints
+        return f
+
+    def _apply_record(self):
+        if self._st is not None:
+            f = self._rec_flags()
+            if f != getattr(self, "_rec_applied", None):
+                self._st.record(f)
+                self._rec_applied = f
+
+    def _rec(self, what):
+        st = self._ensure_device()
+        self._apply_record()
+        if not (self._rec_applied & what):
+            return None
+        return st.get_record(what)
+
+    @property
+    def ps(self):
+        """md.ps (md.py:374-375): (nmd, nph), or (ntraj, nmd, nph); recorded on the device."""
+        r = self._rec(_native.REC_P)
+        if r is None:
+            return None
+        return r[0] if self.ntraj == 1 else r
+
+    @ps.setter
+    def ps(self, v):
+        self._ensure_device()
+        self._apply_record()
+        self._st.set_record(_native.REC_P, np.asarray(v, dtype=float))
+
+    @property
+    def qs(self):
+        """md.qs (md.py:376-377): (nmd, nph), or (ntraj, nmd, nph); recorded on the device."""
+        r = self._rec(_native.REC_Q)
+        if r is None:
+            return None
+        return r[0] if self.ntraj == 1 else r
+
+    @qs.setter
+    def qs(self, v):
+        self._ensure_device()
+        self._apply_record()
+        self._st.set_record(_native.REC_Q, np.asarray(v, dtype=float))
+
+    def fhis_of(self, i):
+        """md.fhis[i] (md.py:398): bath i's id0 force of every step of the run on all DOFs, (nmd, nph)
+        or (ntraj, nmd, nph); recorded on the device with SaveAll."""
+        st = self._ensure_device()
+        self._apply_record()
+        if not (self._rec_applied & _native.REC_F):
+            return None
+        r = st.get_record(_native.REC_F, i)
+        out = np.zeros((self.ntraj, self.nmd, self.nph))
+        out[:, :, np.asarray(self.baths[i].cids)] = r
+        return out[0] if self.ntraj == 1 else out
 
     def energy(self):
         """Kinetic energy 1/2 p.p (md.py:161-165)."""
@@ -481,17 +548,11 @@ class md:
                 st.set_history(i, None)
             self._reset_his = False
         self._sync_injected_noise()
-        need_host = self.savep or self.saveq or self.cf
-        if need_host:
-            t = self.t
-            p, q = np.asarray(self.p), np.asarray(self.q)
-            if self.savep:
-                self.ps[t % self.nmd] = p if self.ntraj == 1 else p[0]
-            if self.saveq:
-                self.qs[t % self.nmd] = q if self.ntraj == 1 else q[0]
-            if self.cf:
-                qq = q if self.ntraj == 1 else q[0]
-                self.cflist.append(self.forcedriver.force(qq) + mdot(self.dyn, qq))
+        self._apply_record()  # ps / qs / fhis / histories are recorded on the device by the step
+        if self.cf:  # CompareForce: a host driver call per step (md.py:378-379), trajectory 0
+            q = np.asarray(self.q)
+            qq = q if self.ntraj == 1 else q[0]
+            self.cflist.append(self.forcedriver.force(qq) + mdot(self.dyn, qq))
         if self.pforce is not None:
             if not hasattr(self, "_fcache") or len(self._fcache) != self.ntraj:
                 self._fcache = [([], None)] * self.ntraj
@@ -517,10 +578,11 @@ class md:
 
     def steps(self, n):
         """n steps; fully on the device when no host work is needed per step."""
-        if self.pforce is None and not (self.savep or self.saveq or self.cf or self.nstep):
+        if self.pforce is None and not self.cf:
             st = self._ensure_device()
             self._push_state()
             self._sync_injected_noise()
+            self._apply_record()
             st.run(n)
             self._dev_newer = True
         else:
@@ -553,10 +615,15 @@ class md:
     @property
     def phis(self):
         """Velocity history, newest first: (ml, nph), or (ntraj, ml, nph) (md.py:345-346, 386-387).
-        The device keeps the history of the bath-coupled DOFs only (the only ones the friction
-        reads); the columns of other DOFs, and rows past a bath's own ml, read as zeros."""
+        The bath DOFs come from the bath history rings the friction reads; the other DOFs from the
+        device recording of every DOF's history (md.Run records it; outside Run they read as
+        zeros, as do rows past a bath's own ml)."""
         st = self._ensure_device()
         out = np.zeros((self.ntraj, self.ml, self.nph))
+        if (getattr(self, "_rec_applied", 0) or 0) & _native.REC_HIST:
+            ph, _ = st.get_record_history()
+            n = min(self.ml, ph.shape[1])
+            out[:, :n] = ph[:, :n]
         for i, b in enumerate(self.baths):
             h = st.get_history(i)                      # (ntraj, ml_b, nc_b)
             out[:, : h.shape[1], np.asarray(b.cids)] = h
@@ -564,18 +631,34 @@ class md:
 
     @property
     def qhis(self):
-        """Position history (md.py:346, 387).  Only its newest row (the current q) ever enters a
-        force (ebath bias, baths.py:245-247), so the device keeps none: zeros of the reference's
-        shape."""
-        shp = (self.ml, self.nph) if self.ntraj == 1 else (self.ntraj, self.ml, self.nph)
-        return np.zeros(shp)
+        """Position history (md.py:346, 387), newest first: (ml, nph) or (ntraj, ml, nph), from the
+        device recording of every DOF's history (md.Run records it; zeros otherwise -- only its
+        newest row, the current q, ever enters a force, baths.py:245-247)."""
+        shp = (self.ntraj, self.ml, self.nph)
+        out = np.zeros(shp)
+        if self._st is not None and (getattr(self, "_rec_applied", 0) or 0) & _native.REC_HIST:
+            _, qh = self._st.get_record_history()
+            n = min(self.ml, qh.shape[1])
+            out[:, :n] = qh[:, :n]
+        return out[0] if self.ntraj == 1 else out
 
-    def _load_phis(self, phis):
+    def _load_phis(self, phis, qhis=None):
         st = self._ensure_device()
         self._push_state()  # history slots are relative to the device's t: set p, q, t first
         ph = np.asarray(phis, dtype=float)
         if ph.ndim == 2:
             ph = np.broadcast_to(ph, (self.ntraj,) + ph.shape)
+        self._apply_record()
+        if (self._rec_applied or 0) & _native.REC_HIST:
+            qh = np.zeros_like(ph) if qhis is None else np.asarray(qhis, dtype=float)
+            if qh.ndim == 2:
+                qh = np.broadcast_to(qh, (self.ntraj,) + qh.shape)
+            ml_r = st.get_record_history()[0].shape[1]
+            full_p = np.zeros((self.ntraj, ml_r, self.nph))
+            full_q = np.zeros((self.ntraj, ml_r, self.nph))
+            n = min(ml_r, ph.shape[1])
+            full_p[:, :n], full_q[:, :n] = ph[:, :n], qh[:, :n]
+            st.set_record_history(full_p, full_q)
         for i, b in enumerate(self.baths):
             ml_b = st.bath_ml[i]
             h = np.zeros((self.ntraj, ml_b, len(b.cids)))
@@ -585,10 +668,12 @@ class md:
         self._reset_his = False
 
     def dump(self, ipie, id):
-        """Write MD{id}.nc (md.py:684-764): energy, p, q, t, ipie, phis, qhis, and with saveall the
-        noise series (and ps/qs with savep/saveq), with savep the power spectrum.  Deviations: NetCDF
-        classic format (netCDF4 is not installed; see sclmd_amd.checkpoint); fhis{i} (the per-step
-        bath forces) is not recorded on the device and is not written."""
+        """Write MD{id}.nc (md.py:684-764): energy, p, q, t, ipie, phis, qhis, with SaveAll the noise
+        series and fhis{i} (and ps / qs with savep / saveq), with savep the power spectra.  With
+        ntraj > 1 a trajectory dimension is added.  Deviations: NetCDF classic format (netCDF4 is not
+        installed; see sclmd_amd.checkpoint), where only the first dimension may be the unlimited
+        'nnmd', so poweratomlist is stored as ('nnmd', 'atomlist', 'two') (transposed back on
+        resume)."""
         from . import checkpoint as C
 
         multi = self.ntraj > 1
@@ -606,6 +691,14 @@ class md:
             f.createDimension("atomlist", len(self.atomlist))
         for i, b in enumerate(self.baths):
             f.createDimension("n" + str(i), b.nc)
+
+        def series(name, a):  # (nmd, X) or (ntraj, nmd, X) -> record dimension first
+            a = np.asarray(a)
+            if multi:
+                C.Write2NetCDFFile(f, np.transpose(a, (1, 0, 2)), name, ("nnmd", "traj", "nph"), units="")
+            else:
+                C.Write2NetCDFFile(f, a, name, ("nnmd", "nph"), units="")
+
         if self.saveall:
             for i, b in enumerate(self.baths):
                 nz = np.asarray(b.noise)
@@ -617,14 +710,18 @@ class md:
                                        ("nnmd", "traj" + str(i), "n" + str(i)), units="")
                 else:
                     C.Write2NetCDFFile(f, nz, "noise" + str(i), ("nnmd", "n" + str(i)), units="")
+                fh = self.fhis_of(i)
+                if fh is not None:
+                    series("fhis" + str(i), fh)
             if self.savep:
-                C.Write2NetCDFFile(f, self.ps, "ps", ("nnmd", "nph"), units="")
+                series("ps", self.ps)
             if self.saveq:
-                C.Write2NetCDFFile(f, self.qs, "qs", ("nnmd", "nph"), units="")
+                series("qs", self.qs)
         if self.savep:
             C.Write2NetCDFFile(f, self.power, "power", ("nnmd", "two"), units="")
             if self.atomlist is not None:
-                C.Write2NetCDFFile(f, self.poweratomlist, "poweratomlist", ("atomlist", "nnmd", "two"), units="")
+                C.Write2NetCDFFile(f, np.transpose(self.poweratomlist, (1, 0, 2)), "poweratomlist",
+                                   ("nnmd", "atomlist", "two"), units="")
         e = np.asarray(self.etot)
         C.Write2NetCDFFile(f, e.T if multi else e, "energy", ("nnmd",) + tr, units="")
         C.Write2NetCDFFile(f, self.p, "p", tr + ("nph",), units="")
@@ -652,12 +749,13 @@ class md:
                 self.p = ReadNetCDFVar(fn, "p")
                 self.q = ReadNetCDFVar(fn, "q")
                 self.t = int(ReadNetCDFVar(fn, "t")[0])
-                self._load_phis(ReadNetCDFVar(fn, "phis"))
+                self._load_phis(ReadNetCDFVar(fn, "phis"), ReadNetCDFVar(fn, "qhis"))
                 self.power = ReadNetCDFVar(fn, "power")
                 if self.atomlist is not None:
-                    self.poweratomlist = ReadNetCDFVar(fn, "poweratomlist")
-                self.qs = ReadNetCDFVar(fn, "qs")
-                self.ps = ReadNetCDFVar(fn, "ps")
+                    self.poweratomlist = np.transpose(ReadNetCDFVar(fn, "poweratomlist"), (1, 0, 2))
+                qs, ps = ReadNetCDFVar(fn, "qs"), ReadNetCDFVar(fn, "ps")
+                self.qs = np.transpose(qs, (1, 0, 2)) if qs.ndim == 3 else qs
+                self.ps = np.transpose(ps, (1, 0, 2)) if ps.ndim == 3 else ps
                 for i, b in enumerate(self.baths):
                     nz = ReadNetCDFVar(fn, "noise" + str(i))
                     b.noise = np.transpose(nz, (1, 0, 2)) if nz.ndim == 3 else nz
@@ -667,7 +765,7 @@ class md:
                 if self.savep:
                     self.power = ReadNetCDFVar(fn, "power")
                     if self.atomlist is not None:
-                        self.poweratomlist = ReadNetCDFVar(fn, "poweratomlist")
+                        self.poweratomlist = np.transpose(ReadNetCDFVar(fn, "poweratomlist"), (1, 0, 2))
                 self.t = int(ReadNetCDFVar(fn, "t")[0])
                 return None
             raise RuntimeError("md.Run: ipie error in %s (ipie = %d)" % (fn, ipie))
@@ -677,8 +775,9 @@ class md:
             self.q = ReadNetCDFVar(fnm, "q")
             self.t = int(ReadNetCDFVar(fnm, "t")[0])
             ph = ReadNetCDFVar(fnm, "phis")
+            qh = ReadNetCDFVar(fnm, "qhis")
             if ph.shape[-2:] == (self.ml, self.nph):
-                self._load_phis(ph)
+                self._load_phis(ph, qh if qh.shape == ph.shape else None)
         elif j != 0:
             raise RuntimeError("md.Run: no previous nc file exists (%s)" % fnm)
         for i in range(len(self.baths)):
@@ -690,11 +789,15 @@ class md:
         """Independent runs nstart..nstop-1 (md.py:493-682): fresh noise per run, state and history
         carried over, per-run time-averaged heat current written to kappa.{T}.bath{i}.run{j}.dat,
         MD{j}.nc written after every piece and read back to resume an unfinished run or to continue
-        from the previous run (md.py:506-567)."""
+        from the previous run (md.py:506-567).  ps / qs / fhis and every DOF's p / q history are
+        recorded on the device by the step itself; nothing crosses PCIe per step unless a host
+        force driver or CompareForce needs it."""
         self.initialise()
         self.ResetHis()
         self.info()
         self._ensure_device()
+        self._in_run = True
+        self._apply_record()
         for j in range(self.nstart, self.nstop):
             self._log("\nMD run: " + str(j))
             ipie = self._resume(j)
@@ -709,8 +812,15 @@ class md:
                 if self.nstep is None:
                     self.steps(nsteps)
                 else:
-                    for _s in range(nsteps):
-                        self.vv(j)
+                    # frames at tt = 0 and tt % nstep == 0 (tt = t - 1 after the step, md.py:586-595):
+                    # run on the device up to each frame step, then read that one state back
+                    done = 0
+                    while done < nsteps:
+                        t = self.t
+                        nxt = t if t == 0 else ((t + self.nstep - 1) // self.nstep) * self.nstep
+                        k = min(nsteps - done, nxt - t + 1)
+                        self.steps(k)
+                        done += k
                         tt = self.t - 1
                         if traj is not None and (tt == 0 or tt % self.nstep == 0):
                             self._write_frame(traj, tt)
@@ -739,6 +849,7 @@ class md:
             if self.rmnc and os.path.exists(self._ncname(j - 1)):
                 self._log("Remove " + self._ncname(j - 1))
                 os.remove(self._ncname(j - 1))
+        self._in_run = False
 
     def _write_frame(self, fh, tt):
         q = self.q if self.ntraj == 1 else self.q[0]
@@ -750,22 +861,57 @@ class md:
                      str(s[ip * 3 + 2]) + "   " + str(f[ip * 3]) + "   " + str(f[ip * 3 + 1]) + "   " +
                      str(f[ip * 3 + 2]) + "\n")
 
+    def power_spectra(self):
+        """md.GetPower (md.py:351-360) on the device: functions.powerspecp of the recorded ps for all
+        DOFs and for each AddPowerSection group, averaged over this rank's trajectories (one
+        trajectory: exactly the reference's).  Returns (power (nmd, 2), [poweratomlist rows])."""
+        st = self._ensure_device()
+        self._apply_record()
+        groups = [np.arange(self.nph)]
+        if self.atomlist is not None:
+            groups += [np.asarray(list(a), dtype=np.int64) for a in self.atomlist]
+        spec = st.power_spectrum(groups)                  # (ngroup, ntraj, nmd): sum_k |DFT|^2
+        from . import ensemble  # ensemble mean over every rank's trajectories (a no-op reduce alone)
+
+        tot = ensemble.allreduce_sums(np.concatenate([spec.sum(axis=1).ravel(), [self.ntraj]]), self.comm,
+                                      device=self._device_ordinal())
+        mean = tot[:-1].reshape(len(groups), self.nmd) / tot[-1]
+        dw = 2.0 * np.pi / self.dt / self.nmd
+        w = dw * np.arange(self.nmd)
+        rows = [np.stack([w, m * self.dt / self.nmd], axis=1) for m in mean]  # functions.py:233-236
+        return rows[0], rows[1:]
+
     def _power(self, j):
-        """Running average of the velocity power spectrum over runs (md.py:604-653)."""
+        """Running average of the velocity power spectra over runs, power.*.dat and
+        poweratomlist.*.dat files (md.py:604-653)."""
         prev = np.copy(self.power)
-        self.power = powerspecp(self.ps, self.dt, self.nmd)
+        prev_al = None if self.atomlist is None else np.copy(self.poweratomlist)
+        power, al = self.power_spectra()
         k = j - self.nstart
-        if k > 0:
-            self.power = (prev * k + self.power) / float(k + 1)
+        self.power = (prev * k + power) / float(k + 1) if k > 0 else power
+        if self.atomlist is not None:
+            al = np.array(al)
+            self.poweratomlist = (prev_al * k + al) / float(k + 1) if k > 0 else al
         if self._is_root():
-            with open("power." + str(self.T) + ".run" + str(j) + ".dat", "w") as f:
-                for ni in range(len(self.power)):
-                    if self.hw is not None and self.power[ni, 0] >= 1.5 * max(self.hw):
-                        break
-                    f.write("%f     %f \n" % (self.power[ni, 0], self.power[ni, 1]))
+            def write(fn, pw):
+                with open(fn, "w") as f:
+                    for ni in range(len(pw)):
+                        if self.hw is not None and pw[ni, 0] >= 1.5 * max(self.hw):
+                            break
+                        f.write("%f     %f \n" % (pw[ni, 0], pw[ni, 1]))
+
+            write("power." + str(self.T) + ".run" + str(j) + ".dat", self.power)
+            if self.atomlist is not None:
+                for layer in range(len(self.atomlist)):
+                    write("poweratomlist." + str(layer) + "." + str(self.T) + ".run" + str(j) + ".dat",
+                          self.poweratomlist[layer])
 
     def _avestructure(self, j):
-        ave = self.conv * (self.qs.mean(axis=0)) + self.xyz
+        """avestructure.{T}.run{j}.dat (md.py:665-675): time average of the recorded qs (and over this
+        rank's trajectories)."""
+        qs = np.asarray(self.qs)
+        qm = qs.mean(axis=0) if qs.ndim == 2 else qs.mean(axis=(0, 1))
+        ave = self.conv * qm + self.xyz
         with open("avestructure." + str(self.T) + ".run" + str(j) + ".dat", "w") as f:
             f.write(str(len(self.els)) + "\n" + "average structure" + "\n")
             for ip in range(len(self.els)):

@@ -18,6 +18,13 @@ Fixtures (each < 1 MB):
   vv_*.npz        md.vv trajectories with injected noise/kernels        (md.py:367-474, baths.py:224-255, 448-458)
   run_seeded.npz  initialise + per-run gnoi + vv + kappa, seeded numpy RNG (md.py:294-338, 493-664)
   tools.npz       calHF / calTC outputs on synthetic kappa files        (tools.py:132-215)
+  power.npz       savep / saveq vv run: ps, qs, fhis, GetPower's power and per-section spectra,
+                  average structure                                     (md.py:351-360, 374-398, 604-675,
+                                                                         functions.py:221-236)
+  ggamma.npz      phbath built from a self-energy sig: gamma = -Im sig / w, gmem kernel
+                                                                        (baths.py:294-340, 375-395, 412-445)
+
+    python3 tests/golden/make_golden.py [name ...]     (default: all)
 """
 import contextlib
 import io
@@ -414,13 +421,78 @@ def make_tools():
     np.savez_compressed(os.path.join(HERE, "tools.npz"), **out)
 
 
+# ----------------------------------------------------------------------------- power spectra
+def make_power():
+    """A vv run with CalPowerSpec + AddPowerSection + CalAveStruct (md.py:185-197): the recorded ps /
+    qs / fhis, GetPower's power and poweratomlist (md.py:351-360), the average structure
+    (md.py:665-675).  Same system shape as vv_mixed; nsteps = nmd so every ps row is written."""
+    dt = 0.25 / 0.658
+    T = 300.0
+    rng = np.random.default_rng(41)
+    natom, nmd = 5, 32
+    dyn = chain_dyn(natom, seed=42)
+    ecids = [0, 1, 2, 3]
+    pcids = [10, 11, 12, 13, 14]
+    with quiet():
+        eb = RB.ebath(ecids, T * 1.05, dt, nmd, wmax=1.0, nw=100, bias=0.0,
+                      efric=spd(len(ecids), rng, 0.658 / 100))
+        gwl, gam = gamma_table(len(pcids), rng)
+        pb = RB.phbath(T * 0.95, pcids, debye=0.2, nw=60, dt=dt, nmd=nmd, ml=16, gamma=gam, gwl=gwl)
+        pb.gmem()
+    eb.noise = rng.normal(size=(nmd, len(ecids))) * 1e-3
+    pb.noise = rng.normal(size=(nmd, len(pcids))) * 1e-3
+    atomlist = [[0, 1, 2, 3, 4, 5], [9, 10, 11, 12, 13, 14]]
+    m = build_md(natom, dt, nmd, T, dyn, [eb, pb], [range(5, 7)], seed_init=43)
+    with quiet():
+        m.CalPowerSpec()
+        m.AddPowerSection(atomlist)
+        m.CalAveStruct()
+        m.ResetSavepq()
+        p0, q0 = np.array(m.p), np.array(m.q)
+        run_vv(m, nmd)
+        m.GetPower()
+    ave = m.conv * (m.qs.mean(axis=0)) + m.xyz
+    out = {"natom": natom, "nmd": nmd, "dt": dt, "T": T, "dyn": dyn, "nsteps": nmd, "noranvel": False,
+           "p0": p0, "q0": q0, "nbath": 2, "dyn_md": np.array(m.dyn),
+           "constr": np.array([5, 6]), "constr_ranges": np.array([[5, 7]]),
+           "atomlist": np.array(atomlist), "ps": np.array(m.ps), "qs": np.array(m.qs),
+           "power": np.array(m.power), "poweratomlist": np.array(m.poweratomlist),
+           "fhis0": np.array(m.fhis[0]), "fhis1": np.array(m.fhis[1]), "avestructure": ave,
+           "hw": np.array(m.hw), "p_end": np.array(m.p), "q_end": np.array(m.q)}
+    for i, b in enumerate([eb, pb]):
+        bath_record("b%d" % i, b, out)
+        out["b%d_kind" % i] = "ebath" if isinstance(b, RB.ebath) else "phbath"
+        if isinstance(b, RB.ebath):
+            out["b%d_bias" % i] = b.bias
+            for nm in ("efric", "exim", "exip", "zeta1", "zeta2"):
+                out["b%d_%s" % (i, nm)] = np.array(getattr(b, nm))
+    np.savez_compressed(os.path.join(HERE, "power.npz"), **out)
+
+
+# ----------------------------------------------------------------------------- ggamma
+def make_ggamma():
+    """phbath from a self-energy: gamma(w) = -Im sig(w) / w, the w = 0 row from the next point
+    (baths.py:375-395), then gmem (baths.py:412-445)."""
+    dt = 0.25 / 0.658
+    rng = np.random.default_rng(51)
+    nc, ngw, ml, nmd = 4, 21, 24, 32
+    gwl = np.linspace(0.0, 0.4, ngw)
+    base = spd(nc, rng, 0.658 / 100)
+    sig = np.array([(rng.normal(size=(nc, nc)) * 1e-4 + 0.0j) - 1j * w * (base * np.exp(-(w / 0.15) ** 2))
+                    for w in gwl])
+    with quiet():
+        b = RB.phbath(300.0, [3, 4, 5, 6], debye=0.2, nw=50, dt=dt, nmd=nmd, ml=ml, sig=sig, gwl=gwl)
+        gamma = np.array(b.gamma)
+        b.gmem()
+    np.savez_compressed(os.path.join(HERE, "ggamma.npz"), sig=sig, gwl=gwl, nc=nc, ml=ml, nmd=nmd, dt=dt,
+                        debye=0.2, nw=50, cids=np.array([3, 4, 5, 6]), gamma=gamma, kernel=np.array(b.kernel))
+
+
 if __name__ == "__main__":
-    make_scalars()
-    make_gamt()
-    make_noise()
-    make_vv_cases()
-    make_run_seeded()
-    make_tools()
+    makers = {"scalars": make_scalars, "gamt": make_gamt, "noise": make_noise, "vv": make_vv_cases,
+              "run_seeded": make_run_seeded, "tools": make_tools, "power": make_power, "ggamma": make_ggamma}
+    for name in (sys.argv[1:] or list(makers)):
+        makers[name]()
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))
