@@ -148,6 +148,17 @@ int gle_noise_factors(gle_handle* h, int32_t bath, int64_t nfreq, const double* 
 int gle_noise_generate(gle_handle* h, int32_t bath, const double* x_host, uint64_t seed,
                        uint64_t traj_offset);
 
+/* Streamed generation for baths whose per-frequency factors do not fit on the device beside the
+ * spectral kernels (C5: 4097 x 1000^2 doubles per bath): begin allocates the spectrum; each chunk
+ * hands over the factors M_w of frequencies [w0, w0 + nw) (row-major [nw][nc][nc], real, or real
+ * and imaginary parts), draws N(0,1) on the device with the same Philox keys as
+ * gle_noise_generate (so both give the same realisation for the same factors and seed) and forms
+ * a_w = M_w x_w; end mirrors, transforms and scales exactly as gle_noise_generate. */
+int gle_noise_stream_begin(gle_handle* h, int32_t bath, int32_t is_complex, int64_t max_chunk);
+int gle_noise_stream_chunk(gle_handle* h, int32_t bath, int64_t w0, int64_t nw, const double* m_re,
+                           const double* m_im, uint64_t seed, uint64_t traj_offset);
+int gle_noise_stream_end(gle_handle* h, int32_t bath);
+
 /* ---- stepping (md.vv, md.py:367-411) -------------------------------------------------- */
 /* Phase A of one step: F0 = Fpot(q_t) + sum_b bforce_b(t, id=0), current, half kick, drift.
  * fpot  [ntraj][nph] host force at q_t (driver.force(q), md.py:463-464) or NULL to use the

@@ -28,7 +28,8 @@ EXPORTS = [
     "gle_profile_read", "gle_plan_info", "gle_add_bath_gmem", "gle_get_kernel", "gle_gamt",
     "gle_profile_levels", "gle_step_work", "gle_reduce_current", "gle_comm_unique_id", "gle_comm_init",
     "gle_comm_destroy", "gle_record", "gle_record_zero", "gle_get_record", "gle_get_record_history",
-    "gle_power_spectrum", "gle_set_record", "gle_set_record_history",
+    "gle_power_spectrum", "gle_set_record", "gle_set_record_history", "gle_noise_stream_begin",
+    "gle_noise_stream_chunk", "gle_noise_stream_end",
 ]
 
 REC_P, REC_Q, REC_F, REC_HIST = 1, 2, 4, 8
@@ -99,6 +100,10 @@ _SIGS = {
     "gle_power_spectrum": (ctypes.c_int, [_P, ctypes.c_int32, _I64, _I64, _D]),
     "gle_set_record": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, _D]),
     "gle_set_record_history": (ctypes.c_int, [_P, _D, _D]),
+    "gle_noise_stream_begin": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64]),
+    "gle_noise_stream_chunk": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, _D, _D,
+                                              ctypes.c_uint64, ctypes.c_uint64]),
+    "gle_noise_stream_end": (ctypes.c_int, [_P, ctypes.c_int32]),
 }
 
 _lib = None
@@ -328,6 +333,18 @@ class Stepper:
             x = _f64(x)
         self._chk(self.lib.gle_noise_generate(self.h, int(bath), _ptr(x), int(seed) & (2**64 - 1),
                                               int(traj_offset)), "gle_noise_generate")
+
+    def noise_stream(self, bath, factor_chunks, is_complex, seed, traj_offset=0, max_chunk=64):
+        """Streamed device noise: factor_chunks yields (w0, M) with M (nw, nc, nc) real or complex."""
+        self._chk(self.lib.gle_noise_stream_begin(self.h, int(bath), 1 if is_complex else 0, int(max_chunk)),
+                  "gle_noise_stream_begin")
+        for w0, m in factor_chunks:
+            mre = _f64(np.real(m))
+            mim = _f64(np.imag(m)) if is_complex else None
+            self._chk(self.lib.gle_noise_stream_chunk(self.h, int(bath), int(w0), int(m.shape[0]), _ptr(mre),
+                                                      _ptr(mim), int(seed) & (2**64 - 1), int(traj_offset)),
+                      "gle_noise_stream_chunk")
+        self._chk(self.lib.gle_noise_stream_end(self.h, int(bath)), "gle_noise_stream_end")
 
     # --------------------------------------------------------------------------- stepping
     def step_begin(self, fpot=None, want_qt=True):

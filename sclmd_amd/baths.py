@@ -11,6 +11,7 @@ from concurrent.futures import ThreadPoolExecutor
 import numpy as np
 
 from . import noise as _noise
+from . import units as U
 from .functions import antisymmetrize, chkShape, flinterp_many, interp_weights, symmetrize
 
 
@@ -187,6 +188,36 @@ class ebath(_BathBase):
         return _noise.electron_spectrum(self.efric, self.exim, self.exip, self.bias, self.T, self.wmax,
                                         self.dt, self.nmd, self.classical, self.zpmotion)
 
+    # streamed factors (noise.stream_factor_chunks): A(w) = aw (efric - exip) + awm/2 (exip + i exim)
+    # + awp/2 (exip - i exim), hermitianised (noise.py:171-186), with aw, awm, awp >= 0
+    def _shared_matrices(self):
+        from .functions import hermitianize
+
+        e = np.asarray(self.efric, dtype=float)
+        x = np.asarray(self.exip, dtype=float)
+        y = np.asarray(self.exim, dtype=float)
+        return [("0", hermitianize((e - x).astype(complex))), ("m", hermitianize(0.5 * (x + 1j * y))),
+                ("p", hermitianize(0.5 * (x - 1j * y)))]
+
+    def _spectrum_term(self, i):
+        dw = 2.0 * np.pi / self.dt / self.nmd
+        delta = self.dt * self.nmd
+        w = dw * i
+        c = np.array([delta * _noise.equ(w, self.wmax, self.T, self.classical, self.zpmotion),
+                      delta * _noise.equ(U.hbar * w - self.bias, self.wmax, self.T, self.classical, self.zpmotion),
+                      delta * _noise.equ(U.hbar * w + self.bias, self.wmax, self.T, self.classical, self.zpmotion)])
+        nz = np.flatnonzero(c)
+        if len(nz) == 0:
+            return "zero", None, 0.0, None
+        if len(nz) == 1:
+            return "shared", "0mp"[nz[0]], float(c[nz[0]]), None
+        m = c[0] * self.efric
+        m = m + (-0.5 * c[0] * self.exip + 0.5 * c[1] * (self.exip + 1j * self.exim))
+        m = m + (-0.5 * c[0] * self.exip + 0.5 * c[2] * (self.exip - 1j * self.exim))
+        from .functions import hermitianize
+
+        return "dense", None, 1.0, hermitianize(m)
+
 
 class phbath(_BathBase):
     """Phonon bath (baths.py:258-458)."""
@@ -316,3 +347,26 @@ class phbath(_BathBase):
     def _spectrum(self):
         return _noise.phonon_spectrum(self.gamma, self.gwl, self.T, self.wmax, self.dt, self.nmd,
                                       self.classical, self.zpmotion)
+
+    # streamed factors (noise.stream_factor_chunks): A(w) = Delta equ(w) flinterp(w, gwl, gamma),
+    # hermitianised (noise.py:73-79); where flinterp returns a node (its flat end half-cells,
+    # functions.py:124-127) A is a non-negative multiple of that node's matrix
+    def _shared_matrices(self):
+        from .functions import hermitianize
+
+        g = np.asarray(self.gamma)
+        return [(0, hermitianize(g[0])), (len(g) - 1, hermitianize(g[-1]))]
+
+    def _spectrum_term(self, i):
+        from .functions import flinterp, hermitianize, nearest
+
+        dw = 2.0 * np.pi / self.dt / self.nmd
+        delta = self.dt * self.nmd
+        w = dw * i
+        c = delta * _noise.equ(w, self.wmax, self.T, self.classical, self.zpmotion)
+        if c == 0.0:
+            return "zero", None, 0.0, None
+        n = nearest(w, self.gwl)
+        if n == 0 or n == len(self.gwl) - 1:
+            return "shared", (0 if n == 0 else len(self.gwl) - 1), float(c), None
+        return "dense", None, 1.0, hermitianize(c * flinterp(w, self.gwl, self.gamma))

@@ -94,6 +94,11 @@ struct Bath {
   bool fac_complex = false;
   int fac_rows = 0, fac_nrt = 0;
   double* d_fac = nullptr;
+  // streamed noise generation (gle_noise_stream_*): spectrum a [nfreq][rows][B], per-chunk draws
+  // [cap][ncp][B] and factor chunk [cap][nc][nc] (x2 when complex); scratch between begin and end
+  double *d_sa = nullptr, *d_sx = nullptr, *d_sm = nullptr;
+  int64_t s_cap = 0;
+  bool s_complex = false;
 };
 
 // One level of the memory-sum ladder for one bath.
@@ -2549,6 +2554,80 @@ int gle_noise_generate(gle_handle* h, int32_t bath, const double* x_host, uint64
     }
   }
   cleanup();
+  b.noise_set = true;
+  return GLE_OK;
+}
+
+namespace {
+void free_stream(Bath& b) {
+  for (double** p : {&b.d_sa, &b.d_sx, &b.d_sm}) {
+    if (*p) hipFree(*p);
+    *p = nullptr;
+  }
+  b.s_cap = 0;
+}
+}  // namespace
+
+int gle_noise_stream_begin(gle_handle* h, int32_t bath, int32_t is_complex, int64_t max_chunk) {
+  int rc = check_bath(h, bath);
+  if (rc) return rc;
+  if (max_chunk < 1) return fail(h, GLE_ERR_ARG, "max_chunk must be >= 1");
+  hipSetDevice(h->cfg.device);
+  Bath& b = h->baths[bath];
+  free_stream(b);
+  const int64_t nf = h->nmd / 2 + 1, B = h->B;
+  const int64_t rows = is_complex ? 2 * b.nc : b.nc;
+  b.s_complex = is_complex != 0;
+  b.s_cap = std::min(max_chunk, nf);
+  const size_t na = (size_t)nf * rows * B, nx = (size_t)b.s_cap * b.ncp * B,
+               nm = (size_t)b.s_cap * b.nc * b.nc * (is_complex ? 2 : 1);
+  if (hipMalloc((void**)&b.d_sa, na * 8) != hipSuccess || hipMalloc((void**)&b.d_sx, nx * 8) != hipSuccess ||
+      hipMalloc((void**)&b.d_sm, nm * 8) != hipSuccess) {
+    free_stream(b);
+    return fail(h, GLE_ERR_NOMEM, "noise stream buffers (" + std::to_string((na + nx + nm) >> 17) + " MiB)");
+  }
+  HIPCHK(h, hipMemsetAsync(b.d_sa, 0, na * 8, h->stream));
+  return GLE_OK;
+}
+
+int gle_noise_stream_chunk(gle_handle* h, int32_t bath, int64_t w0, int64_t nw, const double* m_re,
+                           const double* m_im, uint64_t seed, uint64_t traj_offset) {
+  int rc = check_bath(h, bath);
+  if (rc) return rc;
+  Bath& b = h->baths[bath];
+  if (!b.d_sa) return fail(h, GLE_ERR_STATE, "gle_noise_stream_begin first");
+  const int64_t nf = h->nmd / 2 + 1;
+  if (!m_re || w0 < 0 || nw < 1 || nw > b.s_cap || w0 + nw > nf || (b.s_complex && !m_im))
+    return fail(h, GLE_ERR_ARG, "bad noise stream chunk");
+  hipSetDevice(h->cfg.device);
+  const int64_t B = h->B, nc = b.nc, rows = b.s_complex ? 2 * nc : nc;
+  const size_t nm = (size_t)nw * nc * nc;
+  // the previous chunk's products read d_sx / d_sm: the copies below are stream-ordered after them
+  HIPCHK(h, hipMemcpyAsync(b.d_sm, m_re, nm * 8, hipMemcpyHostToDevice, h->stream));
+  if (b.s_complex) HIPCHK(h, hipMemcpyAsync(b.d_sm + nm, m_im, nm * 8, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemsetAsync(b.d_sx, 0, (size_t)nw * b.ncp * B * 8, h->stream));
+  launch_philox_normal(b.d_sx, nw, b.ncp, nc, B, seed, traj_offset, h->stream, w0);
+  launch_noise_gemm(b.d_sm, (int)nc, (int)nc, b.d_sx, b.ncp, (int)B, b.d_sa, (int)rows, 0, w0, (int)nw, h->stream);
+  if (b.s_complex)
+    launch_noise_gemm(b.d_sm + nm, (int)nc, (int)nc, b.d_sx, b.ncp, (int)B, b.d_sa, (int)rows, (int)nc, w0, (int)nw,
+                      h->stream);
+  HIPCHK(h, hipStreamSynchronize(h->stream));  // the caller reuses its host chunk buffers
+  return GLE_OK;
+}
+
+int gle_noise_stream_end(gle_handle* h, int32_t bath) {
+  int rc = check_bath(h, bath);
+  if (rc) return rc;
+  Bath& b = h->baths[bath];
+  if (!b.d_sa) return fail(h, GLE_ERR_STATE, "gle_noise_stream_begin first");
+  hipSetDevice(h->cfg.device);
+  const double scale = 1.0 / (h->dt * (double)h->nmd);  // dw/2pi (functions.py:51)
+  const int frc = launch_fft_noise(b.d_sa, b.d_noise, h->d_tw, h->nmd, b.nc, b.s_complex ? 2 * b.nc : b.nc, h->B,
+                                   b.s_complex ? 1 : 0, scale, h->stream);
+  const hipError_t e = hipStreamSynchronize(h->stream);
+  free_stream(b);
+  if (frc) return fail(h, GLE_ERR_UNSUP, "device noise FFT needs nmd a power of two <= 8192");
+  if (e != hipSuccess) return fail(h, GLE_ERR_HIP, std::string("noise stream: ") + hipGetErrorString(e));
   b.noise_set = true;
   return GLE_OK;
 }

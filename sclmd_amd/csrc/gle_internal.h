@@ -256,7 +256,10 @@ void launch_chain(int stage, int nw, int drn, size_t lds_bytes, const ChTile* ti
                   StepArgs ta, int mode, hipStream_t s);
 void launch_finalize(const StepDev* sd, int B, int nmd, int nbath, hipStream_t s);
 void launch_philox_normal(double* x, int64_t nfreq, int64_t ncp, int64_t nc, int64_t B,
-                          uint64_t seed, uint64_t traj_offset, hipStream_t s);
+                          uint64_t seed, uint64_t traj_offset, hipStream_t s, int64_t w_off = 0);
+// streamed noise: a[w0 + w][row_off + r][b] = sum_k M[w][r][k] x[w][k][b] for w < nw
+void launch_noise_gemm(const double* M, int nc, int kc, const double* x, int ncp, int B, double* a, int rows,
+                       int row_off, int64_t w0, int nw, hipStream_t s);
 void launch_near_fill(const double* H, int64_t ldh, int R, int B, int ncp, double* NR, int64_t vs, int NRS,
                       int64_t t, hipStream_t s);
 void launch_ring_copy(double* H, int64_t ldh, int R, int B, int nc, int64_t tau0, int nt, double* buf,

@@ -448,20 +448,77 @@ __device__ __forceinline__ double philox_normal(uint64_t seed, uint32_t a, uint3
 }
 
 __global__ void philox_kernel(double* x, int64_t nfreq, int64_t ncp, int64_t nc, int64_t B,
-                              uint64_t seed, uint64_t traj_offset) {
+                              uint64_t seed, uint64_t traj_offset, int64_t w_off) {
   const int64_t n = nfreq * ncp * B;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t b = e % B;
     const int64_t k = (e / B) % ncp;
-    const int64_t w = e / (B * ncp);
+    const int64_t w = e / (B * ncp) + w_off;
     x[e] = (k < nc) ? philox_normal(seed, (uint32_t)k, (uint32_t)w, (uint32_t)(traj_offset + b)) : 0.0;
   }
 }
 
 void launch_philox_normal(double* x, int64_t nfreq, int64_t ncp, int64_t nc, int64_t B,
-                          uint64_t seed, uint64_t traj_offset, hipStream_t s) {
-  philox_kernel<<<2048, 256, 0, s>>>(x, nfreq, ncp, nc, B, seed, traj_offset);
+                          uint64_t seed, uint64_t traj_offset, hipStream_t s, int64_t w_off) {
+  philox_kernel<<<2048, 256, 0, s>>>(x, nfreq, ncp, nc, B, seed, traj_offset, w_off);
+}
+
+// Streamed noise generation (C5-size baths, whose per-frequency factors do not fit next to the
+// spectral kernels): for the frequencies of one chunk, a[w0 + w][row_off + r][b] =
+//   sum_k M[w][r][k] x[w][k][b]  with M row-major [nw][nc][kc] (a real factor, or the real or the
+// imaginary part of a complex one) and x the chunk's N(0,1) draws [nw][ncp][B].  Setup work
+// (once per run), LDS-tiled fp64 FMA: 64 rows x 32 columns per block, k in steps of 32.
+constexpr int NG_R = 64, NG_C = 32, NG_K = 32;
+__global__ __launch_bounds__(256) void noise_gemm_kernel(const double* __restrict__ M, int nc, int kc,
+                                                         const double* __restrict__ x, int ncp, int B,
+                                                         double* __restrict__ a, int rows, int row_off,
+                                                         int64_t w0) {
+  __shared__ double Ms[NG_R][NG_K + 1];
+  __shared__ double Xs[NG_K][NG_C + 1];
+  const int w = blockIdx.z;
+  const int r0 = blockIdx.x * NG_R, c0 = blockIdx.y * NG_C;
+  const int tid = threadIdx.x;
+  const int ty = tid / 8, tx = tid % 8;  // rows 2 ty, 2 ty + 1; columns 4 tx .. 4 tx + 3
+  const double* Mw = M + (int64_t)w * nc * kc;
+  const double* xw = x + (int64_t)w * ncp * B;
+  double acc[2][4] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+  for (int k0 = 0; k0 < kc; k0 += NG_K) {
+    for (int e = tid; e < NG_R * NG_K; e += 256) {
+      const int r = e / NG_K, k = e % NG_K;
+      Ms[r][k] = (r0 + r < nc && k0 + k < kc) ? Mw[(int64_t)(r0 + r) * kc + k0 + k] : 0.0;
+    }
+    for (int e = tid; e < NG_K * NG_C; e += 256) {
+      const int k = e / NG_C, c = e % NG_C;
+      Xs[k][c] = (k0 + k < kc && c0 + c < B) ? xw[(int64_t)(k0 + k) * B + c0 + c] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int k = 0; k < NG_K; ++k) {
+      const double m0 = Ms[2 * ty][k], m1 = Ms[2 * ty + 1][k];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const double xv = Xs[k][4 * tx + j];
+        acc[0][j] += m0 * xv;
+        acc[1][j] += m1 * xv;
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = r0 + 2 * ty + i, c = c0 + 4 * tx + j;
+      if (r < nc && c < B) a[((w0 + w) * rows + row_off + r) * (int64_t)B + c] = acc[i][j];
+    }
+}
+
+void launch_noise_gemm(const double* M, int nc, int kc, const double* x, int ncp, int B, double* a, int rows,
+                       int row_off, int64_t w0, int nw, hipStream_t s) {
+  if (nw <= 0) return;
+  const dim3 grid((unsigned)((nc + NG_R - 1) / NG_R), (unsigned)((B + NG_C - 1) / NG_C), (unsigned)nw);
+  noise_gemm_kernel<<<grid, 256, 0, s>>>(M, nc, kc, x, ncp, B, a, rows, row_off, w0);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -471,10 +471,29 @@ class md:
                 self._st.set_noise(i, n)
                 self._noise_versions[i] = v
 
+    # factors above this size are streamed to the device by frequency chunk instead of being held
+    # there whole (C5: 4097 x 1000^2 doubles per bath beside ~200 GB of spectral kernels)
+    noise_stream_bytes = 4 << 30
+
+    def _noise_seed(self, i, run):
+        base = 0 if self.seed is None else int(self.seed)
+        return (base * 0x9E3779B97F4A7C15 + (run + 1) * 0xBF58476D1CE4E5B9 + (i + 1) * 0x94D049BB133111EB) % 2**64
+
     def gen_noise(self, i, run=0):
         """New noise realisation for bath i on the device (bath.gnoi, md.py:569-570)."""
+        from . import noise as _noise
+
         st = self._ensure_device()
         b = self.baths[i]
+        nfreq = int(self.nmd / 2) + 1
+        fac_bytes = nfreq * b.nc * b.nc * 8 * (2 if b.kind == "ebath" else 1)
+        if self.noise_mode == "device" and fac_bytes > self.noise_stream_bytes:
+            st.noise_stream(i, _noise.stream_factor_chunks(b), b.kind == "ebath", self._noise_seed(i, run),
+                            self.traj_offset)
+            b._noise_src = (st, i)
+            b._noise_version = getattr(b, "_noise_version", 0) + 1
+            self._noise_versions[i] = b._noise_version
+            return
         fac = b.noise_factor()
         key = (self.noise_mode, b._fac_key)
         if getattr(self, "_fac_loaded", {}).get(i) != key:
@@ -485,9 +504,7 @@ class md:
             x = np.stack([fac.draws(self._rng(bb)) for bb in range(self.ntraj)])
             st.noise_generate(i, x)
         else:
-            base = 0 if self.seed is None else int(self.seed)
-            key64 = (base * 0x9E3779B97F4A7C15 + (run + 1) * 0xBF58476D1CE4E5B9 + (i + 1) * 0x94D049BB133111EB) % 2**64
-            st.noise_generate(i, None, seed=key64, traj_offset=self.traj_offset)
+            st.noise_generate(i, None, seed=self._noise_seed(i, run), traj_offset=self.traj_offset)
         b._noise_src = (st, i)
         b._noise_version = getattr(b, "_noise_version", 0) + 1
         self._noise_versions[i] = b._noise_version

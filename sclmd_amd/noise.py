@@ -101,6 +101,71 @@ class NoiseFactor:
         return r
 
 
+# ---------------------------------------------------------------------------------------------
+# streamed factors (baths whose nfreq x nc x nc factors do not fit on the device, e.g. C5)
+def positive_factor(a):
+    """U diag(sqrt(max(lambda, 0))) of a Hermitian matrix: the covariance vargau draws from
+    (noise.py:273-305, only positive eigenvalues)."""
+    ev, vec = np.linalg.eigh(a)
+    return vec * np.sqrt(np.where(ev > 0, ev, 0.0))[None, :]
+
+
+def dense_factor(a):
+    """A factor M with M M^H = A_+ for one frequency.  Real symmetric positive-definite A: its
+    Cholesky factor (the same Gaussian distribution as the eigen factor for real draws, at ~1/10 of
+    the cost); otherwise (complex Hermitian, or not positive definite) the eigen factor, so complex
+    baths keep the reference's eigenvector phases."""
+    if not np.iscomplexobj(a):
+        try:
+            return np.linalg.cholesky(a)
+        except np.linalg.LinAlgError:
+            pass
+    return positive_factor(a)
+
+
+def stream_factor_chunks(bath, chunk=64, workers=None):
+    """Yield (w0, M) with M (nw, nc, nc) the factors of frequencies [w0, w0 + nw), built on a
+    thread pool (LAPACK releases the GIL; BLAS pinned to one thread per worker).  The bath supplies
+    per frequency either nothing (A = 0), a shared matrix with a non-negative scale (A = s H: factor
+    sqrt(s) H_+^(1/2), one eigendecomposition for all such frequencies) or the dense A."""
+    import os
+    from concurrent.futures import ThreadPoolExecutor
+
+    from threadpoolctl import threadpool_limits
+
+    nfreq = int(bath.nmd / 2) + 1
+    nc = bath.nc
+    cplx = bath.kind == "ebath"
+    dtype = complex if cplx else float
+    shared = {}
+    if workers is None:
+        try:
+            workers = len(os.sched_getaffinity(0))
+        except AttributeError:  # pragma: no cover
+            workers = os.cpu_count() or 1
+        workers = max(1, min(16, workers))
+
+    def one(i):
+        kind, key, s, a = bath._spectrum_term(i)
+        if kind == "zero":
+            return np.zeros((nc, nc), dtype=dtype)
+        if kind == "shared":
+            return np.sqrt(s) * shared[key]
+        return dense_factor(a).astype(dtype, copy=False)
+
+    with threadpool_limits(1, user_api="blas"), ThreadPoolExecutor(max_workers=workers) as pool:
+        for key, h in bath._shared_matrices():
+            shared[key] = positive_factor(h).astype(dtype, copy=False)
+        futs = []
+        for w0 in range(0, nfreq, chunk):
+            futs.append((w0, [pool.submit(one, i) for i in range(w0, min(nfreq, w0 + chunk))]))
+            if len(futs) > 2:  # two chunks in flight ahead of the device
+                w, fl = futs.pop(0)
+                yield w, np.stack([f.result() for f in fl])
+        for w, fl in futs:
+            yield w, np.stack([f.result() for f in fl])
+
+
 def generate(factor, dt, nmd, ntraj=1, rngs=None, seed=None, device=0):
     """Standalone device generation of ntraj realisations (ntraj, nmd, nc) for one factor."""
     st = _native.Stepper(factor.nc, ntraj, nmd, dt, device)
