@@ -45,6 +45,13 @@ def measure(args, meta, dyn, baths):
         st.run(args.short)
         st.sync()
         el_short = time.perf_counter() - t0
+        # the same window started on a piece-slot boundary (t = 0 mod P0)
+        st.run((-(2 * ptop + 5 + args.short)) % st.plan_info()["block_len"])
+        st.sync()
+        t0 = time.perf_counter()
+        st.run(args.short)
+        st.sync()
+        el_aligned = time.perf_counter() - t0
         st.run(64)
         st.sync()
         t0 = time.perf_counter()
@@ -55,6 +62,7 @@ def measure(args, meta, dyn, baths):
     finally:
         st.close()
     return {"ms_per_step": el / args.steps * 1e3, "short_ms_per_step": el_short / max(args.short, 1) * 1e3,
+            "aligned_short_ms_per_step": el_aligned / max(args.short, 1) * 1e3,
             "traj_steps_per_s": B * args.steps / el, "finite": bool(np.isfinite(p).all() and np.isfinite(q).all())}
 
 
