@@ -138,7 +138,8 @@ def main():
     ap.add_argument("--fill", type=int, default=-1,
                     help="untimed steps before the warm-up that bring the memory-sum ladder to its steady "
                          "state (history older than the largest level's window); -1 = 2 x the largest "
-                         "block length")
+                         "block length, rounded up so that the timed window starts on a piece-slot "
+                         "boundary")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
                          "rehearse the multi-rank path, e.g. with --same-device on a one-GPU box)")
@@ -201,6 +202,12 @@ def main():
     levels = st.profile_levels()
     ptop = max([P for P, _ in levels] + [1])
     fill = 2 * ptop if args.fill < 0 else args.fill
+    # start the timed window on a piece-slot boundary (t = 0 mod P0): the window then holds whole
+    # slots of background ladder work, as the steady state does, whatever --warmup is
+    p0 = max(1, plan["block_len"])
+    t_now = st.get_state()[2]
+    if args.fill < 0:
+        fill += (-(t_now + fill + args.warmup)) % p0
     t_fill = time.perf_counter()
     m.steps(fill)
     st.sync()
@@ -254,6 +261,7 @@ def main():
         "value_per_gpu": value / world,
         "setup_s": setup_s,
         "fill_steps": fill,
+        "window_t0": int(t_now + fill + args.warmup),
         # per ladder level: blocks issued in the timed window vs the steady-state share K / P
         "ladder_window": [{"P": P, "blocks": round(bl, 3), "steady": round(args.steps / P, 3)}
                           for P, bl in window_levels],

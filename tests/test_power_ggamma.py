@@ -134,9 +134,11 @@ def test_run_power_files_and_checkpoint_histories(tmp_path, monkeypatch):
     assert rel(ReadNetCDFVar("MD0.nc", "qhis"), sim.qhis) < 1e-10
     assert rel(ReadNetCDFVar("MD0.nc", "fhis1"), g["fhis1"]) < 1e-10
     assert rel(np.transpose(ReadNetCDFVar("MD0.nc", "poweratomlist"), (1, 0, 2)), g["poweratomlist"]) < 1e-10
-    pw = np.loadtxt("power.%s.run0.dat" % str(m.T))
+    # the file stops at 1.5 max(hw) (md.py:631-636): here after the first row; the whole spectrum is m.power
+    pw = np.loadtxt("power.%s.run0.dat" % str(m.T), ndmin=2)
     n = len(pw)
     assert 0 < n <= int(g["nmd"]) and np.allclose(pw, np.round(g["power"][:n], 6), atol=2e-6)
+    assert rel(m.power, g["power"]) < 1e-10
     for layer in range(len(g["atomlist"])):
         assert os.path.isfile("poweratomlist.%d.%s.run0.dat" % (layer, str(m.T)))
     m.close()
