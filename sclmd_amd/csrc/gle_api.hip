@@ -15,6 +15,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -229,8 +231,95 @@ int fail(gle_handle* h, int code, const std::string& msg) {
   return code;
 }
 
-int dalloc(gle_handle* h, void** p, size_t bytes) {
+// ---- -DGLE_BOUNDS audit: process-wide table of live allocations with their logical extents
+#ifdef GLE_BOUNDS
+namespace {
+std::mutex g_bmu;
+std::map<uint64_t, uint64_t> g_blive;  // start -> logical end
+bool g_bdirty = true;
+uint64_t* g_dlo = nullptr;
+uint64_t* g_dhi = nullptr;
+unsigned long long* g_dviol = nullptr;
+size_t g_bcap = 0;
+}  // namespace
+void bounds_add(void* p, size_t logical) {
+  std::lock_guard<std::mutex> lk(g_bmu);
+  g_blive[(uint64_t)p] = (uint64_t)p + logical;
+  g_bdirty = true;
+}
+void bounds_del(void* p) {
+  std::lock_guard<std::mutex> lk(g_bmu);
+  g_blive.erase((uint64_t)p);
+  g_bdirty = true;
+}
+// upload the table before kernels that check against it (audit build: synchronises the device)
+void bounds_sync() {
+  std::lock_guard<std::mutex> lk(g_bmu);
+  if (!g_bdirty) return;
+  hipDeviceSynchronize();
+  const size_t n = g_blive.size();
+  if (n > g_bcap) {
+    if (g_dlo) hipFree(g_dlo);
+    if (g_dhi) hipFree(g_dhi);
+    g_bcap = std::max<size_t>(2 * n, 1024);
+    hipMalloc((void**)&g_dlo, g_bcap * 8);
+    hipMalloc((void**)&g_dhi, g_bcap * 8);
+  }
+  if (!g_dviol) {
+    hipMalloc((void**)&g_dviol, (1 + 2 * BND_KEEP) * 8);
+    hipMemset(g_dviol, 0, (1 + 2 * BND_KEEP) * 8);
+  }
+  std::vector<uint64_t> lo, hi;
+  for (auto& kv : g_blive) {
+    lo.push_back(kv.first);
+    hi.push_back(kv.second);
+  }
+  hipMemcpy(g_dlo, lo.data(), n * 8, hipMemcpyHostToDevice);
+  hipMemcpy(g_dhi, hi.data(), n * 8, hipMemcpyHostToDevice);
+  BoundsTab t;
+  t.n = (int)n;
+  t.viol = g_dviol;
+  t.lo = g_dlo;
+  t.hi = g_dhi;
+  bounds_publish_chain(t);
+  bounds_publish_kernels(t);
+  hipDeviceSynchronize();
+  g_bdirty = false;
+}
+// reads out-of-allocation accesses recorded so far (after a device synchronisation)
+int bounds_report(gle_handle* h) {
+  std::lock_guard<std::mutex> lk(g_bmu);
+  if (!g_dviol) return GLE_OK;
+  unsigned long long v[1 + 2 * BND_KEEP];
+  hipMemcpy(v, g_dviol, sizeof(v), hipMemcpyDeviceToHost);
+  if (v[0] == 0) return GLE_OK;
+  std::string msg = "bounds audit: " + std::to_string(v[0]) + " accesses outside their allocation;";
+  for (unsigned long long k = 0; k < std::min<unsigned long long>(v[0], BND_KEEP); ++k) {
+    const uint64_t a = v[1 + 2 * k];
+    auto it = g_blive.upper_bound(a);
+    std::string where = "no allocation";
+    if (it != g_blive.begin()) {
+      --it;
+      where = "alloc+" + std::to_string((int64_t)(a - it->first)) + " (logical " +
+              std::to_string((int64_t)(it->second - it->first)) + " B)";
+    }
+    msg += " [line " + std::to_string(v[2 + 2 * k]) + ": " + where + "]";
+  }
+  fprintf(stderr, "%s\n", msg.c_str());
+  hipMemset(g_dviol, 0, (1 + 2 * BND_KEEP) * 8);
+  return fail(h, GLE_ERR_HIP, msg);
+}
+#else
+inline void bounds_add(void*, size_t) {}
+inline void bounds_del(void*) {}
+inline void bounds_sync() {}
+inline int bounds_report(gle_handle*) { return GLE_OK; }
+#endif
+
+// slack: bytes past the logical extent that the audit build treats as out of bounds
+int dalloc(gle_handle* h, void** p, size_t bytes, size_t slack = 0) {
   if (bytes == 0) bytes = 16;
+  bytes += slack;
   hipError_t e = hipMalloc(p, bytes);
   if (e != hipSuccess) {
     *p = nullptr;
@@ -240,12 +329,13 @@ int dalloc(gle_handle* h, void** p, size_t bytes) {
   if (e != hipSuccess) return fail(h, GLE_ERR_HIP, std::string("hipMemset: ") + hipGetErrorString(e));
   h->allocs.push_back(*p);
   h->dev_bytes += bytes;
+  bounds_add(*p, bytes - slack);
   return GLE_OK;
 }
 
 template <class T>
-int dalloc_n(gle_handle* h, T** p, size_t n) {
-  return dalloc(h, (void**)p, n * sizeof(T));
+int dalloc_n(gle_handle* h, T** p, size_t n, size_t slack_n = 0) {
+  return dalloc(h, (void**)p, n * sizeof(T), slack_n * sizeof(T));
 }
 
 inline int64_t rup(int64_t a, int64_t m) { return (a + m - 1) / m * m; }
@@ -981,7 +1071,7 @@ int plan_chain(gle_handle* h) {
   const int raw_ks = env ? std::max(4, atoi(env)) : 24;
   for (auto& b : h->baths) {
     b.NRS = std::max(2, b.nn + 1);
-    int rc0 = dalloc_n(h, &b.d_NR, (size_t)b.NRS * b.vs + 4096);
+    int rc0 = dalloc_n(h, &b.d_NR, (size_t)b.NRS * b.vs, 4096);
     if (rc0) return rc0;
     b.nqn = 0;
     if (b.nn > 2) {
@@ -992,7 +1082,7 @@ int plan_chain(gle_handle* h) {
       q = std::max(1, std::min<int>(q, (int)W));
       if (q > CH_NPMAX) return fail(h, GLE_ERR_UNSUP, "near field too long for the chain (block_len)");
       b.nqn = q;
-      int rc = dalloc_n(h, &b.d_NP, (size_t)2 * q * b.vs + 4096);
+      int rc = dalloc_n(h, &b.d_NP, (size_t)2 * q * b.vs, 4096);
       if (rc) return rc;
     }
   }
@@ -1355,7 +1445,7 @@ int freeze(gle_handle* h) {
   for (auto& b : h->baths) {
     b.R = b.ml + 3 * Ptop + 2;
     b.ldh = 2 * (int64_t)b.R * B + 512 + 16 * rn_for((int64_t)Ptop * B);
-    int rc = dalloc_n(h, &b.d_H, (size_t)b.ncp * b.ldh + 4096);
+    int rc = dalloc_n(h, &b.d_H, (size_t)b.ncp * b.ldh, 4096);
     if (rc) return rc;
   }
   if (h->far_mode == GLE_FAR_SPECTRAL) {
@@ -1398,7 +1488,7 @@ int freeze(gle_handle* h) {
       if (b.ml <= lv.lag0) continue;
       L.active = true;
       L.lag1 = std::min(lv.lag1, b.ml);
-      int rc = dalloc_n(h, &L.d_out, (size_t)b.ncp * 2 * lv.P * B + 4096);
+      int rc = dalloc_n(h, &L.d_out, (size_t)b.ncp * 2 * lv.P * B, 4096);
       if (rc) return rc;
       if (!lv.spectral) continue;
       L.M = (L.lag1 + lv.P - 1) / lv.P - 2;
@@ -1408,8 +1498,8 @@ int freeze(gle_handle* h) {
       L.seg_fstride = (int64_t)3 * b.ncp * L.ldseg;             // Re + Im, Im, Re rows
       L.yfstride = (int64_t)3 * b.nc * B;                       // T_0, T_1, T_2
       rc = dalloc_n(h, &L.d_khat, (size_t)(lv.P + 1) * L.khat_fstride);
-      if (!rc) rc = dalloc_n(h, &L.d_seg, (size_t)(lv.P + 1) * L.seg_fstride + 4096);
-      if (!rc) rc = dalloc_n(h, &L.d_Yspec, (size_t)lv.cg_split * (lv.P + 1) * L.yfstride + 4096);
+      if (!rc) rc = dalloc_n(h, &L.d_seg, (size_t)(lv.P + 1) * L.seg_fstride, 4096);
+      if (!rc) rc = dalloc_n(h, &L.d_Yspec, (size_t)lv.cg_split * (lv.P + 1) * L.yfstride, 4096);
       if (rc) return rc;
       launch_khat_pack(b.d_K, b.ml, b.nks, L.d_khat, lv.P, 2, L.M, b.nc, b.nrt, b.nks, h->d_cstab,
                        lv.cstride, h->stream);
@@ -1753,6 +1843,7 @@ int prime(gle_handle* h) {
 
 int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
   if (!h->state_set) return fail(h, GLE_ERR_STATE, "gle_set_state has not been called");
+  bounds_sync();
   for (size_t j = 0; j < h->baths.size(); ++j)
     if (!h->baths[j].noise_set) return fail(h, GLE_ERR_STATE, "bath " + std::to_string(j) + " has no noise");
   if (fpot_host_T == nullptr && !h->has_dyn)
@@ -1867,7 +1958,7 @@ void from_dev_layout(const std::vector<double>& src, double* dst, int64_t B, int
 int download(gle_handle* h, void* dst, const void* src, size_t bytes) {
   HIPCHK(h, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
-  return GLE_OK;
+  return bounds_report(h);
 }
 
 }  // namespace
@@ -1954,15 +2045,15 @@ int gle_create(const gle_config* cfg, gle_handle** out) {
     gle_destroy(h);
     return fail(nullptr, GLE_ERR_HIP, std::string("stream/event creation: ") + hipGetErrorString(e));
   }
-  const size_t nst = (size_t)(h->nphp + 64) * h->B + 1024;  // row slack for static windows
+  const size_t nst = (size_t)h->nphp * h->B, nsl = (size_t)64 * h->B + 1024;  // row slack for static windows
   int rc = 0;
-  rc |= dalloc_n(h, &h->d_P, nst);
-  rc |= dalloc_n(h, &h->d_Q, nst);
-  rc |= dalloc_n(h, &h->d_Ph, nst);
-  rc |= dalloc_n(h, &h->d_Qt, nst);
-  rc |= dalloc_n(h, &h->d_Fc, nst);
-  rc |= dalloc_n(h, &h->d_Flast, nst);
-  rc |= dalloc_n(h, &h->d_Q0, nst);
+  rc |= dalloc_n(h, &h->d_P, nst, nsl);
+  rc |= dalloc_n(h, &h->d_Q, nst, nsl);
+  rc |= dalloc_n(h, &h->d_Ph, nst, nsl);
+  rc |= dalloc_n(h, &h->d_Qt, nst, nsl);
+  rc |= dalloc_n(h, &h->d_Fc, nst, nsl);
+  rc |= dalloc_n(h, &h->d_Flast, nst, nsl);
+  rc |= dalloc_n(h, &h->d_Q0, nst, nsl);
   rc |= dalloc_n(h, &h->d_etot, (size_t)h->nmd * h->B);
   rc |= dalloc_n(h, &h->d_qvalid, (size_t)h->B);
   if (rc) {
@@ -2040,7 +2131,10 @@ int gle_destroy(gle_handle* h) {
   for (int i = 0; i < gle_handle::NBG; ++i)
     if (h->bg[i]) hipStreamSynchronize(h->bg[i]);
   if (h->stream) hipStreamSynchronize(h->stream);
-  for (void* p : h->allocs) hipFree(p);
+  for (void* p : h->allocs) {
+    bounds_del(p);
+    hipFree(p);
+  }
   for (auto e : h->ev) hipEventDestroy(e);
   for (auto& lv : h->levels)
     for (auto e : lv.ev)
@@ -2097,7 +2191,7 @@ int commit_bath(gle_handle* h, Bath&& b, int32_t* bath_id) {
   if (!rc) rc = upload(h, b.d_inv, b.inv.data(), b.inv.size() * 4);
   // zero tail of (ncp - nc) rows: the fused stage reads noise(t+1) as an MFMA operand of ncp rows
   // (K0 columns past nc are zero), which runs past the last time slot by ncp - nc rows
-  rc |= dalloc_n(h, &b.d_noise, ((size_t)h->nmd * nc + (b.ncp - nc)) * B + 64);
+  rc |= dalloc_n(h, &b.d_noise, (size_t)h->nmd * nc * B, (size_t)(b.ncp - nc) * B + 64);
   rc |= dalloc_n(h, &b.d_S, 2 * nbuf);
   rc |= dalloc_n(h, &b.d_Xcur, 2 * nbuf);
   rc |= dalloc_n(h, &b.d_Xq, 2 * nbuf);
@@ -2686,7 +2780,7 @@ int gle_sync(gle_handle* h) {
   if (rc) return rc;
   HIPCHK(h, hipStreamSynchronize(h->stream));
   HIPCHK(h, hipGetLastError());
-  return GLE_OK;
+  return bounds_report(h);
 }
 
 int gle_get_current(gle_handle* h, double* cur) {

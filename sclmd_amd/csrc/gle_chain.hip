@@ -31,10 +31,32 @@ typedef const __attribute__((address_space(1))) double gdouble;
 
 // global-address-space view of a pointer: loads and stores become global_* instructions (flat ones
 // also count on lgkmcnt and would make every scalar-load wait drain the vector loads in flight)
+#ifndef GLE_BOUNDS
 template <class T>
 __device__ __forceinline__ __attribute__((address_space(1))) T* G(T* p) {
   return (__attribute__((address_space(1))) T*)p;
 }
+#else
+// audit build: every G(p)[i] / *G(p) access is checked against the live allocations
+template <class T>
+struct BndPtr {
+  T* p;
+  int site;
+  __device__ T& operator[](int64_t i) const {
+    bcheck(p + i, (int)sizeof(T), site);
+    return p[i];
+  }
+  __device__ T& operator*() const {
+    bcheck(p, (int)sizeof(T), site);
+    return *p;
+  }
+};
+template <class T>
+__device__ __forceinline__ BndPtr<T> Gb(T* p, int site) {
+  return BndPtr<T>{p, site};
+}
+#define G(p) Gb((p), __LINE__)
+#endif
 
 __device__ __forceinline__ int64_t cmod(int64_t a, int64_t m) {
   int64_t r = a % m;
@@ -123,6 +145,11 @@ __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave,
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int s = min(s0 + u, nks - 1);
+#ifdef GLE_BOUNDS
+        bcheck(tk.A + lane + (int64_t)s * aks, 8, __LINE__);
+        for (int n = 0; n < RN; ++n)
+          bcheck(tk.X + col + (int64_t)brow * tk.ldx + bcol + (int64_t)s * xs + 16 * n, 8, __LINE__);
+#endif
         a[u] = A[(int64_t)s * aks];
 #pragma unroll
         for (int n = 0; n < RN; ++n) b[u][n] = X[(int64_t)s * xs + 16 * n];
@@ -542,7 +569,7 @@ __device__ __forceinline__ void dof_C(const ChTile* __restrict__ T, const StepDe
         // ladder's ring and the chain's near ring
         const int64_t kb = (int64_t)kk[x][u] * B + E[x].b;
         const int64_t slot = cmod(t + 1, bd.R);
-        __attribute__((address_space(1))) double* h = G(bd.H + (int64_t)kk[x][u] * bd.ldh + E[x].b);
+        auto h = G(bd.H + (int64_t)kk[x][u] * bd.ldh + E[x].b);
         h[slot * B] = p2;
         h[(slot + bd.R) * B] = p2;
         G(bd.NR)[cmod(t + 1, bd.NRS) * bd.vs + kb] = p2;
@@ -671,7 +698,7 @@ __device__ __forceinline__ void dof_BC(const ChTile* __restrict__ T, const StepD
         const ChBath& bd = T->tb[u];
         const int64_t kb = (int64_t)kk[x][u] * B + E[x].b;
         const int64_t slot = cmod(t + 1, bd.R);
-        __attribute__((address_space(1))) double* hh = G(bd.H + (int64_t)kk[x][u] * bd.ldh + E[x].b);
+        auto hh = G(bd.H + (int64_t)kk[x][u] * bd.ldh + E[x].b);
         hh[slot * B] = p2;
         hh[(slot + bd.R) * B] = p2;
         G(bd.NR)[cmod(t + 1, bd.NRS) * bd.vs + kb] = p2;
@@ -723,7 +750,7 @@ __device__ __forceinline__ void sfin(const ChTile* __restrict__ T, const StepDev
     // near-field partials and level blocks, all loads in flight together, added in slot / level
     // order
     double v[CH_NPMAX], lv[MAXLVL];
-    gdouble* np = G(sf.NP) + (sf.nqn > 0 ? (int64_t)par1 * sf.nqn * sf.vs + (ok[x] ? kb[x] : 0) : 0);
+    auto np = G(sf.NP + (sf.nqn > 0 ? (int64_t)par1 * sf.nqn * sf.vs + (ok[x] ? kb[x] : 0) : 0));
     // unconditional loads (slot min(q, nqn-1); nqn == 0 reads the zero row), masked in the sum
 #pragma unroll
     for (int q = 0; q < CH_NPMAX; ++q) v[q] = np[(int64_t)min(q, max(sf.nqn - 1, 0)) * sf.vs];
@@ -854,6 +881,14 @@ void launch_chain(int stage, int nw, int drn, size_t lds_bytes, const ChTile* ti
   else if (stage == 1) launch_st<1>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
   else if (stage == 2) launch_st<2>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
   else launch_st<3>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
+}
+
+void bounds_publish_chain(const BoundsTab& t) {
+#ifdef GLE_BOUNDS
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_btab), &t, sizeof(t));
+#else
+  (void)t;
+#endif
 }
 
 }  // namespace gle

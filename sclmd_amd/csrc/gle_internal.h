@@ -29,6 +29,45 @@ inline const char* gle_env(const char* name) {
 #endif
 }
 
+// -DGLE_BOUNDS audit build (`make experiments EXPNAME=bounds EXPFLAGS=-DGLE_BOUNDS`): the chain,
+// cgemm and contraction operand loads and the chain's stores check their address against the
+// live allocations, each with its LOGICAL extent (without the slack some allocations carry).  A
+// miss never faults: it is counted and the first BND_KEEP (address, site) pairs kept; gle_sync
+// and gle_run then fail with them.  Sites are source lines.
+struct BoundsTab {
+  int n = 0;
+  unsigned long long* viol = nullptr;  // [0] count, then (address, site) pairs
+  const uint64_t* lo = nullptr;        // sorted allocation starts
+  const uint64_t* hi = nullptr;        // logical ends
+};
+constexpr int BND_KEEP = 32;
+#ifdef GLE_BOUNDS
+static __device__ BoundsTab g_btab;  // one copy per translation unit, set by its bounds_publish_*
+__device__ inline void bcheck(const void* p, int bytes, int site) {
+  const BoundsTab& T = g_btab;
+  if (!T.viol) return;
+  const uint64_t a = (uint64_t)p;
+  int lo = 0, hi = T.n;  // last allocation starting at or below a
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (T.lo[mid] <= a) lo = mid;
+    else hi = mid;
+  }
+  if (T.n > 0 && a >= T.lo[lo] && a + (uint64_t)bytes <= T.hi[lo]) return;
+  const unsigned long long k = atomicAdd(&T.viol[0], 1ull);
+  if (k < BND_KEEP) {
+    T.viol[1 + 2 * k] = a;
+    T.viol[2 + 2 * k] = (unsigned long long)site;
+  }
+}
+#define GLE_BCHK(p) ::gle::bcheck((const void*)(p), (int)sizeof(*(p)), __LINE__)
+#else
+#define GLE_BCHK(p) ((void)0)
+#endif
+#define BLD(p) (GLE_BCHK(p), *(p))  // checked load (a plain load outside the audit build)
+void bounds_publish_chain(const BoundsTab& t);
+void bounds_publish_kernels(const BoundsTab& t);
+
 constexpr int WG = 256;            // threads per workgroup of the contraction kernel (4 waves)
 constexpr int KC = 2;              // k-steps (4 rows each) staged per LDS stage
 constexpr int KROWS = 4 * KC;      // 8 staged X rows

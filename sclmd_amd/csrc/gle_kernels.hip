@@ -89,11 +89,11 @@ __global__ __launch_bounds__(WG, 2) void contract_kernel(const CItem* __restrict
 #pragma unroll
       for (int u = 0; u < CU; ++u) {
         const int c = tid + WG * u;
-        xr[r * CU + u] = (c < ww) ? xs0[(int64_t)r * it.ldx + c] : 0.0;
+        xr[r * CU + u] = (c < ww) ? BLD(&xs0[(int64_t)r * it.ldx + c]) : 0.0;
       }
     if (active) {
-      na0 = As0[0];
-      na1 = As0[it.a_ks];
+      na0 = BLD(&As0[0]);
+      na1 = BLD(&As0[it.a_ks]);
     }
     for (int st = 0; st < nst; ++st) {
       __syncthreads();  // previous stage's LDS reads are done
@@ -114,25 +114,25 @@ __global__ __launch_bounds__(WG, 2) void contract_kernel(const CItem* __restrict
 #pragma unroll
           for (int u = 0; u < CU; ++u) {
             const int c = tid + WG * u;
-            xr[r * CU + u] = (c < ww) ? xs[(int64_t)r * it.ldx + c] : 0.0;
+            xr[r * CU + u] = (c < ww) ? BLD(&xs[(int64_t)r * it.ldx + c]) : 0.0;
           }
         if (active) {
-          na0 = Ak[KC * it.a_ks];
-          na1 = Ak[(KC + 1) * it.a_ks];
+          na0 = BLD(&Ak[KC * it.a_ks]);
+          na1 = BLD(&Ak[(KC + 1) * it.a_ks]);
         }
       }
       if (active) {
         // A fragments run two slices ahead of the MFMAs that consume them
         double m0 = 0.0, m1 = 0.0;
         if (ns > 1) {
-          m0 = Ak[64];
-          m1 = Ak[it.a_ks + 64];
+          m0 = BLD(&Ak[64]);
+          m1 = BLD(&Ak[it.a_ks + 64]);
         }
         for (int ss = 0; ss < ns; ++ss) {
           double n0 = 0.0, n1 = 0.0;
           if (ss + 2 < ns) {
-            n0 = Ak[(ss + 2) * 64];
-            n1 = Ak[it.a_ks + (ss + 2) * 64];
+            n0 = BLD(&Ak[(ss + 2) * 64]);
+            n1 = BLD(&Ak[it.a_ks + (ss + 2) * 64]);
           }
           const int off = (ns - 1 - ss) * it.cs;
           const double* b0 = lds + brow * wwp + off + bcol;
@@ -159,7 +159,10 @@ __global__ __launch_bounds__(WG, 2) void contract_kernel(const CItem* __restrict
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = wave * 16 + brow + 4 * r;
-        if (row < it.nrows && col < it.ncols) it.out[(int64_t)row * it.ldo + col] = acc[n][r];
+        if (row < it.nrows && col < it.ncols) {
+          GLE_BCHK(&it.out[(int64_t)row * it.ldo + col]);
+          it.out[(int64_t)row * it.ldo + col] = acc[n][r];
+        }
       }
     }
   }
@@ -216,7 +219,7 @@ __global__ __launch_bounds__(WG, 2) void contract_cplx_kernel(const CItem* __res
 #pragma unroll
         for (int u = 0; u < CU; ++u) {
           const int c = tid + WG * u;
-          xr[(h * KROWS + r) * CU + u] = (c < ww) ? xs0[h * it.x_im + (int64_t)r * it.ldx + c] : 0.0;
+          xr[(h * KROWS + r) * CU + u] = (c < ww) ? BLD(&xs0[h * it.x_im + (int64_t)r * it.ldx + c]) : 0.0;
         }
     for (int st = 0; st < nst; ++st) {
       __syncthreads();
@@ -240,7 +243,7 @@ __global__ __launch_bounds__(WG, 2) void contract_cplx_kernel(const CItem* __res
 #pragma unroll
             for (int u = 0; u < CU; ++u) {
               const int c = tid + WG * u;
-              xr[(h * KROWS + r) * CU + u] = (c < ww) ? xs[h * it.x_im + (int64_t)r * it.ldx + c] : 0.0;
+              xr[(h * KROWS + r) * CU + u] = (c < ww) ? BLD(&xs[h * it.x_im + (int64_t)r * it.ldx + c]) : 0.0;
             }
       }
       if (active) {
@@ -248,15 +251,15 @@ __global__ __launch_bounds__(WG, 2) void contract_cplx_kernel(const CItem* __res
         double ar[KC], ai[KC];
 #pragma unroll
         for (int kk = 0; kk < KC; ++kk) {
-          ar[kk] = Ak[kk * it.a_ks];
-          ai[kk] = Ak[it.a_im + kk * it.a_ks];
+          ar[kk] = BLD(&Ak[kk * it.a_ks]);
+          ai[kk] = BLD(&Ak[it.a_im + kk * it.a_ks]);
         }
         for (int ss = 0; ss < ns; ++ss) {
           double nr[KC], ni_[KC];
 #pragma unroll
           for (int kk = 0; kk < KC; ++kk) {
-            nr[kk] = (ss + 1 < ns) ? Ak[kk * it.a_ks + (ss + 1) * 64] : 0.0;
-            ni_[kk] = (ss + 1 < ns) ? Ak[it.a_im + kk * it.a_ks + (ss + 1) * 64] : 0.0;
+            nr[kk] = (ss + 1 < ns) ? BLD(&Ak[kk * it.a_ks + (ss + 1) * 64]) : 0.0;
+            ni_[kk] = (ss + 1 < ns) ? BLD(&Ak[it.a_im + kk * it.a_ks + (ss + 1) * 64]) : 0.0;
           }
           const int off = (ns - 1 - ss) * it.cs;
 #pragma unroll
@@ -290,12 +293,22 @@ __global__ __launch_bounds__(WG, 2) void contract_cplx_kernel(const CItem* __res
       for (int r = 0; r < 4; ++r) {
         const int row = wave * 16 + brow + 4 * r;
         if (row < it.nrows && col < it.ncols) {
+          GLE_BCHK(&it.out[(int64_t)row * it.ldo + col]);
+          GLE_BCHK(&it.out[it.o_im + (int64_t)row * it.ldo + col]);
           it.out[(int64_t)row * it.ldo + col] = accr[n][r];
           it.out[it.o_im + (int64_t)row * it.ldo + col] = acci[n][r];
         }
       }
     }
   }
+}
+
+void bounds_publish_kernels(const BoundsTab& t) {
+#ifdef GLE_BOUNDS
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_btab), &t, sizeof(t));
+#else
+  (void)t;
+#endif
 }
 
 void launch_contract_cplx(int rn, const CItem* items, int nitems, StepArgs ta, hipStream_t s) {
@@ -873,6 +886,15 @@ __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, doubl
   d4 acc[RN];
 #pragma unroll
   for (int n = 0; n < RN; ++n) acc[n] = d4{0.0, 0.0, 0.0, 0.0};
+#ifdef GLE_BOUNDS
+#define CG_BCHK_X(u)                                                                                  \
+  GLE_BCHK(it.X + (int64_t)(4 * ks_ + (xr & 3)) * it.ldx + (int64_t)slot_ * it.cs + it.col0 + xc + (u))
+#define CG_BCHK_A(s)                                                                                  \
+  GLE_BCHK(it.A + (int64_t)(active ? wave : 0) * it.a_rt + (int64_t)it.s0 * 64 + lane + (int64_t)(s) * 64)
+#else
+#define CG_BCHK_X(u) ((void)0)
+#define CG_BCHK_A(s) ((void)0)
+#endif
 #define CG_LOAD_X(c, XV)                                                                              \
   do {                                                                                                \
     const int s0_ = (c) * KC + (xr >> 2);                                                          \
@@ -882,7 +904,10 @@ __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, doubl
     slot_ += slot_ < 0 ? it.Rseg : 0; /* i < M < Rseg */                                              \
     gdbl* xp_ = (gdbl*)(it.X + (int64_t)(4 * ks_ + (xr & 3)) * it.ldx + (int64_t)slot_ * it.cs +      \
                         it.col0 + xc);                                                                \
-    _Pragma("unroll") for (int u = 0; u < XPT; ++u) XV[u] = xp_[u];                                   \
+    _Pragma("unroll") for (int u = 0; u < XPT; ++u) {                                               \
+      CG_BCHK_X(u);                                                                                   \
+      XV[u] = xp_[u];                                                                                 \
+    }                                                                                                 \
   } while (0)
   /* rows past S are stored as zeros (the multiply waits for the load only here, at the store) */
 #define CG_STORE_X(c, buf, XV)                                                                        \
@@ -894,6 +919,7 @@ __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, doubl
   do {                                                                                                \
     _Pragma("unroll") for (int u = 0; u < KC; ++u) {                                               \
       const int s0_ = (c) * KC + u;                                                                \
+      CG_BCHK_A(s0_ < S ? s0_ : S - 1);                                                               \
       AV[u] = (DBG & 1) ? 1e-3 * (s0_ + 1) : CG_ALOAD(&Aw[(int64_t)(s0_ < S ? s0_ : S - 1) * 64]); /* masked */ \
     }                                                                                                 \
   } while (0)
@@ -936,6 +962,8 @@ __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, doubl
 #undef CG_LOAD_A
 #undef CG_STORE_X
 #undef CG_LOAD_X
+#undef CG_BCHK_X
+#undef CG_BCHK_A
   if (active) {
     // f64 MFMA C/D map: col = lane & 15, row = (lane >> 4) + 4 * reg
 #pragma unroll
@@ -943,7 +971,10 @@ __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, doubl
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int row = 16 * wave + brow + 4 * q, col = 16 * n + bcol;
-        if (row < it.nrows && col < it.ncols) it.out[(int64_t)row * it.ldo + col] = acc[n][q];
+        if (row < it.nrows && col < it.ncols) {
+          GLE_BCHK(&it.out[(int64_t)row * it.ldo + col]);
+          it.out[(int64_t)row * it.ldo + col] = acc[n][q];
+        }
       }
   }
 }
