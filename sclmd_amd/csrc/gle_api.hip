@@ -316,6 +316,18 @@ inline void bounds_sync() {}
 inline int bounds_report(gle_handle*) { return GLE_OK; }
 #endif
 
+// scratch / stream buffers outside the handle's allocation list (registered with the audit too)
+template <class T>
+hipError_t tmalloc(T** p, size_t bytes) {
+  const hipError_t e = hipMalloc((void**)p, bytes);
+  if (e == hipSuccess) bounds_add((void*)*p, bytes);
+  return e;
+}
+inline hipError_t tfree(void* p) {
+  bounds_del(p);
+  return hipFree(p);
+}
+
 // slack: bytes past the logical extent that the audit build treats as out of bounds
 int dalloc(gle_handle* h, void** p, size_t bytes, size_t slack = 0) {
   if (bytes == 0) bytes = 16;
@@ -2216,7 +2228,7 @@ std::vector<double> transpose_w(const double* W, int64_t ml, int64_t ngw, int64_
 struct DevTmp {  // scratch device buffer freed on scope exit (setup paths)
   void* p = nullptr;
   ~DevTmp() {
-    if (p) hipFree(p);
+    if (p) tfree(p);
   }
 };
 
@@ -2279,9 +2291,9 @@ int gle_add_bath_gmem(gle_handle* h, const int64_t* cids, int64_t nc, int64_t ml
   int64_t mlp = 0;
   std::vector<double> wt = transpose_w(W, ml, ngw, &mlp);
   DevTmp d_wt, d_gam, d_gf;
-  HIPCHK(h, hipMalloc(&d_wt.p, wt.size() * 8));
-  HIPCHK(h, hipMalloc(&d_gam.p, (size_t)ngw * nc * nc * 8));
-  HIPCHK(h, hipMalloc(&d_gf.p, (size_t)nfrag * ngwp * 64 * 8));
+  HIPCHK(h, tmalloc(&d_wt.p, wt.size() * 8));
+  HIPCHK(h, tmalloc(&d_gam.p, (size_t)ngw * nc * nc * 8));
+  HIPCHK(h, tmalloc(&d_gf.p, (size_t)nfrag * ngwp * 64 * 8));
   HIPCHK(h, hipMemcpyAsync(d_wt.p, wt.data(), wt.size() * 8, hipMemcpyHostToDevice, h->stream));
   HIPCHK(h, hipMemcpyAsync(d_gam.p, gamma, (size_t)ngw * nc * nc * 8, hipMemcpyHostToDevice, h->stream));
   launch_gamma_pack((const double*)d_gam.p, (int)ngw, (int)ngwp, b.nc, b.nrt, b.nks, (double*)d_gf.p, h->stream);
@@ -2339,8 +2351,8 @@ int gle_gamt(int32_t device, int64_t ml, int64_t ngw, int64_t nel, const double*
   const int64_t nblk = (nel + 63) / 64;
   DevTmp d_wt, d_g, d_o;
   auto ok = [](hipError_t e) { return e == hipSuccess; };
-  if (!ok(hipMalloc(&d_wt.p, wt.size() * 8)) || !ok(hipMalloc(&d_g.p, (size_t)ngw * nel * 8)) ||
-      !ok(hipMalloc(&d_o.p, (size_t)ml * nel * 8)))
+  if (!ok(tmalloc(&d_wt.p, wt.size() * 8)) || !ok(tmalloc(&d_g.p, (size_t)ngw * nel * 8)) ||
+      !ok(tmalloc(&d_o.p, (size_t)ml * nel * 8)))
     return fail(nullptr, GLE_ERR_NOMEM, "gamt: device allocation failed");
   if (!ok(hipMemcpy(d_wt.p, wt.data(), wt.size() * 8, hipMemcpyHostToDevice)) ||
       !ok(hipMemcpy(d_g.p, G, (size_t)ngw * nel * 8, hipMemcpyHostToDevice)))
@@ -2406,12 +2418,12 @@ int gle_set_state(gle_handle* h, const double* p, const double* q, int64_t t) {
         colq[(size_t)k * B + j] = q[(size_t)j * n + b.cids[k]];
       }
     double* d_tmp = nullptr;
-    HIPCHK(h, hipMalloc((void**)&d_tmp, col.size() * 8));
+    HIPCHK(h, tmalloc((void**)&d_tmp, col.size() * 8));
     hipMemcpyAsync(d_tmp, col.data(), col.size() * 8, hipMemcpyHostToDevice, h->stream);
     launch_ring_copy(b.d_H, b.ldh, b.R, (int)B, b.nc, t, 1, d_tmp, 0, h->stream);
     hipMemcpyAsync(b.d_Xq, colq.data(), colq.size() * 8, hipMemcpyHostToDevice, h->stream);
     hipError_t e = hipStreamSynchronize(h->stream);
-    hipFree(d_tmp);
+    tfree(d_tmp);
     if (e != hipSuccess) return fail(h, GLE_ERR_HIP, std::string("set_state: ") + hipGetErrorString(e));
   }
   h->state_set = true;
@@ -2456,11 +2468,11 @@ int gle_set_history(gle_handle* h, int32_t bath, const double* phis) {
       for (int64_t i = 0; i < b.ml; ++i)
         for (int64_t k = 0; k < b.nc; ++k)
           buf[((size_t)i * b.nc + k) * B + j] = phis[((size_t)j * b.ml + i) * b.nc + k];
-    HIPCHK(h, hipMalloc((void**)&d_tmp, buf.size() * 8));
+    HIPCHK(h, tmalloc((void**)&d_tmp, buf.size() * 8));
     hipMemcpyAsync(d_tmp, buf.data(), buf.size() * 8, hipMemcpyHostToDevice, h->stream);
     launch_ring_copy(b.d_H, b.ldh, b.R, (int)B, b.nc, h->t - 1, b.ml, d_tmp, 0, h->stream);
     hipError_t e = hipStreamSynchronize(h->stream);
-    hipFree(d_tmp);
+    tfree(d_tmp);
     if (e != hipSuccess) return fail(h, GLE_ERR_HIP, std::string("set_history: ") + hipGetErrorString(e));
   } else {
     launch_ring_copy(b.d_H, b.ldh, b.R, (int)B, b.nc, h->t - 1, b.ml, nullptr, 0, h->stream);
@@ -2480,11 +2492,11 @@ int gle_get_history(gle_handle* h, int32_t bath, double* phis) {
   const int64_t B = h->B;
   std::vector<double> buf((size_t)b.ml * b.nc * B);
   double* d_tmp = nullptr;
-  HIPCHK(h, hipMalloc((void**)&d_tmp, buf.size() * 8));
+  HIPCHK(h, tmalloc((void**)&d_tmp, buf.size() * 8));
   launch_ring_copy(b.d_H, b.ldh, b.R, (int)B, b.nc, h->t - 1, b.ml, d_tmp, 1, h->stream);
   hipMemcpyAsync(buf.data(), d_tmp, buf.size() * 8, hipMemcpyDeviceToHost, h->stream);
   hipError_t e = hipStreamSynchronize(h->stream);
-  hipFree(d_tmp);
+  tfree(d_tmp);
   if (e != hipSuccess) return fail(h, GLE_ERR_HIP, std::string("get_history: ") + hipGetErrorString(e));
   for (int64_t j = 0; j < B; ++j)
     for (int64_t i = 0; i < b.ml; ++i)
@@ -2548,7 +2560,7 @@ int gle_noise_factors(gle_handle* h, int32_t bath, int64_t nfreq, const double* 
   b.nfreq = nfreq;
   std::vector<double> f = pack_frags(m_re, nfreq, b.nc, b.nc, b.fac_nrt, b.nks, m_im);
   if (b.d_fac) {
-    hipFree(b.d_fac);
+    tfree(b.d_fac);
     auto it = std::find(h->allocs.begin(), h->allocs.end(), (void*)b.d_fac);
     if (it != h->allocs.end()) h->allocs.erase(it);
     b.d_fac = nullptr;
@@ -2570,15 +2582,15 @@ int gle_noise_generate(gle_handle* h, int32_t bath, const double* x_host, uint64
   double* d_a = nullptr;
   const size_t nx = (size_t)nf * ncp * B + (size_t)(64 + 16) * B + 4096;
   const size_t na = (size_t)nf * b.fac_rows * B + 4096;
-  HIPCHK(h, hipMalloc((void**)&d_x, nx * 8));
-  if (hipMalloc((void**)&d_a, na * 8) != hipSuccess) {
-    hipFree(d_x);
+  HIPCHK(h, tmalloc((void**)&d_x, nx * 8));
+  if (tmalloc((void**)&d_a, na * 8) != hipSuccess) {
+    tfree(d_x);
     return fail(h, GLE_ERR_NOMEM, "noise work buffers");
   }
   auto cleanup = [&]() {
     hipStreamSynchronize(h->stream);
-    hipFree(d_x);
-    hipFree(d_a);
+    tfree(d_x);
+    tfree(d_a);
   };
   if (hipMemsetAsync(d_x, 0, nx * 8, h->stream) != hipSuccess) {
     cleanup();
@@ -2624,7 +2636,7 @@ int gle_noise_generate(gle_handle* h, int32_t bath, const double* x_host, uint64
     std::vector<bool> part(op.items.size(), false);
     // direct-write items only: allocate descriptors temporarily
     CItem* d_items = nullptr;
-    hipError_t e = hipMalloc((void**)&d_items, op.items.size() * sizeof(CItem));
+    hipError_t e = tmalloc((void**)&d_items, op.items.size() * sizeof(CItem));
     if (e != hipSuccess) {
       cleanup();
       return fail(h, GLE_ERR_NOMEM, "noise items");
@@ -2637,7 +2649,7 @@ int gle_noise_generate(gle_handle* h, int32_t bath, const double* x_host, uint64
     const double scale = 1.0 / (h->dt * (double)h->nmd);  // dw/2pi (functions.py:51)
     int frc = launch_fft_noise(d_a, b.d_noise, h->d_tw, h->nmd, nc, b.fac_rows, B, b.fac_complex ? 1 : 0, scale, h->stream);
     e = hipStreamSynchronize(h->stream);
-    hipFree(d_items);
+    tfree(d_items);
     if (frc) {
       cleanup();
       return fail(h, GLE_ERR_UNSUP, "device noise FFT needs nmd a power of two <= 8192 (got " + std::to_string(h->nmd) + ")");
@@ -2655,7 +2667,7 @@ int gle_noise_generate(gle_handle* h, int32_t bath, const double* x_host, uint64
 namespace {
 void free_stream(Bath& b) {
   for (double** p : {&b.d_sa, &b.d_sx, &b.d_sm}) {
-    if (*p) hipFree(*p);
+    if (*p) tfree(*p);
     *p = nullptr;
   }
   b.s_cap = 0;
@@ -2675,8 +2687,8 @@ int gle_noise_stream_begin(gle_handle* h, int32_t bath, int32_t is_complex, int6
   b.s_cap = std::min(max_chunk, nf);
   const size_t na = (size_t)nf * rows * B, nx = (size_t)b.s_cap * b.ncp * B,
                nm = (size_t)b.s_cap * b.nc * b.nc * (is_complex ? 2 : 1);
-  if (hipMalloc((void**)&b.d_sa, na * 8) != hipSuccess || hipMalloc((void**)&b.d_sx, nx * 8) != hipSuccess ||
-      hipMalloc((void**)&b.d_sm, nm * 8) != hipSuccess) {
+  if (tmalloc((void**)&b.d_sa, na * 8) != hipSuccess || tmalloc((void**)&b.d_sx, nx * 8) != hipSuccess ||
+      tmalloc((void**)&b.d_sm, nm * 8) != hipSuccess) {
     free_stream(b);
     return fail(h, GLE_ERR_NOMEM, "noise stream buffers (" + std::to_string((na + nx + nm) >> 17) + " MiB)");
   }
@@ -3068,10 +3080,10 @@ int gle_power_spectrum(gle_handle* h, int32_t ngroup, const int64_t* group_len, 
   for (int64_t i = 0; i < off[ngroup]; ++i)
     if (dofs[i] < 0 || dofs[i] >= h->nph) return fail(h, GLE_ERR_ARG, "power spectrum DOF out of range");
   DevTmp d_off, d_dofs, d_out;
-  HIPCHK(h, hipMalloc(&d_off.p, off.size() * 8));
-  HIPCHK(h, hipMalloc(&d_dofs.p, std::max<int64_t>(1, off[ngroup]) * 8));
+  HIPCHK(h, tmalloc(&d_off.p, off.size() * 8));
+  HIPCHK(h, tmalloc(&d_dofs.p, std::max<int64_t>(1, off[ngroup]) * 8));
   const size_t no = (size_t)ngroup * h->B * h->nmd;
-  HIPCHK(h, hipMalloc(&d_out.p, no * 8));
+  HIPCHK(h, tmalloc(&d_out.p, no * 8));
   HIPCHK(h, hipMemcpyAsync(d_off.p, off.data(), off.size() * 8, hipMemcpyHostToDevice, h->stream));
   if (off[ngroup] > 0)
     HIPCHK(h, hipMemcpyAsync(d_dofs.p, dofs, off[ngroup] * 8, hipMemcpyHostToDevice, h->stream));
@@ -3136,13 +3148,13 @@ int gle_reduce_current(gle_handle* h, void* comm, double* out) {
   if (rc || !comm) return rc;
   hipSetDevice(h->cfg.device);
   double* d = nullptr;
-  HIPCHK(h, hipMalloc((void**)&d, n * 8));
+  HIPCHK(h, tmalloc((void**)&d, n * 8));
   hipError_t e = hipMemcpyAsync(d, out, n * 8, hipMemcpyHostToDevice, h->stream);
   ncclResult_t r = ncclSuccess;
   if (e == hipSuccess) r = ncclAllReduce(d, d, n, ncclDouble, ncclSum, (ncclComm_t)comm, h->stream);
   if (e == hipSuccess && r == ncclSuccess) e = hipMemcpyAsync(out, d, n * 8, hipMemcpyDeviceToHost, h->stream);
   const hipError_t es = hipStreamSynchronize(h->stream);
-  hipFree(d);
+  tfree(d);
   if (r != ncclSuccess) return fail(h, GLE_ERR_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
   if (e != hipSuccess || es != hipSuccess)
     return fail(h, GLE_ERR_HIP, std::string("reduce copies: ") + hipGetErrorString(e != hipSuccess ? e : es));

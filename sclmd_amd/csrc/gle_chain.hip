@@ -112,6 +112,11 @@ __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave,
   d4 acc[RN];
 #pragma unroll
   for (int n = 0; n < RN; ++n) acc[n] = d4{0.0, 0.0, 0.0, 0.0};
+  // X columns past the tile's valid ones (trajectories >= B) read the last valid column: their
+  // products land in output columns nobody stores, and no read leaves the operand's rows
+  int xc[RN];
+#pragma unroll
+  for (int n = 0; n < RN; ++n) xc[n] = min(bcol + 16 * n, max(T->ncols - 1, 0));
   int cur = -1;
   auto flush = [&]() {
 #pragma unroll
@@ -134,7 +139,7 @@ __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave,
     int64_t col = T->c0;
     if (tk.ring) col += cmod(t + tk.tshift, tk.ring) * (int64_t)tk.sst;
     gdouble* A = (gdouble*)(tk.A + lane);
-    gdouble* X = (gdouble*)(tk.X + col + (int64_t)brow * tk.ldx + bcol);
+    gdouble* X = (gdouble*)(tk.X + col + (int64_t)brow * tk.ldx);
     const int64_t xs = 4 * (int64_t)tk.ldx;
     const int nks = tk.nks, aks = tk.a_ks;
     // Loads are branch-free (index clamped to the task's last k-step) and MFMAs past the end
@@ -147,12 +152,11 @@ __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave,
         const int s = min(s0 + u, nks - 1);
 #ifdef GLE_BOUNDS
         bcheck(tk.A + lane + (int64_t)s * aks, 8, __LINE__);
-        for (int n = 0; n < RN; ++n)
-          bcheck(tk.X + col + (int64_t)brow * tk.ldx + bcol + (int64_t)s * xs + 16 * n, 8, __LINE__);
+        for (int n = 0; n < RN; ++n) bcheck(tk.X + col + (int64_t)brow * tk.ldx + (int64_t)s * xs + xc[n], 8, __LINE__);
 #endif
         a[u] = A[(int64_t)s * aks];
 #pragma unroll
-        for (int n = 0; n < RN; ++n) b[u][n] = X[(int64_t)s * xs + 16 * n];
+        for (int n = 0; n < RN; ++n) b[u][n] = X[(int64_t)s * xs + xc[n]];
       }
     };
     auto compute = [&](int s0, double (&a)[U], double (&b)[U][RN]) {

@@ -41,6 +41,8 @@ def measure(args, meta, dyn, baths):
         ptop = max([P for P, _ in st.profile_levels()] + [1])
         st.run(2 * ptop + 5)
         st.sync()
+        if args.profile:
+            st.profile(True)
         t0 = time.perf_counter()
         st.run(args.short)
         st.sync()
@@ -75,6 +77,7 @@ def main():
     ap.add_argument("--variants", default="", help="';'-separated variants of ','-separated GLE_X=V")
     ap.add_argument("--rounds", type=int, default=1)
     ap.add_argument("--tag", default="")
+    ap.add_argument("--profile", type=int, default=0, help="HIP-event timing of the far-field launches on")
     args = ap.parse_args()
     from sclmd_amd import synthetic
 
@@ -90,7 +93,7 @@ def main():
                 k, val = kv.split("=", 1)
                 env[k] = val
             os.environ.update(env)
-            out = {"tag": args.tag, "variant": v, "round": r,
+            out = {"tag": args.tag, "profile": args.profile, "variant": v, "round": r,
                    "lib": os.path.basename(os.environ.get("SCLMD_AMD_LIB", "libhipgle.so")), "env": env,
                    "config": args.config, "ntraj": args.ntraj, "steps": args.steps}
             out.update(measure(args, meta, dyn, baths))
