@@ -170,6 +170,7 @@ struct gle_handle {
   double* d_zero = nullptr;            // zero row (chain S(t+1) tiles' unused level slots)
   bool dbg_no_ladder = false;  // GLE_DBG_NO_LADDER: skip the ladder blocks (timing experiments only)
   int bg_grid = 0;             // GLE_BG_GRID: cap of the far-field GEMM grid (grid-stride over items)
+  bool bg_serial = false;      // GLE_BG_SERIAL=1: ladder pieces on the main stream (time-sliced, experiment)
   int piece_slack = 1;         // GLE_PIECE_SLACK: boundaries left between a block's last piece and its use
   bool merge_waits = true;     // GLE_MERGE_WAITS=0: one main-stream wait per level
   int64_t ev_seq_counter = 0;
@@ -1875,7 +1876,7 @@ int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
   int64_t wait_seq[gle_handle::NBG] = {};
   if (!h->dbg_no_ladder && t % h->P0 == 0) {
     for (auto& lv : h->levels) {
-      hipStream_t bs = h->bg[lv.sidx];
+      hipStream_t bs = h->bg_serial ? h->stream : h->bg[lv.sidx];
       const int64_t k = floordiv(t, lv.P);
       if (t % lv.P == 0 && k + 1 > lv.last_block) {
         if (lv.pend_block != INT64_MIN) {  // (cannot happen: the last piece is due at T + P - P0)
@@ -2024,6 +2025,7 @@ int gle_create(const gle_config* cfg, gle_handle** out) {
   if (const char* e = gle_env("GLE_DBG_SKIP")) h->dbg_skip = atoi(e);
   if (const char* e = gle_env("GLE_BG_GRID")) h->bg_grid = std::max(0, atoi(e));
   if (const char* e = gle_env("GLE_PIECE_SLACK")) h->piece_slack = std::max(0, atoi(e));
+  if (const char* e = gle_env("GLE_BG_SERIAL")) h->bg_serial = atoi(e) != 0;
   if (const char* e = gle_env("GLE_MERGE_WAITS")) h->merge_waits = atoi(e) != 0;
   // main stream (the latency-bound per-step chain) at the highest priority, background streams
   // (ladder blocks) at the lowest
