@@ -236,16 +236,16 @@ int fail(gle_handle* h, int code, const std::string& msg) {
 #ifdef GLE_BOUNDS
 namespace {
 std::mutex g_bmu;
-std::map<uint64_t, uint64_t> g_blive;  // start -> logical end
+std::map<uint64_t, std::pair<uint64_t, int>> g_blive;  // start -> (logical end, allocating line)
 bool g_bdirty = true;
 uint64_t* g_dlo = nullptr;
 uint64_t* g_dhi = nullptr;
 unsigned long long* g_dviol = nullptr;
 size_t g_bcap = 0;
 }  // namespace
-void bounds_add(void* p, size_t logical) {
+void bounds_add(void* p, size_t logical, int line) {
   std::lock_guard<std::mutex> lk(g_bmu);
-  g_blive[(uint64_t)p] = (uint64_t)p + logical;
+  g_blive[(uint64_t)p] = {(uint64_t)p + logical, line};
   g_bdirty = true;
 }
 void bounds_del(void* p) {
@@ -273,7 +273,7 @@ void bounds_sync() {
   std::vector<uint64_t> lo, hi;
   for (auto& kv : g_blive) {
     lo.push_back(kv.first);
-    hi.push_back(kv.second);
+    hi.push_back(kv.second.first);
   }
   hipMemcpy(g_dlo, lo.data(), n * 8, hipMemcpyHostToDevice);
   hipMemcpy(g_dhi, hi.data(), n * 8, hipMemcpyHostToDevice);
@@ -301,8 +301,8 @@ int bounds_report(gle_handle* h) {
     std::string where = "no allocation";
     if (it != g_blive.begin()) {
       --it;
-      where = "alloc+" + std::to_string((int64_t)(a - it->first)) + " (logical " +
-              std::to_string((int64_t)(it->second - it->first)) + " B)";
+      where = "alloc@" + std::to_string(it->second.second) + "+" + std::to_string((int64_t)(a - it->first)) +
+              " (logical " + std::to_string((int64_t)(it->second.first - it->first)) + " B)";
     }
     msg += " [line " + std::to_string(v[2 + 2 * k]) + ": " + where + "]";
   }
@@ -311,7 +311,7 @@ int bounds_report(gle_handle* h) {
   return fail(h, GLE_ERR_HIP, msg);
 }
 #else
-inline void bounds_add(void*, size_t) {}
+inline void bounds_add(void*, size_t, int) {}
 inline void bounds_del(void*) {}
 inline void bounds_sync() {}
 inline int bounds_report(gle_handle*) { return GLE_OK; }
@@ -319,9 +319,9 @@ inline int bounds_report(gle_handle*) { return GLE_OK; }
 
 // scratch / stream buffers outside the handle's allocation list (registered with the audit too)
 template <class T>
-hipError_t tmalloc(T** p, size_t bytes) {
+hipError_t tmalloc(T** p, size_t bytes, int line = __builtin_LINE()) {
   const hipError_t e = hipMalloc((void**)p, bytes);
-  if (e == hipSuccess) bounds_add((void*)*p, bytes);
+  if (e == hipSuccess) bounds_add((void*)*p, bytes, line);
   return e;
 }
 inline hipError_t tfree(void* p) {
@@ -330,7 +330,7 @@ inline hipError_t tfree(void* p) {
 }
 
 // slack: bytes past the logical extent that the audit build treats as out of bounds
-int dalloc(gle_handle* h, void** p, size_t bytes, size_t slack = 0) {
+int dalloc(gle_handle* h, void** p, size_t bytes, size_t slack = 0, int line = __builtin_LINE()) {
   if (bytes == 0) bytes = 16;
   bytes += slack;
   hipError_t e = hipMalloc(p, bytes);
@@ -342,13 +342,13 @@ int dalloc(gle_handle* h, void** p, size_t bytes, size_t slack = 0) {
   if (e != hipSuccess) return fail(h, GLE_ERR_HIP, std::string("hipMemset: ") + hipGetErrorString(e));
   h->allocs.push_back(*p);
   h->dev_bytes += bytes;
-  bounds_add(*p, bytes - slack);
+  bounds_add(*p, bytes - slack, line);
   return GLE_OK;
 }
 
 template <class T>
-int dalloc_n(gle_handle* h, T** p, size_t n, size_t slack_n = 0) {
-  return dalloc(h, (void**)p, n * sizeof(T), slack_n * sizeof(T));
+int dalloc_n(gle_handle* h, T** p, size_t n, size_t slack_n = 0, int line = __builtin_LINE()) {
+  return dalloc(h, (void**)p, n * sizeof(T), slack_n * sizeof(T), line);
 }
 
 inline int64_t rup(int64_t a, int64_t m) { return (a + m - 1) / m * m; }
