@@ -711,6 +711,7 @@ struct Seg {
   int ldx, ring, tshift, nks;
   int sst;       // ring: doubles between slots
   int cond = 0;  // 0 / CH_HIT / CH_MISS (ChTask::cond)
+  int xrows = 0; // rows of X that exist from its row 0 (0: all 4 nks)
 };
 
 // Split the k-steps [g_begin, g_end) of the concatenated segments evenly over the CH_NW waves of
@@ -764,6 +765,7 @@ int fill_tasks(gle_handle* h, ChTile& T, const std::vector<Seg>& segs, int nout,
         tk.nks = (int32_t)(s1 - s0);
         tk.slot = cur_slot;
         tk.cond = sg.cond;
+        tk.xrows = (int32_t)((sg.xrows > 0 ? sg.xrows : 4 * sg.nks) - 4 * kl);
         *flops += 2048.0 * T.rn * (double)(s1 - s0);
       }
       pos += sg.nks;
@@ -1188,9 +1190,11 @@ int plan_chain(gle_handle* h) {
         segs.push_back(Seg{CH_OYB + u, b.d_K0sqd + b.tofs[rt], 64, b.d_Xcur, (int)B, 0, 0, b.nks, 0});
         if (b.ml >= 2)  // V = n1 - c S1 from the S(t+1) tiles
           segs.push_back(Seg{CH_OYB + u, b.d_hK0d + b.tofs[rt], 64, b.d_V, (int)B, 0, 0, b.nks, 0});
-        else            // no memory sum: V = noise(t+1), read from the noise ring
-          segs.push_back(Seg{CH_OYB + u, b.d_hK0d + b.tofs[rt], 64, b.d_noise, (int)B, (int)h->nmd, 1, b.nks,
-                             (int)(b.nc * B)});
+        else {          // no memory sum: V = noise(t+1), read from the noise ring (nc rows per slot)
+          Seg sg{CH_OYB + u, b.d_hK0d + b.tofs[rt], 64, b.d_noise, (int)B, (int)h->nmd, 1, b.nks, (int)(b.nc * B)};
+          sg.xrows = b.nc;
+          segs.push_back(sg);
+        }
         if (b.has_q)
           segs.push_back(Seg{CH_OYB + u, b.d_KKqd + b.tofs[rt], 64, b.d_Xq + b.vs, (int)B, 0, 0, b.nks, 0});
       }

@@ -139,8 +139,9 @@ __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave,
     int64_t col = T->c0;
     if (tk.ring) col += cmod(t + tk.tshift, tk.ring) * (int64_t)tk.sst;
     gdouble* A = (gdouble*)(tk.A + lane);
-    gdouble* X = (gdouble*)(tk.X + col + (int64_t)brow * tk.ldx);
-    const int64_t xs = 4 * (int64_t)tk.ldx;
+    gdouble* X = (gdouble*)(tk.X + col);
+    const int64_t ldx = tk.ldx;
+    const int xr = max(tk.xrows - 1, 0);
     const int nks = tk.nks, aks = tk.a_ks;
     // Loads are branch-free (index clamped to the task's last k-step) and MFMAs past the end
     // multiply a zero A operand: a load under a branch makes the waitcnt pass drain every load in
@@ -150,13 +151,14 @@ __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave,
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int s = min(s0 + u, nks - 1);
+        const int64_t xo = (int64_t)min(4 * s + brow, xr) * ldx;
 #ifdef GLE_BOUNDS
         bcheck(tk.A + lane + (int64_t)s * aks, 8, __LINE__);
-        for (int n = 0; n < RN; ++n) bcheck(tk.X + col + (int64_t)brow * tk.ldx + (int64_t)s * xs + xc[n], 8, __LINE__);
+        for (int n = 0; n < RN; ++n) bcheck(tk.X + col + xo + xc[n], 8, __LINE__);
 #endif
         a[u] = A[(int64_t)s * aks];
 #pragma unroll
-        for (int n = 0; n < RN; ++n) b[u][n] = X[(int64_t)s * xs + xc[n]];
+        for (int n = 0; n < RN; ++n) b[u][n] = X[xo + xc[n]];
       }
     };
     auto compute = [&](int s0, double (&a)[U], double (&b)[U][RN]) {
