@@ -254,7 +254,7 @@ void bounds_del(void* p) {
   g_bdirty = true;
 }
 // upload the table before kernels that check against it (audit build: synchronises the device)
-void bounds_sync() {
+void bounds_table_sync() {
   std::lock_guard<std::mutex> lk(g_bmu);
   if (!g_bdirty) return;
   hipDeviceSynchronize();
@@ -313,7 +313,7 @@ int bounds_report(gle_handle* h) {
 #else
 inline void bounds_add(void*, size_t, int) {}
 inline void bounds_del(void*) {}
-inline void bounds_sync() {}
+inline void bounds_table_sync() {}
 inline int bounds_report(gle_handle*) { return GLE_OK; }
 #endif
 
@@ -1860,7 +1860,7 @@ int prime(gle_handle* h) {
 
 int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
   if (!h->state_set) return fail(h, GLE_ERR_STATE, "gle_set_state has not been called");
-  bounds_sync();
+  bounds_table_sync();
   for (size_t j = 0; j < h->baths.size(); ++j)
     if (!h->baths[j].noise_set) return fail(h, GLE_ERR_STATE, "bath " + std::to_string(j) + " has no noise");
   if (fpot_host_T == nullptr && !h->has_dyn)
@@ -1979,6 +1979,10 @@ int download(gle_handle* h, void* dst, const void* src, size_t bytes) {
 }
 
 }  // namespace
+
+#ifdef GLE_BOUNDS
+void gle::bounds_sync() { bounds_table_sync(); }
+#endif
 
 // =========================================================================================
 extern "C" {

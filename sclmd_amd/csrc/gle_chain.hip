@@ -883,6 +883,7 @@ void launch_st(int nw, int drn, size_t lds, const ChTile* tiles, int ntiles, con
 void launch_chain(int stage, int nw, int drn, size_t lds_bytes, const ChTile* tiles, int ntiles, const StepDev* sd,
                   StepArgs ta, int mode, hipStream_t s) {
   if (ntiles <= 0) return;
+  GLE_BOUNDS_SYNC();
   if (stage == 0) launch_st<0>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
   else if (stage == 1) launch_st<1>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
   else if (stage == 2) launch_st<2>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);

@@ -65,6 +65,12 @@ __device__ inline void bcheck(const void* p, int bytes, int site) {
 #define GLE_BCHK(p) ((void)0)
 #endif
 #define BLD(p) (GLE_BCHK(p), *(p))  // checked load (a plain load outside the audit build)
+#ifdef GLE_BOUNDS
+void bounds_sync();  // publishes the allocation table if it changed (called by every checked launch)
+#define GLE_BOUNDS_SYNC() ::gle::bounds_sync()
+#else
+#define GLE_BOUNDS_SYNC() ((void)0)
+#endif
 void bounds_publish_chain(const BoundsTab& t);
 void bounds_publish_kernels(const BoundsTab& t);
 

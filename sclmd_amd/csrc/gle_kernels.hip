@@ -313,6 +313,7 @@ void bounds_publish_kernels(const BoundsTab& t) {
 
 void launch_contract_cplx(int rn, const CItem* items, int nitems, StepArgs ta, hipStream_t s) {
   if (nitems <= 0) return;
+  GLE_BOUNDS_SYNC();
   dim3 g(nitems), b(WG);
   switch (rn) {
     case 1: contract_cplx_kernel<1><<<g, b, 0, s>>>(items, ta); break;
@@ -335,6 +336,7 @@ static void launch_rn(int cu, const CItem* items, int nitems, StepArgs ta, hipSt
 
 void launch_contract(int rn, int cu, const CItem* items, int nitems, StepArgs ta, hipStream_t s) {
   if (nitems <= 0) return;
+  GLE_BOUNDS_SYNC();
   switch (rn) {
     case 1: launch_rn<1>(cu, items, nitems, ta, s); break;
     case 2: launch_rn<2>(cu, items, nitems, ta, s); break;
@@ -1004,6 +1006,7 @@ static int g_cg_dbg = 0;
 static int g_cg_kc = 0;    // k-steps per LDS chunk: 4 (159 VGPRs, 3 waves/SIMD; 23.9 vs 21.6 TF/s in situ), GLE_CG_KC=8: 8
 void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStream_t s, int max_grid) {
   if (nitems <= 0) return;
+  GLE_BOUNDS_SYNC();
   if (g_cg_xcd < 0) {
     const char* e = gle_env("GLE_CG_XCD");
     g_cg_xcd = (e && atoi(e) == 0) ? 0 : 1;
