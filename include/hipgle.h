@@ -224,8 +224,12 @@ int gle_comm_init(int32_t nranks, int32_t rank, int32_t device, const char* id, 
 int gle_comm_destroy(void* comm);
 
 /* ---- measurement ---------------------------------------------------------------------- */
-/* Record HIP events around every launch of the memory-kernel contraction (the dominant kernel)
- * on the handle's stream. */
+/* enable = GLE_PROFILE_EVENTS | GLE_PROFILE_COUNT: HIP events around every launch of the dominant
+ * far-field kernel, on the stream it is launched on (gle_profile_read), and the ladder's per-level
+ * block counts (gle_profile_levels).  GLE_PROFILE_COUNT alone counts without events (the events
+ * add launch-queue packets); 0 switches both off and resets the counters either way. */
+#define GLE_PROFILE_EVENTS 1
+#define GLE_PROFILE_COUNT 2
 int gle_profile(gle_handle* h, int32_t enable);
 /* launches, total milliseconds, algorithmic flops and bytes of the profiled contraction
  * launches since profiling was enabled (flops/bytes per SURVEY.md section 8d). */

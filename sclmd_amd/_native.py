@@ -13,6 +13,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SCLMD_AMD_LIB", os.path.join(_HERE, "_lib", "libhipgle.so"))
 
 GLE_BATH_PHONON = 0
+PROFILE_EVENTS = 1  # hipgle.h GLE_PROFILE_EVENTS
+PROFILE_COUNT = 2   # hipgle.h GLE_PROFILE_COUNT
 GLE_BATH_ELECTRON = 1
 
 _ERRNAMES = {-1: "GLE_ERR_ARG", -2: "GLE_ERR_HIP", -3: "GLE_ERR_STATE", -4: "GLE_ERR_NOMEM",
@@ -435,8 +437,10 @@ class Stepper:
                   "gle_reduce_current")
         return out
 
-    def profile(self, enable=True):
-        self._chk(self.lib.gle_profile(self.h, 1 if enable else 0), "gle_profile")
+    def profile(self, enable=True, events=True):
+        """enable: count ladder blocks; events: also HIP-event timing of the dominant kernel."""
+        mode = (PROFILE_COUNT | (PROFILE_EVENTS if events else 0)) if enable else 0
+        self._chk(self.lib.gle_profile(self.h, mode), "gle_profile")
 
     def profile_read(self):
         n = ctypes.c_int64(0)

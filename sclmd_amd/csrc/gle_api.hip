@@ -170,6 +170,7 @@ struct gle_handle {
   double* d_zero = nullptr;            // zero row (chain S(t+1) tiles' unused level slots)
   bool dbg_no_ladder = false;  // GLE_DBG_NO_LADDER: skip the ladder blocks (timing experiments only)
   int bg_grid = 0;             // GLE_BG_GRID: cap of the far-field GEMM grid (grid-stride over items)
+  bool prof_ev = false;         // gle_profile: HIP events around the dominant kernel's launches
   bool bg_serial = false;      // GLE_BG_SERIAL=1: ladder pieces on the main stream (time-sliced, experiment)
   int piece_slack = 1;         // GLE_PIECE_SLACK: boundaries left between a block's last piece and its use
   bool merge_waits = true;     // GLE_MERGE_WAITS=0: one main-stream wait per level
@@ -641,7 +642,7 @@ void drain_profile(gle_handle* h) {
 // kernel) on that same stream.
 void run_op(gle_handle* h, Op& op, hipStream_t s, const StepArgs& ta, bool profile) {
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (profile && h->prof && !op.items.empty()) {
+  if (profile && h->prof_ev && !op.items.empty()) {
     if (h->ev_used + 2 > h->ev.size()) drain_profile(h);
     e0 = h->ev[h->ev_used];
     e1 = h->ev[h->ev_used + 1];
@@ -664,7 +665,7 @@ void run_op(gle_handle* h, Op& op, hipStream_t s, const StepArgs& ta, bool profi
 // One chain launch; profiled (HIP events, same stream) when the ladder has no levels.
 void run_chain(gle_handle* h, int stage, Chain& c, const StepArgs& ta, int mode, bool profile) {
   hipEvent_t e1 = nullptr;
-  if (profile && h->prof && !c.tiles.empty()) {
+  if (profile && h->prof_ev && !c.tiles.empty()) {
     if (h->ev_used + 2 > h->ev.size()) drain_profile(h);
     hipEventRecord(h->ev[h->ev_used], h->stream);
     e1 = h->ev[h->ev_used + 1];
@@ -1775,7 +1776,7 @@ int launch_level_pieces(gle_handle* h, Level& lv, int64_t k, hipStream_t s, bool
       const int64_t c0 = n * (j - 1) / lv.ncg_chunk, c1 = n * j / lv.ncg_chunk;
       if (c1 <= c0) continue;
       hipEvent_t e1 = nullptr;
-      if (h->prof) {
+      if (h->prof_ev) {
         if (h->ev_used + 2 > h->ev.size()) drain_profile(h);
         hipEventRecord(h->ev[h->ev_used], s);
         e1 = h->ev[h->ev_used + 1];
@@ -2211,9 +2212,9 @@ int commit_bath(gle_handle* h, Bath&& b, int32_t* bath_id) {
   b.vs = (int64_t)nbuf;
   rc |= dalloc_n(h, &b.d_inv, (size_t)h->nph);
   if (!rc) rc = upload(h, b.d_inv, b.inv.data(), b.inv.size() * 4);
-  // zero tail of (ncp - nc) rows: the fused stage reads noise(t+1) as an MFMA operand of ncp rows
-  // (K0 columns past nc are zero), which runs past the last time slot by ncp - nc rows
-  rc |= dalloc_n(h, &b.d_noise, (size_t)h->nmd * nc * B, (size_t)(b.ncp - nc) * B + 64);
+  // exact size: the fused stage reads noise(t+1) as an MFMA operand of ncp rows (K0 columns past nc
+  // are zero), its tasks clamp the rows past nc to row nc - 1 (ChTask::xrows, GLE_BOUNDS-audited)
+  rc |= dalloc_n(h, &b.d_noise, (size_t)h->nmd * nc * B);
   rc |= dalloc_n(h, &b.d_S, 2 * nbuf);
   rc |= dalloc_n(h, &b.d_Xcur, 2 * nbuf);
   rc |= dalloc_n(h, &b.d_Xq, 2 * nbuf);
@@ -2858,11 +2859,12 @@ int gle_current_sums(gle_handle* h, double* out) {
 int gle_profile(gle_handle* h, int32_t enable) {
   if (!h) return GLE_ERR_ARG;
   hipSetDevice(h->cfg.device);
-  if (enable && h->ev.empty()) {
+  if ((enable & GLE_PROFILE_EVENTS) && h->ev.empty()) {
     h->ev.resize(4096);
     for (auto& e : h->ev) HIPCHK(h, hipEventCreate(&e));
   }
   h->prof = enable != 0;
+  h->prof_ev = (enable & GLE_PROFILE_EVENTS) != 0;
   h->ev_used = 0;
   h->prof_n = 0;
   h->prof_ms = h->prof_flops = h->prof_bytes = 0;

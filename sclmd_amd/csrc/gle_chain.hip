@@ -141,7 +141,7 @@ __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave,
     gdouble* A = (gdouble*)(tk.A + lane);
     gdouble* X = (gdouble*)(tk.X + col);
     const int64_t ldx = tk.ldx;
-    const int xr = max(tk.xrows - 1, 0);
+    const int xr = tk.xrows - 1;  // < 0 when the task starts past the rows: all read the last row
     const int nks = tk.nks, aks = tk.a_ks;
     // Loads are branch-free (index clamped to the task's last k-step) and MFMAs past the end
     // multiply a zero A operand: a load under a branch makes the waitcnt pass drain every load in

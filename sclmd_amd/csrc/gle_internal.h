@@ -225,8 +225,9 @@ struct ChTask {
   int32_t slot;      // LDS partial slot
   int32_t cond;      // 0: always; CH_HIT / CH_MISS: only when some trajectory of the tile takes the
                      // potential-cache hit / miss branch at q~ (the fused velocity stage)
-  int32_t xrows;     // rows of X that exist from the task's first row (operand rows past them, the
-                     // zero-padded k of A, read the last one instead of leaving the operand)
+  int32_t xrows;     // rows of X that exist from the task's first row, <= 0 when it starts past them
+                     // (operand rows past them, the zero-padded k of A, read the last existing
+                     // row instead of leaving the operand)
   int32_t pad;
 };
 constexpr int32_t CH_HIT = 1;

@@ -56,3 +56,16 @@ def test_missing_library_message(monkeypatch, tmp_path):
     monkeypatch.setattr(_native, "LIB_PATH", str(tmp_path / "nope.so"))
     with pytest.raises(_native.GLEError, match="not found"):
         _native.load()
+
+
+def test_header_constants_match_binding():
+    """Every #define of include/hipgle.h that the ctypes binding mirrors has the same value."""
+    from sclmd_amd import _native
+
+    src = open(os.path.join(ROOT, "include", "hipgle.h")).read()
+    defs = {k: int(v) for k, v in re.findall(r"^#define\s+(GLE_\w+)\s+\(?(-?\d+)\)?", src, re.M)}
+    mirror = {"GLE_REC_P": _native.REC_P, "GLE_REC_Q": _native.REC_Q, "GLE_REC_F": _native.REC_F,
+              "GLE_REC_HIST": _native.REC_HIST, "GLE_PROFILE_EVENTS": _native.PROFILE_EVENTS,
+              "GLE_PROFILE_COUNT": _native.PROFILE_COUNT, "GLE_COMM_ID_BYTES": _native.COMM_ID_BYTES}
+    for k, v in mirror.items():
+        assert defs.get(k) == v, (k, defs.get(k), v)
