@@ -137,9 +137,9 @@ def main():
                          "to bath.noise (throughput runs only; the step does the same work)")
     ap.add_argument("--fill", type=int, default=-1,
                     help="untimed steps before the warm-up that bring the memory-sum ladder to its steady "
-                         "state (history older than the largest level's window); -1 = 2 x the largest "
-                         "block length, rounded up so that the timed window starts on a piece-slot "
-                         "boundary")
+                         "state (history older than the largest level's window); -1 = at least 2 x the "
+                         "largest block length, then to the piece-slot phase whose ladder work matches "
+                         "the steady state")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
                          "rehearse the multi-rank path, e.g. with --same-device on a one-GPU box)")
@@ -201,15 +201,43 @@ def main():
 
     levels = st.profile_levels()
     ptop = max([P for P, _ in levels] + [1])
-    fill = 2 * ptop if args.fill < 0 else args.fill
-    # start the timed window on a piece-slot boundary (t = 0 mod P0): the window then holds whole
-    # slots of background ladder work, as the steady state does, whatever --warmup is
     p0 = max(1, plan["block_len"])
     t_now = st.get_state()[2]
-    if args.fill < 0:
-        fill += (-(t_now + fill + args.warmup)) % p0
     t_fill = time.perf_counter()
-    m.steps(fill)
+    phase = None
+    if args.fill >= 0 or not levels or ptop < 2 * p0:
+        fill = 2 * ptop if args.fill < 0 else args.fill
+        m.steps(fill)
+    else:
+        # Fill to a top-level block boundary (>= 2 ptop steps: every level in its steady state), then
+        # count the ladder blocks issued per piece slot over one top-level period (host counters, no
+        # events).  The timed window is then started at the slot phase whose issued ladder work, in
+        # step-equivalents per level (P x blocks), is closest to the steady state K per level: pieces
+        # go out unevenly within a block's window, so a short window's work depends on its phase
+        # (ladder_window below reports what the timed window actually issued).
+        f0 = 2 * ptop + (-(t_now + 2 * ptop)) % ptop
+        m.steps(f0)
+        st.profile(True, events=False)
+        nslot = ptop // p0
+        cum = [np.array([b for _, b in st.profile_levels()])]
+        for _ in range(nslot):
+            m.steps(p0)
+            cum.append(np.array([b for _, b in st.profile_levels()]))
+        st.profile(False)
+        per = np.diff(np.array(cum), axis=0)  # (slot, level): blocks issued in the slot
+        Ps = np.array([P for P, _ in levels], dtype=float)
+        nw = -(-args.steps // p0)
+        best = None
+        for phi in range(nslot):
+            idx = [(phi + k) % nslot for k in range(nw)]
+            dev = float(np.sum(np.abs(Ps * per[idx].sum(axis=0) - args.steps)))
+            if best is None or dev < best[0] - 1e-9:
+                best = (dev, phi)
+        adv = (best[1] * p0 - args.warmup) % ptop
+        m.steps(adv)
+        fill = f0 + nslot * p0 + adv
+        phase = {"slot": best[1], "slots_per_period": nslot,
+                 "ladder_deviation_steps": round(best[0], 3)}
     st.sync()
     log("[bench] rank %d ladder fill %d steps (%.2fs)" % (rank, fill, time.perf_counter() - t_fill))
     m.steps(args.warmup)
@@ -268,6 +296,7 @@ def main():
         "setup_s": setup_s,
         "fill_steps": fill,
         "window_t0": int(t_now + fill + args.warmup),
+        "window_phase": phase,
         # per ladder level: blocks issued in the timed window vs the steady-state share K / P
         "ladder_window": [{"P": P, "blocks": round(bl, 3), "steady": round(args.steps / P, 3)}
                           for P, bl in window_levels],
