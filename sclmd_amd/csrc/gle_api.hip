@@ -170,6 +170,7 @@ struct gle_handle {
   double* d_zero = nullptr;            // zero row (chain S(t+1) tiles' unused level slots)
   bool dbg_no_ladder = false;  // GLE_DBG_NO_LADDER: skip the ladder blocks (timing experiments only)
   int bg_grid = 0;             // GLE_BG_GRID: cap of the far-field GEMM grid (grid-stride over items)
+  int piece_g = 1;              // steps per piece slot (P0 once planned; GLE_PIECE_STEP=1: every step)
   bool prof_ev = false;         // gle_profile: HIP events around the dominant kernel's launches
   bool bg_serial = false;      // GLE_BG_SERIAL=1: ladder pieces on the main stream (time-sliced, experiment)
   int piece_slack = 1;         // GLE_PIECE_SLACK: boundaries left between a block's last piece and its use
@@ -1410,6 +1411,8 @@ int freeze(gle_handle* h) {
     Pmax = L;
   }
   h->P0 = P0;
+  h->piece_g = P0;
+  if (const char* e = gle_env("GLE_PIECE_STEP")) h->piece_g = std::max(1, std::min(P0, atoi(e)));
   h->near_end = std::min(mlmax, 2 * P0);
   h->levels.clear();
   for (int64_t P = P0; 2 * P < mlmax; P *= 2) {
@@ -1879,11 +1882,12 @@ int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
   bool bg_waited[gle_handle::NBG] = {};
   hipEvent_t wait_ev[gle_handle::NBG] = {};
   int64_t wait_seq[gle_handle::NBG] = {};
-  if (!h->dbg_no_ladder && t % h->P0 == 0) {
+  const bool boundary = t % h->P0 == 0, tick = t % h->piece_g == 0;
+  if (!h->dbg_no_ladder && (boundary || tick)) {
     for (auto& lv : h->levels) {
       hipStream_t bs = h->bg_serial ? h->stream : h->bg[lv.sidx];
       const int64_t k = floordiv(t, lv.P);
-      if (t % lv.P == 0 && k + 1 > lv.last_block) {
+      if (boundary && t % lv.P == 0 && k + 1 > lv.last_block) {
         if (lv.pend_block != INT64_MIN) {  // (cannot happen: the last piece is due at T + P - P0)
           rc = launch_level_pieces(h, lv, lv.pend_block, bs, false, lv.next_piece, lv.npiece);
           if (rc) return rc;
@@ -1898,11 +1902,12 @@ int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
         lv.last_block = k + 1;
         lv.bg_block[(k + 1) & 1] = k + 1;
       }
-      if (lv.pend_block != INT64_MIN) {
-        // the pieces go out over the first nslot - slack boundaries: the last one then has at least
-        // `slack` first-level blocks of time to drain before the main stream needs the block
-        const int nslot = std::max(1, lv.P / h->P0 - h->piece_slack);
-        const int slot = (int)((t - lv.pend_t0) / h->P0);
+      if (tick && lv.pend_block != INT64_MIN) {
+        // the pieces go out over the first slots (piece_g steps each) of the block's window up to
+        // `slack` first-level blocks before the main stream needs the block, which leaves them that
+        // long to drain
+        const int nslot = std::max(1, (lv.P - h->piece_slack * h->P0) / h->piece_g);
+        const int slot = (int)((t - lv.pend_t0) / h->piece_g);
         const int j1 = slot + 1 >= nslot ? lv.npiece : (int)(((int64_t)(slot + 1) * lv.npiece + nslot - 1) / nslot);
         if (j1 > lv.next_piece) {
           rc = launch_level_pieces(h, lv, lv.pend_block, bs, false, lv.next_piece, j1);
@@ -1911,7 +1916,7 @@ int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
         }
         if (lv.next_piece >= lv.npiece) lv.pend_block = INT64_MIN;
       }
-      if (t % lv.P == 0 && lv.bg_block[k & 1] == k) {
+      if (boundary && t % lv.P == 0 && lv.bg_block[k & 1] == k) {
         // per background stream, waiting for the block enqueued last implies the earlier ones
         // (in-order streams): one barrier packet per stream instead of one per level
         if (h->merge_waits) {

@@ -60,11 +60,19 @@ def measure(args, meta, dyn, baths):
         st.run(args.steps)
         st.sync()
         el = time.perf_counter() - t0
+        reps = []
+        for _ in range(args.short_reps):  # bench-like short windows: sync, K steps, sync
+            st.run(37)
+            st.sync()
+            t0 = time.perf_counter()
+            st.run(args.short)
+            st.sync()
+            reps.append(round((time.perf_counter() - t0) / args.short * 1e3, 5))
         p, q, _ = st.get_state()
     finally:
         st.close()
     return {"ms_per_step": el / args.steps * 1e3, "short_ms_per_step": el_short / max(args.short, 1) * 1e3,
-            "aligned_short_ms_per_step": el_aligned / max(args.short, 1) * 1e3,
+            "aligned_short_ms_per_step": el_aligned / max(args.short, 1) * 1e3, "short_reps_ms": reps,
             "traj_steps_per_s": B * args.steps / el, "finite": bool(np.isfinite(p).all() and np.isfinite(q).all())}
 
 
@@ -77,6 +85,7 @@ def main():
     ap.add_argument("--variants", default="", help="';'-separated variants of ','-separated GLE_X=V")
     ap.add_argument("--rounds", type=int, default=1)
     ap.add_argument("--tag", default="")
+    ap.add_argument("--short-reps", type=int, default=0, help="extra short windows at drifting phases")
     ap.add_argument("--profile", type=int, default=0, help="HIP-event timing of the far-field launches on")
     args = ap.parse_args()
     from sclmd_amd import synthetic
