@@ -19,6 +19,7 @@ cpu_baseline: the oracle's reference-equivalent numpy step timed on this host fo
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -137,9 +138,9 @@ def main():
                          "to bath.noise (throughput runs only; the step does the same work)")
     ap.add_argument("--fill", type=int, default=-1,
                     help="untimed steps before the warm-up that bring the memory-sum ladder to its steady "
-                         "state (history older than the largest level's window); -1 = at least 2 x the "
-                         "largest block length, then to the piece-slot phase whose ladder work matches "
-                         "the steady state")
+                         "state (history older than the largest level's window); -1 = 2 x the largest "
+                         "block length, then a scan of K-step windows over the largest level's period "
+                         "and the timed window at the phase closest to the mean")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
                          "rehearse the multi-rank path, e.g. with --same-device on a one-GPU box)")
@@ -201,43 +202,37 @@ def main():
 
     levels = st.profile_levels()
     ptop = max([P for P, _ in levels] + [1])
-    p0 = max(1, plan["block_len"])
     t_now = st.get_state()[2]
     t_fill = time.perf_counter()
     phase = None
-    if args.fill >= 0 or not levels or ptop < 2 * p0:
-        fill = 2 * ptop if args.fill < 0 else args.fill
-        m.steps(fill)
-    else:
-        # Fill to a top-level block boundary (>= 2 ptop steps: every level in its steady state), then
-        # count the ladder blocks issued per piece slot over one top-level period (host counters, no
-        # events).  The timed window is then started at the slot phase whose issued ladder work, in
-        # step-equivalents per level (P x blocks), is closest to the steady state K per level: pieces
-        # go out unevenly within a block's window, so a short window's work depends on its phase
-        # (ladder_window below reports what the timed window actually issued).
-        f0 = 2 * ptop + (-(t_now + 2 * ptop)) % ptop
-        m.steps(f0)
-        st.profile(True, events=False)
-        nslot = ptop // p0
-        cum = [np.array([b for _, b in st.profile_levels()])]
-        for _ in range(nslot):
-            m.steps(p0)
-            cum.append(np.array([b for _, b in st.profile_levels()]))
-        st.profile(False)
-        per = np.diff(np.array(cum), axis=0)  # (slot, level): blocks issued in the slot
-        Ps = np.array([P for P, _ in levels], dtype=float)
-        nw = -(-args.steps // p0)
-        best = None
-        for phi in range(nslot):
-            idx = [(phi + k) % nslot for k in range(nw)]
-            dev = float(np.sum(np.abs(Ps * per[idx].sum(axis=0) - args.steps)))
-            if best is None or dev < best[0] - 1e-9:
-                best = (dev, phi)
-        adv = (best[1] * p0 - args.warmup) % ptop
+    fill = 2 * ptop if args.fill < 0 else args.fill
+    m.steps(fill)
+    nscan = ptop // math.gcd(args.steps, ptop)
+    if args.fill < 0 and levels and nscan > 1:
+        # The ladder's background work within a short window depends on where the window falls in
+        # the largest level's period (blocks start at multiples of P, their pieces follow), so a
+        # K-step window is timed at every phase it can take (consecutive untimed windows, each
+        # bracketed like the timed one), and the timed window starts at the phase whose time is
+        # closest to the mean over all phases, i.e. a window representative of the steady state.
+        nscan = min(nscan, 128)
+        times = []
+        for _ in range(nscan):
+            tp = (t_now + fill) % ptop
+            st.sync()
+            ts = time.perf_counter()
+            m.steps(args.steps)
+            st.sync()
+            times.append((tp, (time.perf_counter() - ts) / args.steps * 1e3))
+            fill += args.steps
+        mean = float(np.mean([x for _, x in times]))
+        phi, tphi = min(times, key=lambda pt: abs(pt[1] - mean))
+        adv = (phi - args.warmup - (t_now + fill)) % ptop
         m.steps(adv)
-        fill = f0 + nslot * p0 + adv
-        phase = {"slot": best[1], "slots_per_period": nslot,
-                 "ladder_deviation_steps": round(best[0], 3)}
+        fill += adv
+        ms = [x for _, x in times]
+        phase = {"t_mod_ptop": int(phi), "ptop": int(ptop), "phases_scanned": len(times),
+                 "scan_ms_per_step": {"mean": round(mean, 5), "min": round(min(ms), 5), "max": round(max(ms), 5),
+                                      "chosen": round(tphi, 5)}}
     st.sync()
     log("[bench] rank %d ladder fill %d steps (%.2fs)" % (rank, fill, time.perf_counter() - t_fill))
     m.steps(args.warmup)
