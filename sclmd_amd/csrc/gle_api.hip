@@ -2807,8 +2807,16 @@ int gle_run(gle_handle* h, int64_t nsteps) {
 int gle_sync(gle_handle* h) {
   if (!h) return GLE_ERR_ARG;
   hipSetDevice(h->cfg.device);
-  int rc = sync_bg(h);
-  if (rc) return rc;
+  // one host wait: the main stream joins the background streams, then is synchronised (one
+  // wake-up instead of one per stream; GLE_SYNC_JOIN=0: per-stream synchronisation)
+  const char* ej = gle_env("GLE_SYNC_JOIN");
+  const bool per_stream = ej && atoi(ej) == 0;
+  if (per_stream) {
+    int rc = sync_bg(h);
+    if (rc) return rc;
+  } else {
+    join_bg(h);
+  }
   HIPCHK(h, hipStreamSynchronize(h->stream));
   HIPCHK(h, hipGetLastError());
   return bounds_report(h);
