@@ -800,12 +800,17 @@ void xcd_order(gle_handle* h, Chain& c) {
   if (c.tiles.size() < 2 * NX) return;
   if (const char* e = gle_env("GLE_XCD_ORDER"))
     if (atoi(e) == 0) return;
+  // a tile costs a fixed latency (descriptor, prologue loads, epilogue, ~ the time of 48 k-steps of
+  // 16-column MFMAs) plus its products: with the products alone, light tiles (DOFs outside every
+  // bath) piled up on a few XCDs and the padding to equal list lengths tripled the launch
+  double tile_cost = 48.0;
+  if (const char* e = gle_env("GLE_XCD_TILE_COST")) tile_cost = std::max(0.0, atof(e));
   std::vector<std::pair<int64_t, std::vector<size_t>>> groups;  // (key, tiles)
   std::vector<double> gwork;
   for (size_t i = 0; i < c.tiles.size(); ++i) {
     const ChTile& T = c.tiles[i];
     const int64_t key = T.kind == CH_DOF ? (int64_t)(T.row0 / 16) : ((int64_t)(T.tile + 1) << 32) + T.row0 / 16;
-    double w = 1.0;
+    double w = 1.0 + tile_cost;
     for (int wv = 0; wv < CH_NW; ++wv)
       for (int k = 0; k < T.ntw[wv] && k < CH_TPW; ++k) w += (double)T.task[wv][k].nks * T.rn;
     size_t g = 0;
