@@ -798,8 +798,10 @@ int fill_tasks(gle_handle* h, ChTile& T, const std::vector<Seg>& segs, int nout,
 void xcd_order(gle_handle* h, Chain& c) {
   constexpr int NX = 8;
   if (c.tiles.size() < 2 * NX) return;
-  if (const char* e = gle_env("GLE_XCD_ORDER"))
-    if (atoi(e) == 0) return;
+  // off by default: measured 1.5-2 % slower per step at C3 than plan order (r02, 3 interleaved
+  // rounds), the L2 locality not paying for the imbalance; GLE_XCD_ORDER=1 (experiment build) on
+  const char* e = gle_env("GLE_XCD_ORDER");
+  if (!e || atoi(e) == 0) return;
   // a tile costs a fixed latency (descriptor, prologue loads, epilogue, ~ the time of 48 k-steps of
   // 16-column MFMAs) plus its products: with the products alone, light tiles (DOFs outside every
   // bath) piled up on a few XCDs and the padding to equal list lengths tripled the launch
