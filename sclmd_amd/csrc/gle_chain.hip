@@ -80,6 +80,10 @@ __device__ __forceinline__ int64_t cmod(int64_t a, int64_t m) {
 #ifndef CH_WPE
 #define CH_WPE 4
 #endif
+// CH_PRIO: wave issue priority of the chain kernels (s_setprio 0..3; the ladder kernels run at 0)
+#ifndef CH_PRIO
+#define CH_PRIO 3
+#endif
 // CH_DB: double-buffered operand batches (the next batch of a task in flight during this one's MFMAs)
 #ifndef CH_DB
 #define CH_DB 0
@@ -810,6 +814,10 @@ template <int STAGE, int NW, int DRN>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(DRN == 1 && NW <= 8 ? CH_WPE : 1, 8))) void chain_kernel(const ChTile* __restrict__ tiles, const StepDev* sd,
                                                         StepArgs ta, int mode) {
   extern __shared__ double lds[];
+  // The chain is the step's latency-bound critical path and shares SIMDs with the background
+  // ladder's GEMM waves: its waves take issue priority (MFMA pipe and memory issue go to the
+  // highest-priority ready wave first, then the oldest)
+  __builtin_amdgcn_s_setprio(CH_PRIO);
   // The tile descriptor and the step descriptor's header are copied into LDS with one round of
   // coalesced vector loads: every later field access is an LDS read instead of a chain of
   // dependent scalar loads.
