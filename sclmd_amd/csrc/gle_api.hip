@@ -74,12 +74,6 @@ struct Bath {
   // (fused stage: d_K0sqd = M1 = K0 - a K0^2, d_hK0d = h K0, d_KKqd = -h K0 Kq, d_KDd = -h K0 P dyn)
   double *d_Xf = nullptr, *d_V = nullptr, *d_K0sqd = nullptr, *d_KKqd = nullptr, *d_KDd = nullptr;
   double* d_hK0d = nullptr;
-  // next-step products (CH_NXT tiles, light stage A): K_j p_{t+1} (j = 0, 1) and the bath-row
-  // fragments of K_j R, K_j Qm, -K_j Qm Kq (j = 0) and -K_j Qm P dyn (runs per bath row tile)
-  double *d_Y0n = nullptr, *d_Y1n = nullptr;
-  double *d_Np[2] = {}, *d_Nv[2] = {}, *d_Nq = nullptr, *d_Nd[2] = {};
-  std::vector<std::vector<std::pair<int, int>>> nd_rng[2];
-  std::vector<int64_t> nd_tofs[2];
   std::vector<std::vector<std::pair<int, int>>> kd_rng;
   std::vector<int64_t> kd_tofs;
   // K0 / Kq rows in DOF order for the chain's DOF tiles: tile rt at [tofs[rt]][ks][64]
@@ -196,9 +190,6 @@ struct gle_handle {
   Op op_prime;
   Chain chA[2], chB[2], chC, chNear;  // [with dyn.q]; chNear: all near-field partial tiles (priming)
   Chain chBC;                          // stages B + C fused (harmonic force, disjoint baths)
-  Chain chAL;                          // light stage A: products taken from the previous chBC
-  bool lite_plan = false;              // chBC computes the next step's K0 p / K_1 p / Kq q
-  bool lite_ready = false;             // ... and the last step was such a fused step
   bool fuse_bc = false;
   int ch_nw[3] = {4, 8, 4};            // chain workgroup waves per stage
   int ch_drn = 1;                      // DOF-tile 16-column MFMA tiles
@@ -868,205 +859,6 @@ int upload_chain(gle_handle* h, Chain& c) {
   return rc;
 }
 
-// C = A B for dense row-major n x n (host fp64, row streaming)
-void host_mm(const std::vector<double>& A, const std::vector<double>& Bm, std::vector<double>& C, int64_t n) {
-  C.assign((size_t)n * n, 0.0);
-  for (int64_t r = 0; r < n; ++r)
-    for (int64_t k = 0; k < n; ++k) {
-      const double a = A[(size_t)(r * n + k)];
-      if (a == 0.0) continue;
-      const double* src = &Bm[(size_t)(k * n)];
-      double* dst = &C[(size_t)(r * n)];
-      for (int64_t c2 = 0; c2 < n; ++c2) dst[c2] += a * src[c2];
-    }
-}
-
-// host copy of kernel slice i of bath b (fragment-native d_K: [rt][ks][slice][64])
-int host_slice(gle_handle* h, const Bath& b, int i, std::vector<double>& out) {
-  const int64_t nc = b.nc, nfrag = (int64_t)b.nrt * b.nks;
-  std::vector<double> f((size_t)nfrag * 64);
-  HIPCHK(h, hipMemcpy2DAsync(f.data(), 64 * 8, b.d_K + (int64_t)i * 64, (size_t)b.ml * 64 * 8, 64 * 8, (size_t)nfrag,
-                             hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
-  out.assign((size_t)nc * nc, 0.0);
-  for (int rt = 0; rt < b.nrt; ++rt)
-    for (int ks = 0; ks < b.nks; ++ks)
-      for (int l = 0; l < 64; ++l) {
-        const int64_t r = 16 * rt + (l & 15), c = 4 * ks + (l >> 4);
-        if (r < nc && c < nc) out[(size_t)(r * nc + c)] = f[((size_t)rt * b.nks + ks) * 64 + l];
-      }
-  return GLE_OK;
-}
-
-// Next-step products of the fused step (CH_NXT tiles in chBC) and the light stage A (chAL) that
-// reads them instead of forming K0 p_t, K_1 p_t and Kq q_t itself.  Without constraints
-// q_{t+1} = q~ and p_{t+1} = p2 = p_half + h (g - c K0 p1) with g = Fpot_b(q~) + V - Kq q~,
-// K0 p1 = M1 p_half + h K0 g, so K_j p2 = K_j R p_half + K_j Qm g with R = I - c h K0 + (c h K0)^2,
-// Qm = h (I - c h K0): every operand is already an operand of the fused step.  The sums are
-// re-associated (rounding only).
-int plan_next(gle_handle* h, int drn, int ncol1) {
-  const int64_t B = h->B, nph = h->nph;
-  const double hh = h->dt / 2.0;
-  const int nksd = (int)(h->nphp / 4);
-  for (size_t j = 0; j < h->baths.size(); ++j) {
-    Bath& b = h->baths[j];
-    const int64_t nc = b.nc;
-    const double ch = b.c * hh;
-    std::vector<double> k2, k3;
-    host_mm(b.K0, b.K0, k2, nc);
-    host_mm(b.K0, k2, k3, nc);
-    // I - c h K0 + (c h)^2 K0^2 and h (I - c h K0) as operators on the right of K_j
-    std::vector<double> Rm((size_t)nc * nc), Qm((size_t)nc * nc);
-    for (int64_t r = 0; r < nc; ++r)
-      for (int64_t c2 = 0; c2 < nc; ++c2) {
-        const size_t e = (size_t)(r * nc + c2);
-        const double id = r == c2 ? 1.0 : 0.0;
-        Rm[e] = id - ch * b.K0[e] + ch * ch * k2[e];
-        Qm[e] = hh * (id - ch * b.K0[e]);
-      }
-    const int nj = b.ml >= 2 ? 2 : 1;
-    int rc = dalloc_n(h, &b.d_Y0n, (size_t)b.vs);
-    if (!rc && nj == 2) rc = dalloc_n(h, &b.d_Y1n, (size_t)b.vs);
-    if (rc) return rc;
-    for (int jj = 0; jj < nj; ++jj) {
-      std::vector<double> Kj;
-      if (jj == 0) {
-        Kj = b.K0;
-      } else {
-        rc = host_slice(h, b, 1, Kj);
-        if (rc) return rc;
-      }
-      std::vector<double> np, nv;
-      if (jj == 0) {  // K0 R = K0 - ch K0^2 + ch^2 K0^3, K0 Qm = h (K0 - ch K0^2)
-        np.resize((size_t)nc * nc);
-        nv.resize((size_t)nc * nc);
-        for (size_t e = 0; e < np.size(); ++e) {
-          np[e] = b.K0[e] - ch * k2[e] + ch * ch * k3[e];
-          nv[e] = hh * (b.K0[e] - ch * k2[e]);
-        }
-      } else {
-        host_mm(Kj, Rm, np, nc);
-        host_mm(Kj, Qm, nv, nc);
-      }
-      std::vector<double> f = pack_frags(np.data(), 1, nc, nc, b.nrt, b.nks);
-      rc = dalloc_n(h, &b.d_Np[jj], f.size());
-      if (!rc) rc = upload(h, b.d_Np[jj], f.data(), f.size() * 8);
-      f = pack_frags(nv.data(), 1, nc, nc, b.nrt, b.nks);
-      if (!rc) rc = dalloc_n(h, &b.d_Nv[jj], f.size());
-      if (!rc) rc = upload(h, b.d_Nv[jj], f.data(), f.size() * 8);
-      if (rc) return rc;
-      if (jj == 0 && b.has_q) {  // -(K0 Qm) Kq on q~
-        std::vector<double> nq;
-        host_mm(nv, b.Kq, nq, nc);
-        for (double& v : nq) v = -v;
-        f = pack_frags(nq.data(), 1, nc, nc, b.nrt, b.nks);
-        rc = dalloc_n(h, &b.d_Nq, f.size());
-        if (!rc) rc = upload(h, b.d_Nq, f.data(), f.size() * 8);
-        if (rc) return rc;
-      }
-      // -(K_j Qm) P dyn (nc x nph), fragments of the nonzero 16 x 4 blocks, <= 2 runs per row tile
-      std::vector<double> nd((size_t)nc * nph, 0.0);
-      for (int64_t k = 0; k < nc; ++k) {
-        const double* drow = &h->dyn_h[(size_t)(b.cids[k] * nph)];
-        std::vector<int64_t> nzc;
-        for (int64_t c2 = 0; c2 < nph; ++c2)
-          if (drow[c2] != 0.0) nzc.push_back(c2);
-        for (int64_t r = 0; r < nc; ++r) {
-          const double a = nv[(size_t)(r * nc + k)];
-          if (a == 0.0) continue;
-          for (int64_t c2 : nzc) nd[(size_t)(r * nph + c2)] -= a * drow[c2];
-        }
-      }
-      b.nd_rng[jj].assign(b.nrt, {});
-      b.nd_tofs[jj].assign(b.nrt, 0);
-      int64_t n = 0;
-      for (int rt = 0; rt < b.nrt; ++rt) {
-        std::vector<std::pair<int, int>> rg;
-        for (int ks = 0; ks < nksd; ++ks) {
-          bool nz = false;
-          for (int r = 16 * rt; r < 16 * rt + 16 && r < nc && !nz; ++r)
-            for (int64_t c2 = 4 * ks; c2 < 4 * ks + 4 && c2 < nph; ++c2) nz |= nd[(size_t)(r * nph + c2)] != 0.0;
-          if (!nz) continue;
-          if (!rg.empty() && rg.back().first + rg.back().second == ks) ++rg.back().second;
-          else rg.push_back({ks, 1});
-        }
-        while (rg.size() > 2) {  // merge the closest runs (zero blocks in between are multiplied)
-          size_t bi = 0;
-          int bg = INT32_MAX;
-          for (size_t i = 0; i + 1 < rg.size(); ++i) {
-            const int gap = rg[i + 1].first - (rg[i].first + rg[i].second);
-            if (gap < bg) {
-              bg = gap;
-              bi = i;
-            }
-          }
-          rg[bi].second = rg[bi + 1].first + rg[bi + 1].second - rg[bi].first;
-          rg.erase(rg.begin() + bi + 1);
-        }
-        b.nd_tofs[jj][rt] = n;
-        for (auto& r : rg) n += (int64_t)r.second * 64;
-        b.nd_rng[jj][rt] = rg;
-      }
-      std::vector<double> fd((size_t)std::max<int64_t>(n, 64), 0.0);
-      for (int rt = 0; rt < b.nrt; ++rt) {
-        int64_t o = b.nd_tofs[jj][rt];
-        for (auto& r : b.nd_rng[jj][rt])
-          for (int ks = r.first; ks < r.first + r.second; ++ks, o += 64)
-            for (int l = 0; l < 64; ++l) {
-              const int64_t row = 16 * rt + (l & 15), c2 = 4 * ks + (l >> 4);
-              if (row < nc && c2 < nph) fd[(size_t)(o + l)] = nd[(size_t)(row * nph + c2)];
-            }
-      }
-      rc = dalloc_n(h, &b.d_Nd[jj], fd.size());
-      if (!rc) rc = upload(h, b.d_Nd[jj], fd.data(), fd.size() * 8);
-      if (rc) return rc;
-      // the CH_NXT tiles of this (bath, j)
-      for (int rt = 0; rt < b.nrt; ++rt)
-        for (int ct = 0; ct < ncol1; ++ct) {
-          ChTile T{};
-          T.kind = CH_NXT;
-          T.rn = drn;
-          T.row0 = 16 * rt;
-          T.c0 = 16 * drn * ct;
-          T.tile = (int)j;
-          T.nrows = (int)std::min<int64_t>(16, nc - 16 * rt);
-          T.ncols = (int)std::min<int64_t>(16 * drn, B - T.c0);
-          T.dst = jj == 0 ? b.d_Y0n : b.d_Y1n;
-          T.ldd = (int32_t)B;
-          const int64_t ao = (int64_t)rt * b.nks * 64;
-          std::vector<Seg> segs;
-          segs.push_back(Seg{0, b.d_Np[jj] + ao, 64, b.d_Xcur, (int)B, 0, 0, b.nks, 0});
-          if (b.ml >= 2) {
-            segs.push_back(Seg{0, b.d_Nv[jj] + ao, 64, b.d_V, (int)B, 0, 0, b.nks, 0});
-          } else {  // V = noise(t+1) from the noise ring (nc rows per slot)
-            Seg sg{0, b.d_Nv[jj] + ao, 64, b.d_noise, (int)B, (int)h->nmd, 1, b.nks, (int)(b.nc * B)};
-            sg.xrows = b.nc;
-            segs.push_back(sg);
-          }
-          if (jj == 0 && b.has_q) segs.push_back(Seg{0, b.d_Nq + ao, 64, b.d_Xq + b.vs, (int)B, 0, 0, b.nks, 0});
-          {
-            Seg sg{1, b.d_Nv[jj] + ao, 64, b.d_Xf, (int)B, 0, 0, b.nks, 0};
-            sg.cond = CH_HIT;
-            segs.push_back(sg);
-          }
-          int64_t o = b.nd_tofs[jj][rt];
-          for (auto& r : b.nd_rng[jj][rt]) {
-            Seg sg{2, b.d_Nd[jj] + o, 64, h->d_Qt + (int64_t)4 * r.first * B, (int)B, 0, 0, r.second, 0};
-            sg.cond = CH_MISS;
-            segs.push_back(sg);
-            o += (int64_t)r.second * 64;
-          }
-          int64_t W = 0;
-          for (auto& sg : segs) W += sg.nks;
-          rc = fill_tasks(h, T, segs, 3, 0, W, h->chBC);
-          if (rc) return rc;
-          h->chBC.tiles.push_back(T);
-        }
-    }
-  }
-  return GLE_OK;
-}
-
 int plan_chain(gle_handle* h) {
   const int64_t B = h->B;
   const int nb = (int)h->baths.size();
@@ -1562,39 +1354,7 @@ int plan_chain(gle_handle* h) {
         }
     }
   }
-  // light stage A (fused harmonic step without constraints, GLE_LITE_A=0 switches it off): the
-  // fused step also forms the next step's K0 p, K_1 p (CH_NXT tiles) and Kq q (its DOF tiles), and
-  // stage A after such a step is product-free
-  h->chAL.tiles.clear();
-  h->chAL.flops = 0;
-  h->lite_plan = false;
-  h->lite_ready = false;
-  {
-    const char* e = gle_env("GLE_LITE_A");
-    if (h->fuse_bc && h->constr.empty() && !(e && atoi(e) == 0)) {
-      int rc = plan_next(h, drn, ncol1);
-      if (rc) return rc;
-      for (ChTile& T : h->chBC.tiles)
-        if (T.kind == CH_DOF) T.lite = 1;  // store Kq q~ for the next stage A
-      h->chAL.nw = h->chA[0].nw;
-      h->chAL.lds = h->chA[0].lds;
-      for (const ChTile& T0 : h->chA[0].tiles) {
-        ChTile T = T0;
-        T.lite = 1;
-        for (int w = 0; w < CH_NW; ++w) T.ntw[w] = 0;
-        for (int o = 0; o <= CH_NOUT; ++o) T.ob[o] = 0;
-        if (T.kind == CH_DOF) {
-          for (int u = 0; u < CH_TB; ++u)
-            T.tb[u].Y0n = T.tb[u].bath >= 0 ? h->baths[T.tb[u].bath].d_Y0n : h->d_zero;
-        } else if (T.kind == CH_SFIN) {
-          T.sf.Y1n = h->baths[T.tile].d_Y1n;
-        }
-        h->chAL.tiles.push_back(T);
-      }
-      h->lite_plan = true;
-    }
-  }
-  for (Chain* c : {&h->chA[0], &h->chA[1], &h->chB[0], &h->chB[1], &h->chC, &h->chNear, &h->chBC, &h->chAL}) {
+  for (Chain* c : {&h->chA[0], &h->chA[1], &h->chB[0], &h->chB[1], &h->chC, &h->chNear, &h->chBC}) {
     int rc = upload_chain(h, *c);
     if (rc) return rc;
   }
@@ -2075,7 +1835,6 @@ int launch_level_block(gle_handle* h, Level& lv, int64_t k, hipStream_t s, bool 
 // at the first step), so every window of steps after a prime carries the steady-state share of
 // far-field work.
 int prime(gle_handle* h) {
-  h->lite_ready = false;  // the next stage A forms its own products (state / history were set)
   join_bg(h);  // blocks still in flight read the ring and write the buffers recomputed here
   const StepArgs ta = step_args(h);
   // S(t) into S[t&1]: the prime op writes S[0]; copy when t is odd
@@ -2188,9 +1947,7 @@ int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
   const StepArgs ta = step_args(h);
   if (fpot_host_T)
     HIPCHK(h, hipMemcpyAsync(h->d_Fc, fpot_host_T, (size_t)h->nph * h->B * 8, hipMemcpyHostToDevice, h->stream));
-  const bool lite = h->lite_ready && !need_pot && fpot_host_T == nullptr;
-  run_chain(h, 0, lite ? h->chAL : h->chA[need_pot ? 1 : 0], ta, (need_pot ? 1 : 0) | (fpot_host_T ? 0 : 2),
-            h->levels.empty());
+  run_chain(h, 0, h->chA[need_pot ? 1 : 0], ta, (need_pot ? 1 : 0) | (fpot_host_T ? 0 : 2), h->levels.empty());
   h->host_force_step = fpot_host_T != nullptr;
   return GLE_OK;
 }
@@ -2207,11 +1964,9 @@ int step_end_impl(gle_handle* h, const double* fpot_host_T) {
   }
   if (h->fuse_bc && mode1 == 1) {
     run_chain(h, 3, h->chBC, ta, mode1, h->levels.empty());
-    h->lite_ready = h->lite_plan;
   } else {
     run_chain(h, 1, h->chB[mode1], ta, mode1, h->levels.empty());
     run_chain(h, 2, h->chC, ta, mode1, h->levels.empty());
-    h->lite_ready = false;
   }
   // the next step is a block boundary: the background blocks started there wait for this step
   if (!h->levels.empty() && (h->t + 1) % h->P0 == 0) HIPCHK(h, hipEventRecord(h->ev_step, h->stream));
@@ -3194,18 +2949,6 @@ int gle_step_work(gle_handle* h, double* flops, double* bytes) {
     if (h->fuse_bc) {
       fl += 2.0 * kd_nnz * B;  // (K0 P dyn).q~ on a potential-cache miss (every harmonic step)
       by += 8.0 * kd_nnz;
-    }
-    if (h->lite_plan) {  // K_j p_{t+1} from the fused step's operands replace stage A's K0 p_t, K_1 p_t
-      const int nj = b.ml >= 2 ? 2 : 1;
-      for (int jj = 0; jj < nj; ++jj) {
-        double nd_nnz = 0.0;
-        for (size_t rt = 0; rt < b.nd_rng[jj].size(); ++rt) {
-          const double rows = (double)std::min<int64_t>(16, b.nc - 16 * (int64_t)rt);
-          for (const auto& r : b.nd_rng[jj][rt]) nd_nnz += 4.0 * r.second * rows;
-        }
-        fl += 2.0 * nc2 * B * 1.0 + 2.0 * nd_nnz * B;  // (K_j R).p_half, (K_j Qm).V (net +1 product), miss
-        by += 8.0 * (2.0 * nc2 + nd_nnz);
-      }
     }
     by += 8.0 * 12.0 * b.nc * B;  // bath-local vectors: noise rows, S, V, gathers, ring pushes
   }

@@ -308,8 +308,7 @@ __device__ __forceinline__ void dof_A(const ChTile* __restrict__ T, const StepDe
   unsigned long long w0[EPT];
   int qv[EPT];
   int kk[EPT][CH_TB];
-  double nz[EPT][CH_TB], sv[EPT][CH_TB], y0[EPT][CH_TB], yq[EPT][CH_TB];
-  const bool lite = T->lite != 0;
+  double nz[EPT][CH_TB], sv[EPT][CH_TB];
 #pragma unroll
   for (int x = 0; x < EPT; ++x) {
     E[x] = elem_of<NW, DRN>(T, sd, x);
@@ -328,11 +327,6 @@ __device__ __forceinline__ void dof_A(const ChTile* __restrict__ T, const StepDe
       const int64_t kb = bath_idx(E[x], kk[x][u], B);
       nz[x][u] = G(bd.noise)[(int64_t)tn * bd.nc * B + kb];
       sv[x][u] = G(bd.S)[(int64_t)par * bd.vs + kb];
-      y0[x][u] = yq[x][u] = 0.0;
-      if (lite) {  // tile-uniform: K0 p_t and Kq q_t from the previous fused step
-        y0[x][u] = G(bd.Y0n)[kb];
-        yq[x][u] = G(bd.Yq)[bd.has_q ? kb : 0];
-      }
     }
   }
   if (T->first && threadIdx.x < Geo::NT && T->c0 + (int)threadIdx.x < B)
@@ -363,8 +357,8 @@ __device__ __forceinline__ void dof_A(const ChTile* __restrict__ T, const StepDe
       cur[x][u] = 0.0;
       if (kk[x][u] >= 0) {
         const ChBath& bd = T->tb[u];
-        double fb = nz[x][u] - bd.c * ((lite ? y0[x][u] : out_sum(T, lds, u, e, Geo::NE)) + sv[x][u]);
-        if (bd.has_q) fb -= lite ? yq[x][u] : out_sum(T, lds, CH_TB + u, e, Geo::NE);
+        double fb = nz[x][u] - bd.c * (out_sum(T, lds, u, e, Geo::NE) + sv[x][u]);
+        if (bd.has_q) fb -= out_sum(T, lds, CH_TB + u, e, Geo::NE);
         f += fb;                 // pf = pf + fbaths[i]  (md.py:432-434)
         cur[x][u] = fb * p[x];   // cur[t] = fbaths[i].p (md.py:397)
         if (double* rf = sd->rec_f[bd.bath])  // fhis[i][t] = fbaths[i] (md.py:398), bath rows
@@ -692,12 +686,7 @@ __device__ __forceinline__ void dof_BC(const ChTile* __restrict__ T, const StepD
       if (kk[x][u] >= 0) {
         const ChBath& bd = T->tb[u];
         f2 += nz[x][u] - bd.c * sv[x][u];
-        if (bd.has_q) {
-          const double kqq = out_sum(T, lds, CH_TB + u, e, Geo::NE);
-          f2 -= kqq;
-          // Kq q_{t+1} of the next (light) stage A: q_{t+1} = q~ without constraints
-          if (T->lite && E[x].ok) G(bd.Yq)[(int64_t)kk[x][u] * B + E[x].b] = kqq;
-        }
+        if (bd.has_q) f2 -= out_sum(T, lds, CH_TB + u, e, Geo::NE);
         const double k0p1 = out_sum(T, lds, CH_OYB + u, e, Geo::NE) +
                             (hit1[x] ? out_sum(T, lds, CH_OYE + u, e, Geo::NE) : out_sum(T, lds, CH_OYD + u, e, Geo::NE));
         f2 -= bd.c * k0p1;
@@ -758,10 +747,9 @@ __device__ __forceinline__ void sfin(const ChTile* __restrict__ T, const StepDev
   const ChSfin& sf = T->sf;
   constexpr int NT = 16 * DRN, NE = 16 * NT;  // S(t+1) tiles have the DOF tiles' width
   constexpr int EPT = (NE + NW * 64 - 1) / (NW * 64);
-  double pre[EPT], y1[EPT];
+  double pre[EPT];
   int64_t kb[EPT];
   bool ok[EPT];
-  const bool lite = T->lite != 0;
 #pragma unroll
   for (int x = 0; x < EPT; ++x) {
     const int e = threadIdx.x + x * NW * 64;
@@ -769,7 +757,6 @@ __device__ __forceinline__ void sfin(const ChTile* __restrict__ T, const StepDev
     const int b = T->c0 + e % NT;
     ok[x] = e < NE && k < sf.nc && b < B;
     kb[x] = (int64_t)k * B + b;
-    y1[x] = lite ? G(sf.Y1n)[ok[x] ? kb[x] : 0] : 0.0;  // K_1 p_t from the previous fused step
     // near-field partials and level blocks, all loads in flight together, added in slot / level
     // order
     double v[CH_NPMAX], lv[MAXLVL];
@@ -794,51 +781,13 @@ __device__ __forceinline__ void sfin(const ChTile* __restrict__ T, const StepDev
   for (int x = 0; x < EPT; ++x) {
     const int e = threadIdx.x + x * NW * 64;
     if (ok[x]) {
-      const double s1 = (lite ? y1[x] : out_sum(T, lds, 0, e, NE)) + pre[x];
+      const double s1 = out_sum(T, lds, 0, e, NE) + pre[x];
       G(sf.S)[(int64_t)par1 * sf.vs + kb[x]] = s1;
       if (sf.V) {  // fused B+C: V = noise(t+1) - c S(t+1), the bath part of F1 that K0 acts on
         const int t1 = (int)((t + 1) % sd->nmd);
         const int k = (int)(kb[x] / B), b = (int)(kb[x] - (int64_t)k * B);
         G(sf.V)[kb[x]] = G(sf.noise)[((int64_t)t1 * sf.nc + k) * B + b] - sf.c * s1;
       }
-    }
-  }
-}
-
-// CH_NXT (fused step): K_j p_{t+1} of bath rows [row0, row0 + 16) for the next step's light stage
-// A, j = 0 or 1.  With h = dt/2, g = Fpot_b(q~) + V - Kq q~ and p2 = p_half + h (g - c K0 p1):
-//   K_j p2 = K_j R p_half + K_j Qm g,   R = I - c h K0 + (c h K0)^2,  Qm = h (I - c h K0)
-// output 0: (K_j R) p_half + (K_j Qm) V - (K_j Qm Kq) q~;  1: (K_j Qm) Fc (potential-cache hit at
-// q~);  2: -(K_j Qm P dyn) q~ (miss).  The branch is per trajectory (the pmax word of this step).
-template <int NW, int DRN>
-__device__ __forceinline__ void nxt(const ChTile* __restrict__ T, const StepDev* __restrict__ sd,
-                                    const StepArgs& ta, int mode, double* lds) {
-  constexpr int NT = 16 * DRN, NE = 16 * NT;
-  constexpr int EPT = (NE + NW * 64 - 1) / (NW * 64);
-  const int64_t t = ta.t;
-  const int par = (int)(t & 1);
-  bool hit[EPT], ok[EPT];
-  int anyhit = 0, anymiss = 0;
-#pragma unroll
-  for (int x = 0; x < EPT; ++x) {
-    const int e = threadIdx.x + x * NW * 64;
-    const int r = e / NT, c = e % NT;
-    ok[x] = e < NE && r < T->nrows && c < T->ncols;
-    const unsigned long long w1 = *G(pmax_word(sd, 1, par, ok[x] ? T->c0 + c : 0));
-    hit[x] = mode != 0 ? word_hit(w1) : true;
-    anyhit |= (ok[x] && hit[x]) ? 1 : 0;
-    anymiss |= (ok[x] && !hit[x]) ? 1 : 0;
-  }
-  anyhit = __syncthreads_or(anyhit);
-  anymiss = __syncthreads_or(anymiss);
-  run_products<NW>(T, t, lds, (anyhit ? 0 : 1) | (anymiss ? 0 : 2));
-  __syncthreads();
-#pragma unroll
-  for (int x = 0; x < EPT; ++x) {
-    const int e = threadIdx.x + x * NW * 64;
-    if (ok[x]) {
-      const double y = out_sum(T, lds, 0, e, NE) + (hit[x] ? out_sum(T, lds, 1, e, NE) : out_sum(T, lds, 2, e, NE));
-      G(T->dst)[(int64_t)(T->row0 + e / NT) * T->ldd + T->c0 + e % NT] = y;
     }
   }
 }
@@ -897,8 +846,6 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(DRN == 
     else dof_BC<NW, DRN>(T, sd, ta, mode, lds);
   } else if (kind == CH_SFIN) {
     sfin<NW, DRN>(T, sd, ta, lds, STAGE);
-  } else if (STAGE == 3 && kind == CH_NXT) {
-    nxt<NW, DRN>(T, sd, ta, mode, lds);
   } else {
     raw<NW>(T, sd, ta, lds, STAGE);
   }

@@ -194,9 +194,6 @@ struct StepDev {
 //            constraints, history push)
 //   CH_SFIN  16 bath rows: S(t+1) = K_1 p_t + near-field partials + ladder levels
 //   CH_RAW   16 bath rows x 16*rn columns of a near-field partial (lags >= 2, target t+2)
-//   CH_NXT   (fused step, no constraints) 16 bath rows: K0 p_{t+1} or K_1 p_{t+1} from the fused
-//            step's own operands (p_half, V, the potential force at q~, q~), so that the next
-//            step's stage A is product-free (ChTile::lite)
 constexpr int CH_NW = 16;       // waves per chain workgroup (max)
 constexpr int CH_TPW = 3;       // tasks per wave
 constexpr int CH_TB = 3;        // baths a DOF tile may intersect
@@ -214,7 +211,7 @@ constexpr int CH_OYF = CH_OYE + CH_TB;
 constexpr int CH_NOUT = CH_OYF + CH_TB;
 constexpr int CH_LDS_PER_WAVE = 1024;  // doubles of LDS partial slots per wave
 constexpr int CH_NPMAX = 16;    // near-field partial slots read by one SFIN element
-enum { CH_DOF = 0, CH_SFIN = 1, CH_RAW = 2, CH_NXT = 3 };
+enum { CH_DOF = 0, CH_SFIN = 1, CH_RAW = 2 };
 
 struct ChTask {
   const double* A;   // fragment of the first k-step (lane offset added in the kernel)
@@ -244,7 +241,6 @@ struct ChBath {
   double *S, *Xcur, *Xq, *Yq, *H, *NR;
   double* Xf;        // fused B+C: bath-local copy of the cached potential force after stage A
   double* V;         // fused B+C: noise(t+1) - c S(t+1), bath-local (written by the S(t+1) tiles)
-  const double* Y0n; // light stage A: K0 p_t, written by the previous fused step's CH_NXT tiles
   const int32_t* inv;
   double c;
   int64_t vs;
@@ -261,7 +257,6 @@ struct ChSfin {
   double* S;
   const double* noise;  // fused B+C: V = noise(t+1) - c S(t+1) into V (nullptr: not fused)
   double* V;
-  const double* Y1n;    // light stage A: K_1 p_t, written by the previous fused step's CH_NXT tiles
   double c;
   const double* lvl[MAXLVL];
   int32_t lvl_ld[MAXLVL];
@@ -281,7 +276,6 @@ struct ChTile {
   double* dst;       // CH_RAW: row 0, column 0 of the tile in parity buffer 0
   int32_t ldd;
   int32_t first;     // CH_DOF: the tile that zeroes the other-parity cache words
-  int32_t lite;      // light stage A (no products): K0 p_t / K_1 p_t / Kq q_t read from Y0n / Y1n / Yq
   int32_t ntw[CH_NW]; // tasks of wave w (32-bit: read with scalar loads)
   int32_t ob[CH_NOUT + 1];  // output o adds LDS slots [ob[o], ob[o+1]); outputs: Y of tile bath u
                             // (u < CH_TB), YQ of tile bath u (CH_TB + u), YD (2 CH_TB);
