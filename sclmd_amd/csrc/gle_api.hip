@@ -203,12 +203,6 @@ struct gle_handle {
   hipStream_t bg[NBG] = {};
   hipEvent_t ev_step = nullptr;    // end of the latest block-boundary step on the main stream
   hipEvent_t ev_bg[NBG] = {};      // join points of the background streams
-  // near-field partials on a side stream (off the chain's critical path): the partials of target
-  // t+2 run beside stages A(t) and BC(t); A(t+1) waits for them
-  bool side_on = false;
-  hipStream_t side = nullptr;
-  hipEvent_t ev_side_in = nullptr, ev_side_out = nullptr, ev_side_join = nullptr;
-  Chain chRaw;
   std::vector<void*> allocs;
   size_t dev_bytes = 0;
   // profiling of the dominant contraction
@@ -693,16 +687,11 @@ void join_bg(gle_handle* h) {
       hipEventRecord(h->ev_bg[i], h->bg[i]);
       hipStreamWaitEvent(h->stream, h->ev_bg[i], 0);
     }
-  if (h->side) {
-    hipEventRecord(h->ev_side_join, h->side);
-    hipStreamWaitEvent(h->stream, h->ev_side_join, 0);
-  }
 }
 
 int sync_bg(gle_handle* h) {
   for (int i = 0; i < gle_handle::NBG; ++i)
     if (h->bg[i]) HIPCHK(h, hipStreamSynchronize(h->bg[i]));
-  if (h->side) HIPCHK(h, hipStreamSynchronize(h->side));
   return GLE_OK;
 }
 
@@ -1312,16 +1301,7 @@ int plan_chain(gle_handle* h) {
         }
       }
   }
-  // near-field partial tiles (chains A and C / BC, alternating items; with the side stream all in
-  // chRaw, launched beside the chain every step)
-  h->chRaw.tiles.clear();
-  h->chRaw.flops = 0;
-  h->chRaw.nw = 4;
-  h->chRaw.lds = 0;
-  {
-    const char* e = gle_env("GLE_NEAR_SIDE");
-    h->side_on = e && atoi(e) != 0;
-  }
+  // near-field partial tiles (chains B and C, alternating items)
   for (int j = 0; j < nb; ++j) {
     Bath& b = h->baths[j];
     if (b.nqn == 0) continue;
@@ -1350,9 +1330,7 @@ int plan_chain(gle_handle* h) {
           const int ns = (int)strlen(near_in);
           const char st = near_in[q % std::max(1, ns)];
           Chain* pair[3] = {nullptr, nullptr, nullptr};
-          if (h->side_on) {
-            pair[0] = &h->chRaw;
-          } else if (st == 'A') {
+          if (st == 'A') {
             pair[0] = &h->chA[0];
             pair[1] = &h->chA[1];
           } else if (st == 'B') {
@@ -1361,7 +1339,7 @@ int plan_chain(gle_handle* h) {
           } else {
             pair[0] = &h->chC;
           }
-          if (!h->side_on && st != 'A' && h->fuse_bc) pair[2] = &h->chBC;  // the fused launch replaces B and C
+          if (st != 'A' && h->fuse_bc) pair[2] = &h->chBC;  // the fused launch replaces B and C
           for (Chain* c : pair) {
             if (!c) continue;
             ChTile Tc = T;
@@ -1376,7 +1354,7 @@ int plan_chain(gle_handle* h) {
         }
     }
   }
-  for (Chain* c : {&h->chA[0], &h->chA[1], &h->chB[0], &h->chB[1], &h->chC, &h->chNear, &h->chBC, &h->chRaw}) {
+  for (Chain* c : {&h->chA[0], &h->chA[1], &h->chB[0], &h->chB[1], &h->chC, &h->chNear, &h->chBC}) {
     int rc = upload_chain(h, *c);
     if (rc) return rc;
   }
@@ -1967,16 +1945,6 @@ int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
   }
   const bool need_pot = (fpot_host_T == nullptr) && !h->pot_cache_exact;
   const StepArgs ta = step_args(h);
-  if (h->side_on && !h->chRaw.tiles.empty()) {
-    // A(t) reads the partials of target t+1 (issued at step t-1); p_t is in the near ring, so the
-    // partials of target t+2 can start now and run beside A(t) and BC(t)
-    HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_side_out, 0));
-    HIPCHK(h, hipEventRecord(h->ev_side_in, h->stream));
-    HIPCHK(h, hipStreamWaitEvent(h->side, h->ev_side_in, 0));
-    launch_chain(1, h->chRaw.nw, h->ch_drn, h->chRaw.lds, h->chRaw.d, (int)h->chRaw.tiles.size(), h->d_sd, ta, 0,
-                 h->side);
-    HIPCHK(h, hipEventRecord(h->ev_side_out, h->side));
-  }
   if (fpot_host_T)
     HIPCHK(h, hipMemcpyAsync(h->d_Fc, fpot_host_T, (size_t)h->nph * h->B * 8, hipMemcpyHostToDevice, h->stream));
   run_chain(h, 0, h->chA[need_pot ? 1 : 0], ta, (need_pot ? 1 : 0) | (fpot_host_T ? 0 : 2), h->levels.empty());
@@ -2111,13 +2079,6 @@ int gle_create(const gle_config* cfg, gle_handle** out) {
     }
   }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_step, hipEventDisableTiming | hipEventReleaseToDevice);
-  if (e == hipSuccess) {
-    int lo = 0, hi = 0;
-    hipDeviceGetStreamPriorityRange(&lo, &hi);
-    e = hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, hi);
-    for (hipEvent_t* ev : {&h->ev_side_in, &h->ev_side_out, &h->ev_side_join})
-      if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming | hipEventReleaseToDevice);
-  }
   if (e != hipSuccess) {
     gle_destroy(h);
     return fail(nullptr, GLE_ERR_HIP, std::string("stream/event creation: ") + hipGetErrorString(e));
@@ -2217,9 +2178,6 @@ int gle_destroy(gle_handle* h) {
     for (auto e : lv.ev)
       if (e) hipEventDestroy(e);
   if (h->ev_step) hipEventDestroy(h->ev_step);
-  for (hipEvent_t e : {h->ev_side_in, h->ev_side_out, h->ev_side_join})
-    if (e) hipEventDestroy(e);
-  if (h->side) hipStreamDestroy(h->side);
   for (int i = 0; i < gle_handle::NBG; ++i) {
     if (h->ev_bg[i]) hipEventDestroy(h->ev_bg[i]);
     if (h->bg[i]) hipStreamDestroy(h->bg[i]);
