@@ -1432,7 +1432,9 @@ int freeze(gle_handle* h) {
     const bool last = P >= Pmax || 4 * P >= mlmax || (int)h->levels.size() == MAXLVL - 1;
     lv.lag1 = last ? mlmax : (int)(4 * P);
     const bool pow2 = (P & (P - 1)) == 0;
-    lv.spectral = spec_ok && pow2 && P >= (mode == GLE_FAR_SPECTRAL ? 2 : 8) && 2 * P <= 8192;
+    int pmin = mode == GLE_FAR_SPECTRAL ? 2 : 8;
+    if (const char* e = gle_env("GLE_SPEC_MIN")) pmin = std::max(2, atoi(e));
+    lv.spectral = spec_ok && pow2 && P >= pmin && 2 * P <= 8192;
     h->levels.push_back(lv);
     if (last) break;
   }

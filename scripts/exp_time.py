@@ -24,7 +24,8 @@ def measure(args, meta, dyn, baths):
     from sclmd_amd import _native as N
 
     B = args.ntraj
-    st = N.Stepper(meta["nph"], B, meta["nmd"], meta["dt"], 0, 0, "auto", 0)
+    st = N.Stepper(meta["nph"], B, meta["nmd"], meta["dt"], 0, int(os.environ.get("EXP_BLOCK_LEN", "0")), "auto",
+                   int(os.environ.get("EXP_MAX_BLOCK", "0")))
     try:
         for b in baths:
             if b.kind == "ebath":
@@ -92,10 +93,10 @@ def main():
 
     dyn, _, baths, meta = synthetic.junction(args.config, seed=1234, gmem_device=True)
     variants = [v for v in args.variants.split(";")] if args.variants else [""]
-    base = {k: v for k, v in os.environ.items() if k.startswith("GLE_")}
+    base = {k: v for k, v in os.environ.items() if k.startswith("GLE_") or k.startswith("EXP_")}
     for r in range(args.rounds):
         for v in variants:
-            for k in [k for k in os.environ if k.startswith("GLE_")]:
+            for k in [k for k in os.environ if k.startswith("GLE_") or k.startswith("EXP_")]:
                 del os.environ[k]
             env = dict(base)
             for kv in filter(None, v.split(",")):
