@@ -11,6 +11,7 @@ boxes differ by several percent; prints one JSON line per measurement.
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
@@ -99,7 +100,7 @@ def main():
             for k in [k for k in os.environ if k.startswith("GLE_") or k.startswith("EXP_")]:
                 del os.environ[k]
             env = dict(base)
-            for kv in filter(None, v.split(",")):
+            for kv in filter(None, re.split(r",(?=(?:GLE_|EXP_))", v)):
                 k, val = kv.split("=", 1)
                 env[k] = val
             os.environ.update(env)
