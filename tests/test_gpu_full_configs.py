@@ -1,7 +1,8 @@
 """The benched configurations themselves against the oracle (VERDICT r01 "benched but never tested").
 
 C3 as benched: 300-atom junction, 2 phonon baths nc = 300, ml = 1024, 64 trajectories with the
-spectral ladder plan bench.py runs (levels P = 4 ... 256, XCD-grouped split-K cgemm items), started
+spectral ladder plan bench.py runs (levels P = 8 ... 256 at the default first block length, and
+P = 4 ... 256 at block_len = 4; split-K cgemm items), started
 at an unaligned t0 from a random nonzero history, run 540 steps so that every level's blocks are
 computed from nonzero data (the P = 256 level fires at 256 and 512).  Reduced C5: three baths (two
 phonon baths and a biased electron bath with exim, zeta1, zeta2 != 0, nc = 96-99), ml = 1024, 32
@@ -29,14 +30,14 @@ def _obath(O, b, noise, dt, nmd):
     return O.Bath("ph", b.cids, b.kernel, noise, dt, nmd)
 
 
-def _run_vs_oracle(config, natom, B, check, t0=37, nst=540, nmd=1024, ml=1024, seed=1234):
+def _run_vs_oracle(config, natom, B, check, t0=37, nst=540, nmd=1024, ml=1024, seed=1234, block_len=0):
     from oracle import sclmd_oracle as O
     from sclmd_amd import _native as N
     from sclmd_amd import synthetic
 
     dyn, _, baths, meta = synthetic.junction(config, natom=natom, ml=ml, nmd=nmd, seed=seed)
     nph, dt = meta["nph"], meta["dt"]
-    st = N.Stepper(nph, B, nmd, dt, 0, 0, "auto", 0)
+    st = N.Stepper(nph, B, nmd, dt, 0, block_len, "auto", 0)
     try:
         for b in baths:
             if b.kind == "ebath":
@@ -67,8 +68,10 @@ def _run_vs_oracle(config, natom, B, check, t0=37, nst=540, nmd=1024, ml=1024, s
     finally:
         st.close()
     assert t == t0 + nst
-    # every ladder level computed blocks inside the run (P = 4 ... 256 at ml = 1024)
-    assert [P for P, _ in levels] == [4, 8, 16, 32, 64, 128, 256], levels
+    # every ladder level computed blocks inside the run (P = P0 ... 256 at ml = 1024)
+    P0 = info["block_len"]
+    assert P0 == (block_len or 8), info
+    assert [P for P, _ in levels] == [P0 << k for k in range((256 // P0).bit_length())], levels
     assert all(bl >= 1.0 for _, bl in levels), levels
     ob = [_obath(O, b, noise[i], dt, nmd) for i, b in enumerate(baths)]
     sim = O.GLEBatch(nph, dt, nmd, ob, dyn, ntr=len(check))
@@ -86,8 +89,9 @@ def _run_vs_oracle(config, natom, B, check, t0=37, nst=540, nmd=1024, ml=1024, s
     return sim
 
 
-def test_c3_bench_plan_vs_oracle():
-    _run_vs_oracle("C3", None, 64, [0, 29, 63])
+@pytest.mark.parametrize("block_len", [0, 4])
+def test_c3_bench_plan_vs_oracle(block_len):
+    _run_vs_oracle("C3", None, 64, [0, 29, 63], block_len=block_len)
 
 
 def test_c5_reduced_biased_vs_oracle():
