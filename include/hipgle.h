@@ -235,6 +235,10 @@ int gle_profile(gle_handle* h, int32_t enable);
  * launches since profiling was enabled (flops/bytes per SURVEY.md section 8d). */
 int gle_profile_read(gle_handle* h, int64_t* nlaunch, double* total_ms, double* flops,
                      double* bytes);
+/* The same launches timed on the device: first workgroup start to last workgroup end of each
+ * launch (s_memrealtime, 100 MHz), i.e. the kernel duration a kernel trace reports; the HIP events
+ * of gle_profile_read also include each launch's wait for free compute units. */
+int gle_profile_read_device(gle_handle* h, int64_t* nlaunch, double* total_ms);
 /* Planner summary of the current configuration: block length L, far-field work items, bytes of
  * device memory in use, far-field mode actually chosen. */
 int gle_plan_info(gle_handle* h, int64_t* block_len, int64_t* far_items, int64_t* device_bytes,

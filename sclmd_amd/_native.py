@@ -27,7 +27,7 @@ EXPORTS = [
     "gle_set_history", "gle_get_history", "gle_get_force", "gle_set_noise", "gle_get_noise",
     "gle_noise_factors", "gle_noise_generate", "gle_step_begin", "gle_step_end", "gle_run",
     "gle_sync", "gle_get_current", "gle_get_energy", "gle_current_sums", "gle_profile",
-    "gle_profile_read", "gle_plan_info", "gle_add_bath_gmem", "gle_get_kernel", "gle_gamt",
+    "gle_profile_read", "gle_profile_read_device", "gle_plan_info", "gle_add_bath_gmem", "gle_get_kernel", "gle_gamt",
     "gle_profile_levels", "gle_step_work", "gle_reduce_current", "gle_comm_unique_id", "gle_comm_init",
     "gle_comm_destroy", "gle_record", "gle_record_zero", "gle_get_record", "gle_get_record_history",
     "gle_power_spectrum", "gle_set_record", "gle_set_record_history", "gle_noise_stream_begin",
@@ -86,6 +86,7 @@ _SIGS = {
     "gle_current_sums": (ctypes.c_int, [_P, _D]),
     "gle_profile": (ctypes.c_int, [_P, ctypes.c_int32]),
     "gle_profile_read": (ctypes.c_int, [_P, _I64, _D, _D, _D]),
+    "gle_profile_read_device": (ctypes.c_int, [_P, _I64, _D]),
     "gle_plan_info": (ctypes.c_int, [_P, _I64, _I64, _I64, ctypes.POINTER(ctypes.c_int32)]),
     "gle_profile_levels": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32),
                                           ctypes.POINTER(ctypes.c_int32), _D]),
@@ -447,7 +448,12 @@ class Stepper:
         ms, fl, by = ctypes.c_double(0), ctypes.c_double(0), ctypes.c_double(0)
         self._chk(self.lib.gle_profile_read(self.h, ctypes.byref(n), ctypes.byref(ms),
                                             ctypes.byref(fl), ctypes.byref(by)), "gle_profile_read")
-        return {"launches": int(n.value), "ms": ms.value, "flops": fl.value, "bytes": by.value}
+        out = {"launches": int(n.value), "ms": ms.value, "flops": fl.value, "bytes": by.value}
+        nd, msd = ctypes.c_int64(0), ctypes.c_double(0)
+        self._chk(self.lib.gle_profile_read_device(self.h, ctypes.byref(nd), ctypes.byref(msd)),
+                  "gle_profile_read_device")
+        out["launches_device"], out["ms_device"] = int(nd.value), msd.value
+        return out
 
     def plan_info(self):
         a, b, c = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int64(0)

@@ -170,6 +170,11 @@ struct gle_handle {
   double* d_zero = nullptr;            // zero row (chain S(t+1) tiles' unused level slots)
   bool dbg_no_ladder = false;  // GLE_DBG_NO_LADDER: skip the ladder blocks (timing experiments only)
   int bg_grid = 0;             // GLE_BG_GRID: cap of the far-field GEMM grid (grid-stride over items)
+  // device timestamps of the profiled far-field launches ([start, end] pairs, s_memrealtime)
+  unsigned long long* d_tst = nullptr;
+  size_t tst_cap = 4096, tst_used = 0;
+  int64_t prof_n_dev = 0;
+  double prof_ms_dev = 0.0;
   int piece_g = 1;              // steps per piece slot (P0 once planned; GLE_PIECE_STEP=1: every step)
   bool prof_ev = false;         // gle_profile: HIP events around the dominant kernel's launches
   bool bg_serial = false;      // GLE_BG_SERIAL=1: ladder pieces on the main stream (time-sliced, experiment)
@@ -627,6 +632,17 @@ StepArgs step_args(const gle_handle* h, int64_t t) {
 }
 StepArgs step_args(const gle_handle* h) { return step_args(h, h->t); }
 
+// [start, end] pairs ready for atomicMin / atomicMax
+void reset_tst(gle_handle* h, size_t n, hipStream_t s) {
+  std::vector<unsigned long long> init(2 * n);
+  for (size_t i = 0; i < n; ++i) {
+    init[2 * i] = ~0ull;
+    init[2 * i + 1] = 0ull;
+  }
+  hipMemcpyAsync(h->d_tst, init.data(), init.size() * 8, hipMemcpyHostToDevice, s);
+  hipStreamSynchronize(s);
+}
+
 void drain_profile(gle_handle* h) {
   hipStreamSynchronize(h->stream);
   for (int i = 0; i < gle_handle::NBG; ++i)
@@ -637,6 +653,17 @@ void drain_profile(gle_handle* h) {
     h->prof_ms += ms;
   }
   h->ev_used = 0;
+  if (h->d_tst && h->tst_used > 0) {
+    std::vector<unsigned long long> v(2 * h->tst_used);
+    hipMemcpy(v.data(), h->d_tst, v.size() * 8, hipMemcpyDeviceToHost);
+    for (size_t i = 0; i < h->tst_used; ++i)
+      if (v[2 * i + 1] >= v[2 * i] && v[2 * i] != ~0ull) {
+        h->prof_ms_dev += (double)(v[2 * i + 1] - v[2 * i]) * 1e-5;  // 100 MHz ticks -> ms
+        h->prof_n_dev += 1;
+      }
+    reset_tst(h, h->tst_used, h->stream);
+    h->tst_used = 0;
+  }
 }
 
 // Launch one op on stream s; profile: HIP events around the contraction launch (the dominant
@@ -1796,14 +1823,16 @@ int launch_level_pieces(gle_handle* h, Level& lv, int64_t k, hipStream_t s, bool
       const int64_t c0 = n * (j - 1) / lv.ncg_chunk, c1 = n * j / lv.ncg_chunk;
       if (c1 <= c0) continue;
       hipEvent_t e1 = nullptr;
+      unsigned long long* ts = nullptr;
       if (h->prof_ev) {
-        if (h->ev_used + 2 > h->ev.size()) drain_profile(h);
+        if (h->ev_used + 2 > h->ev.size() || h->tst_used >= h->tst_cap) drain_profile(h);
         hipEventRecord(h->ev[h->ev_used], s);
         e1 = h->ev[h->ev_used + 1];
         h->ev_used += 2;
+        if (h->d_tst && !priming) ts = h->d_tst + 2 * h->tst_used++;
       }
       if (priming || !(h->dbg_skip & 1))
-        launch_cgemm(lv.cg_rn, lv.d_cg + c0, (int)(c1 - c0), T / lv.P, s, priming ? 0 : h->bg_grid);
+        launch_cgemm(lv.cg_rn, lv.d_cg + c0, (int)(c1 - c0), T / lv.P, s, priming ? 0 : h->bg_grid, ts);
       if (h->prof && !priming) h->prof_blocks[li] += (double)(c1 - c0) / (double)n;
       if (e1) {
         hipEventRecord(e1, s);
@@ -2893,6 +2922,18 @@ int gle_profile(gle_handle* h, int32_t enable) {
     h->ev.resize(4096);
     for (auto& e : h->ev) HIPCHK(h, hipEventCreate(&e));
   }
+  if ((enable & GLE_PROFILE_EVENTS) && !h->d_tst) {
+    int rc = dalloc_n(h, &h->d_tst, 2 * h->tst_cap);
+    if (rc) return rc;
+    reset_tst(h, h->tst_cap, h->stream);
+  }
+  if (h->d_tst && h->tst_used > 0) {
+    HIPCHK(h, hipDeviceSynchronize());
+    reset_tst(h, h->tst_used, h->stream);
+  }
+  h->tst_used = 0;
+  h->prof_n_dev = 0;
+  h->prof_ms_dev = 0.0;
   h->prof = enable != 0;
   h->prof_ev = (enable & GLE_PROFILE_EVENTS) != 0;
   h->ev_used = 0;
@@ -2911,6 +2952,16 @@ int gle_profile_read(gle_handle* h, int64_t* nlaunch, double* total_ms, double* 
   if (total_ms) *total_ms = h->prof_ms;
   if (flops) *flops = h->prof_flops;
   if (bytes) *bytes = h->prof_bytes;
+  return GLE_OK;
+}
+
+int gle_profile_read_device(gle_handle* h, int64_t* nlaunch, double* total_ms) {
+  if (!h) return GLE_ERR_ARG;
+  hipSetDevice(h->cfg.device);
+  drain_profile(h);
+  HIPCHK(h, hipGetLastError());
+  if (nlaunch) *nlaunch = h->prof_n_dev;
+  if (total_ms) *total_ms = h->prof_ms_dev;
   return GLE_OK;
 }
 

@@ -314,7 +314,10 @@ void launch_near_fill(const double* H, int64_t ldh, int R, int B, int ncp, doubl
 void launch_ring_copy(double* H, int64_t ldh, int R, int B, int nc, int64_t tau0, int nt, double* buf,
                       int dir, hipStream_t s);
 void launch_contract_cplx(int rn, const CItem* items, int nitems, StepArgs ta, hipStream_t s);
-void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStream_t s, int max_grid = 0);
+// ts (profiling, may be null): [0] <- min over workgroups of the start, [1] <- max of the end
+// (s_memrealtime, 100 MHz): the launch's kernel duration as a kernel trace reports it
+void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStream_t s, int max_grid = 0,
+                  unsigned long long* ts = nullptr);
 void launch_khat_pack(const double* Kf, int ml, int nks_k, double* khat, int P, int m0, int M,
                       int nc, int nrt2, int nks2, const double* cstab, int cstride, hipStream_t s);
 int launch_seg_fft(const double* H, int64_t ldh, int R, int B, int nc, int ncp, int P, int64_t T,

@@ -987,24 +987,30 @@ __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, doubl
 // each fetching the window into a different XCD.
 template <int RN, int KC, int DBG = 0>
 __global__ __launch_bounds__(256, KC <= 4 ? 3 : 2) void cgemm_kernel(const CgItem* __restrict__ items, int nitems, int64_t tseg,
-                                                       int xcd) {
+                                                       int xcd, unsigned long long* ts) {
   __shared__ double xs[2][4 * KC * CG_LD];
+  if (ts && threadIdx.x == 0) atomicMin(ts, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   if (xcd) {
     const int per = gridDim.x >> 3;
     const int item = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
     if (item < nitems) cgemm_item<RN, KC, DBG>(items[item], tseg, xs);
-    return;
+  } else {
+    for (int item = blockIdx.x; item < nitems; item += gridDim.x) {
+      const CgItem it = items[item];
+      cgemm_item<RN, KC, DBG>(it, tseg, xs);
+      __syncthreads();
+    }
   }
-  for (int item = blockIdx.x; item < nitems; item += gridDim.x) {
-    const CgItem it = items[item];
-    cgemm_item<RN, KC, DBG>(it, tseg, xs);
+  if (ts) {  // launch-uniform
     __syncthreads();
+    if (threadIdx.x == 0) atomicMax(ts + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   }
 }
 static int g_cg_xcd = -1;  // GLE_CG_XCD=0 switches the XCD grouping off (experiment switch)
 static int g_cg_dbg = 0;
 static int g_cg_kc = 0;    // k-steps per LDS chunk: 4 (159 VGPRs, 3 waves/SIMD; 23.9 vs 21.6 TF/s in situ), GLE_CG_KC=8: 8
-void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStream_t s, int max_grid) {
+void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStream_t s, int max_grid,
+                  unsigned long long* ts) {
   if (nitems <= 0) return;
   GLE_BOUNDS_SYNC();
   if (g_cg_xcd < 0) {
@@ -1029,26 +1035,26 @@ void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStre
   const int grid = capped ? max_grid : (xcd ? (nitems + 7) / 8 * 8 : nitems);
 #ifdef GLE_EXPERIMENTS
   if (g_cg_dbg && rn == 4 && g_cg_kc == 4) {  // GLE_CG_DBG timing experiments (results invalid)
-    if (g_cg_dbg == 1) cgemm_kernel<4, 4, 1><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd);
-    else if (g_cg_dbg == 2) cgemm_kernel<4, 4, 2><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd);
-    else if (g_cg_dbg == 3) cgemm_kernel<4, 4, 3><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd);
-    else if (g_cg_dbg == 4) cgemm_kernel<4, 4, 4><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd);
-    else cgemm_kernel<4, 4, 7><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd);
+    if (g_cg_dbg == 1) cgemm_kernel<4, 4, 1><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts);
+    else if (g_cg_dbg == 2) cgemm_kernel<4, 4, 2><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts);
+    else if (g_cg_dbg == 3) cgemm_kernel<4, 4, 3><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts);
+    else if (g_cg_dbg == 4) cgemm_kernel<4, 4, 4><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts);
+    else cgemm_kernel<4, 4, 7><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts);
     return;
   }
 #endif
   if (g_cg_kc == 4) {
     switch (rn) {
-      case 1: cgemm_kernel<1, 4><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd); break;
-      case 2: cgemm_kernel<2, 4><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd); break;
-      default: cgemm_kernel<4, 4><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd); break;
+      case 1: cgemm_kernel<1, 4><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts); break;
+      case 2: cgemm_kernel<2, 4><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts); break;
+      default: cgemm_kernel<4, 4><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts); break;
     }
     return;
   }
   switch (rn) {
-    case 1: cgemm_kernel<1, CG_KC><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd); break;
-    case 2: cgemm_kernel<2, CG_KC><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd); break;
-    default: cgemm_kernel<4, CG_KC><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd); break;
+    case 1: cgemm_kernel<1, CG_KC><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts); break;
+    case 2: cgemm_kernel<2, CG_KC><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts); break;
+    default: cgemm_kernel<4, CG_KC><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts); break;
   }
 }
 
