@@ -196,7 +196,7 @@ struct gle_handle {
   Chain chA[2], chB[2], chC, chNear;  // [with dyn.q]; chNear: all near-field partial tiles (priming)
   Chain chBC;                          // stages B + C fused (harmonic force, disjoint baths)
   bool fuse_bc = false;
-  int ch_nw[3] = {4, 8, 4};            // chain workgroup waves per stage
+  int ch_nw[3] = {4, 4, 4};            // chain workgroup waves per stage (A, B / fused BC, C)
   int ch_drn = 1;                      // DOF-tile 16-column MFMA tiles
   int P0 = 1;          // first level block; near field = lags [1, 2 P0)
   int near_end = 1;
@@ -891,7 +891,7 @@ int plan_chain(gle_handle* h) {
   const int nb = (int)h->baths.size();
   const int ntile = h->ndblk;
   if (const char* e = gle_env("GLE_CHAIN_NW")) {
-    int v[3] = {4, 8, 4};
+    int v[3] = {4, 4, 4};
     sscanf(e, "%d,%d,%d", &v[0], &v[1], &v[2]);
     for (int i = 0; i < 3; ++i) h->ch_nw[i] = v[i] >= 16 ? 16 : (v[i] >= 8 ? 8 : 4);
   }
@@ -1687,7 +1687,9 @@ int freeze(gle_handle* h) {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, h->cfg.device) == hipSuccess) ncu = prop.multiProcessorCount;
         const int nslot = std::max(1, lv.P / h->P0);
-        double per_cu = 2.0;  // GLE_CG_PER_CU: workgroups per CU per chunk (experiment switch)
+        // workgroups per CU per cgemm chunk (GLE_CG_PER_CU): with 4-wave fused-stage tiles,
+        // chunks of ~1 workgroup per CU measured 53.3 vs 55.3 us/step at C3 (2 per CU before)
+        double per_cu = 1.0;
         if (const char* e = gle_env("GLE_CG_PER_CU")) per_cu = std::max(0.25, atof(e));
         const double want = (double)lv.cg.size() / (per_cu * ncu);
         const int64_t nch = gle_env("GLE_CG_CEIL") ? (int64_t)std::ceil(want - 1e-9) : (int64_t)want;
