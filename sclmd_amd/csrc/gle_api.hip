@@ -196,7 +196,8 @@ struct gle_handle {
   Chain chA[2], chB[2], chC, chNear;  // [with dyn.q]; chNear: all near-field partial tiles (priming)
   Chain chBC;                          // stages B + C fused (harmonic force, disjoint baths)
   bool fuse_bc = false;
-  int ch_nw[3] = {4, 4, 4};            // chain workgroup waves per stage (A, B / fused BC, C)
+  int ch_nw[3] = {4, 8, 4};            // chain workgroup waves per stage (A, B / fused BC, C)
+  bool small_baths = false;            // every bath has nc <= 512 (the chain is latency-bound)
   int ch_drn = 1;                      // DOF-tile 16-column MFMA tiles
   int P0 = 1;          // first level block; near field = lags [1, 2 P0)
   int near_end = 1;
@@ -891,7 +892,7 @@ int plan_chain(gle_handle* h) {
   const int nb = (int)h->baths.size();
   const int ntile = h->ndblk;
   if (const char* e = gle_env("GLE_CHAIN_NW")) {
-    int v[3] = {4, 4, 4};
+    int v[3] = {4, 8, 4};
     sscanf(e, "%d,%d,%d", &v[0], &v[1], &v[2]);
     for (int i = 0; i < 3; ++i) h->ch_nw[i] = v[i] >= 16 ? 16 : (v[i] >= 8 ? 8 : 4);
   }
@@ -1437,7 +1438,11 @@ int freeze(gle_handle* h) {
   // -14 % per step), 4 for the larger baths (C5: +4 % at 8)
   int ncmax = 0;
   for (auto& b : h->baths) ncmax = std::max(ncmax, b.nc);
-  const int P0 = h->cfg.block_len > 0 ? h->cfg.block_len : (ncmax <= 512 ? 8 : 4);
+  h->small_baths = ncmax <= 512;
+  const int P0 = h->cfg.block_len > 0 ? h->cfg.block_len : (h->small_baths ? 8 : 4);
+  // fused-stage tile waves: 4 when the chain is latency-bound (C3: 53.3 vs 55.3 us/step with the
+  // 1-workgroup-per-CU far-field chunks below), 8 for large baths (C5: 447 vs ~410 us at 4)
+  h->ch_nw[1] = h->small_baths ? 4 : 8;
   int Pmax;
   if (h->cfg.max_block > 0) {
     Pmax = std::max(P0, h->cfg.max_block);
@@ -1687,9 +1692,10 @@ int freeze(gle_handle* h) {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, h->cfg.device) == hipSuccess) ncu = prop.multiProcessorCount;
         const int nslot = std::max(1, lv.P / h->P0);
-        // workgroups per CU per cgemm chunk (GLE_CG_PER_CU): with 4-wave fused-stage tiles,
-        // chunks of ~1 workgroup per CU measured 53.3 vs 55.3 us/step at C3 (2 per CU before)
-        double per_cu = 1.0;
+        // workgroups per CU per cgemm chunk (GLE_CG_PER_CU): with small baths and 4-wave fused
+        // tiles, chunks of ~1 workgroup per CU (53.3 vs 55.3 us/step at C3; the chain finds slots
+        // sooner, the far-field launches run at a lower MFMA occupancy); 2 per CU for large baths
+        double per_cu = h->small_baths ? 1.0 : 2.0;
         if (const char* e = gle_env("GLE_CG_PER_CU")) per_cu = std::max(0.25, atof(e));
         const double want = (double)lv.cg.size() / (per_cu * ncu);
         const int64_t nch = gle_env("GLE_CG_CEIL") ? (int64_t)std::ceil(want - 1e-9) : (int64_t)want;
