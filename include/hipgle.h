@@ -112,7 +112,10 @@ int gle_get_kernel(gle_handle* h, int32_t bath, int64_t i0, int64_t n, double* o
 int gle_gamt(int32_t device, int64_t ml, int64_t ngw, int64_t nel, const double* W, const double* G,
              double* out);
 /* md.setDyn (md.py:250-292): harmonic potential force -dyn.q used when no host force is given
- * (md.potforce, md.py:466-467).  dyn [nph][nph] as already processed by setDyn. */
+ * (md.potforce, md.py:466-467).  dyn [nph][nph] as already processed by setDyn.  setDyn's
+ * U diag(w^2) U^T reconstruction leaves roundoff in the entries the matrix does not couple; the
+ * device copy drops every entry with |d_ij| <= 16 * 2^-52 * max_j |d_ij| (its sparsity pattern
+ * then stays the physical one; the dropped part is at the dense product's own rounding level). */
 int gle_set_dyn(gle_handle* h, const double* dyn);
 /* md.AddConstr (md.py:189) flattened: the DOF indices ApplyConstraint zeroes (md.py:782-794) */
 int gle_set_constraint(gle_handle* h, const int64_t* dofs, int64_t n);

@@ -155,7 +155,8 @@ struct gle_handle {
   bool has_dyn = false;
   int dyn_nrt = 0, dyn_nks = 0;
   double* d_dyn = nullptr;
-  std::vector<double> dyn_h;   // host copy [nph][nph]
+  std::vector<double> dyn_h;   // host copy [nph][nph] (roundoff entries dropped, gle_set_dyn)
+  int64_t dyn_dropped = 0;     // entries gle_set_dyn dropped as eigen-reconstruction roundoff
   double* d_dynd = nullptr;    // block-sparse DOF-tile fragments of dyn
   std::vector<std::vector<std::pair<int, int>>> dyn_rng;  // per DOF tile: (first k-step, count)
   std::vector<int64_t> dyn_tofs;
@@ -2441,8 +2442,26 @@ int gle_set_dyn(gle_handle* h, const double* dyn) {
   hipSetDevice(h->cfg.device);
   h->dyn_nrt = (int)((h->nph + 15) / 16);
   h->dyn_nks = (int)(h->nphp / 4);
+  // md.setDyn stores U diag(w^2) U^T (md.py:264-292): its eigen-reconstruction leaves roundoff
+  // (<= ~10 eps of the row's largest entry at C3 / C5) in every entry the dynamical matrix does not
+  // couple, so the block-sparse device copy would turn dense.  Entries at or below DYN_DROP_EPS
+  // unit roundoffs of their row's largest magnitude are dropped: per row the dropped part is at
+  // most nph * 16 eps * max|d_i.| * max|q|, the order of the dense product's own rounding bound.
+  constexpr double DYN_DROP_EPS = 16.0;
   h->dyn_h.assign(dyn, dyn + h->nph * h->nph);
-  std::vector<double> f = pack_frags(dyn, 1, h->nph, h->nph, h->dyn_nrt, h->dyn_nks);
+  h->dyn_dropped = 0;
+  for (int64_t i = 0; i < h->nph; ++i) {
+    double* row = &h->dyn_h[(size_t)(i * h->nph)];
+    double mx = 0.0;
+    for (int64_t j = 0; j < h->nph; ++j) mx = std::max(mx, std::fabs(row[j]));
+    const double thr = DYN_DROP_EPS * 0x1p-52 * mx;
+    for (int64_t j = 0; j < h->nph; ++j)
+      if (row[j] != 0.0 && std::fabs(row[j]) <= thr) {
+        row[j] = 0.0;
+        ++h->dyn_dropped;
+      }
+  }
+  std::vector<double> f = pack_frags(h->dyn_h.data(), 1, h->nph, h->nph, h->dyn_nrt, h->dyn_nks);
   int rc = dalloc_n(h, &h->d_dyn, f.size());
   if (!rc) rc = upload(h, h->d_dyn, f.data(), f.size() * 8);
   if (rc) return rc;

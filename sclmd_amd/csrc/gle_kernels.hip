@@ -862,8 +862,21 @@ typedef const __attribute__((address_space(1))) double gdbl;
 #define CG_ALOAD(p) (*(p))
 #endif
 
-template <int RN, int KC, int DBG = 0>
+// Prefetch rings.  A fragments (HBM, the streamed operand) go AD chunks ahead of the MFMAs into a
+// ring of AD + 1 register chunks; X (segment ring, L2/MALL) goes XD chunks ahead into a ring of XD
+// register chunks and from there into the other LDS buffer at the end of the chunk before its use.
+// With one workgroup per CU (one wave per SIMD, the far-field chunking beside the chain) nothing
+// else on the SIMD hides a load: the rings have to cover an HBM round trip by themselves.
+#ifndef CG_AD
+#define CG_AD 2
+#endif
+#ifndef CG_XD
+#define CG_XD 1
+#endif
+template <int RN, int KC, int AD, int XD, int DBG = 0>
 __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, double (&xs)[2][4 * KC * CG_LD]) {
+  static_assert(XD == 1 || XD == 2, "X ring of one or two chunks");
+  static_assert((AD + 1) % XD == 0, "the A ring period carries the X ring's");
   constexpr int NT = 16 * RN;
   constexpr int XPT = 4 * KC * NT / 256;  // X doubles per thread per chunk
   constexpr int TPR = NT / XPT;              // staging threads per X row
@@ -879,12 +892,9 @@ __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, doubl
   gdbl* Aw = (gdbl*)(it.A + (int64_t)(active ? wave : 0) * it.a_rt + (int64_t)it.s0 * 64 + lane);
   const int xr = tid / TPR, xc = (tid % TPR) * XPT;
   const int tbase = (int)pmod(tseg, it.Rseg);  // ring slot of segment tseg (32-bit from here on)
-  // Prefetch depth: A fragments (HBM, the streamed operand) 2 chunks ahead of the MFMAs; X
-  // (segment ring, L2/MALL) into registers one chunk ahead, then into the other LDS buffer.  One
-  // chunk (8 k-steps, 8 RN MFMAs per wave) is too short to cover an HBM round trip on its own.
   // Loads are branch-free (clamped address, zero by multiplication): a branch around a load makes
   // the waitcnt pass drain every load in flight.
-  double xv[XPT], a0[KC], a1[KC], a2[KC];
+  double xv[XD][XPT], av[AD + 1][KC];
   d4 acc[RN];
 #pragma unroll
   for (int n = 0; n < RN; ++n) acc[n] = d4{0.0, 0.0, 0.0, 0.0};
@@ -925,42 +935,44 @@ __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, doubl
       AV[u] = (DBG & 1) ? 1e-3 * (s0_ + 1) : CG_ALOAD(&Aw[(int64_t)(s0_ < S ? s0_ : S - 1) * 64]); /* masked */ \
     }                                                                                                 \
   } while (0)
-  // chunk c: MFMAs on A chunk c (registers) and X chunk c (LDS buffer c&1); chunk c+2's A goes
-  // into the registers chunk c-1 used, chunk c+1's X into the other LDS buffer.  The A register
-  // roles rotate with period 3, spelled out so every role is static.
-#define CG_STEP(c, ACUR, ANEXT)                                                                       \
-  do {                                                                                                \
-    const int c_ = (c);                                                                               \
-    /* X first: vmcnt retires in order, so the X store at the end of the step then waits for X  */ \
-    /* (and older loads) only, while chunk c+2's A stays in flight                              */ \
-    /* unconditional (clamped) loads: paths that skip a load confuse the waitcnt pass          */ \
-    if (!(DBG & 4)) CG_LOAD_X(c_ + 1, xv);                                                            \
-    CG_LOAD_A(c_ + 2, ANEXT);                                                                         \
-    const double* xb_ = xs[c_ & 1] + brow * CG_LD + bcol;                                             \
-    _Pragma("unroll") for (int u = 0; u < KC; ++u) {                                               \
-      const double a_ = ACUR[u] * ((active && c_ * KC + u < S) ? 1.0 : 0.0);                       \
-      _Pragma("unroll") for (int n = 0; n < RN; ++n) acc[n] =                                         \
-          __builtin_amdgcn_mfma_f64_16x16x4f64(a_, (DBG & 2) ? a_ * (n + 1) : xb_[4 * u * CG_LD + 16 * n], \
-                                               acc[n], 0, 0, 0);                                      \
-    }                                                                                                 \
-    if (!(DBG & 4)) {                                                                                 \
-      CG_STORE_X(c_ + 1, (c_ & 1) ^ 1, xv);                                                           \
-      __syncthreads();                                                                                \
-    }                                                                                                 \
-  } while (0)
-  CG_LOAD_A(0, a0);
-  CG_LOAD_A(1, a1);
-  CG_LOAD_X(0, xv);
-  CG_STORE_X(0, 0, xv);
+  // chunk c (ring position r = c mod (AD + 1), a compile-time constant inside the unrolled period):
+  // X chunk c + XD into the X ring, A chunk c + AD into the A registers chunk c - 1 used, MFMAs on
+  // A chunk c and the LDS buffer c & 1, then X chunk c + 1 into the other LDS buffer.  X is issued
+  // first: vmcnt retires in order, so the X store at the end waits for X (and older loads) only.
+  CG_LOAD_A(0, av[0]);
+  if (AD > 1) CG_LOAD_A(1, av[1 % (AD + 1)]);
+  if (AD > 2) CG_LOAD_A(2, av[2 % (AD + 1)]);
+  if (AD > 3) CG_LOAD_A(3, av[3 % (AD + 1)]);
+  if (AD > 4) CG_LOAD_A(4, av[4 % (AD + 1)]);
+  if (AD > 5) CG_LOAD_A(5, av[5 % (AD + 1)]);
+  if (AD > 6) CG_LOAD_A(6, av[6 % (AD + 1)]);
+  static_assert(AD <= 7, "prologue covers AD <= 7");
+  CG_LOAD_X(0, xv[0]);
+  if (XD > 1) CG_LOAD_X(1, xv[1 % XD]);
+  CG_STORE_X(0, 0, xv[0]);
   __syncthreads();
-  for (int c = 0; c < nch; c += 3) {
-    CG_STEP(c, a0, a2);
-    if (c + 1 >= nch) break;
-    CG_STEP(c + 1, a1, a0);
-    if (c + 2 >= nch) break;
-    CG_STEP(c + 2, a2, a1);
+  for (int c0 = 0; c0 < nch; c0 += AD + 1) {
+#pragma unroll
+    for (int r = 0; r <= AD; ++r) {
+      const int c = c0 + r;
+      if (c >= nch) break;
+      if (!(DBG & 4)) CG_LOAD_X(c + XD, xv[r % XD]);
+      CG_LOAD_A(c + AD, av[(r + AD) % (AD + 1)]);
+      const double* xb_ = xs[c & 1] + brow * CG_LD + bcol;
+#pragma unroll
+      for (int u = 0; u < KC; ++u) {
+        const double a_ = av[r][u] * ((active && c * KC + u < S) ? 1.0 : 0.0);
+#pragma unroll
+        for (int n = 0; n < RN; ++n)
+          acc[n] = __builtin_amdgcn_mfma_f64_16x16x4f64(a_, (DBG & 2) ? a_ * (n + 1) : xb_[4 * u * CG_LD + 16 * n],
+                                                        acc[n], 0, 0, 0);
+      }
+      if (!(DBG & 4)) {
+        CG_STORE_X(c + 1, (c & 1) ^ 1, xv[(r + 1) % XD]);
+        __syncthreads();
+      }
+    }
   }
-#undef CG_STEP
 #undef CG_LOAD_A
 #undef CG_STORE_X
 #undef CG_LOAD_X
@@ -985,7 +997,7 @@ __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, doubl
 // dispatch), so XCD b % 8 gets the contiguous item range [(b % 8) per, (b % 8 + 1) per): the row
 // groups of one (f, g) product, which read the same X window, then share that XCD's L2 instead of
 // each fetching the window into a different XCD.
-template <int RN, int KC, int DBG = 0>
+template <int RN, int KC, int AD = CG_AD, int XD = CG_XD, int DBG = 0>
 __global__ __launch_bounds__(256, KC <= 4 ? 3 : 2) void cgemm_kernel(const CgItem* __restrict__ items, int nitems, int64_t tseg,
                                                        int xcd, unsigned long long* ts) {
   __shared__ double xs[2][4 * KC * CG_LD];
@@ -993,11 +1005,11 @@ __global__ __launch_bounds__(256, KC <= 4 ? 3 : 2) void cgemm_kernel(const CgIte
   if (xcd) {
     const int per = gridDim.x >> 3;
     const int item = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
-    if (item < nitems) cgemm_item<RN, KC, DBG>(items[item], tseg, xs);
+    if (item < nitems) cgemm_item<RN, KC, AD, XD, DBG>(items[item], tseg, xs);
   } else {
     for (int item = blockIdx.x; item < nitems; item += gridDim.x) {
       const CgItem it = items[item];
-      cgemm_item<RN, KC, DBG>(it, tseg, xs);
+      cgemm_item<RN, KC, AD, XD, DBG>(it, tseg, xs);
       __syncthreads();
     }
   }
@@ -1009,6 +1021,7 @@ __global__ __launch_bounds__(256, KC <= 4 ? 3 : 2) void cgemm_kernel(const CgIte
 static int g_cg_xcd = -1;  // GLE_CG_XCD=0 switches the XCD grouping off (experiment switch)
 static int g_cg_dbg = 0;
 static int g_cg_kc = 0;    // k-steps per LDS chunk: 4 (159 VGPRs, 3 waves/SIMD; 23.9 vs 21.6 TF/s in situ), GLE_CG_KC=8: 8
+static int g_cg_ring = 0;  // GLE_CG_RING=AD*10+XD (experiment switch): prefetch ring depths
 void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStream_t s, int max_grid,
                   unsigned long long* ts) {
   if (nitems <= 0) return;
@@ -1021,6 +1034,10 @@ void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStre
     // 1: no K-hat loads, 2: no LDS operand reads, 4: no X staging / barrier; 3, 7: combinations
     const char* d = gle_env("GLE_CG_DBG");
     g_cg_dbg = d ? std::max(0, std::min(7, atoi(d))) : 0;
+  }
+  {  // re-read per launch: variants of one process (scripts/exp_time.py --variants) switch it
+    const char* r = gle_env("GLE_CG_RING");
+    g_cg_ring = r ? atoi(r) : 0;
   }
   // GLE_CG_LDS_PAD (bytes, experiment switch): unused dynamic LDS per workgroup, capping how many
   // far-field workgroups a CU holds so the per-step chain's workgroups find room beside them
@@ -1035,12 +1052,22 @@ void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStre
   const int grid = capped ? max_grid : (xcd ? (nitems + 7) / 8 * 8 : nitems);
 #ifdef GLE_EXPERIMENTS
   if (g_cg_dbg && rn == 4 && g_cg_kc == 4) {  // GLE_CG_DBG timing experiments (results invalid)
-    if (g_cg_dbg == 1) cgemm_kernel<4, 4, 1><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts);
-    else if (g_cg_dbg == 2) cgemm_kernel<4, 4, 2><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts);
-    else if (g_cg_dbg == 3) cgemm_kernel<4, 4, 3><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts);
-    else if (g_cg_dbg == 4) cgemm_kernel<4, 4, 4><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts);
-    else cgemm_kernel<4, 4, 7><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts);
+    if (g_cg_dbg == 1) cgemm_kernel<4, 4, CG_AD, CG_XD, 1><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts);
+    else if (g_cg_dbg == 2) cgemm_kernel<4, 4, CG_AD, CG_XD, 2><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts);
+    else if (g_cg_dbg == 3) cgemm_kernel<4, 4, CG_AD, CG_XD, 3><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts);
+    else if (g_cg_dbg == 4) cgemm_kernel<4, 4, CG_AD, CG_XD, 4><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts);
+    else cgemm_kernel<4, 4, CG_AD, CG_XD, 7><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts);
     return;
+  }
+  if (g_cg_ring && rn == 4 && g_cg_kc == 4) {  // prefetch-ring variants
+    switch (g_cg_ring) {
+      case 31: cgemm_kernel<4, 4, 3, 1><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts); return;
+      case 32: cgemm_kernel<4, 4, 3, 2><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts); return;
+      case 51: cgemm_kernel<4, 4, 5, 1><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts); return;
+      case 52: cgemm_kernel<4, 4, 5, 2><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts); return;
+      case 72: cgemm_kernel<4, 4, 7, 2><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts); return;
+      default: break;
+    }
   }
 #endif
   if (g_cg_kc == 4) {

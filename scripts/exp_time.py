@@ -62,6 +62,9 @@ def measure(args, meta, dyn, baths):
         st.run(args.steps)
         st.sync()
         el = time.perf_counter() - t0
+        prof = st.profile_read() if args.profile else None
+        if args.profile:
+            st.profile(False)
         reps = []
         for _ in range(args.short_reps):  # bench-like short windows: sync, K steps, sync
             st.run(37)
@@ -73,7 +76,12 @@ def measure(args, meta, dyn, baths):
         p, q, _ = st.get_state()
     finally:
         st.close()
-    return {"ms_per_step": el / args.steps * 1e3, "short_ms_per_step": el_short / max(args.short, 1) * 1e3,
+    extra = {}
+    if prof and prof.get("launches"):
+        ms = prof.get("ms_device") or prof["ms"]
+        extra = {"cgemm_launches": prof["launches"], "cgemm_avg_us": ms / prof["launches"] * 1e3,
+                 "cgemm_tflops": prof["flops"] / (ms * 1e-3) / 1e12}
+    return {**extra, "ms_per_step": el / args.steps * 1e3, "short_ms_per_step": el_short / max(args.short, 1) * 1e3,
             "aligned_short_ms_per_step": el_aligned / max(args.short, 1) * 1e3, "short_reps_ms": reps,
             "traj_steps_per_s": B * args.steps / el, "finite": bool(np.isfinite(p).all() and np.isfinite(q).all())}
 
