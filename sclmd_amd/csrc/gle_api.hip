@@ -156,7 +156,8 @@ struct gle_handle {
   int dyn_nrt = 0, dyn_nks = 0;
   double* d_dyn = nullptr;
   std::vector<double> dyn_h;   // host copy [nph][nph] (roundoff entries dropped, gle_set_dyn)
-  int64_t dyn_dropped = 0;     // entries gle_set_dyn dropped as eigen-reconstruction roundoff
+  int64_t dyn_dropped = 0;
+  int dbg_a = 1;               // GLE_CHAIN_DBG: stage-A chain launched at the recorded step     // entries gle_set_dyn dropped as eigen-reconstruction roundoff
   double* d_dynd = nullptr;    // block-sparse DOF-tile fragments of dyn
   std::vector<std::vector<std::pair<int, int>>> dyn_rng;  // per DOF tile: (first k-step, count)
   std::vector<int64_t> dyn_tofs;
@@ -831,6 +832,10 @@ void xcd_order(gle_handle* h, Chain& c) {
   // rounds), the L2 locality not paying for the imbalance; GLE_XCD_ORDER=1 (experiment build) on
   const char* e = gle_env("GLE_XCD_ORDER");
   if (!e || atoi(e) == 0) return;
+  // mode 1: DOF tiles grouped by row tile (shared K rows), near-field tiles by (bath, row tile);
+  // mode 2: near-field tiles grouped by (bath, k-range, columns) -- the 19 row tiles that read the
+  // same history operand X share an L2 -- every other tile on its own; mode 3: 2 + DOF by row
+  const int mode = atoi(e);
   // a tile costs a fixed latency (descriptor, prologue loads, epilogue, ~ the time of 48 k-steps of
   // 16-column MFMAs) plus its products: with the products alone, light tiles (DOFs outside every
   // bath) piled up on a few XCDs and the padding to equal list lengths tripled the launch
@@ -840,7 +845,11 @@ void xcd_order(gle_handle* h, Chain& c) {
   std::vector<double> gwork;
   for (size_t i = 0; i < c.tiles.size(); ++i) {
     const ChTile& T = c.tiles[i];
-    const int64_t key = T.kind == CH_DOF ? (int64_t)(T.row0 / 16) : ((int64_t)(T.tile + 1) << 32) + T.row0 / 16;
+    int64_t key = T.kind == CH_DOF ? (int64_t)(T.row0 / 16) : ((int64_t)(T.tile + 1) << 32) + T.row0 / 16;
+    if (mode >= 2) {
+      if (T.kind == CH_RAW) key = (int64_t)(uintptr_t)(T.dst - (int64_t)T.row0 * T.ldd);  // (bath, q, c0)
+      else if (T.kind != CH_DOF || mode == 2) key = -1 - (int64_t)i;                       // ungrouped
+    }
     double w = 1.0 + tile_cost;
     for (int wv = 0; wv < CH_NW; ++wv)
       for (int k = 0; k < T.ntw[wv] && k < CH_TPW; ++k) w += (double)T.task[wv][k].nks * T.rn;
@@ -1694,9 +1703,10 @@ int freeze(gle_handle* h) {
         if (hipGetDeviceProperties(&prop, h->cfg.device) == hipSuccess) ncu = prop.multiProcessorCount;
         const int nslot = std::max(1, lv.P / h->P0);
         // workgroups per CU per cgemm chunk (GLE_CG_PER_CU): with small baths and 4-wave fused
-        // tiles, chunks of ~1 workgroup per CU (53.3 vs 55.3 us/step at C3; the chain finds slots
-        // sooner, the far-field launches run at a lower MFMA occupancy); 2 per CU for large baths
-        double per_cu = h->small_baths ? 1.0 : 2.0;
+        // tiles, chunks of ~1/2 workgroup per CU (C3: 53.3 vs 55.3 us/step at 1 vs 2; 0.5 another
+        // 1 % after the dyn roundoff drop, 3 A/B rounds; the chain finds slots sooner, the
+        // far-field launches run at a lower MFMA occupancy); 2 per CU for large baths
+        double per_cu = h->small_baths ? 0.5 : 2.0;
         if (const char* e = gle_env("GLE_CG_PER_CU")) per_cu = std::max(0.25, atof(e));
         const double want = (double)lv.cg.size() / (per_cu * ncu);
         const int64_t nch = gle_env("GLE_CG_CEIL") ? (int64_t)std::ceil(want - 1e-9) : (int64_t)want;
@@ -1757,7 +1767,7 @@ int freeze(gle_handle* h) {
   sd.ndblk = h->ndblk;
   if (const char* dbg = gle_env("GLE_CHAIN_DBG")) {
     size_t n = 0;
-    for (Chain* c : {&h->chA[1], &h->chB[1], &h->chC}) n = std::max(n, c->tiles.size());
+    for (Chain* c : {&h->chA[0], &h->chA[1], &h->chB[1], &h->chC, &h->chBC}) n = std::max(n, c->tiles.size());
     sd.dbg_ntile = (int32_t)n;
     sd.dbg_t = atoll(dbg);
     rc = dalloc_n(h, &h->d_dbg, (size_t)3 * n * 4);
@@ -1992,6 +2002,7 @@ int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
   const StepArgs ta = step_args(h);
   if (fpot_host_T)
     HIPCHK(h, hipMemcpyAsync(h->d_Fc, fpot_host_T, (size_t)h->nph * h->B * 8, hipMemcpyHostToDevice, h->stream));
+  if (h->d_dbg && t == h->dbg_t) h->dbg_a = need_pot ? 1 : 0;  // GLE_CHAIN_DBG: the stage-A variant recorded
   run_chain(h, 0, h->chA[need_pot ? 1 : 0], ta, (need_pot ? 1 : 0) | (fpot_host_T ? 0 : 2), h->levels.empty());
   h->host_force_step = fpot_host_T != nullptr;
   return GLE_OK;
@@ -2171,7 +2182,7 @@ static void dump_chain_dbg(gle_handle* h) {
   if (hipMemcpy(st.data(), h->d_dbg, st.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
   const char* kn[3] = {"DOF", "SFIN", "RAW"};
   for (int g = 0; g < 3; ++g) {
-    const Chain& c = g == 0 ? h->chA[1] : (g == 1 ? h->chB[1] : h->chC);
+    const Chain& c = g == 0 ? h->chA[h->dbg_a] : (g == 1 ? h->chB[1] : (h->fuse_bc ? h->chBC : h->chC));
     unsigned long long t0 = ~0ull, t1 = 0;
     for (size_t i = 0; i < c.tiles.size(); ++i) {
       const unsigned long long* r = &st[((size_t)g * n + i) * 4];

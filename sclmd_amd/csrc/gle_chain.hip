@@ -106,16 +106,29 @@ __device__ __forceinline__ void stamp(const StepDev* __restrict__ sd, int stage,
 // waits for about one memory round trip per task (<= CH_TPW) plus its MFMA chain instead of one
 // round trip per batch.  skip: bit 0 drops the tasks of cond CH_HIT (no trajectory of the tile
 // takes the potential-cache hit branch), bit 1 those of cond CH_MISS; their slots read as zeros.
+//
+// Accumulator sets (CH_NA, compile-time experiment): k-step u of a batch goes into set u mod NA,
+// the NA x RN independent accumulators keep several MFMAs of a wave in flight, and the sets are
+// added in fixed order when a run ends.  At C3 four sets measured 0.5-0.9 % slower per step than
+// one: a launch is bound by the matrix pipes' throughput (~115k f64 MFMAs per fused launch over
+// 1024 SIMDs, 73 % of them near-field tiles), not by one wave's accumulator chain.
+#ifndef CH_NA
+#define CH_NA 1
+#endif
 template <int RN, int NW>
 __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave, int lane, int64_t t,
                                          double* lds, int skip) {
   constexpr int U = Batch<RN, NW>::U;
   constexpr int NT = 16 * RN;
+  constexpr int NA = (CH_NA / RN) > 1 ? (CH_NA / RN) : 1;  // independent accumulators: NA * RN
+  static_assert(U % NA == 0, "a batch fills every accumulator set equally");
   const int nt = T->ntw[wave];
   const int brow = lane >> 4, bcol = lane & 15;
-  d4 acc[RN];
+  d4 acc[NA][RN];
 #pragma unroll
-  for (int n = 0; n < RN; ++n) acc[n] = d4{0.0, 0.0, 0.0, 0.0};
+  for (int j = 0; j < NA; ++j)
+#pragma unroll
+    for (int n = 0; n < RN; ++n) acc[j][n] = d4{0.0, 0.0, 0.0, 0.0};
   // X columns past the tile's valid ones (trajectories >= B) read the last valid column: their
   // products land in output columns nobody stores, and no read leaves the operand's rows
   int xc[RN];
@@ -127,8 +140,12 @@ __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave,
     for (int n = 0; n < RN; ++n)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        lds[cur * 16 * NT + (brow + 4 * q) * NT + 16 * n + bcol] = acc[n][q];
-        acc[n][q] = 0.0;
+        double v = acc[0][n][q];
+#pragma unroll
+        for (int j = 1; j < NA; ++j) v += acc[j][n][q];
+        lds[cur * 16 * NT + (brow + 4 * q) * NT + 16 * n + bcol] = v;
+#pragma unroll
+        for (int j = 0; j < NA; ++j) acc[j][n][q] = 0.0;
       }
   };
   for (int i = 0; i < CH_TPW; ++i) {
@@ -160,9 +177,18 @@ __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave,
         bcheck(tk.A + lane + (int64_t)s * aks, 8, __LINE__);
         for (int n = 0; n < RN; ++n) bcheck(tk.X + col + xo + xc[n], 8, __LINE__);
 #endif
+#if defined(CH_DBG) && (CH_DBG & 1)  // timing diagnostics only (wrong results): no A loads
+        a[u] = 1e-3 * (s + 1);
+#else
         a[u] = A[(int64_t)s * aks];
+#endif
 #pragma unroll
-        for (int n = 0; n < RN; ++n) b[u][n] = X[xo + xc[n]];
+        for (int n = 0; n < RN; ++n)
+#if defined(CH_DBG) && (CH_DBG & 2)  // no X loads
+          b[u][n] = 1e-3 * (xo + n);
+#else
+          b[u][n] = X[xo + xc[n]];
+#endif
       }
     };
     auto compute = [&](int s0, double (&a)[U], double (&b)[U][RN]) {
@@ -170,26 +196,27 @@ __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave,
       for (int u = 0; u < U; ++u) {
         const double av = s0 + u < nks ? a[u] : 0.0;
 #pragma unroll
-        for (int n = 0; n < RN; ++n) acc[n] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b[u][n], acc[n], 0, 0, 0);
+        for (int n = 0; n < RN; ++n)
+          acc[u % NA][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b[u][n], acc[u % NA][n], 0, 0, 0);
       }
     };
-#if CH_DB
-    fetch(0, a0, b0);
-    for (int s0 = 0; s0 < nks; s0 += 2 * U) {
-      fetch(min(s0 + U, nks - 1), a1, b1);
-      compute(s0, a0, b0);
-      if (s0 + U >= nks) break;
-      fetch(min(s0 + 2 * U, nks - 1), a0, b0);
-      compute(s0 + U, a1, b1);
+    if constexpr (CH_DB != 0 && RN == 1) {  // CH_DB: the one-column-tile tasks only (registers)
+      fetch(0, a0, b0);
+      for (int s0 = 0; s0 < nks; s0 += 2 * U) {
+        fetch(min(s0 + U, nks - 1), a1, b1);
+        compute(s0, a0, b0);
+        if (s0 + U >= nks) break;
+        fetch(min(s0 + 2 * U, nks - 1), a0, b0);
+        compute(s0 + U, a1, b1);
+      }
+    } else {
+      (void)a1;
+      (void)b1;
+      for (int s0 = 0; s0 < nks; s0 += U) {
+        fetch(s0, a0, b0);
+        compute(s0, a0, b0);
+      }
     }
-#else
-    (void)a1;
-    (void)b1;
-    for (int s0 = 0; s0 < nks; s0 += U) {
-      fetch(s0, a0, b0);
-      compute(s0, a0, b0);
-    }
-#endif
   }
   if (cur >= 0) flush();
 }
