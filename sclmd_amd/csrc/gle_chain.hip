@@ -847,18 +847,30 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(DRN == 
   __builtin_amdgcn_s_setprio(CH_PRIO);
   // The tile descriptor and the step descriptor's header are copied into LDS with one round of
   // coalesced vector loads: every later field access is an LDS read instead of a chain of
-  // dependent scalar loads.
-  constexpr int NTW = sizeof(ChTile) / 8, NSW = (offsetof(StepDev, bath) + 7) / 8;
-  __shared__ unsigned long long tdw[NTW], sdw[NSW];
+  // dependent scalar loads.  Only the task lists of this launch's NW waves are copied (task[] is
+  // the descriptor's last member, wave-major): with 4 waves the copy is one word per thread, all
+  // loads issued before the first LDS store.
+  static_assert(offsetof(ChTile, task) + sizeof(ChTask) * CH_NW * CH_TPW == sizeof(ChTile), "task[] last");
+  constexpr int NTW = (int)((offsetof(ChTile, task) + sizeof(ChTask) * NW * CH_TPW) / 8);
+  constexpr int NSW = (offsetof(StepDev, bath) + 7) / 8;
+  constexpr int NCP = NTW + NSW, NIT = (NCP + NW * 64 - 1) / (NW * 64);
+  __shared__ unsigned long long tdw[sizeof(ChTile) / 8], sdw[NSW];
   stamp(sd, STAGE, 0, ta);
   {
-    const __attribute__((address_space(1))) unsigned long long* tsrc =
-        (const __attribute__((address_space(1))) unsigned long long*)(tiles + blockIdx.x);
-    const __attribute__((address_space(1))) unsigned long long* ssrc =
-        (const __attribute__((address_space(1))) unsigned long long*)sd;
-    for (int i = threadIdx.x; i < NTW + NSW; i += NW * 64) {
-      if (i < NTW) tdw[i] = tsrc[i];
-      else sdw[i - NTW] = ssrc[i - NTW];
+    typedef const __attribute__((address_space(1))) unsigned long long gull;
+    gull* tsrc = (gull*)(tiles + blockIdx.x);
+    gull* ssrc = (gull*)sd;
+    unsigned long long v[NIT];
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int j = min((int)threadIdx.x + k * NW * 64, NCP - 1);
+      v[k] = *(j < NTW ? tsrc + j : ssrc + (j - NTW));
+    }
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int i = threadIdx.x + k * NW * 64;
+      if (i < NTW) tdw[i] = v[k];
+      else if (i < NCP) sdw[i - NTW] = v[k];
     }
   }
   __syncthreads();
