@@ -157,7 +157,8 @@ struct gle_handle {
   double* d_dyn = nullptr;
   std::vector<double> dyn_h;   // host copy [nph][nph] (roundoff entries dropped, gle_set_dyn)
   int64_t dyn_dropped = 0;
-  int dbg_a = 1;               // GLE_CHAIN_DBG: stage-A chain launched at the recorded step     // entries gle_set_dyn dropped as eigen-reconstruction roundoff
+  int dbg_a = 1;               // GLE_CHAIN_DBG: stage-A chain launched at the recorded step
+  bool bc_balance = true;      // fused stage: branch classes split over the waves separately     // entries gle_set_dyn dropped as eigen-reconstruction roundoff
   double* d_dynd = nullptr;    // block-sparse DOF-tile fragments of dyn
   std::vector<std::vector<std::pair<int, int>>> dyn_rng;  // per DOF tile: (first k-step, count)
   std::vector<int64_t> dyn_tofs;
@@ -818,6 +819,78 @@ int fill_tasks(gle_handle* h, ChTile& T, const std::vector<Seg>& segs, int nout,
   return GLE_OK;
 }
 
+// Fused velocity stage: the k-steps of each branch class (always / potential-cache hit / miss) are
+// split evenly over the waves on their own, so whichever of hit and miss the tile takes at run
+// time, every wave carries 1/NW of the products (the plain even split of the concatenation left
+// the wave holding the skipped branch idle: 75 k-steps per busy wave at C3 instead of ~57).
+// Returns 1 (nothing changed) when a wave would need more than CH_TPW runs; the caller then
+// uses fill_tasks.
+int fill_tasks_balanced(ChTile& T, const std::vector<Seg>& segs, int nout, Chain& c) {
+  const int NW = c.nw;
+  struct Run {
+    int seg;
+    int64_t kl, n;
+  };
+  std::vector<std::vector<Run>> runs(NW);
+  for (int cond : {0, CH_MISS, CH_HIT}) {
+    int64_t G = 0;
+    for (const Seg& sg : segs)
+      if (sg.cond == cond) G += sg.nks;
+    for (int w = 0; w < NW; ++w) {
+      const int64_t g0 = G * w / NW, g1 = G * (w + 1) / NW;
+      int64_t pos = 0;
+      for (size_t i = 0; i < segs.size(); ++i) {
+        if (segs[i].cond != cond) continue;
+        const int64_t s0 = std::max(g0, pos), s1 = std::min(g1, pos + segs[i].nks);
+        if (s1 > s0) runs[w].push_back(Run{(int)i, s0 - pos, s1 - s0});
+        pos += segs[i].nks;
+      }
+    }
+  }
+  for (int w = 0; w < NW; ++w) {
+    std::stable_sort(runs[w].begin(), runs[w].end(),
+                     [&](const Run& a, const Run& b) { return segs[a.seg].o < segs[b.seg].o; });
+    if ((int)runs[w].size() > CH_TPW) return 1;
+  }
+  // one LDS slot per (wave, output), the slots of an output contiguous (output order, then waves)
+  std::vector<std::vector<int>> slot_of(NW, std::vector<int>(nout, -1));
+  int slot = 0;
+  for (int o = 0; o < nout; ++o) {
+    T.ob[o] = (int8_t)slot;
+    for (int w = 0; w < NW; ++w)
+      for (const Run& r : runs[w])
+        if (segs[r.seg].o == o) {
+          slot_of[w][o] = slot++;
+          break;
+        }
+  }
+  for (int o = nout; o <= CH_NOUT; ++o) T.ob[o] = (int8_t)slot;
+  for (int w = 0; w < CH_NW; ++w) T.ntw[w] = 0;
+  for (int w = 0; w < NW; ++w) {
+    int cnt = 0;
+    for (const Run& r : runs[w]) {
+      const Seg& sg = segs[r.seg];
+      ChTask& tk = T.task[w][cnt++];
+      tk = ChTask{};
+      tk.A = sg.A + r.kl * sg.a_ks;
+      tk.a_ks = sg.a_ks;
+      tk.X = sg.X + 4 * r.kl * sg.ldx;
+      tk.ldx = sg.ldx;
+      tk.ring = sg.ring;
+      tk.tshift = sg.tshift;
+      tk.sst = sg.sst;
+      tk.nks = (int32_t)r.n;
+      tk.slot = slot_of[w][sg.o];
+      tk.cond = sg.cond;
+      tk.xrows = (int32_t)((sg.xrows > 0 ? sg.xrows : 4 * sg.nks) - 4 * r.kl);
+      c.flops += 2048.0 * T.rn * (double)r.n;
+    }
+    T.ntw[w] = cnt;
+  }
+  c.lds = std::max(c.lds, (size_t)slot * 256 * T.rn * 8);
+  return 0;
+}
+
 // XCD-aware tile order.  Workgroups are dispatched round-robin over the 8 XCDs (block b on XCD
 // b mod 8, observed, not guaranteed: speed only, never correctness), each with its own L2.  Tiles
 // that read the same matrix rows (the column tiles of one DOF row tile; the near-field and S(t+1)
@@ -907,6 +980,7 @@ int plan_chain(gle_handle* h) {
     for (int i = 0; i < 3; ++i) h->ch_nw[i] = v[i] >= 16 ? 16 : (v[i] >= 8 ? 8 : 4);
   }
   if (const char* e = gle_env("GLE_CHAIN_DRN")) h->ch_drn = atoi(e) >= 2 ? 2 : 1;
+  if (const char* e = gle_env("GLE_BC_BALANCE")) h->bc_balance = atoi(e) != 0;
   const char* near_in = gle_env("GLE_NEAR_IN");
   if (!near_in) near_in = "AC";
   const int drn = (int)std::min<int64_t>(h->ch_drn, (B + 15) / 16);
@@ -1264,8 +1338,12 @@ int plan_chain(gle_handle* h) {
     }
     int64_t W = 0;
     for (auto& sg : segs) W += sg.nks;
-    int rc = fill_tasks(h, T, segs, CH_NOUT, 0, W, c);
-    if (rc) return rc;
+    const bool bal = stage == 3 && h->bc_balance && c.lds <= 150 * 1024;
+    if (!bal || fill_tasks_balanced(T, segs, CH_NOUT, c)) {
+      int rc = fill_tasks(h, T, segs, CH_NOUT, 0, W, c);
+      if (rc) return rc;
+    }
+    if (c.lds > 150 * 1024) return fail(h, GLE_ERR_UNSUP, "chain plan: LDS slots");
     c.tiles.push_back(T);
     return GLE_OK;
   };

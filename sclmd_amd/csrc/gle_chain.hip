@@ -84,6 +84,10 @@ __device__ __forceinline__ int64_t cmod(int64_t a, int64_t m) {
 #ifndef CH_PRIO
 #define CH_PRIO 3
 #endif
+// CH_PRIO_RAW: issue priority of the near-field partial tiles (default: that of the whole chain)
+#ifndef CH_PRIO_RAW
+#define CH_PRIO_RAW CH_PRIO
+#endif
 // CH_DB: double-buffered operand batches (the next batch of a task in flight during this one's MFMAs)
 #ifndef CH_DB
 #define CH_DB 0
@@ -877,6 +881,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(DRN == 
   const ChTile* T = (const ChTile*)tdw;
   sd = (const StepDev*)sdw;  // header only: bath[] is not copied (tiles carry their baths)
   const int kind = T->kind;
+#if CH_PRIO_RAW != CH_PRIO
+  // near-field partial tiles (consumed one step later) below the DOF / S(t+1) tiles of the stage
+  if (kind == CH_RAW) __builtin_amdgcn_s_setprio(CH_PRIO_RAW);
+#endif
   stamp(sd, STAGE, 1, ta);
   if (kind == CH_DOF) {
     if (STAGE == 0) dof_A<NW, DRN>(T, sd, ta, mode, lds);

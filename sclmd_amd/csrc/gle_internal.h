@@ -195,7 +195,7 @@ struct StepDev {
 //   CH_SFIN  16 bath rows: S(t+1) = K_1 p_t + near-field partials + ladder levels
 //   CH_RAW   16 bath rows x 16*rn columns of a near-field partial (lags >= 2, target t+2)
 constexpr int CH_NW = 16;       // waves per chain workgroup (max)
-constexpr int CH_TPW = 3;       // tasks per wave
+constexpr int CH_TPW = 4;       // tasks per wave
 constexpr int CH_TB = 3;        // baths a DOF tile may intersect
 // DOF-tile outputs: Y = K0.x of tile bath u (u), YQ = Kq.q (CH_TB + u), YD = dyn.q (2 CH_TB); the
 // fused velocity-iteration stage (STAGE 3) uses per tile bath u (h = dt/2, a = c dt/2):
