@@ -255,6 +255,13 @@ def main():
     m.steps(args.steps)
     st.sync()
     prof = st.profile_read()
+    # the chain's own per-workgroup stamps in a third window of the same K steps (apart from the
+    # far-field timing, whose launches the chain stamps would otherwise share the window with)
+    st.profile(True, events=False, chain=True)
+    m.steps(args.steps)
+    st.sync()
+    pch = st.profile_read()
+    prof.update({k: pch[k] for k in ("chain_launches", "chain_ms", "chain_flops")})
     st.profile(False)
     # one reduce of the time-averaged current statistics (the ensemble output)
     sums = m._reduce(st.current_sums())
@@ -340,6 +347,20 @@ def main():
                      "timing": "device timestamps" if prof["launches_device"] == prof["launches"] else "HIP events",
                      "algorithmic_flops_per_launch": fl, "algorithmic_bytes_per_launch": by})
         res["roofline"] = roof
+    if prof.get("chain_launches", 0) > 0 and plan["far_mode"] == "spectral":
+        # the per-step chain (md.vv stages, the step's critical path) in the same window, timed by
+        # its own device timestamps: algorithmic flops of its products / its kernel durations;
+        # us_per_step = chain kernel time per step (beside the far field, so > its time alone)
+        cms = prof["chain_ms"]
+        res["chain_roofline"] = {
+            "kernel": "chain_kernel (per-step md.vv stages: A and the fused velocity stage)",
+            "bound": "mfma", "achieved": prof["chain_flops"] / (cms * 1e-3) / 1e12,
+            "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": prof["chain_flops"] / (cms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS,
+            "launches": prof["chain_launches"], "us_per_step": cms / args.steps * 1e3,
+            "algorithmic_flops_per_step": prof["chain_flops"] / args.steps,
+            "timing": "device timestamps (per-workgroup stores)",
+            "window": "third window of the same %d steps" % args.steps}
     kap = sums[:, 0] / sums[:, 2] * 243414.0
     res["heat_current_nW"] = [float(x) for x in kap]
 

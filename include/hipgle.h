@@ -233,6 +233,7 @@ int gle_comm_destroy(void* comm);
  * add launch-queue packets); 0 switches both off and resets the counters either way. */
 #define GLE_PROFILE_EVENTS 1
 #define GLE_PROFILE_COUNT 2
+#define GLE_PROFILE_CHAIN 4 /* per-workgroup start / end stamps of the chain launches (gle_profile_read_chain) */
 int gle_profile(gle_handle* h, int32_t enable);
 /* launches, total milliseconds, algorithmic flops and bytes of the profiled contraction
  * launches since profiling was enabled (flops/bytes per SURVEY.md section 8d). */
@@ -242,6 +243,10 @@ int gle_profile_read(gle_handle* h, int64_t* nlaunch, double* total_ms, double* 
  * launch (s_memrealtime, 100 MHz), i.e. the kernel duration a kernel trace reports; the HIP events
  * of gle_profile_read also include each launch's wait for free compute units. */
 int gle_profile_read_device(gle_handle* h, int64_t* nlaunch, double* total_ms);
+/* The per-step chain's launches (md.vv stages: A and the fused velocity stage, or A / B / C) since
+ * profiling was enabled with GLE_PROFILE_CHAIN, timed like gle_profile_read_device (first
+ * workgroup start to last end), with the algorithmic flops of their products. */
+int gle_profile_read_chain(gle_handle* h, int64_t* nlaunch, double* total_ms, double* flops);
 /* Planner summary of the current configuration: block length L, far-field work items, bytes of
  * device memory in use, far-field mode actually chosen. */
 int gle_plan_info(gle_handle* h, int64_t* block_len, int64_t* far_items, int64_t* device_bytes,

@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("SCLMD_AMD_LIB", os.path.join(_HERE, "_lib", "libhipgl
 GLE_BATH_PHONON = 0
 PROFILE_EVENTS = 1  # hipgle.h GLE_PROFILE_EVENTS
 PROFILE_COUNT = 2   # hipgle.h GLE_PROFILE_COUNT
+PROFILE_CHAIN = 4   # hipgle.h GLE_PROFILE_CHAIN
 GLE_BATH_ELECTRON = 1
 
 _ERRNAMES = {-1: "GLE_ERR_ARG", -2: "GLE_ERR_HIP", -3: "GLE_ERR_STATE", -4: "GLE_ERR_NOMEM",
@@ -27,7 +28,7 @@ EXPORTS = [
     "gle_set_history", "gle_get_history", "gle_get_force", "gle_set_noise", "gle_get_noise",
     "gle_noise_factors", "gle_noise_generate", "gle_step_begin", "gle_step_end", "gle_run",
     "gle_sync", "gle_get_current", "gle_get_energy", "gle_current_sums", "gle_profile",
-    "gle_profile_read", "gle_profile_read_device", "gle_plan_info", "gle_add_bath_gmem", "gle_get_kernel", "gle_gamt",
+    "gle_profile_read", "gle_profile_read_device", "gle_profile_read_chain", "gle_plan_info", "gle_add_bath_gmem", "gle_get_kernel", "gle_gamt",
     "gle_profile_levels", "gle_step_work", "gle_reduce_current", "gle_comm_unique_id", "gle_comm_init",
     "gle_comm_destroy", "gle_record", "gle_record_zero", "gle_get_record", "gle_get_record_history",
     "gle_power_spectrum", "gle_set_record", "gle_set_record_history", "gle_noise_stream_begin",
@@ -87,6 +88,7 @@ _SIGS = {
     "gle_profile": (ctypes.c_int, [_P, ctypes.c_int32]),
     "gle_profile_read": (ctypes.c_int, [_P, _I64, _D, _D, _D]),
     "gle_profile_read_device": (ctypes.c_int, [_P, _I64, _D]),
+    "gle_profile_read_chain": (ctypes.c_int, [_P, _I64, _D, _D]),
     "gle_plan_info": (ctypes.c_int, [_P, _I64, _I64, _I64, ctypes.POINTER(ctypes.c_int32)]),
     "gle_profile_levels": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32),
                                           ctypes.POINTER(ctypes.c_int32), _D]),
@@ -438,9 +440,10 @@ class Stepper:
                   "gle_reduce_current")
         return out
 
-    def profile(self, enable=True, events=True):
-        """enable: count ladder blocks; events: also HIP-event timing of the dominant kernel."""
-        mode = (PROFILE_COUNT | (PROFILE_EVENTS if events else 0)) if enable else 0
+    def profile(self, enable=True, events=True, chain=False):
+        """enable: count ladder blocks; events: also HIP-event timing of the dominant kernel;
+        chain: per-workgroup device stamps of the per-step chain's launches."""
+        mode = (PROFILE_COUNT | (PROFILE_EVENTS if events else 0) | (PROFILE_CHAIN if chain else 0)) if enable else 0
         self._chk(self.lib.gle_profile(self.h, mode), "gle_profile")
 
     def profile_read(self):
@@ -453,6 +456,10 @@ class Stepper:
         self._chk(self.lib.gle_profile_read_device(self.h, ctypes.byref(nd), ctypes.byref(msd)),
                   "gle_profile_read_device")
         out["launches_device"], out["ms_device"] = int(nd.value), msd.value
+        nc, msc, flc = ctypes.c_int64(0), ctypes.c_double(0), ctypes.c_double(0)
+        self._chk(self.lib.gle_profile_read_chain(self.h, ctypes.byref(nc), ctypes.byref(msc), ctypes.byref(flc)),
+                  "gle_profile_read_chain")
+        out["chain_launches"], out["chain_ms"], out["chain_flops"] = int(nc.value), msc.value, flc.value
         return out
 
     def plan_info(self):

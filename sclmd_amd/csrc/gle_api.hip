@@ -176,6 +176,12 @@ struct gle_handle {
   // device timestamps of the profiled far-field launches ([start, end] pairs, s_memrealtime)
   unsigned long long* d_tst = nullptr;
   size_t tst_cap = 4096, tst_used = 0;
+  bool prof_ch = false;                  // GLE_PROFILE_CHAIN: per-workgroup stamps of the chain launches
+  unsigned long long* d_ctst = nullptr;  // [launch slot][workgroup][start, end]
+  size_t ctst_cap = 1024, ctst_tiles = 0, ctst_used = 0;
+  std::vector<int> ctst_n;               // workgroups of each used slot
+  int64_t prof_ch_n = 0;                 // chain launches timed on the device
+  double prof_ch_ms = 0, prof_ch_flops = 0;
   int64_t prof_n_dev = 0;
   double prof_ms_dev = 0.0;
   int piece_g = 1;              // steps per piece slot (P0 once planned; GLE_PIECE_STEP=1: every step)
@@ -668,6 +674,23 @@ void drain_profile(gle_handle* h) {
     reset_tst(h, h->tst_used, h->stream);
     h->tst_used = 0;
   }
+  if (h->d_ctst && h->ctst_used > 0) {  // chain launches: first workgroup start to last end
+    std::vector<unsigned long long> v(2 * h->ctst_used * h->ctst_tiles);
+    hipMemcpy(v.data(), h->d_ctst, v.size() * 8, hipMemcpyDeviceToHost);
+    for (size_t i = 0; i < h->ctst_used; ++i) {
+      unsigned long long t0 = ~0ull, t1 = 0;
+      for (int b = 0; b < h->ctst_n[i]; ++b) {
+        t0 = std::min(t0, v[2 * (i * h->ctst_tiles + b)]);
+        t1 = std::max(t1, v[2 * (i * h->ctst_tiles + b) + 1]);
+      }
+      if (t1 >= t0 && t0 != 0) {
+        h->prof_ch_ms += (double)(t1 - t0) * 1e-5;
+        h->prof_ch_n += 1;
+      }
+    }
+    h->ctst_used = 0;
+    h->ctst_n.clear();
+  }
 }
 
 // Launch one op on stream s; profile: HIP events around the contraction launch (the dominant
@@ -703,7 +726,15 @@ void run_chain(gle_handle* h, int stage, Chain& c, const StepArgs& ta, int mode,
     e1 = h->ev[h->ev_used + 1];
     h->ev_used += 2;
   }
-  launch_chain(stage, c.nw, h->ch_drn, c.lds, c.d, (int)c.tiles.size(), h->d_sd, ta, mode, h->stream);
+  StepArgs tc = ta;
+  if (h->prof_ch && h->d_ctst && !c.tiles.empty() && c.tiles.size() <= h->ctst_tiles) {
+    if (h->ctst_used >= h->ctst_cap) drain_profile(h);
+    tc.ts = h->d_ctst + 2 * h->ctst_used * h->ctst_tiles;
+    h->ctst_used += 1;
+    h->ctst_n.push_back((int)c.tiles.size());
+    h->prof_ch_flops += c.flops;
+  }
+  launch_chain(stage, c.nw, h->ch_drn, c.lds, c.d, (int)c.tiles.size(), h->d_sd, tc, mode, h->stream);
   if (e1) {
     hipEventRecord(e1, h->stream);
     h->prof_n += 1;
@@ -3047,9 +3078,24 @@ int gle_profile(gle_handle* h, int32_t enable) {
     HIPCHK(h, hipDeviceSynchronize());
     reset_tst(h, h->tst_used, h->stream);
   }
+  if ((enable & GLE_PROFILE_CHAIN) && !h->d_ctst) {
+    size_t n = 0;
+    for (Chain* c : {&h->chA[0], &h->chA[1], &h->chB[0], &h->chB[1], &h->chC, &h->chBC}) n = std::max(n, c->tiles.size());
+    h->ctst_tiles = n;
+    if (n > 0) {
+      int rc = dalloc_n(h, &h->d_ctst, 2 * h->ctst_cap * n);
+      if (rc) return rc;
+    }
+  }
+  if (h->ctst_used > 0) HIPCHK(h, hipDeviceSynchronize());
+  h->ctst_used = 0;
+  h->ctst_n.clear();
+  h->prof_ch = (enable & GLE_PROFILE_CHAIN) != 0;
   h->tst_used = 0;
   h->prof_n_dev = 0;
   h->prof_ms_dev = 0.0;
+  h->prof_ch_n = 0;
+  h->prof_ch_ms = h->prof_ch_flops = 0.0;
   h->prof = enable != 0;
   h->prof_ev = (enable & GLE_PROFILE_EVENTS) != 0;
   h->ev_used = 0;
@@ -3068,6 +3114,17 @@ int gle_profile_read(gle_handle* h, int64_t* nlaunch, double* total_ms, double* 
   if (total_ms) *total_ms = h->prof_ms;
   if (flops) *flops = h->prof_flops;
   if (bytes) *bytes = h->prof_bytes;
+  return GLE_OK;
+}
+
+int gle_profile_read_chain(gle_handle* h, int64_t* nlaunch, double* total_ms, double* flops) {
+  if (!h) return GLE_ERR_ARG;
+  hipSetDevice(h->cfg.device);
+  drain_profile(h);
+  HIPCHK(h, hipGetLastError());
+  if (nlaunch) *nlaunch = h->prof_ch_n;
+  if (total_ms) *total_ms = h->prof_ch_ms;
+  if (flops) *flops = h->prof_ch_flops;
   return GLE_OK;
 }
 

@@ -849,6 +849,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(DRN == 
   // ladder's GEMM waves: its waves take issue priority (MFMA pipe and memory issue go to the
   // highest-priority ready wave first, then the oldest)
   __builtin_amdgcn_s_setprio(CH_PRIO);
+  // profiling: per-workgroup start / end stamps with plain stores (one device-scope counter that
+  // every workgroup hits would serialise ~600 arrivals per launch and stretch the chain)
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
   // The tile descriptor and the step descriptor's header are copied into LDS with one round of
   // coalesced vector loads: every later field access is an LDS read instead of a chain of
   // dependent scalar loads.  Only the task lists of this launch's NW waves are copied (task[] is
@@ -897,6 +900,13 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(DRN == 
     raw<NW>(T, sd, ta, lds, STAGE);
   }
   stamp(sd, STAGE, 3, ta);
+  if (ta.ts) {  // launch-uniform
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      G(ta.ts)[2 * blockIdx.x] = t_start;
+      G(ta.ts)[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
 }
 
 // dynamic LDS above the 64 KiB default needs the kernel's limit raised (once per kernel and device)

@@ -294,6 +294,8 @@ struct StepArgs {
   int32_t dbg;               // GLE_CHAIN_DBG: record this launch's timeline
   int32_t pad;
   int64_t lvl_off[MAXLVL];   // per level: offset (doubles) of target t+1 in its block buffer
+  unsigned long long* ts;    // chain launches under GLE_PROFILE_CHAIN: workgroup b stores its start /
+                             // end (s_memrealtime) at ts[2b], ts[2b+1] (plain stores), else nullptr
 };
 void launch_contract(int rn, int cu, const CItem* items, int nitems, StepArgs ta, hipStream_t s);
 void launch_reduce(const RItem* items, int nitems, int max_elems, StepArgs ta,
