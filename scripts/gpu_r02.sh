@@ -19,5 +19,5 @@ for f in ['bench_20','bench','bench_c2']:
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
   python3 bench.py --no-cpu-baseline > gpurun_out/prof/bench.json 2> gpurun_out/prof/bench.err || { echo "prof failed"; tail -20 gpurun_out/prof/bench.err; exit 1; }
 N=$(python3 -c "import json;print(json.load(open('gpurun_out/prof/bench.json'))['roofline']['launches'])")
-python3 scripts/trace_summary.py gpurun_out/prof/run_kernel_trace.csv --steps --gaps --last cgemm $N > gpurun_out/prof/summary.txt
+python3 scripts/trace_summary.py gpurun_out/prof/run_kernel_trace.csv --steps --gaps --last cgemm $N --skip $N > gpurun_out/prof/summary.txt
 tail -12 gpurun_out/prof/summary.txt

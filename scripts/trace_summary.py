@@ -31,9 +31,14 @@ if "--last" in sys.argv:
     # average duration of the last N dispatches of a kernel (the bench's timed region)
     i = sys.argv.index("--last")
     kn, n = sys.argv[i + 1], int(sys.argv[i + 2])
-    ks = sorted([r for r in rows if kn in r["n"]], key=lambda r: r["s"])[-n:]
+    # --skip M: leave out the M newest dispatches (bench.py's third window, the chain stamps, follows
+    # the far-field timing window)
+    skip = int(sys.argv[sys.argv.index("--skip") + 1]) if "--skip" in sys.argv else 0
+    allk = sorted([r for r in rows if kn in r["n"]], key=lambda r: r["s"])
+    ks = allk[len(allk) - n - skip:len(allk) - skip]
     if ks:
-        print("\nlast %d dispatches of %s: avg %.2f us" % (len(ks), kn, sum(r["e"] - r["s"] for r in ks) / len(ks) / 1e3))
+        print("\n%d dispatches of %s before the newest %d: avg %.2f us"
+              % (len(ks), kn, skip, sum(r["e"] - r["s"] for r in ks) / len(ks) / 1e3))
 
 if "--steps" in sys.argv:
     rows.sort(key=lambda r: r["s"])
