@@ -13,13 +13,16 @@ import json
 import os
 
 
-def per_launch(path, kernel, last=0):
-    """Counter value per dispatch of `kernel`, in dispatch order; last > 0 keeps only the final
-    `last` dispatches (the bench's timed region: nothing of that kernel runs after it)."""
+def per_launch(path, kernel, last=0, skip=0):
+    """Counter value per dispatch of `kernel`, in dispatch order; last > 0 keeps only `last`
+    dispatches before the newest `skip` (bench.py's roofline window is followed by one more window
+    of the same steps, the chain stamps: skip = last)."""
     rows = [r for r in csv.DictReader(open(path)) if kernel in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r.get("Dispatch_Id", r.get("Correlation_Id", 0))))
     vals = [float(r["Counter_Value"]) for r in rows]
-    return vals[-last:] if last > 0 else vals
+    if last <= 0:
+        return vals
+    return vals[len(vals) - last - skip:len(vals) - skip]
 
 
 def main():
@@ -30,6 +33,8 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--ntraj", type=int, default=64)
     ap.add_argument("--far-mode", default="spectral")
+    ap.add_argument("--skip-chain-window", type=int, default=1,
+                    help="1: the newest `last` dispatches are bench.py's chain-stamp window; skip them")
     ap.add_argument("--last", type=int, default=-1,
                     help="dispatches of the timed region (default: the bench JSON's roofline.launches)")
     a = ap.parse_args()
@@ -39,8 +44,9 @@ def main():
             last = int(json.load(open(os.path.join(a.pmcdir, "FETCH_SIZE.json")))["roofline"]["launches"])
         except (OSError, ValueError, KeyError):
             last = 0
-    f = per_launch(os.path.join(a.pmcdir, "FETCH_SIZE", "run_counter_collection.csv"), a.kernel, last)
-    w = per_launch(os.path.join(a.pmcdir, "WRITE_SIZE", "run_counter_collection.csv"), a.kernel, last)
+    skip = last if a.skip_chain_window else 0
+    f = per_launch(os.path.join(a.pmcdir, "FETCH_SIZE", "run_counter_collection.csv"), a.kernel, last, skip)
+    w = per_launch(os.path.join(a.pmcdir, "WRITE_SIZE", "run_counter_collection.csv"), a.kernel, last, skip)
     fetch = sum(f) / len(f) * 1024.0
     write = sum(w) / len(w) * 1024.0
     res = {"config": a.config, "ntraj": a.ntraj, "far_mode": a.far_mode, "kernel": a.kernel,
