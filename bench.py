@@ -14,8 +14,12 @@ comparison), --config C5 --ntraj 32.
     torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU, RCCL reduce)
 
 Prints one JSON line (rank 0).  roofline: the dominant kernel (far-field memory-kernel
-contraction) timed with HIP events on its own stream inside the library over the timed region;
-cpu_baseline: the oracle's reference-equivalent numpy step timed on this host for one trajectory.
+contraction, cgemm_kernel) timed by its own device timestamps (first workgroup start to last
+workgroup end of every launch, s_memrealtime) over a second window of the same K steps, HIP events
+on its stream reported beside them; chain_roofline: the per-step chain's launches timed the same
+way in a third window; cpu_baseline: the oracle's reference-equivalent numpy step (phonon and
+electron baths as the reference builds them, bias terms included) timed on this host for one
+trajectory.
 """
 import argparse
 import json
@@ -82,7 +86,9 @@ def cpu_baseline(baths_host, dyn, nph, dt, nmd, budget_s=20.0, nsample=5):
     `nsample` samples of about budget_s / nsample seconds each, after one warm-up step."""
     from oracle import sclmd_oracle as O
 
-    bs = [O.Bath("ph", c, k, n, dt, nmd) for (c, k, n) in baths_host]
+    # baths_host: (kind, cids, kernel, noise, bias terms) -- electron baths keep their bias matrices
+    # (ebath.bforce, baths.py:224-255), so a biased C5 bath costs the reference its four matvecs
+    bs = [O.Bath(kind, c, k, n, dt, nmd, **extra) for (kind, c, k, n, extra) in baths_host]
     sim = O.GLE(nph, dt, nmd, bs, dyn=dyn)
     rng = np.random.default_rng(0)
     sim.p = rng.normal(size=nph) * 1e-3
@@ -366,7 +372,13 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         noise = [st.get_noise(i)[0] for i in range(len(baths))]
-        bh = [(b.cids, st.get_kernel(i), noise[i]) for i, b in enumerate(baths)]
+        bh = []
+        for i, b in enumerate(baths):
+            if b.kind == "ebath":  # the host kernel (efric, ml = 1): the device copy has zeta2 folded in
+                bh.append(("e", b.cids, b.kernel, noise[i],
+                           dict(bias=b.bias, exim=b.exim, zeta1=b.zeta1, zeta2=b.zeta2)))
+            else:
+                bh.append(("ph", b.cids, st.get_kernel(i), noise[i], {}))
         res["cpu_baseline"] = cpu_baseline(bh, m.dyn, meta["nph"], meta["dt"], meta["nmd"], args.cpu_budget)
         res["speedup_vs_cpu_baseline"] = value / res["cpu_baseline"]["value"]
     if rank == 0:

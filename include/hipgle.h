@@ -53,7 +53,8 @@ typedef struct gle_config {
     double dt;          /* MD time step, md.dt (md.py:59)                                    */
     int32_t device;     /* HIP device ordinal                                                */
     int32_t block_len;  /* P0: first block length of the memory-sum ladder (near field = lags
-                           [1, 2 P0) every step); 0 = auto (4)                                  */
+                           [1, 2 P0) every step); 0 = auto by the plan class (gle_set_plan_class):
+                           8 when every bath has nc <= 512, 4 otherwise                          */
     int32_t far_mode;   /* GLE_FAR_AUTO / GLE_FAR_DIRECT / GLE_FAR_SPECTRAL                      */
     int32_t max_block;  /* largest ladder block length; 0 = auto (256 spectral, direct: L with
                            L * ntraj >= 256, L <= 32)                                           */
@@ -73,6 +74,14 @@ typedef struct gle_config {
 #define GLE_FAR_DIRECT 1
 #define GLE_FAR_SPECTRAL 2
 
+/* Plan class.  AUTO picks by the largest bath: SMALL when every bath has nc <= 512 (the per-step
+ * chain is latency-bound: first block length 8, 4-wave fused velocity-stage tiles, far-field GEMM
+ * chunks of ~1/2 workgroup per CU), LARGE otherwise (first block length 4, 8-wave fused tiles, 2
+ * workgroups per CU).  Forcing a class changes only the schedule, never the result beyond fp64
+ * rounding; tests use it to run the large-bath plan at small sizes. */
+#define GLE_PLAN_AUTO 0
+#define GLE_PLAN_SMALL_BATHS 1
+#define GLE_PLAN_LARGE_BATHS 2
 /* ---- lifetime ------------------------------------------------------------------------- */
 int gle_abi_version(void);
 /* replaces md.__init__ (md.py:56-130) for the state the hot path needs */
@@ -114,8 +123,9 @@ int gle_gamt(int32_t device, int64_t ml, int64_t ngw, int64_t nel, const double*
 /* md.setDyn (md.py:250-292): harmonic potential force -dyn.q used when no host force is given
  * (md.potforce, md.py:466-467).  dyn [nph][nph] as already processed by setDyn.  setDyn's
  * U diag(w^2) U^T reconstruction leaves roundoff in the entries the matrix does not couple; the
- * device copy drops every entry with |d_ij| <= 16 * 2^-52 * max_j |d_ij| (its sparsity pattern
- * then stays the physical one; the dropped part is at the dense product's own rounding level). */
+ * device copy drops every pair d_ij, d_ji with max(|d_ij|, |d_ji|) <= 16 * 2^-52 * max(max_k |d_ik|,
+ * max_k |d_jk|) (its sparsity pattern then stays the physical, symmetric one; the dropped part is at
+ * the dense product's own rounding level; the count is in gle_plan_detail). */
 int gle_set_dyn(gle_handle* h, const double* dyn);
 /* md.AddConstr (md.py:189) flattened: the DOF indices ApplyConstraint zeroes (md.py:782-794) */
 int gle_set_constraint(gle_handle* h, const int64_t* dofs, int64_t n);
@@ -161,6 +171,9 @@ int gle_noise_stream_begin(gle_handle* h, int32_t bath, int32_t is_complex, int6
 int gle_noise_stream_chunk(gle_handle* h, int32_t bath, int64_t w0, int64_t nw, const double* m_re,
                            const double* m_im, uint64_t seed, uint64_t traj_offset);
 int gle_noise_stream_end(gle_handle* h, int32_t bath);
+/* Release a begun stream's scratch without generating (an error between begin and end); the bath's
+ * previous noise stays.  gle_destroy releases any stream still open. */
+int gle_noise_stream_abort(gle_handle* h, int32_t bath);
 
 /* ---- stepping (md.vv, md.py:367-411) -------------------------------------------------- */
 /* Phase A of one step: F0 = Fpot(q_t) + sum_b bforce_b(t, id=0), current, half kick, drift.
@@ -218,6 +231,9 @@ int gle_power_spectrum(gle_handle* h, int32_t ngroup, const int64_t* group_len, 
  * comm: an RCCL communicator (ncclComm_t, e.g. from gle_comm_init) with one rank per handle, or
  * NULL for this handle's trajectories alone.  Collective: every rank of comm must call it. */
 int gle_reduce_current(gle_handle* h, void* comm, double* out);
+/* Sum n doubles (host buffer, in place) over the ranks of comm on the handle's stream, fp64 (the
+ * ensemble power spectra of md.Run, md.py:604-653).  comm NULL: no-op.  Collective. */
+int gle_comm_allreduce(gle_handle* h, void* comm, double* buf, int64_t n);
 /* RCCL communicator helpers for C callers without their own RCCL setup: rank 0 makes the id
  * (GLE_COMM_ID_BYTES opaque bytes), the caller distributes it (MPI, sockets, torch.distributed),
  * every rank then calls gle_comm_init with its own rank and HIP device. */
@@ -251,6 +267,14 @@ int gle_profile_read_chain(gle_handle* h, int64_t* nlaunch, double* total_ms, do
  * device memory in use, far-field mode actually chosen. */
 int gle_plan_info(gle_handle* h, int64_t* block_len, int64_t* far_items, int64_t* device_bytes,
                   int32_t* far_mode);
+/* Force the plan class (GLE_PLAN_*) before the plan is built (the first gle_set_state). */
+int gle_set_plan_class(gle_handle* h, int32_t plan_class);
+/* The plan actually built: its class (GLE_PLAN_SMALL_BATHS / _LARGE_BATHS), the waves per
+ * workgroup of the fused velocity stage (0 when the stages are not fused), the far-field GEMM
+ * workgroups per CU per chunk, the number of ladder levels, and the dyn entries gle_set_dyn
+ * dropped as reconstruction roundoff.  Requires a plan.  Any pointer may be NULL. */
+int gle_plan_detail(gle_handle* h, int32_t* plan_class, int32_t* fused_waves, double* cg_per_cu,
+                    int32_t* nlevel, int64_t* dyn_dropped);
 /* Memory-sum ladder levels: *nlevel = number of levels; for the first nmax levels the block length
  * P[l] and the blocks of that level issued since profiling was enabled (a block issued in pieces
  * counts its pieces' share).  Over a window of K steps a level in steady state issues K / P. */

@@ -32,7 +32,8 @@ EXPORTS = [
     "gle_profile_levels", "gle_step_work", "gle_reduce_current", "gle_comm_unique_id", "gle_comm_init",
     "gle_comm_destroy", "gle_record", "gle_record_zero", "gle_get_record", "gle_get_record_history",
     "gle_power_spectrum", "gle_set_record", "gle_set_record_history", "gle_noise_stream_begin",
-    "gle_noise_stream_chunk", "gle_noise_stream_end",
+    "gle_noise_stream_chunk", "gle_noise_stream_end", "gle_set_plan_class", "gle_plan_detail",
+    "gle_comm_allreduce", "gle_noise_stream_abort",
 ]
 
 REC_P, REC_Q, REC_F, REC_HIST = 1, 2, 4, 8
@@ -49,6 +50,8 @@ class gle_config(ctypes.Structure):
 
 FAR_AUTO, FAR_DIRECT, FAR_SPECTRAL = 0, 1, 2
 FAR_MODES = {"auto": FAR_AUTO, "direct": FAR_DIRECT, "spectral": FAR_SPECTRAL}
+PLAN_AUTO, PLAN_SMALL_BATHS, PLAN_LARGE_BATHS = 0, 1, 2
+PLAN_CLASSES = {"auto": PLAN_AUTO, "small": PLAN_SMALL_BATHS, "large": PLAN_LARGE_BATHS}
 
 
 _P = ctypes.c_void_p
@@ -93,11 +96,16 @@ _SIGS = {
     "gle_profile_levels": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32),
                                           ctypes.POINTER(ctypes.c_int32), _D]),
     "gle_step_work": (ctypes.c_int, [_P, _D, _D]),
+    "gle_set_plan_class": (ctypes.c_int, [_P, ctypes.c_int32]),
+    "gle_plan_detail": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32), _D,
+                                       ctypes.POINTER(ctypes.c_int32), _I64]),
     "gle_reduce_current": (ctypes.c_int, [_P, _P, _D]),
     "gle_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
     "gle_comm_init": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p,
                                      ctypes.POINTER(_P)]),
     "gle_comm_destroy": (ctypes.c_int, [_P]),
+    "gle_comm_allreduce": (ctypes.c_int, [_P, _P, _D, ctypes.c_int64]),
+    "gle_noise_stream_abort": (ctypes.c_int, [_P, ctypes.c_int32]),
     "gle_record": (ctypes.c_int, [_P, ctypes.c_int32]),
     "gle_record_zero": (ctypes.c_int, [_P, ctypes.c_int32]),
     "gle_get_record": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, _D]),
@@ -196,6 +204,7 @@ class Comm:
             raise GLEError("gle_comm_init failed (%s): %s" % (_ERRNAMES.get(rc, rc),
                                                               self.lib.gle_last_error(None).decode()))
         self.c = c
+        self.nranks, self.rank, self.device = int(nranks), int(rank), int(device)
 
     def close(self):
         if getattr(self, "c", None):
@@ -343,12 +352,18 @@ class Stepper:
         """Streamed device noise: factor_chunks yields (w0, M) with M (nw, nc, nc) real or complex."""
         self._chk(self.lib.gle_noise_stream_begin(self.h, int(bath), 1 if is_complex else 0, int(max_chunk)),
                   "gle_noise_stream_begin")
-        for w0, m in factor_chunks:
-            mre = _f64(np.real(m))
-            mim = _f64(np.imag(m)) if is_complex else None
-            self._chk(self.lib.gle_noise_stream_chunk(self.h, int(bath), int(w0), int(m.shape[0]), _ptr(mre),
-                                                      _ptr(mim), int(seed) & (2**64 - 1), int(traj_offset)),
-                      "gle_noise_stream_chunk")
+        try:
+            for w0, m in factor_chunks:
+                mre = _f64(np.real(m))
+                mim = _f64(np.imag(m)) if is_complex else None
+                self._chk(self.lib.gle_noise_stream_chunk(self.h, int(bath), int(w0), int(m.shape[0]), _ptr(mre),
+                                                          _ptr(mim), int(seed) & (2**64 - 1), int(traj_offset)),
+                          "gle_noise_stream_chunk")
+        except BaseException:
+            # a failed chunk or factor generator (e.g. LinAlgError) must not leave the spectrum
+            # scratch (1-2 GB per C5 bath) on the device
+            self.lib.gle_noise_stream_abort(self.h, int(bath))
+            raise
         self._chk(self.lib.gle_noise_stream_end(self.h, int(bath)), "gle_noise_stream_end")
 
     # --------------------------------------------------------------------------- stepping
@@ -440,6 +455,14 @@ class Stepper:
                   "gle_reduce_current")
         return out
 
+    def comm_allreduce(self, comm, values):
+        """Sum a float64 vector over the ranks of an RCCL Comm (None: unchanged) on this handle's
+        stream -- gle_comm_allreduce."""
+        buf = np.ascontiguousarray(np.asarray(values, dtype=np.float64)).copy()
+        self._chk(self.lib.gle_comm_allreduce(self.h, None if comm is None else comm.c, _ptr(buf), buf.size),
+                  "gle_comm_allreduce")
+        return buf
+
     def profile(self, enable=True, events=True, chain=False):
         """enable: count ladder blocks; events: also HIP-event timing of the dominant kernel;
         chain: per-workgroup device stamps of the per-step chain's launches."""
@@ -470,6 +493,20 @@ class Stepper:
         names = {v: k for k, v in FAR_MODES.items()}
         return {"block_len": int(a.value), "far_items": int(b.value), "device_bytes": int(c.value),
                 "far_mode": names.get(int(m.value), int(m.value))}
+
+    def set_plan_class(self, plan_class):
+        """Force the plan class ("auto", "small", "large"; gle_set_plan_class) before set_state."""
+        self._chk(self.lib.gle_set_plan_class(self.h, PLAN_CLASSES[plan_class]), "gle_set_plan_class")
+
+    def plan_detail(self):
+        """The built plan: class, fused-stage waves, far-field workgroups per CU, ladder levels."""
+        c, w, n = ctypes.c_int32(0), ctypes.c_int32(0), ctypes.c_int32(0)
+        cu, dd = ctypes.c_double(0), ctypes.c_int64(0)
+        self._chk(self.lib.gle_plan_detail(self.h, ctypes.byref(c), ctypes.byref(w), ctypes.byref(cu),
+                                           ctypes.byref(n), ctypes.byref(dd)), "gle_plan_detail")
+        names = {v: k for k, v in PLAN_CLASSES.items()}
+        return {"plan_class": names.get(int(c.value), int(c.value)), "fused_waves": int(w.value),
+                "cg_per_cu": float(cu.value), "nlevel": int(n.value), "dyn_dropped": int(dd.value)}
 
     def profile_levels(self):
         """[(P, blocks issued since profiling was enabled)] per ladder level."""

@@ -33,6 +33,12 @@ def ReadNetCDFVar(file, var):
         return np.array(f.variables[var].data, dtype=np.float64)
 
 
+def var_dims(file, var):
+    """Dimension names of one variable of an MD{j}.nc file."""
+    with netcdf_file(file, "r", mmap=False) as f:
+        return tuple(f.variables[var].dimensions)
+
+
 def has_var(file, var):
     with netcdf_file(file, "r", mmap=False) as f:
         return var in f.variables

@@ -207,6 +207,8 @@ struct gle_handle {
   bool fuse_bc = false;
   int ch_nw[3] = {4, 8, 4};            // chain workgroup waves per stage (A, B / fused BC, C)
   bool small_baths = false;            // every bath has nc <= 512 (the chain is latency-bound)
+  int plan_class = GLE_PLAN_AUTO;      // gle_set_plan_class: forces small_baths either way
+  double cg_per_cu = 0.5;              // far-field GEMM workgroups per CU per chunk (plan)
   int ch_drn = 1;                      // DOF-tile 16-column MFMA tiles
   int P0 = 1;          // first level block; near field = lags [1, 2 P0)
   int near_end = 1;
@@ -1557,7 +1559,10 @@ int freeze(gle_handle* h) {
   // -14 % per step), 4 for the larger baths (C5: +4 % at 8)
   int ncmax = 0;
   for (auto& b : h->baths) ncmax = std::max(ncmax, b.nc);
-  h->small_baths = ncmax <= 512;
+  h->small_baths = h->plan_class == GLE_PLAN_SMALL_BATHS ? true
+                  : h->plan_class == GLE_PLAN_LARGE_BATHS ? false
+                                                          : ncmax <= 512;
+  h->cg_per_cu = h->small_baths ? 0.5 : 2.0;
   const int P0 = h->cfg.block_len > 0 ? h->cfg.block_len : (h->small_baths ? 8 : 4);
   // fused-stage tile waves: 4 when the chain is latency-bound (C3: 53.3 vs 55.3 us/step with the
   // 1-workgroup-per-CU far-field chunks below), 8 for large baths (C5: 447 vs ~410 us at 4)
@@ -1817,6 +1822,7 @@ int freeze(gle_handle* h) {
         // far-field launches run at a lower MFMA occupancy); 2 per CU for large baths
         double per_cu = h->small_baths ? 0.5 : 2.0;
         if (const char* e = gle_env("GLE_CG_PER_CU")) per_cu = std::max(0.25, atof(e));
+        h->cg_per_cu = per_cu;
         const double want = (double)lv.cg.size() / (per_cu * ncu);
         const int64_t nch = gle_env("GLE_CG_CEIL") ? (int64_t)std::ceil(want - 1e-9) : (int64_t)want;
         lv.ncg_chunk = (int)std::max<int64_t>(1, std::min<int64_t>(nch, nslot));
@@ -2334,6 +2340,8 @@ int gle_destroy(gle_handle* h) {
   for (int i = 0; i < gle_handle::NBG; ++i)
     if (h->bg[i]) hipStreamSynchronize(h->bg[i]);
   if (h->stream) hipStreamSynchronize(h->stream);
+  // streamed-noise scratch (tmalloc, not in allocs) of a stream that was begun and never ended
+  for (int j = 0; j < (int)h->baths.size(); ++j) gle_noise_stream_abort(h, j);
   for (void* p : h->allocs) {
     bounds_del(p);
     hipFree(p);
@@ -2565,22 +2573,28 @@ int gle_set_dyn(gle_handle* h, const double* dyn) {
   // md.setDyn stores U diag(w^2) U^T (md.py:264-292): its eigen-reconstruction leaves roundoff
   // (<= ~10 eps of the row's largest entry at C3 / C5) in every entry the dynamical matrix does not
   // couple, so the block-sparse device copy would turn dense.  Entries at or below DYN_DROP_EPS
-  // unit roundoffs of their row's largest magnitude are dropped: per row the dropped part is at
-  // most nph * 16 eps * max|d_i.| * max|q|, the order of the dense product's own rounding bound.
+  // unit roundoffs of the larger of their two rows' largest magnitudes are dropped, d_ij and d_ji
+  // together (the pattern stays symmetric): per row the dropped part is at most
+  // nph * 16 eps * max(max|d_i.|, max|d_j.|) * max|q|, the order of the dense product's own
+  // rounding bound.  The count is reported by gle_plan_detail.
   constexpr double DYN_DROP_EPS = 16.0;
-  h->dyn_h.assign(dyn, dyn + h->nph * h->nph);
+  const int64_t n = h->nph;
+  h->dyn_h.assign(dyn, dyn + n * n);
   h->dyn_dropped = 0;
-  for (int64_t i = 0; i < h->nph; ++i) {
-    double* row = &h->dyn_h[(size_t)(i * h->nph)];
-    double mx = 0.0;
-    for (int64_t j = 0; j < h->nph; ++j) mx = std::max(mx, std::fabs(row[j]));
-    const double thr = DYN_DROP_EPS * 0x1p-52 * mx;
-    for (int64_t j = 0; j < h->nph; ++j)
-      if (row[j] != 0.0 && std::fabs(row[j]) <= thr) {
-        row[j] = 0.0;
-        ++h->dyn_dropped;
-      }
-  }
+  std::vector<double> rmax(n, 0.0);
+  for (int64_t i = 0; i < n; ++i)
+    for (int64_t j = 0; j < n; ++j) rmax[i] = std::max(rmax[i], std::fabs(h->dyn_h[(size_t)(i * n + j)]));
+  for (int64_t i = 0; i < n; ++i)
+    for (int64_t j = i; j < n; ++j) {
+      double& a = h->dyn_h[(size_t)(i * n + j)];
+      double& b = h->dyn_h[(size_t)(j * n + i)];
+      if (a == 0.0 && b == 0.0) continue;
+      const double thr = DYN_DROP_EPS * 0x1p-52 * std::max(rmax[i], rmax[j]);
+      if (std::max(std::fabs(a), std::fabs(b)) > thr) continue;
+      h->dyn_dropped += (a != 0.0) + (i != j && b != 0.0);
+      a = 0.0;
+      b = 0.0;
+    }
   std::vector<double> f = pack_frags(h->dyn_h.data(), 1, h->nph, h->nph, h->dyn_nrt, h->dyn_nks);
   int rc = dalloc_n(h, &h->d_dyn, f.size());
   if (!rc) rc = upload(h, h->d_dyn, f.data(), f.size() * 8);
@@ -2882,6 +2896,15 @@ void free_stream(Bath& b) {
   b.s_cap = 0;
 }
 }  // namespace
+
+int gle_noise_stream_abort(gle_handle* h, int32_t bath) {
+  int rc = check_bath(h, bath);
+  if (rc) return rc;
+  hipSetDevice(h->cfg.device);
+  HIPCHK(h, hipStreamSynchronize(h->stream));  // chunks in flight read the scratch
+  free_stream(h->baths[bath]);
+  return GLE_OK;
+}
 
 int gle_noise_stream_begin(gle_handle* h, int32_t bath, int32_t is_complex, int64_t max_chunk) {
   int rc = check_bath(h, bath);
@@ -3374,6 +3397,26 @@ int gle_plan_info(gle_handle* h, int64_t* block_len, int64_t* far_items, int64_t
   return GLE_OK;
 }
 
+int gle_set_plan_class(gle_handle* h, int32_t plan_class) {
+  if (!h) return GLE_ERR_ARG;
+  if (plan_class < GLE_PLAN_AUTO || plan_class > GLE_PLAN_LARGE_BATHS) return fail(h, GLE_ERR_ARG, "bad plan class");
+  if (h->frozen) return fail(h, GLE_ERR_STATE, "the plan is already built (set the plan class before gle_set_state)");
+  h->plan_class = plan_class;
+  return GLE_OK;
+}
+
+int gle_plan_detail(gle_handle* h, int32_t* plan_class, int32_t* fused_waves, double* cg_per_cu, int32_t* nlevel,
+                    int64_t* dyn_dropped) {
+  if (!h) return GLE_ERR_ARG;
+  if (!h->frozen) return fail(h, GLE_ERR_STATE, "no plan yet (gle_set_state builds it)");
+  if (plan_class) *plan_class = h->small_baths ? GLE_PLAN_SMALL_BATHS : GLE_PLAN_LARGE_BATHS;
+  if (fused_waves) *fused_waves = h->fuse_bc ? h->chBC.nw : 0;
+  if (cg_per_cu) *cg_per_cu = h->cg_per_cu;
+  if (nlevel) *nlevel = (int32_t)h->levels.size();
+  if (dyn_dropped) *dyn_dropped = h->dyn_dropped;
+  return GLE_OK;
+}
+
 // ---- ensemble reduce over RCCL (SURVEY.md 8b gle_reduce_current, 8e) ----------------------
 static_assert(GLE_COMM_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "RCCL unique-id size");
 
@@ -3406,25 +3449,31 @@ int gle_comm_destroy(void* comm) {
   return GLE_OK;
 }
 
-int gle_reduce_current(gle_handle* h, void* comm, double* out) {
-  if (!h || !out) return GLE_ERR_ARG;
-  const size_t n = 3 * h->baths.size();
-  if (n == 0) return GLE_OK;
-  int rc = gle_current_sums(h, out);  // this handle's [sum mean, sum mean^2, ntraj] per bath
-  if (rc || !comm) return rc;
+int gle_comm_allreduce(gle_handle* h, void* comm, double* buf, int64_t n) {
+  if (!h || (!buf && n > 0) || n < 0) return GLE_ERR_ARG;
+  if (!comm || n == 0) return GLE_OK;
   hipSetDevice(h->cfg.device);
   double* d = nullptr;
-  HIPCHK(h, tmalloc((void**)&d, n * 8));
-  hipError_t e = hipMemcpyAsync(d, out, n * 8, hipMemcpyHostToDevice, h->stream);
+  HIPCHK(h, tmalloc((void**)&d, (size_t)n * 8));
+  hipError_t e = hipMemcpyAsync(d, buf, (size_t)n * 8, hipMemcpyHostToDevice, h->stream);
   ncclResult_t r = ncclSuccess;
-  if (e == hipSuccess) r = ncclAllReduce(d, d, n, ncclDouble, ncclSum, (ncclComm_t)comm, h->stream);
-  if (e == hipSuccess && r == ncclSuccess) e = hipMemcpyAsync(out, d, n * 8, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) r = ncclAllReduce(d, d, (size_t)n, ncclDouble, ncclSum, (ncclComm_t)comm, h->stream);
+  if (e == hipSuccess && r == ncclSuccess) e = hipMemcpyAsync(buf, d, (size_t)n * 8, hipMemcpyDeviceToHost, h->stream);
   const hipError_t es = hipStreamSynchronize(h->stream);
   tfree(d);
   if (r != ncclSuccess) return fail(h, GLE_ERR_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
   if (e != hipSuccess || es != hipSuccess)
     return fail(h, GLE_ERR_HIP, std::string("reduce copies: ") + hipGetErrorString(e != hipSuccess ? e : es));
   return GLE_OK;
+}
+
+int gle_reduce_current(gle_handle* h, void* comm, double* out) {
+  if (!h || !out) return GLE_ERR_ARG;
+  const int64_t n = 3 * (int64_t)h->baths.size();
+  if (n == 0) return GLE_OK;
+  int rc = gle_current_sums(h, out);  // this handle's [sum mean, sum mean^2, ntraj] per bath
+  if (rc) return rc;
+  return gle_comm_allreduce(h, comm, out, n);
 }
 
 }  // extern "C"

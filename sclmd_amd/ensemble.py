@@ -18,12 +18,21 @@ def _dist():
     return dist if dist.is_available() and dist.is_initialized() else None
 
 
+def _is_gle_comm(group):
+    """An RCCL communicator of the C-ABI (sclmd_amd._native.Comm, gle_comm_init)."""
+    return group is not None and hasattr(group, "nranks") and hasattr(group, "c")
+
+
 def rank(group=None):
+    if _is_gle_comm(group):
+        return group.rank
     d = _dist()
     return d.get_rank(group) if d else 0
 
 
 def world_size(group=None):
+    if _is_gle_comm(group):
+        return group.nranks
     d = _dist()
     return d.get_world_size(group) if d else 1
 
@@ -41,7 +50,10 @@ def allreduce_sums(sums, group=None, device=None):
     single collective (fp64).  A no-op without an initialised process group.  device: the HIP
     device of this rank's stepper; with the nccl backend (RCCL) the tensor goes there and it
     becomes torch's current device (a script that never called torch.cuda.set_device would
-    otherwise put every rank's all-reduce on device 0)."""
+    otherwise put every rank's all-reduce on device 0).  A C-ABI communicator (md.comm given as a
+    _native.Comm) reduces through the stepper instead (md._allreduce, gle_comm_allreduce)."""
+    if _is_gle_comm(group):
+        raise TypeError("a gle RCCL communicator reduces through its stepper (md._allreduce)")
     d = _dist()
     sums = np.asarray(sums, dtype=np.float64)
     if d is None:

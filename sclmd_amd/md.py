@@ -608,9 +608,21 @@ class md:
 
     # ------------------------------------------------------------------------------ Run
     def _reduce(self, sums):
+        """Per-run current statistics of every rank: gle_reduce_current over the C-ABI's RCCL
+        communicator when comm is a _native.Comm, else one torch.distributed all-reduce."""
+        if isinstance(self.comm, _native.Comm):
+            return self._ensure_device().reduce_current(self.comm)
         from . import ensemble
 
         return ensemble.allreduce_sums(sums, self.comm, device=self._device_ordinal())
+
+    def _allreduce(self, values):
+        """Sum a vector over the ensemble's ranks (gle_comm_allreduce or torch.distributed)."""
+        if isinstance(self.comm, _native.Comm):
+            return self._ensure_device().comm_allreduce(self.comm, values)
+        from . import ensemble
+
+        return ensemble.allreduce_sums(values, self.comm, device=self._device_ordinal())
 
     def _device_ordinal(self):
         if self.device is not None:
@@ -749,6 +761,26 @@ class md:
         C.Write2NetCDFFile(f, self.qhis, "qhis", tr + ("mem", "nph"), units="")
         C.commit(f, tmp, self._ncname(id))
 
+    def _read_poweratomlist(self, fn):
+        """poweratomlist (natomlist, nmd, 2) from an MD{j}.nc file in either layout: this build's
+        ('nnmd', 'atomlist', 'two') or the reference's ('atomlist', 'nnmd', 'two') (md.py:742-744),
+        told apart by the variable's dimension names, and by its shape when those are unnamed."""
+        from . import checkpoint as C
+
+        arr = C.ReadNetCDFVar(fn, "poweratomlist")
+        dims = C.var_dims(fn, "poweratomlist")
+        na = len(self.atomlist)
+        if dims and dims[0] == "nnmd":
+            return np.transpose(arr, (1, 0, 2))
+        if dims and dims[0] == "atomlist":
+            return arr
+        if arr.shape == (na, self.nmd, 2):
+            return arr
+        if arr.shape == (self.nmd, na, 2):
+            return np.transpose(arr, (1, 0, 2))
+        raise ValueError("poweratomlist in %s has shape %s, dims %s: not (%d, %d, 2) in either layout"
+                         % (fn, arr.shape, dims, na, self.nmd))
+
     def _resume(self, j):
         """The reference's per-run file logic (md.py:506-567).  Returns the last finished piece
         (-1 for a new run) or None when run j is already complete."""
@@ -769,7 +801,7 @@ class md:
                 self._load_phis(ReadNetCDFVar(fn, "phis"), ReadNetCDFVar(fn, "qhis"))
                 self.power = ReadNetCDFVar(fn, "power")
                 if self.atomlist is not None:
-                    self.poweratomlist = np.transpose(ReadNetCDFVar(fn, "poweratomlist"), (1, 0, 2))
+                    self.poweratomlist = self._read_poweratomlist(fn)
                 qs, ps = ReadNetCDFVar(fn, "qs"), ReadNetCDFVar(fn, "ps")
                 self.qs = np.transpose(qs, (1, 0, 2)) if qs.ndim == 3 else qs
                 self.ps = np.transpose(ps, (1, 0, 2)) if ps.ndim == 3 else ps
@@ -782,7 +814,7 @@ class md:
                 if self.savep:
                     self.power = ReadNetCDFVar(fn, "power")
                     if self.atomlist is not None:
-                        self.poweratomlist = np.transpose(ReadNetCDFVar(fn, "poweratomlist"), (1, 0, 2))
+                        self.poweratomlist = self._read_poweratomlist(fn)
                 self.t = int(ReadNetCDFVar(fn, "t")[0])
                 return None
             raise RuntimeError("md.Run: ipie error in %s (ipie = %d)" % (fn, ipie))
@@ -880,18 +912,17 @@ class md:
 
     def power_spectra(self):
         """md.GetPower (md.py:351-360) on the device: functions.powerspecp of the recorded ps for all
-        DOFs and for each AddPowerSection group, averaged over this rank's trajectories (one
-        trajectory: exactly the reference's).  Returns (power (nmd, 2), [poweratomlist rows])."""
+        DOFs and for each AddPowerSection group, averaged over the whole ensemble: every trajectory
+        of every rank of comm (one trajectory on one rank: exactly the reference's).  Returns
+        (power (nmd, 2), [poweratomlist rows])."""
         st = self._ensure_device()
         self._apply_record()
         groups = [np.arange(self.nph)]
         if self.atomlist is not None:
             groups += [np.asarray(list(a), dtype=np.int64) for a in self.atomlist]
         spec = st.power_spectrum(groups)                  # (ngroup, ntraj, nmd): sum_k |DFT|^2
-        from . import ensemble  # ensemble mean over every rank's trajectories (a no-op reduce alone)
-
-        tot = ensemble.allreduce_sums(np.concatenate([spec.sum(axis=1).ravel(), [self.ntraj]]), self.comm,
-                                      device=self._device_ordinal())
+        # ensemble mean over every rank's trajectories (a no-op reduce alone)
+        tot = self._allreduce(np.concatenate([spec.sum(axis=1).ravel(), [self.ntraj]]))
         mean = tot[:-1].reshape(len(groups), self.nmd) / tot[-1]
         dw = 2.0 * np.pi / self.dt / self.nmd
         w = dw * np.arange(self.nmd)

@@ -66,6 +66,8 @@ def test_header_constants_match_binding():
     defs = {k: int(v) for k, v in re.findall(r"^#define\s+(GLE_\w+)\s+\(?(-?\d+)\)?", src, re.M)}
     mirror = {"GLE_REC_P": _native.REC_P, "GLE_REC_Q": _native.REC_Q, "GLE_REC_F": _native.REC_F,
               "GLE_REC_HIST": _native.REC_HIST, "GLE_PROFILE_EVENTS": _native.PROFILE_EVENTS,
-              "GLE_PROFILE_COUNT": _native.PROFILE_COUNT, "GLE_COMM_ID_BYTES": _native.COMM_ID_BYTES}
+              "GLE_PROFILE_COUNT": _native.PROFILE_COUNT, "GLE_COMM_ID_BYTES": _native.COMM_ID_BYTES,
+              "GLE_PLAN_AUTO": _native.PLAN_AUTO, "GLE_PLAN_SMALL_BATHS": _native.PLAN_SMALL_BATHS,
+              "GLE_PLAN_LARGE_BATHS": _native.PLAN_LARGE_BATHS}
     for k, v in mirror.items():
         assert defs.get(k) == v, (k, defs.get(k), v)

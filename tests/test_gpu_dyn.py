@@ -1,6 +1,7 @@
 """The device copy of the dynamical matrix (gle_set_dyn, include/hipgle.h) drops the roundoff that
 md.setDyn's U diag(w^2) U^T reconstruction (reference md.py:264-292) leaves in the entries the
-matrix does not couple: |d_ij| <= 16 * 2^-52 * max_j |d_ij|.  Checked here: the rule keeps exactly
+matrix does not couple: the pair d_ij, d_ji goes when max(|d_ij|, |d_ji|) <= 16 * 2^-52 *
+max(max_k |d_ik|, max_k |d_jk|) (symmetric: both entries or neither).  Checked here: the rule keeps exactly
 the physical pattern of the benched junctions (CPU), a run fed the setDyn-processed (dense) matrix
 is bit-identical to one fed the matrix with those entries zeroed, and both match the oracle's
 dense product to the parity tolerance (GPU)."""
@@ -15,8 +16,9 @@ RTOL_TRAJ = 1e-10   # as tests/test_gpu_parity.py
 
 def clean(dyn):
     d = np.array(dyn, dtype=float)
-    thr = DROP * np.max(np.abs(d), axis=1, keepdims=True)
-    d[(np.abs(d) <= thr)] = 0.0
+    rmax = np.max(np.abs(d), axis=1)
+    thr = DROP * np.maximum.outer(rmax, rmax)
+    d[np.maximum(np.abs(d), np.abs(d.T)) <= thr] = 0.0
     return d
 
 
@@ -55,6 +57,8 @@ def _run(g, dyn, nsteps):
         if c:
             st.set_constraint([d for r in c for d in r])
         st.set_state(g["p0"][None], g["q0"][None], 0)
+        dropped = st.plan_detail()["dyn_dropped"]
+        assert dropped == np.count_nonzero(dyn) - np.count_nonzero(clean(dyn)), dropped
         for i in range(int(g["nbath"])):
             st.set_history(i, None)
             st.set_noise(i, g["b%d_noise" % i][None])

@@ -9,7 +9,13 @@ phonon baths and a biased electron bath with exim, zeta1, zeta2 != 0, nc = 96-99
 trajectories, same protocol.  Three trajectories of each batch are checked against the batched
 oracle (oracle.GLEBatch, pinned to the reference-shaped oracle and the reference's fixtures):
 1e-9 relative on q, p and the heat currents.  The noise period is 1024 (the period does not enter
-the ladder plan; wrap-around is covered in test_gpu_md.py)."""
+the ladder plan; wrap-around is covered in test_gpu_md.py).
+
+The large-bath plan (any bath with nc > 512: first block length 4 with a direct P = 4 level, the
+8-wave fused velocity stage, 2 far-field GEMM workgroups per CU per chunk) is what bench.py runs at
+C5 (nc = 999 / 1002).  It is checked twice against the oracle: at nc = 522 (natom 522, ml = 512,
+picked by the automatic rule), and at the reduced C5 size with the plan class forced through the
+ABI (gle_set_plan_class), so both plan classes meet the same biased three-bath junction."""
 import numpy as np
 import pytest
 
@@ -30,7 +36,19 @@ def _obath(O, b, noise, dt, nmd):
     return O.Bath("ph", b.cids, b.kernel, noise, dt, nmd)
 
 
-def _run_vs_oracle(config, natom, B, check, t0=37, nst=540, nmd=1024, ml=1024, seed=1234, block_len=0):
+def _expected_levels(P0, ml, pmax=256):
+    """The ladder's block lengths: P = P0 2^l while 2P < ml, the last one at 4P >= ml or P = pmax."""
+    out, P = [], P0
+    while 2 * P < ml:
+        out.append(P)
+        if P >= pmax or 4 * P >= ml:
+            break
+        P *= 2
+    return out
+
+
+def _run_vs_oracle(config, natom, B, check, t0=37, nst=540, nmd=1024, ml=1024, seed=1234, block_len=0,
+                   plan_class="auto", expect_class="small"):
     from oracle import sclmd_oracle as O
     from sclmd_amd import _native as N
     from sclmd_amd import synthetic
@@ -45,6 +63,7 @@ def _run_vs_oracle(config, natom, B, check, t0=37, nst=540, nmd=1024, ml=1024, s
             else:
                 st.add_bath(N.GLE_BATH_PHONON, b.cids, b.kernel)
         st.set_dyn(dyn)
+        st.set_plan_class(plan_class)
         rng = np.random.default_rng(seed + 1)
         p = rng.normal(size=(B, nph)) * 1e-3
         q = rng.normal(size=(B, nph)) * 1e-3
@@ -58,6 +77,7 @@ def _run_vs_oracle(config, natom, B, check, t0=37, nst=540, nmd=1024, ml=1024, s
             hist.append(h[check])
             noise.append(n[check])
         info = st.plan_info()
+        detail = st.plan_detail()
         assert info["far_mode"] == "spectral", info
         st.profile(True)
         st.run(nst)
@@ -68,10 +88,14 @@ def _run_vs_oracle(config, natom, B, check, t0=37, nst=540, nmd=1024, ml=1024, s
     finally:
         st.close()
     assert t == t0 + nst
-    # every ladder level computed blocks inside the run (P = P0 ... 256 at ml = 1024)
+    # the plan class and what it sets: first block length, fused-stage waves, GEMM chunking
+    assert detail["plan_class"] == expect_class, detail
     P0 = info["block_len"]
-    assert P0 == (block_len or 8), info
-    assert [P for P, _ in levels] == [P0 << k for k in range((256 // P0).bit_length())], levels
+    assert P0 == (block_len or (8 if expect_class == "small" else 4)), info
+    assert detail["fused_waves"] == (4 if expect_class == "small" else 8), detail
+    assert detail["cg_per_cu"] == (0.5 if expect_class == "small" else 2.0), detail
+    # every ladder level computed blocks inside the run (P = P0 ... 256 at ml = 1024)
+    assert [P for P, _ in levels] == _expected_levels(P0, ml), levels
     assert all(bl >= 1.0 for _, bl in levels), levels
     ob = [_obath(O, b, noise[i], dt, nmd) for i, b in enumerate(baths)]
     sim = O.GLEBatch(nph, dt, nmd, ob, dyn, ntr=len(check))
@@ -97,3 +121,24 @@ def test_c3_bench_plan_vs_oracle(block_len):
 def test_c5_reduced_biased_vs_oracle():
     sim = _run_vs_oracle("C5", 96, 32, [0, 17, 31])
     assert sum(b.biased() for b in sim.baths) == 1
+
+
+def test_c5_reduced_large_plan_forced_vs_oracle():
+    """The large-bath plan at nc ~ 96: P0 = 4 (direct P = 4 level, spectral P = 8 ... 256), 8-wave
+    fused stage, 2 GEMM workgroups per CU per chunk."""
+    sim = _run_vs_oracle("C5", 96, 32, [0, 17, 31], plan_class="large", expect_class="large")
+    assert sum(b.biased() for b in sim.baths) == 1
+
+
+def test_c5_nc522_large_plan_vs_oracle():
+    """nc = 522 > 512 on all three baths (two phonon baths and the biased electron bath): the plan
+    class the automatic rule picks at C5 (nc = 999 / 1002), ml = 512 (levels P = 4 ... 128, the P =
+    128 level fires at 128 and 256), 300 steps from an unaligned t0 and a random history."""
+    sim = _run_vs_oracle("C5", 522, 32, [0, 17, 31], ml=512, nst=300, expect_class="large")
+    assert [b.nc for b in sim.baths] == [522, 522, 522]
+    assert sum(b.biased() for b in sim.baths) == 1
+
+
+def test_c3_small_plan_forced_matches_auto_expectation():
+    """Forcing the small-bath class where it is already the automatic choice changes nothing."""
+    _run_vs_oracle("C3", 48, 16, [0, 15], nst=540, plan_class="small", expect_class="small")

@@ -73,3 +73,46 @@ def test_md_streamed_noise_covariance_reduced_c5():
         theory = scale ** 2 * (ap[0] + ap[h] + 2.0 * ap[1:h].sum(axis=0))
         assert np.max(np.abs(emp - theory)) < 0.06 * np.max(np.diag(theory)), (i, b.kind)
     m.close()
+
+
+def test_stream_failure_releases_scratch_and_recovers():
+    """A factor generator that raises between gle_noise_stream_begin and _end: the
+    exception reaches the caller, gle_noise_stream_abort releases the spectrum scratch (device
+    memory returns to its level before begin), and a later complete stream gives the same noise as
+    a fresh handle."""
+    import torch
+
+    from sclmd_amd import _native as N
+    from sclmd_amd import synthetic
+
+    rng = np.random.default_rng(4)
+    nmd, B = 4096, 64  # spectrum scratch 2049 x 64 x 64 doubles = 67 MB: a leak shows in mem_get_info
+    b = synthetic.make_phbath(300.0, list(range(64)), 8, nmd, rng, nw=40)
+    fac = b.noise_factor().scaled()
+
+    def chunks(fail_at=None):
+        for w0 in range(0, fac.shape[0], 64):
+            if fail_at is not None and w0 >= fail_at:
+                raise np.linalg.LinAlgError("factorisation failed (test)")
+            yield w0, fac[w0:w0 + 64]
+
+    def fresh():
+        st = N.Stepper(b.nc, B, nmd, synthetic.DT, 0)
+        st.add_bath(N.GLE_BATH_PHONON, np.arange(b.nc), np.zeros((1, b.nc, b.nc)))
+        return st
+
+    st = fresh()
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info(0)[0]
+    with pytest.raises(np.linalg.LinAlgError):
+        st.noise_stream(0, chunks(fail_at=640), False, seed=11, max_chunk=64)
+    torch.cuda.synchronize()
+    assert torch.cuda.mem_get_info(0)[0] >= free0 - (8 << 20)  # 67 MB scratch released (slack 8 MB)
+    st.noise_stream(0, chunks(), False, seed=11, max_chunk=64)
+    got = st.get_noise(0)
+    st.close()
+    ref = fresh()
+    ref.noise_stream(0, chunks(), False, seed=11, max_chunk=64)
+    want = ref.get_noise(0)
+    ref.close()
+    assert np.array_equal(got, want)

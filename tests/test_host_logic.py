@@ -213,3 +213,49 @@ def test_streamed_noise_factors_cover_the_positive_part(kind):
             want = ref[w0 + j] @ np.conj(ref[w0 + j]).T
             assert np.max(np.abs(got - want)) <= 1e-12 * max(np.max(np.abs(want)), 1e-300) + 1e-300
     assert "dense" in kinds and ("shared" in kinds or "zero" in kinds), kinds
+
+
+@pytest.mark.parametrize("layout", ["build", "reference"])
+def test_poweratomlist_resume_reads_either_layout(tmp_path, layout):
+    """md._read_poweratomlist: this build writes ('nnmd', 'atomlist', 'two'), the
+    reference ('atomlist', 'nnmd', 'two') (md.py:742-744); both read back as (natomlist, nmd, 2)."""
+    from sclmd_amd import checkpoint as C
+    from sclmd_amd import md as MD
+
+    nmd, na = 16, 3
+    m = MD.md(0.38, nmd, 300.0, verbose=False)
+    m.AddPowerSection([[0, 1], [2], [3, 4, 5]])
+    want = np.random.default_rng(1).normal(size=(na, nmd, 2))
+    fn = str(tmp_path / "MD0.nc")
+    f, tmp = C.open_for_write(fn)
+    # NetCDF classic allows only a leading record dimension: the reference-layout file (written by
+    # netCDF4 there) gets a fixed nnmd here
+    f.createDimension("nnmd", None if layout == "build" else nmd)
+    f.createDimension("atomlist", na)
+    f.createDimension("two", 2)
+    if layout == "build":
+        C.Write2NetCDFFile(f, np.transpose(want, (1, 0, 2)), "poweratomlist", ("nnmd", "atomlist", "two"))
+    else:
+        C.Write2NetCDFFile(f, want, "poweratomlist", ("atomlist", "nnmd", "two"))
+    C.commit(f, tmp, fn)
+    assert np.array_equal(m._read_poweratomlist(fn), want)
+
+
+def test_cpu_baseline_times_a_biased_electron_bath():
+    """bench.cpu_baseline builds electron baths as electron baths: the biased
+    C5 ebath's bias terms are part of the timed reference-shaped step."""
+    import bench
+    from sclmd_amd import synthetic
+
+    dyn, _, baths, meta = synthetic.junction("C5", natom=24, ml=8, nmd=32, nw=40)
+    rng = np.random.default_rng(0)
+    bh = []
+    for b in baths:
+        n = rng.normal(size=(32, b.nc)) * 1e-3
+        if b.kind == "ebath":
+            bh.append(("e", b.cids, b.kernel, n, dict(bias=b.bias, exim=b.exim, zeta1=b.zeta1, zeta2=b.zeta2)))
+        else:
+            bh.append(("ph", b.cids, b.kernel, n, {}))
+    assert [k for k, *_ in bh] == ["ph", "ph", "e"]
+    r = bench.cpu_baseline(bh, dyn, meta["nph"], meta["dt"], 32, budget_s=0.3, nsample=3)
+    assert r["value"] > 0 and r["kind"] == "port" and len(r["samples"]) == 3
