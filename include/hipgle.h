@@ -90,6 +90,8 @@ int gle_destroy(gle_handle* h);
 /* last error of h, or of the last failed gle_create when h == NULL */
 const char* gle_last_error(const gle_handle* h);
 int gle_device_count(int32_t* count);
+/* Free and total device memory of HIP device `device` (bytes).  Errors: gle_last_error(NULL). */
+int gle_device_mem_info(int32_t device, int64_t* free_bytes, int64_t* total_bytes);
 
 /* ---- system / baths ------------------------------------------------------------------- */
 /* md.AddBath (md.py:167-183) + the bath's bforce parameters (baths.py:224-255, 448-458).

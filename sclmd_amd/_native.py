@@ -33,7 +33,7 @@ EXPORTS = [
     "gle_comm_destroy", "gle_record", "gle_record_zero", "gle_get_record", "gle_get_record_history",
     "gle_power_spectrum", "gle_set_record", "gle_set_record_history", "gle_noise_stream_begin",
     "gle_noise_stream_chunk", "gle_noise_stream_end", "gle_set_plan_class", "gle_plan_detail",
-    "gle_comm_allreduce", "gle_noise_stream_abort",
+    "gle_comm_allreduce", "gle_noise_stream_abort", "gle_device_mem_info",
 ]
 
 REC_P, REC_Q, REC_F, REC_HIST = 1, 2, 4, 8
@@ -64,6 +64,7 @@ _SIGS = {
     "gle_destroy": (ctypes.c_int, [_P]),
     "gle_last_error": (ctypes.c_char_p, [_P]),
     "gle_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int32)]),
+    "gle_device_mem_info": (ctypes.c_int, [ctypes.c_int32, _I64, _I64]),
     "gle_add_bath": (ctypes.c_int, [_P, ctypes.c_int32, _I64, ctypes.c_int64, ctypes.c_int64, _D,
                                     ctypes.c_double, _D, _D, _D, ctypes.POINTER(ctypes.c_int32)]),
     "gle_add_bath_gmem": (ctypes.c_int, [_P, _I64, ctypes.c_int64, ctypes.c_int64, _D, ctypes.c_int64, _D,
@@ -150,6 +151,16 @@ def _f64(a, shape=None):
     if shape is not None and a.shape != tuple(shape):
         a = a.reshape(shape)
     return a
+
+
+def device_mem_info(device=0):
+    """(free, total) bytes of HIP device `device` (gle_device_mem_info)."""
+    lib = load()
+    fr, tot = ctypes.c_int64(0), ctypes.c_int64(0)
+    rc = lib.gle_device_mem_info(int(device), ctypes.byref(fr), ctypes.byref(tot))
+    if rc != 0:
+        raise GLEError("gle_device_mem_info failed: %s" % lib.gle_last_error(None).decode())
+    return int(fr.value), int(tot.value)
 
 
 def device_count():

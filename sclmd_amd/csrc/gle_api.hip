@@ -2180,6 +2180,17 @@ const char* gle_last_error(const gle_handle* h) {
   return h ? h->err.c_str() : g_create_error.c_str();
 }
 
+int gle_device_mem_info(int32_t device, int64_t* free_bytes, int64_t* total_bytes) {
+  if (!free_bytes || !total_bytes) return fail(nullptr, GLE_ERR_ARG, "null argument");
+  if (hipSetDevice(device) != hipSuccess) return fail(nullptr, GLE_ERR_HIP, "gle_device_mem_info: no such device");
+  size_t fr = 0, tot = 0;
+  const hipError_t e = hipMemGetInfo(&fr, &tot);
+  if (e != hipSuccess) return fail(nullptr, GLE_ERR_HIP, std::string("hipMemGetInfo: ") + hipGetErrorString(e));
+  *free_bytes = (int64_t)fr;
+  *total_bytes = (int64_t)tot;
+  return GLE_OK;
+}
+
 int gle_device_count(int32_t* count) {
   int n = 0;
   hipError_t e = hipGetDeviceCount(&n);

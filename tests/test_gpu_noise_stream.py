@@ -80,8 +80,6 @@ def test_stream_failure_releases_scratch_and_recovers():
     exception reaches the caller, gle_noise_stream_abort releases the spectrum scratch (device
     memory returns to its level before begin), and a later complete stream gives the same noise as
     a fresh handle."""
-    import torch
-
     from sclmd_amd import _native as N
     from sclmd_amd import synthetic
 
@@ -102,12 +100,12 @@ def test_stream_failure_releases_scratch_and_recovers():
         return st
 
     st = fresh()
-    torch.cuda.synchronize()
-    free0 = torch.cuda.mem_get_info(0)[0]
+    st.sync()
+    free0 = N.device_mem_info(0)[0]
     with pytest.raises(np.linalg.LinAlgError):
         st.noise_stream(0, chunks(fail_at=640), False, seed=11, max_chunk=64)
-    torch.cuda.synchronize()
-    assert torch.cuda.mem_get_info(0)[0] >= free0 - (8 << 20)  # 67 MB scratch released (slack 8 MB)
+    st.sync()
+    assert N.device_mem_info(0)[0] >= free0 - (8 << 20)  # 67 MB scratch released (slack 8 MB)
     st.noise_stream(0, chunks(), False, seed=11, max_chunk=64)
     got = st.get_noise(0)
     st.close()

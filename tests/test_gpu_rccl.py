@@ -118,24 +118,23 @@ def _free_port():
 
 def test_md_run_torch_nccl_world1_matches_plain(tmp_path):
     """torch.distributed nccl (RCCL) process group of one rank: md.Run's reduce is a real RCCL
-    all-reduce on the stepper's device (ensemble.allreduce_sums), equal to the run without a group."""
-    import torch
-    import torch.distributed as dist
+    all-reduce on the stepper's device (ensemble.allreduce_sums), equal to the run without a group.
+    Run in a child process that initialises torch's HIP context before the library's (as a torchrun
+    rank does); the parent runs the same md without a group and compares."""
+    import json
+    import subprocess
+    import sys
 
     b = _run_md(tmp_path, None, "plain")
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ["MASTER_PORT"] = str(_free_port())
-    torch.cuda.set_device(0)
-    dist.init_process_group("nccl", rank=0, world_size=1)
-    try:
-        assert dist.get_backend() == "nccl"
-        from sclmd_amd import ensemble
-
-        v = np.array([1.5, -2.0, 3.25])
-        assert np.array_equal(ensemble.allreduce_sums(v, device=0), v)
-        a = _run_md(tmp_path, None, "nccl")
-    finally:
-        dist.destroy_process_group()
-    for x, y in zip(a[:4], b[:4]):
-        assert np.array_equal(x, y)
-    assert a[5] == b[5]
+    out = tmp_path / "nccl.npz"
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "nccl_child.py"), str(tmp_path),
+                        str(out)], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    info = json.loads(r.stdout.strip().splitlines()[-1])
+    assert info["backend"] == "nccl" and info["world"] == 1 and info["allreduce_identity"]
+    a = np.load(out)
+    for k, y in zip(["kap", "p", "q", "power"], b[:4]):
+        assert np.array_equal(a[k], y), k
+    assert all(np.array_equal(a["row%d" % i], y) for i, y in enumerate(b[4]))
+    assert json.loads(str(a["files"])) == b[5]
