@@ -3,7 +3,7 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 CXXFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -Wno-unused-value
 SRC := sclmd_amd/csrc/gle_api.hip sclmd_amd/csrc/gle_kernels.hip sclmd_amd/csrc/gle_chain.hip sclmd_amd/csrc/gle_gmem.hip
-HDR := sclmd_amd/csrc/gle_internal.h include/hipgle.h
+HDR := sclmd_amd/csrc/gle_internal.h sclmd_amd/csrc/gle_cgemm.h include/hipgle.h
 LDLIBS := -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 OBJDIR := build/rel
 OBJ := $(patsubst sclmd_amd/csrc/%.hip,$(OBJDIR)/%.o,$(SRC))

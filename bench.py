@@ -200,7 +200,8 @@ def main():
     st.sync()
     setup_s = time.perf_counter() - t_setup
     plan = st.plan_info()
-    log("[bench] rank %d setup %.1fs plan %s" % (rank, setup_s, plan))
+    detail = st.plan_detail()
+    log("[bench] rank %d setup %.1fs plan %s %s" % (rank, setup_s, plan, detail))
 
     def barrier():
         if dist is not None:
@@ -256,11 +257,15 @@ def main():
     window_levels = st.profile_levels()
     # roofline: HIP events around every launch of the dominant kernel over a second window of the
     # same K steps right after the timed one (same steady state, same piece schedule phase); the
-    # events add launch-queue packets (1-6 % per step), so the headline window runs without them
-    st.profile(True, events=True)
-    m.steps(args.steps)
-    st.sync()
-    prof = st.profile_read()
+    # events add launch-queue packets (1-6 % per step), so the headline window runs without them.
+    # Fused schedule: the far-field GEMMs ride in the chain launches, which the third window times.
+    if not detail["far_fused"]:
+        st.profile(True, events=True)
+        m.steps(args.steps)
+        st.sync()
+        prof = st.profile_read()
+    else:
+        prof = {"launches": 0}
     # the chain's own per-workgroup stamps in a third window of the same K steps (apart from the
     # far-field timing, whose launches the chain stamps would otherwise share the window with)
     st.profile(True, events=False, chain=True)
@@ -299,7 +304,8 @@ def main():
                                                 meta["ml"], meta["nmd"], args.ntraj),
                    "ntraj_per_gpu": args.ntraj, "ntraj_total": world * args.ntraj,
                    "block_len": plan["block_len"], "far_mode": plan["far_mode"],
-                   "parallelism": "ensemble-dp%d" % world},
+                   "far_schedule": "fused" if detail["far_fused"] else "background",
+                   "plan_class": detail["plan_class"], "parallelism": "ensemble-dp%d" % world},
         "value_per_gpu": value / world,
         "setup_s": setup_s,
         "fill_steps": fill,
@@ -353,7 +359,32 @@ def main():
                      "timing": "device timestamps" if prof["launches_device"] == prof["launches"] else "HIP events",
                      "algorithmic_flops_per_launch": fl, "algorithmic_bytes_per_launch": by})
         res["roofline"] = roof
-    if prof.get("chain_launches", 0) > 0 and plan["far_mode"] == "spectral":
+    if detail["far_fused"] and prof.get("chain_launches", 0) > 0:
+        # fused schedule: every launch of the step is the chain kernel (md.vv stages plus the
+        # spectral levels' far-field GEMM items), timed by its own per-workgroup device stamps in the
+        # third window; algorithmic flops = the chain products + the items' share of their blocks
+        cms = prof["chain_ms"]
+        nl = prof["chain_launches"]
+        roof = {"bound": "mfma", "achieved": prof["chain_flops"] / (cms * 1e-3) / 1e12, "peak": FP64_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s"}
+        roof["frac"] = roof["achieved"] / roof["peak"]
+        roof["traffic"] = None
+        try:
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+            if (tj.get("config") == args.config and tj.get("ntraj") == args.ntraj
+                    and tj.get("kernel", "").startswith("chain_kernel") and tj.get("far_schedule") == "fused"):
+                roof["traffic"] = tj.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
+        roof.update({"kernel": "chain_kernel (fused: md.vv stage A / velocity stage + far-field GEMM items of the "
+                               "spectral ladder levels)",
+                     "window": "third window of the same %d steps" % args.steps, "launches": nl,
+                     "avg_launch_ms": cms / nl, "us_per_step": cms / args.steps * 1e3,
+                     "timing": "device timestamps (per-workgroup stores)",
+                     "algorithmic_flops_per_launch": prof["chain_flops"] / nl})
+        res["roofline"] = roof
+    if prof.get("chain_launches", 0) > 0 and plan["far_mode"] == "spectral" and not detail["far_fused"]:
         # the per-step chain (md.vv stages, the step's critical path) in the same window, timed by
         # its own device timestamps: algorithmic flops of its products / its kernel durations;
         # us_per_step = chain kernel time per step (beside the far field, so > its time alone)

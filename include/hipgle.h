@@ -273,10 +273,12 @@ int gle_plan_info(gle_handle* h, int64_t* block_len, int64_t* far_items, int64_t
 int gle_set_plan_class(gle_handle* h, int32_t plan_class);
 /* The plan actually built: its class (GLE_PLAN_SMALL_BATHS / _LARGE_BATHS), the waves per
  * workgroup of the fused velocity stage (0 when the stages are not fused), the far-field GEMM
- * workgroups per CU per chunk, the number of ladder levels, and the dyn entries gle_set_dyn
- * dropped as reconstruction roundoff.  Requires a plan.  Any pointer may be NULL. */
+ * workgroups per CU per chunk (background schedule), the number of ladder levels, the dyn entries
+ * gle_set_dyn dropped as reconstruction roundoff, and whether the spectral levels' GEMM items ride
+ * in the per-step chain launches (1, the fused schedule) or run on background streams (0).
+ * Requires a plan.  Any pointer may be NULL. */
 int gle_plan_detail(gle_handle* h, int32_t* plan_class, int32_t* fused_waves, double* cg_per_cu,
-                    int32_t* nlevel, int64_t* dyn_dropped);
+                    int32_t* nlevel, int64_t* dyn_dropped, int32_t* far_fused);
 /* Memory-sum ladder levels: *nlevel = number of levels; for the first nmax levels the block length
  * P[l] and the blocks of that level issued since profiling was enabled (a block issued in pieces
  * counts its pieces' share).  Over a window of K steps a level in steady state issues K / P. */

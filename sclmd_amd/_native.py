@@ -99,7 +99,7 @@ _SIGS = {
     "gle_step_work": (ctypes.c_int, [_P, _D, _D]),
     "gle_set_plan_class": (ctypes.c_int, [_P, ctypes.c_int32]),
     "gle_plan_detail": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32), _D,
-                                       ctypes.POINTER(ctypes.c_int32), _I64]),
+                                       ctypes.POINTER(ctypes.c_int32), _I64, ctypes.POINTER(ctypes.c_int32)]),
     "gle_reduce_current": (ctypes.c_int, [_P, _P, _D]),
     "gle_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
     "gle_comm_init": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p,
@@ -511,13 +511,14 @@ class Stepper:
 
     def plan_detail(self):
         """The built plan: class, fused-stage waves, far-field workgroups per CU, ladder levels."""
-        c, w, n = ctypes.c_int32(0), ctypes.c_int32(0), ctypes.c_int32(0)
+        c, w, n, ff = ctypes.c_int32(0), ctypes.c_int32(0), ctypes.c_int32(0), ctypes.c_int32(0)
         cu, dd = ctypes.c_double(0), ctypes.c_int64(0)
         self._chk(self.lib.gle_plan_detail(self.h, ctypes.byref(c), ctypes.byref(w), ctypes.byref(cu),
-                                           ctypes.byref(n), ctypes.byref(dd)), "gle_plan_detail")
+                                           ctypes.byref(n), ctypes.byref(dd), ctypes.byref(ff)), "gle_plan_detail")
         names = {v: k for k, v in PLAN_CLASSES.items()}
         return {"plan_class": names.get(int(c.value), int(c.value)), "fused_waves": int(w.value),
-                "cg_per_cu": float(cu.value), "nlevel": int(n.value), "dyn_dropped": int(dd.value)}
+                "cg_per_cu": float(cu.value), "nlevel": int(n.value), "dyn_dropped": int(dd.value),
+                "far_fused": bool(ff.value)}
 
     def profile_levels(self):
         """[(P, blocks issued since profiling was enabled)] per ladder level."""

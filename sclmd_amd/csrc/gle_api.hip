@@ -140,6 +140,18 @@ struct Level {
   int64_t pend_block = INT64_MIN;  // block whose pieces are still being issued
   int64_t pend_t0 = 0;
   int next_piece = 0;
+  // fused schedule (spectral levels of 4-wave chain plans): block k+1's GEMM items ride in the
+  // chain launches of the steps kP .. kP+P-1 (split-major item order, k-splits accumulate in
+  // place), its newest segment is transformed by a launch before A(kP), its inverse transform
+  // runs before A((k+1)P)
+  bool fused = false;
+  std::vector<CgItem> fcg;       // fused items: nsplit k-splits x nout products, split-major
+  CgItem* d_fcg = nullptr;
+  int64_t nout = 0;              // products (bath, f, g, row group, column tile) per split
+  int nsplit = 1;
+  double fcg_flops = 0;          // algorithmic flops per block (= cg_flops)
+  int64_t fblock = INT64_MIN;    // block whose items are in flight in the fused schedule
+  int64_t fT = 0;                // first step of its window
 };
 
 }  // namespace
@@ -207,6 +219,9 @@ struct gle_handle {
   bool fuse_bc = false;
   int ch_nw[3] = {4, 8, 4};            // chain workgroup waves per stage (A, B / fused BC, C)
   bool small_baths = false;            // every bath has nc <= 512 (the chain is latency-bound)
+  bool far_fused = false;              // spectral levels ride in the chain launches (fused schedule)
+  double far_afrac = 0.5;              // share of a step's far items in its first chain launch
+  int64_t far_max_items = 0;           // most far items one chain launch can carry
   int plan_class = GLE_PLAN_AUTO;      // gle_set_plan_class: forces small_baths either way
   double cg_per_cu = 0.5;              // far-field GEMM workgroups per CU per chunk (plan)
   int ch_drn = 1;                      // DOF-tile 16-column MFMA tiles
@@ -719,8 +734,39 @@ void run_op(gle_handle* h, Op& op, hipStream_t s, const StepArgs& ta, bool profi
   launch_reduce(op.d_ritems, (int)op.ritems.size(), op.max_elems, ta, s);
 }
 
-// One chain launch; profiled (HIP events, same stream) when the ladder has no levels.
-void run_chain(gle_handle* h, int stage, Chain& c, const StepArgs& ta, int mode, bool profile) {
+// The fused schedule's far-field items for chain launch `part` of step t (0: the step's first
+// launch, 1: its velocity-stage launch, 2: none): per fused level with a block in flight, step
+// i = t - fT of its window carries items [i n / P, (i + 1) n / P), the first far_afrac of them in
+// part 0.  Returns the algorithmic flops of the items (block flops x their share).
+double far_ranges(gle_handle* h, int64_t t, int part, StepArgs& ta) {
+  ta.nfar = 0;
+  double fl = 0.0;
+  if (!h->far_fused || h->dbg_no_ladder || part > 1) return fl;
+  for (size_t l = 0; l < h->levels.size(); ++l) {
+    Level& lv = h->levels[l];
+    if (!lv.fused || lv.fblock == INT64_MIN) continue;
+    const int64_t i = t - lv.fT;
+    if (i < 0 || i >= lv.P) continue;
+    const int64_t n = (int64_t)lv.fcg.size();
+    const int64_t lo = i * n / lv.P, hi = (i + 1) * n / lv.P;
+    const int64_t mid = lo + (int64_t)((double)(hi - lo) * h->far_afrac + 0.5);
+    const int64_t first = part == 0 ? lo : mid, count = part == 0 ? mid - lo : hi - mid;
+    if (count <= 0) continue;
+    FarRange& f = ta.far[ta.nfar++];
+    f.items = lv.d_fcg;
+    f.tseg = lv.fT / lv.P;
+    f.first = (int32_t)first;
+    f.count = (int32_t)count;
+    const double share = (double)count / (double)n;
+    fl += lv.fcg_flops * share;
+    if (h->prof) h->prof_blocks[l] += share;
+  }
+  return fl;
+}
+
+// One chain launch (with the fused schedule's far items of its part); profiled (HIP events, same
+// stream) when the ladder has no levels.
+void run_chain(gle_handle* h, int stage, Chain& c, const StepArgs& ta, int mode, bool profile, int part) {
   hipEvent_t e1 = nullptr;
   if (profile && h->prof_ev && !c.tiles.empty()) {
     if (h->ev_used + 2 > h->ev.size()) drain_profile(h);
@@ -729,12 +775,15 @@ void run_chain(gle_handle* h, int stage, Chain& c, const StepArgs& ta, int mode,
     h->ev_used += 2;
   }
   StepArgs tc = ta;
-  if (h->prof_ch && h->d_ctst && !c.tiles.empty() && c.tiles.size() <= h->ctst_tiles) {
+  const double far_flops = far_ranges(h, ta.t, c.nw == 4 ? part : 2, tc);
+  int64_t nfar = 0;
+  for (int r = 0; r < tc.nfar; ++r) nfar += tc.far[r].count;
+  if (h->prof_ch && h->d_ctst && !c.tiles.empty() && c.tiles.size() + nfar <= h->ctst_tiles) {
     if (h->ctst_used >= h->ctst_cap) drain_profile(h);
     tc.ts = h->d_ctst + 2 * h->ctst_used * h->ctst_tiles;
     h->ctst_used += 1;
-    h->ctst_n.push_back((int)c.tiles.size());
-    h->prof_ch_flops += c.flops;
+    h->ctst_n.push_back((int)(c.tiles.size() + nfar));
+    h->prof_ch_flops += c.flops + far_flops;
   }
   launch_chain(stage, c.nw, h->ch_drn, c.lds, c.d, (int)c.tiles.size(), h->d_sd, tc, mode, h->stream);
   if (e1) {
@@ -1539,6 +1588,88 @@ int apply_record(gle_handle* h) {
   return upload(h, h->d_sd, &sd, sizeof(sd));
 }
 
+// Fused far-field schedule (spectral levels, every chain stage in 4-wave workgroups): per level the
+// block's GEMM products (bath, f, Gauss part, 64-row group, column tile) are cut into nsplit k-splits
+// of about FAR_KS k-steps, ordered split-major; step i of the block window carries items
+// [i n / P, (i + 1) n / P) in its chain launches (A the first part, the velocity stage the rest).
+// Every launch's range is at most nout items long (nsplit <= P), so the k-splits of one product fall
+// into successive launches: the first stores, the others add (deterministic, no partial planes).
+int plan_far_fused(gle_handle* h) {
+  h->far_fused = false;
+  h->far_max_items = 0;
+  bool any = false;
+  for (auto& lv : h->levels) any |= lv.spectral;
+  const bool nw4 = h->chA[0].nw == 4 && h->chA[1].nw == 4 && h->chB[0].nw == 4 && h->chB[1].nw == 4 &&
+                   h->chC.nw == 4 && (!h->fuse_bc || h->chBC.nw == 4);
+  // measured r03 (C3, one MI355X, same box): 83 us/step fused vs 50 us background -- the items,
+  // HBM-latency-bound at the chain's register budget, finish after the chain tiles and add to
+  // every launch; the background schedule overlaps them with the chain across launches.  Off by
+  // default (GLE_FAR_FUSED=1 in the experiment build).
+  if (!any || !nw4 || !gle_env("GLE_FAR_FUSED")) return GLE_OK;
+  int ks_target = 32;  // k-steps per item: ~4 x 32 MFMAs per wave, the length of a chain tile's products
+  if (const char* e = gle_env("GLE_FAR_KS")) ks_target = std::max(4, atoi(e));
+  const int64_t B = h->B;
+  for (auto& lv : h->levels) {
+    if (!lv.spectral) continue;
+    int nsplit = 1;
+    for (size_t j = 0; j < h->baths.size(); ++j)
+      if (lv.lb[j].active) nsplit = std::max(nsplit, (lv.lb[j].M * h->baths[j].nks + ks_target - 1) / ks_target);
+    nsplit = std::min(nsplit, lv.P);
+    for (size_t j = 0; j < h->baths.size(); ++j)
+      if (lv.lb[j].active) nsplit = std::min(nsplit, lv.lb[j].M * h->baths[j].nks);
+    lv.nsplit = std::max(1, nsplit);
+    lv.fcg.clear();
+    const int NT = 16 * lv.cg_rn;
+    for (int sp = 0; sp < lv.nsplit; ++sp) {
+      int64_t nout = 0;
+      for (size_t j = 0; j < h->baths.size(); ++j) {
+        Bath& b = h->baths[j];
+        LevelBath& L = lv.lb[j];
+        if (!L.active) continue;
+        const int64_t a_rt = (int64_t)L.M * b.nks * 64;
+        const int64_t plane = (int64_t)b.nrt * a_rt;
+        const int S = L.M * b.nks;
+        for (int f = 0; f <= lv.P; ++f)
+          for (int g = 0; g < 3; ++g) {
+            if ((f == 0 || f == lv.P) && g != 0) continue;  // real spectra: planes 1, 2 stay zero
+            for (int rg = 0; 4 * rg < b.nrt; ++rg)
+              for (int c0 = 0; c0 < B; c0 += NT) {
+                CgItem it{};
+                it.s0 = (int32_t)((int64_t)S * sp / lv.nsplit);
+                it.ns = (int32_t)((int64_t)S * (sp + 1) / lv.nsplit) - it.s0;
+                it.accum = sp > 0 ? 1 : 0;
+                it.A = L.d_khat + (int64_t)f * L.khat_fstride + g * plane + (int64_t)4 * rg * a_rt;
+                it.X = L.d_seg + (int64_t)f * L.seg_fstride + (int64_t)g * b.ncp * L.ldseg;
+                it.out = L.d_Yspec + (int64_t)f * L.yfstride + (int64_t)g * b.nc * B + (int64_t)64 * rg * B + c0;
+                it.a_rt = a_rt;
+                it.ldx = (int32_t)L.ldseg;
+                it.cs = (int32_t)B;
+                it.Rseg = L.Rseg;
+                it.M = L.M;
+                it.nks = b.nks;
+                it.nrt = std::min(4, b.nrt - 4 * rg);
+                it.nrows = std::min(64, b.nc - 64 * rg);
+                it.ncols = (int)std::min<int64_t>(NT, B - c0);
+                it.ldo = (int32_t)B;
+                it.col0 = c0;
+                lv.fcg.push_back(it);
+                ++nout;
+              }
+          }
+      }
+      lv.nout = nout;
+    }
+    lv.fcg_flops = lv.cg_flops;
+    int rc = dalloc_n(h, &lv.d_fcg, lv.fcg.size());
+    if (!rc) rc = upload(h, lv.d_fcg, lv.fcg.data(), lv.fcg.size() * sizeof(CgItem));
+    if (rc) return rc;
+    lv.fused = true;
+    h->far_max_items += ((int64_t)lv.fcg.size() + lv.P - 1) / lv.P + 1;
+  }
+  h->far_fused = true;
+  return GLE_OK;
+}
+
 int freeze(gle_handle* h) {
   if (h->frozen) return GLE_OK;
   const int64_t B = h->B;
@@ -1860,6 +1991,8 @@ int freeze(gle_handle* h) {
   }
   rc = plan_chain(h);
   if (rc) return rc;
+  rc = plan_far_fused(h);
+  if (rc) return rc;
   // device step descriptor
   StepDev sd{};
   sd.nph = (int32_t)h->nph;
@@ -2020,6 +2153,17 @@ int prime(gle_handle* h) {
     const int64_t k0 = floordiv(h->t, lv.P);
     int rc = launch_level_block(h, lv, k0, h->stream, true);
     if (rc) return rc;
+    if (lv.fused) {
+      // fused schedule: the next block too (its data ends at k0 P <= t), so the items ride from the
+      // next block boundary on with whole windows
+      rc = launch_level_block(h, lv, k0 + 1, h->stream, true);
+      if (rc) return rc;
+      lv.last_block = k0 + 1;
+      lv.fblock = INT64_MIN;
+      lv.pend_block = INT64_MIN;
+      lv.bg_block[0] = lv.bg_block[1] = INT64_MIN;
+      continue;
+    }
     lv.last_block = k0 + 1;
     lv.bg_block[0] = lv.bg_block[1] = INT64_MIN;
     lv.bg_block[(k0 + 1) & 1] = k0 + 1;  // the main stream waits for it at (k0 + 1) P
@@ -2063,8 +2207,42 @@ int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
   hipEvent_t wait_ev[gle_handle::NBG] = {};
   int64_t wait_seq[gle_handle::NBG] = {};
   const bool boundary = t % h->P0 == 0, tick = t % h->piece_g == 0;
+  // fused levels, at their block boundaries t = kP on the main stream: the inverse transform of
+  // block k (its items rode in the chain launches of the last P steps; A(t) reads it), then the
+  // newest segment's transform for block k + 1, whose items start riding in A(t)
+  if (h->far_fused && !h->dbg_no_ladder) {
+    for (auto& lv : h->levels) {
+      if (!lv.fused || t % lv.P != 0) continue;
+      const int64_t k = floordiv(t, lv.P);
+      if (lv.fblock == k) {
+        for (size_t b = 0; b < h->baths.size(); ++b) {
+          Bath& bb = h->baths[b];
+          LevelBath& L = lv.lb[b];
+          if (!L.active) continue;
+          if (launch_far_ifft(L.d_Yspec, L.yfstride, 0, bb.nc, (int)h->B, lv.P, L.d_out + (int64_t)(k & 1) * lv.P * h->B,
+                              (int64_t)2 * lv.P * h->B, h->d_cstab, lv.cstride, h->stream))
+            return fail(h, GLE_ERR_UNSUP, "inverse transform launch failed (P = " + std::to_string(lv.P) + ")");
+        }
+        lv.fblock = INT64_MIN;
+      }
+      if (k + 1 > lv.last_block) {
+        for (size_t b = 0; b < h->baths.size(); ++b) {
+          Bath& bb = h->baths[b];
+          LevelBath& L = lv.lb[b];
+          if (!L.active) continue;
+          if (launch_seg_fft(bb.d_H, bb.ldh, bb.R, (int)h->B, bb.nc, bb.ncp, lv.P, t, 1, L.d_seg, L.seg_fstride,
+                             L.ldseg, L.Rseg, h->d_cstab, lv.cstride, h->stream))
+            return fail(h, GLE_ERR_UNSUP, "segment transform launch failed (P = " + std::to_string(lv.P) + ")");
+        }
+        lv.fblock = k + 1;
+        lv.fT = t;
+        lv.last_block = k + 1;
+      }
+    }
+  }
   if (!h->dbg_no_ladder && (boundary || tick)) {
     for (auto& lv : h->levels) {
+      if (lv.fused) continue;
       hipStream_t bs = h->bg_serial ? h->stream : h->bg[lv.sidx];
       const int64_t k = floordiv(t, lv.P);
       if (boundary && t % lv.P == 0 && k + 1 > lv.last_block) {
@@ -2118,7 +2296,7 @@ int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
   if (fpot_host_T)
     HIPCHK(h, hipMemcpyAsync(h->d_Fc, fpot_host_T, (size_t)h->nph * h->B * 8, hipMemcpyHostToDevice, h->stream));
   if (h->d_dbg && t == h->dbg_t) h->dbg_a = need_pot ? 1 : 0;  // GLE_CHAIN_DBG: the stage-A variant recorded
-  run_chain(h, 0, h->chA[need_pot ? 1 : 0], ta, (need_pot ? 1 : 0) | (fpot_host_T ? 0 : 2), h->levels.empty());
+  run_chain(h, 0, h->chA[need_pot ? 1 : 0], ta, (need_pot ? 1 : 0) | (fpot_host_T ? 0 : 2), h->levels.empty(), 0);
   h->host_force_step = fpot_host_T != nullptr;
   return GLE_OK;
 }
@@ -2134,10 +2312,10 @@ int step_end_impl(gle_handle* h, const double* fpot_host_T) {
     if (h->host_force_step) return fail(h, GLE_ERR_STATE, "step begun with a host force must end with one");
   }
   if (h->fuse_bc && mode1 == 1) {
-    run_chain(h, 3, h->chBC, ta, mode1, h->levels.empty());
+    run_chain(h, 3, h->chBC, ta, mode1, h->levels.empty(), 1);
   } else {
-    run_chain(h, 1, h->chB[mode1], ta, mode1, h->levels.empty());
-    run_chain(h, 2, h->chC, ta, mode1, h->levels.empty());
+    run_chain(h, 1, h->chB[mode1], ta, mode1, h->levels.empty(), 1);
+    run_chain(h, 2, h->chC, ta, mode1, h->levels.empty(), 2);
   }
   // the next step is a block boundary: the background blocks started there wait for this step
   if (!h->levels.empty() && (h->t + 1) % h->P0 == 0) HIPCHK(h, hipEventRecord(h->ev_step, h->stream));
@@ -2228,6 +2406,7 @@ int gle_create(const gle_config* cfg, gle_handle** out) {
   h->dt = cfg->dt;
   h->nphp = rup(h->nph, 8);
   h->dbg_no_ladder = gle_env("GLE_DBG_NO_LADDER") != nullptr;
+  if (const char* e = gle_env("GLE_FAR_AFRAC")) h->far_afrac = std::max(0.0, std::min(1.0, atof(e)));
   if (const char* e = gle_env("GLE_DBG_SKIP")) h->dbg_skip = atoi(e);
   if (const char* e = gle_env("GLE_BG_GRID")) h->bg_grid = std::max(0, atoi(e));
   if (const char* e = gle_env("GLE_PIECE_SLACK")) h->piece_slack = std::max(0, atoi(e));
@@ -3115,6 +3294,7 @@ int gle_profile(gle_handle* h, int32_t enable) {
   if ((enable & GLE_PROFILE_CHAIN) && !h->d_ctst) {
     size_t n = 0;
     for (Chain* c : {&h->chA[0], &h->chA[1], &h->chB[0], &h->chB[1], &h->chC, &h->chBC}) n = std::max(n, c->tiles.size());
+    n += (size_t)h->far_max_items;  // far items of the fused schedule ride in the same grids
     h->ctst_tiles = n;
     if (n > 0) {
       int rc = dalloc_n(h, &h->d_ctst, 2 * h->ctst_cap * n);
@@ -3417,7 +3597,7 @@ int gle_set_plan_class(gle_handle* h, int32_t plan_class) {
 }
 
 int gle_plan_detail(gle_handle* h, int32_t* plan_class, int32_t* fused_waves, double* cg_per_cu, int32_t* nlevel,
-                    int64_t* dyn_dropped) {
+                    int64_t* dyn_dropped, int32_t* far_fused) {
   if (!h) return GLE_ERR_ARG;
   if (!h->frozen) return fail(h, GLE_ERR_STATE, "no plan yet (gle_set_state builds it)");
   if (plan_class) *plan_class = h->small_baths ? GLE_PLAN_SMALL_BATHS : GLE_PLAN_LARGE_BATHS;
@@ -3425,6 +3605,7 @@ int gle_plan_detail(gle_handle* h, int32_t* plan_class, int32_t* fused_waves, do
   if (cg_per_cu) *cg_per_cu = h->cg_per_cu;
   if (nlevel) *nlevel = (int32_t)h->levels.size();
   if (dyn_dropped) *dyn_dropped = h->dyn_dropped;
+  if (far_fused) *far_fused = h->far_fused ? 1 : 0;
   return GLE_OK;
 }
 

@@ -18,9 +18,11 @@
 // the 2R-slot history ring the ladder reads).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstddef>
 
 #include "gle_internal.h"
+#include "gle_cgemm.h"
 
 namespace gle {
 
@@ -841,10 +843,61 @@ __device__ __forceinline__ void raw(const ChTile* __restrict__ T, const StepDev*
   }
 }
 
+// Far-field GEMM item of the fused schedule: workgroup nstatic + j runs item j of the launch's far
+// ranges (the spectral levels' current blocks), at the lowest issue priority, in the launch's
+// dynamic LDS (>= CH_FAR_LDS bytes).  4-wave launches only (the item's 4 waves own its 64 rows).
+constexpr size_t CH_FAR_LDS = sizeof(double) * 2 * 4 * 4 * CG_LD;
+template <int NW>
+__device__ __forceinline__ void far_tile(const StepArgs& ta, double* lds) {
+  if constexpr (NW == 4) {
+    __builtin_amdgcn_s_setprio(0);
+    int j = (int)blockIdx.x - ta.nstatic;
+    const CgItem* items = nullptr;
+    int64_t tseg = 0;
+    int idx = 0;
+    bool found = false;
+    // constant indices into the kernel-argument ranges (a runtime index would copy StepArgs to
+    // scratch)
+#pragma unroll
+    for (int r = 0; r < MAXLVL; ++r) {
+      if (r < ta.nfar && !found) {
+        if (j < ta.far[r].count) {
+          items = ta.far[r].items;
+          tseg = ta.far[r].tseg;
+          idx = ta.far[r].first + j;
+          found = true;
+        } else {
+          j -= ta.far[r].count;
+        }
+      }
+    }
+    if (!found) return;
+    const CgItem it = items[idx];
+    auto& xs = *reinterpret_cast<double(*)[2][4 * 4 * CG_LD]>(lds);
+    switch (it.ncols > 32 ? 4 : (it.ncols > 16 ? 2 : 1)) {
+      case 4: cgemm_item<4, 4, 1, 1>(it, tseg, xs); break;
+      case 2: cgemm_item<2, 4, 1, 1>(it, tseg, xs); break;
+      default: cgemm_item<1, 4, 1, 1>(it, tseg, xs); break;
+    }
+  }
+}
+
 template <int STAGE, int NW, int DRN>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(DRN == 1 && NW <= 8 ? CH_WPE : 1, 8))) void chain_kernel(const ChTile* __restrict__ tiles, const StepDev* sd,
                                                         StepArgs ta, int mode) {
   extern __shared__ double lds[];
+  if ((int)blockIdx.x >= ta.nstatic) {  // far-field item (fused schedule), launch-uniform ranges
+    const unsigned long long t_far = __builtin_amdgcn_s_memrealtime();
+    far_tile<NW>(ta, lds);
+    if (ta.ts) {
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        G(ta.ts)[2 * blockIdx.x] = t_far;
+        G(ta.ts)[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+      }
+    }
+    return;
+  }
   // The chain is the step's latency-bound critical path and shares SIMDs with the background
   // ladder's GEMM waves: its waves take issue priority (MFMA pipe and memory issue go to the
   // highest-priority ready wave first, then the oldest)
@@ -926,12 +979,15 @@ bool lds_limit(K* fn, size_t lds) {
 template <int STAGE, int NW>
 void launch_nd(int drn, size_t lds, const ChTile* tiles, int ntiles, const StepDev* sd, StepArgs ta, int mode,
                hipStream_t s) {
+  int grid = ntiles;
+  for (int r = 0; r < ta.nfar; ++r) grid += ta.far[r].count;
+  if (ta.nfar > 0) lds = std::max(lds, CH_FAR_LDS);
   if (drn == 2) {
     lds_limit(chain_kernel<STAGE, NW, 2>, lds);
-    chain_kernel<STAGE, NW, 2><<<ntiles, NW * 64, lds, s>>>(tiles, sd, ta, mode);
+    chain_kernel<STAGE, NW, 2><<<grid, NW * 64, lds, s>>>(tiles, sd, ta, mode);
   } else {
     lds_limit(chain_kernel<STAGE, NW, 1>, lds);
-    chain_kernel<STAGE, NW, 1><<<ntiles, NW * 64, lds, s>>>(tiles, sd, ta, mode);
+    chain_kernel<STAGE, NW, 1><<<grid, NW * 64, lds, s>>>(tiles, sd, ta, mode);
   }
 }
 
@@ -949,6 +1005,8 @@ void launch_chain(int stage, int nw, int drn, size_t lds_bytes, const ChTile* ti
                   StepArgs ta, int mode, hipStream_t s) {
   if (ntiles <= 0) return;
   GLE_BOUNDS_SYNC();
+  ta.nstatic = ntiles;
+  if (nw != 4) ta.nfar = 0;  // far items need 4-wave workgroups (the planner never gives them others)
   if (stage == 0) launch_st<0>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
   else if (stage == 1) launch_st<1>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
   else if (stage == 2) launch_st<2>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);

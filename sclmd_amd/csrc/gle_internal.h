@@ -123,6 +123,9 @@ struct CgItem {
   int32_t nrows, ncols;  // valid rows (<= 64), columns
   int32_t ldo, col0;
   int32_t s0, ns;    // k-step range [s0, s0 + ns) of this item (split-K halves write separate planes)
+  int32_t accum;     // 1: add the item's partial to out (fused schedule: the k-splits of one product
+                     // run in successive launches, first one stores); 0: store
+  int32_t pad;
 };
 
 // Deterministic fixed-order sum of split partial tiles (+ optional far-field addend).
@@ -289,6 +292,13 @@ constexpr int32_t CH_INV = -0x40000000;
 // launchers (gle_kernels.hip)
 // Every kernel takes the step counter by value: the host knows md.t and the steps at which the
 // current far / mid blocks were computed, so no kernel starts with a dependent load of a clock
+// A range of far-field GEMM items (one spectral level's current block) riding in a chain launch
+// (fused schedule): items[first, first + count) with segment index tseg.
+struct FarRange {
+  const CgItem* items;
+  int64_t tseg;
+  int32_t first, count;
+};
 struct StepArgs {
   int64_t t;                 // md.t of this step
   int32_t dbg;               // GLE_CHAIN_DBG: record this launch's timeline
@@ -296,6 +306,10 @@ struct StepArgs {
   int64_t lvl_off[MAXLVL];   // per level: offset (doubles) of target t+1 in its block buffer
   unsigned long long* ts;    // chain launches under GLE_PROFILE_CHAIN: workgroup b stores its start /
                              // end (s_memrealtime) at ts[2b], ts[2b+1] (plain stores), else nullptr
+  // chain launches: workgroups [0, nstatic) are the launch's chain tiles, the following ones the
+  // far-field items of far[0..nfar) in order (fused schedule; nfar = 0 otherwise)
+  int32_t nstatic, nfar;
+  FarRange far[MAXLVL];
 };
 void launch_contract(int rn, int cu, const CItem* items, int nitems, StepArgs ta, hipStream_t s);
 void launch_reduce(const RItem* items, int nitems, int max_elems, StepArgs ta,
