@@ -715,16 +715,18 @@ void drain_profile(gle_handle* h) {
 void run_op(gle_handle* h, Op& op, hipStream_t s, const StepArgs& ta, bool profile) {
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (profile && h->prof_ev && !op.items.empty()) {
-    if (h->ev_used + 2 > h->ev.size()) drain_profile(h);
+    if (h->ev_used + 2 > h->ev.size() || (h->d_tst && h->tst_used >= h->tst_cap)) drain_profile(h);
     e0 = h->ev[h->ev_used];
     e1 = h->ev[h->ev_used + 1];
     h->ev_used += 2;
     hipEventRecord(e0, s);
   }
+  StepArgs tc = ta;
+  if (e0 && h->d_tst && !op.cplx) tc.ts = h->d_tst + 2 * h->tst_used++;  // device stamps: first start, last end
   if (op.cplx)
     launch_contract_cplx(op.rn, op.d_items, (int)op.items.size(), ta, s);
   else
-    launch_contract(op.rn, op.cu, op.d_items, (int)op.items.size(), ta, s);
+    launch_contract(op.rn, op.cu, op.d_items, (int)op.items.size(), tc, s);
   if (e1) {
     hipEventRecord(e1, s);
     h->prof_n += 1;

@@ -136,6 +136,11 @@ __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, doubl
       if (!(DBG & 4)) CG_LOAD_X(c + XD, xv[r % XD]);
       CG_LOAD_A(c + AD, av[(r + AD) % (AD + 1)]);
       const double* xb_ = xs[c & 1] + brow * CG_LD + bcol;
+      if constexpr ((DBG & 8) != 0) {
+        // timing experiment: hold the workgroup for the chunk's MFMA time without using the pipe
+        __builtin_amdgcn_s_sleep(KC * RN);
+        acc[0][0] += av[r][0];
+      } else {
 #pragma unroll
       for (int u = 0; u < KC; ++u) {
         const double a_ = av[r][u] * ((active && c * KC + u < S) ? 1.0 : 0.0);
@@ -143,6 +148,7 @@ __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, doubl
         for (int n = 0; n < RN; ++n)
           acc[n] = __builtin_amdgcn_mfma_f64_16x16x4f64(a_, (DBG & 2) ? a_ * (n + 1) : xb_[4 * u * CG_LD + 16 * n],
                                                         acc[n], 0, 0, 0);
+      }
       }
       if (!(DBG & 4)) {
         CG_STORE_X(c + 1, (c & 1) ^ 1, xv[(r + 1) % XD]);

@@ -192,6 +192,8 @@ __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave,
         for (int n = 0; n < RN; ++n)
 #if defined(CH_DBG) && (CH_DBG & 2)  // no X loads
           b[u][n] = 1e-3 * (xo + n);
+#elif defined(CH_DBG) && (CH_DBG & 4)  // no X loads in the 64-column (near-field) tiles only
+          b[u][n] = RN == 4 ? 1e-3 * (xo + n) : X[xo + xc[n]];
 #else
           b[u][n] = X[xo + xc[n]];
 #endif

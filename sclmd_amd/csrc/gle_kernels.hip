@@ -45,6 +45,8 @@ template <int RN, int CU>
 __global__ __launch_bounds__(WG, 2) void contract_kernel(const CItem* __restrict__ items,
                                                          StepArgs ta) {
   __shared__ double lds[KROWS * LDS_COLS];
+  // profiling (ta.ts, launch-uniform): [0] <- first workgroup start, [1] <- last workgroup end
+  if (ta.ts && threadIdx.x == 0) atomicMin(ta.ts, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   constexpr int NT = 16 * RN;
   constexpr int WWCAP = (256 * CU < LDS_WW_MAX) ? 256 * CU : LDS_WW_MAX;
   // XCD-aware order (grids are padded to a multiple of 8): blocks b, b+8, b+16, ... share an XCD
@@ -166,6 +168,10 @@ __global__ __launch_bounds__(WG, 2) void contract_kernel(const CItem* __restrict
         }
       }
     }
+  }
+  if (ta.ts) {
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(ta.ts + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   }
 }
 
@@ -882,7 +888,7 @@ void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStre
     g_cg_kc = (k && atoi(k) == 8) ? 8 : 4;
     // 1: no K-hat loads, 2: no LDS operand reads, 4: no X staging / barrier; 3, 7: combinations
     const char* d = gle_env("GLE_CG_DBG");
-    g_cg_dbg = d ? std::max(0, std::min(7, atoi(d))) : 0;
+    g_cg_dbg = d ? std::max(0, std::min(15, atoi(d))) : 0;
   }
   {  // re-read per launch: variants of one process (scripts/exp_time.py --variants) switch it
     const char* r = gle_env("GLE_CG_RING");
@@ -905,6 +911,7 @@ void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStre
     else if (g_cg_dbg == 2) cgemm_kernel<4, 4, CG_AD, CG_XD, 2><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts);
     else if (g_cg_dbg == 3) cgemm_kernel<4, 4, CG_AD, CG_XD, 3><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts);
     else if (g_cg_dbg == 4) cgemm_kernel<4, 4, CG_AD, CG_XD, 4><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts);
+    else if (g_cg_dbg == 15) cgemm_kernel<4, 4, CG_AD, CG_XD, 15><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts);
     else cgemm_kernel<4, 4, CG_AD, CG_XD, 7><<<grid, 256, shm, s>>>(items, nitems, tseg, xcd, ts);
     return;
   }
