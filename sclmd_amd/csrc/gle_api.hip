@@ -145,6 +145,7 @@ struct Level {
   // place), its newest segment is transformed by a launch before A(kP), its inverse transform
   // runs before A((k+1)P)
   bool fused = false;
+  bool bg_split = false;         // background schedule walking the k-split item list (fcg)
   std::vector<CgItem> fcg;       // fused items: nsplit k-splits x nout products, split-major
   CgItem* d_fcg = nullptr;
   int64_t nout = 0;              // products (bath, f, g, row group, column tile) per split
@@ -1607,7 +1608,9 @@ int plan_far_fused(gle_handle* h) {
   // HBM-latency-bound at the chain's register budget, finish after the chain tiles and add to
   // every launch; the background schedule overlaps them with the chain across launches.  Off by
   // default (GLE_FAR_FUSED=1 in the experiment build).
-  if (!any || !nw4 || !gle_env("GLE_FAR_FUSED")) return GLE_OK;
+  const bool fused = nw4 && gle_env("GLE_FAR_FUSED") != nullptr;
+  const bool bg_split = !fused && gle_env("GLE_BG_SPLIT") != nullptr;
+  if (!any || (!fused && !bg_split)) return GLE_OK;
   int ks_target = 32;  // k-steps per item: ~4 x 32 MFMAs per wave, the length of a chain tile's products
   if (const char* e = gle_env("GLE_FAR_KS")) ks_target = std::max(4, atoi(e));
   const int64_t B = h->B;
@@ -1665,10 +1668,21 @@ int plan_far_fused(gle_handle* h) {
     int rc = dalloc_n(h, &lv.d_fcg, lv.fcg.size());
     if (!rc) rc = upload(h, lv.d_fcg, lv.fcg.data(), lv.fcg.size() * sizeof(CgItem));
     if (rc) return rc;
+    if (bg_split) {
+      // chunks of ~cg_per_cu workgroups per CU, at least nsplit of them (each at most nout items)
+      int ncu = 256;
+      hipDeviceProp_t prop;
+      if (hipGetDeviceProperties(&prop, h->cfg.device) == hipSuccess) ncu = prop.multiProcessorCount;
+      const int64_t want = (int64_t)((double)lv.fcg.size() / (h->cg_per_cu * ncu));
+      lv.ncg_chunk = (int)std::max<int64_t>(lv.nsplit, want);
+      lv.npiece = lv.ncg_chunk + 2;
+      lv.bg_split = true;
+      continue;
+    }
     lv.fused = true;
     h->far_max_items += ((int64_t)lv.fcg.size() + lv.P - 1) / lv.P + 1;
   }
-  h->far_fused = true;
+  h->far_fused = fused;
   return GLE_OK;
 }
 
@@ -2070,6 +2084,37 @@ int launch_level_pieces(gle_handle* h, Level& lv, int64_t k, hipStream_t s, bool
   const StepArgs ta = step_args(h, T);
   const int par = (int)(k & 1);
   const int li = (int)(&lv - h->levels.data());
+  if (lv.spectral && priming) {
+    // the whole block at once with the unsplit items (k-halves in separate planes): all M segment
+    // transforms, one GEMM launch, the inverse transform
+    for (size_t b = 0; b < h->baths.size(); ++b) {
+      Bath& bb = h->baths[b];
+      LevelBath& L = lv.lb[b];
+      if (!L.active) continue;
+      if (launch_seg_fft(bb.d_H, bb.ldh, bb.R, (int)h->B, bb.nc, bb.ncp, lv.P, T, L.M, L.d_seg, L.seg_fstride,
+                         L.ldseg, L.Rseg, h->d_cstab, lv.cstride, s))
+        return fail(h, GLE_ERR_UNSUP, "segment transform launch failed (P = " + std::to_string(lv.P) + ")");
+    }
+    launch_cgemm(lv.cg_rn, lv.d_cg, (int)lv.cg.size(), T / lv.P, s, 0, nullptr);
+    for (size_t b = 0; b < h->baths.size(); ++b) {
+      Bath& bb = h->baths[b];
+      LevelBath& L = lv.lb[b];
+      if (!L.active) continue;
+      if (launch_far_ifft(L.d_Yspec, L.yfstride, lv.cg_split > 1 ? (int64_t)(lv.P + 1) * L.yfstride : 0, bb.nc,
+                          (int)h->B, lv.P, L.d_out + (int64_t)par * lv.P * h->B, (int64_t)2 * lv.P * h->B, h->d_cstab,
+                          lv.cstride, s))
+        return fail(h, GLE_ERR_UNSUP, "inverse transform launch failed (P = " + std::to_string(lv.P) + ")");
+    }
+    HIPCHK(h, hipEventRecord(lv.ev[par], s));
+    lv.ev_seq[par] = ++h->ev_seq_counter;
+    return GLE_OK;
+  }
+  // background schedule with k-split items (bg_split): the chunks walk the split-major item list in
+  // order on the level's in-order stream (each chunk at most nout items: the k-splits of a product
+  // land in successive launches, the later ones adding), the inverse transform reads one plane
+  const bool split = lv.bg_split;
+  const CgItem* d_items = split ? lv.d_fcg : lv.d_cg;
+  const int64_t nitems = split ? (int64_t)lv.fcg.size() : (int64_t)lv.cg.size();
   for (int j = j0; j < j1; ++j) {
     if (!lv.spectral) {
       // profiled only when no level is spectral: the roofline then names one kernel class
@@ -2088,7 +2133,7 @@ int launch_level_pieces(gle_handle* h, Level& lv, int64_t k, hipStream_t s, bool
       }
     } else if (j <= lv.ncg_chunk) {
       // one chunk of the batched GEMM of the per-frequency products, profiled like run_op
-      const int64_t n = (int64_t)lv.cg.size();
+      const int64_t n = nitems;
       const int64_t c0 = n * (j - 1) / lv.ncg_chunk, c1 = n * j / lv.ncg_chunk;
       if (c1 <= c0) continue;
       hipEvent_t e1 = nullptr;
@@ -2101,7 +2146,7 @@ int launch_level_pieces(gle_handle* h, Level& lv, int64_t k, hipStream_t s, bool
         if (h->d_tst && !priming) ts = h->d_tst + 2 * h->tst_used++;
       }
       if (priming || !(h->dbg_skip & 1))
-        launch_cgemm(lv.cg_rn, lv.d_cg + c0, (int)(c1 - c0), T / lv.P, s, priming ? 0 : h->bg_grid, ts);
+        launch_cgemm(lv.cg_rn, d_items + c0, (int)(c1 - c0), T / lv.P, s, priming ? 0 : h->bg_grid, ts);
       if (h->prof && !priming) h->prof_blocks[li] += (double)(c1 - c0) / (double)n;
       if (e1) {
         hipEventRecord(e1, s);
@@ -2115,8 +2160,8 @@ int launch_level_pieces(gle_handle* h, Level& lv, int64_t k, hipStream_t s, bool
         Bath& bb = h->baths[b];
         LevelBath& L = lv.lb[b];
         if (!L.active || (!priming && (h->dbg_skip & 4))) continue;
-        if (launch_far_ifft(L.d_Yspec, L.yfstride, lv.cg_split > 1 ? (int64_t)(lv.P + 1) * L.yfstride : 0, bb.nc,
-                            (int)h->B, lv.P, L.d_out + (int64_t)par * lv.P * h->B,
+        if (launch_far_ifft(L.d_Yspec, L.yfstride, (!split && lv.cg_split > 1) ? (int64_t)(lv.P + 1) * L.yfstride : 0,
+                            bb.nc, (int)h->B, lv.P, L.d_out + (int64_t)par * lv.P * h->B,
                             (int64_t)2 * lv.P * h->B, h->d_cstab, lv.cstride, s))
           return fail(h, GLE_ERR_UNSUP, "inverse transform launch failed (P = " + std::to_string(lv.P) + ")");
       }
@@ -2419,19 +2464,37 @@ int gle_create(const gle_config* cfg, gle_handle** out) {
   {
     int lo = 0, hi = 0;
     hipDeviceGetStreamPriorityRange(&lo, &hi);
-    e = hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, hi);
     // GLE_BG_RESERVE=R: the background streams stay off CU mask bits [0, R), which the per-step
     // chain then finds free at every launch
     int reserve = 0;
     if (const char* r = gle_env("GLE_BG_RESERVE")) reserve = std::max(0, atoi(r));
-    std::vector<uint32_t> cumask;
-    if (reserve > 0) {
+    // GLE_CU_SPLIT=N (experiment): the background streams on N CUs spread evenly over the mask, the
+    // main stream (GLE_CU_SPLIT_MAIN=1, default) on the other ones -- disjoint CU sets
+    int split = 0;
+    if (const char* r = gle_env("GLE_CU_SPLIT")) split = std::max(0, atoi(r));
+    const char* split_main = gle_env("GLE_CU_SPLIT_MAIN");
+    std::vector<uint32_t> cumask, mainmask;
+    if (reserve > 0 || split > 0) {
       hipDeviceProp_t prop;
       hipGetDeviceProperties(&prop, cfg->device);
       const int ncu = prop.multiProcessorCount;
       cumask.assign((ncu + 31) / 32, 0u);
-      for (int c = std::min(reserve, ncu - 8); c < ncu; ++c) cumask[c / 32] |= 1u << (c % 32);
+      mainmask.assign((ncu + 31) / 32, 0u);
+      if (split > 0) {
+        split = std::min(split, ncu - 8);
+        for (int c = 0; c < ncu; ++c) {
+          const bool far = (int64_t)(c + 1) * split / ncu > (int64_t)c * split / ncu;
+          (far ? cumask : mainmask)[c / 32] |= 1u << (c % 32);
+        }
+      } else {
+        for (int c = std::min(reserve, ncu - 8); c < ncu; ++c) cumask[c / 32] |= 1u << (c % 32);
+      }
     }
+    if (split > 0 && !(split_main && atoi(split_main) == 0))
+      e = hipExtStreamCreateWithCUMask(&h->stream, (uint32_t)mainmask.size(), mainmask.data());
+    else
+      e = hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, hi);
+    reserve = reserve > 0 || split > 0;
     for (int i = 0; i < gle_handle::NBG && e == hipSuccess; ++i) {
       if (reserve > 0)
         e = hipExtStreamCreateWithCUMask(&h->bg[i], (uint32_t)cumask.size(), cumask.data());

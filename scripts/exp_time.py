@@ -45,6 +45,8 @@ def measure(args, meta, dyn, baths):
         st.sync()
         if args.profile:
             st.profile(True)
+        elif args.chainprof:
+            st.profile(True, events=False, chain=True)
         t0 = time.perf_counter()
         st.run(args.short)
         st.sync()
@@ -62,8 +64,8 @@ def measure(args, meta, dyn, baths):
         st.run(args.steps)
         st.sync()
         el = time.perf_counter() - t0
-        prof = st.profile_read() if args.profile else None
-        if args.profile:
+        prof = st.profile_read() if (args.profile or args.chainprof) else None
+        if args.profile or args.chainprof:
             st.profile(False)
         reps = []
         for _ in range(args.short_reps):  # bench-like short windows: sync, K steps, sync
@@ -77,6 +79,10 @@ def measure(args, meta, dyn, baths):
     finally:
         st.close()
     extra = {}
+    if prof and prof.get("chain_launches"):
+        # chain kernel time per step (launch spans, device stamps) over every profiled step
+        nst = args.short * 2 + 64 + args.steps
+        extra["chain_us_per_step"] = prof["chain_ms"] * 1e3 / max(1, prof["chain_launches"] / 2)
     if prof and prof.get("launches"):
         ms = prof.get("ms_device") or prof["ms"]
         extra = {"cgemm_launches": prof["launches"], "cgemm_avg_us": ms / prof["launches"] * 1e3,
@@ -97,6 +103,7 @@ def main():
     ap.add_argument("--tag", default="")
     ap.add_argument("--short-reps", type=int, default=0, help="extra short windows at drifting phases")
     ap.add_argument("--profile", type=int, default=0, help="HIP-event timing of the far-field launches on")
+    ap.add_argument("--chainprof", type=int, default=0, help="device stamps of the chain launches on")
     args = ap.parse_args()
     from sclmd_amd import synthetic
 
