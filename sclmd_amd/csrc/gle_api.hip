@@ -1611,7 +1611,7 @@ int plan_far_fused(gle_handle* h) {
   const bool fused = nw4 && gle_env("GLE_FAR_FUSED") != nullptr;
   const bool bg_split = !fused && gle_env("GLE_BG_SPLIT") != nullptr;
   if (!any || (!fused && !bg_split)) return GLE_OK;
-  int ks_target = 32;  // k-steps per item: ~4 x 32 MFMAs per wave, the length of a chain tile's products
+  int ks_target = 40;  // k-steps per item: ~4 x 40 MFMAs per wave, about a chain tile's products
   if (const char* e = gle_env("GLE_FAR_KS")) ks_target = std::max(4, atoi(e));
   const int64_t B = h->B;
   for (auto& lv : h->levels) {
@@ -1683,6 +1683,17 @@ int plan_far_fused(gle_handle* h) {
     h->far_max_items += ((int64_t)lv.fcg.size() + lv.P - 1) / lv.P + 1;
   }
   h->far_fused = fused;
+  if (fused && !gle_env("GLE_FAR_AFRAC")) {
+    // a step's items split between its two launches by the workgroup slots each leaves free (4
+    // chain-sized workgroups per CU): every item resident from its launch's start, beside the tiles
+    int ncu = 256;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, h->cfg.device) == hipSuccess) ncu = prop.multiProcessorCount;
+    const double cap = 4.0 * ncu;
+    const double fa = std::max(1.0, cap - (double)h->chA[0].tiles.size());
+    const double fb = std::max(1.0, cap - (double)(h->fuse_bc ? h->chBC.tiles.size() : h->chB[0].tiles.size()));
+    h->far_afrac = fa / (fa + fb);
+  }
   return GLE_OK;
 }
 

@@ -848,6 +848,8 @@ __device__ __forceinline__ void raw(const ChTile* __restrict__ T, const StepDev*
 // Far-field GEMM item of the fused schedule: workgroup nstatic + j runs item j of the launch's far
 // ranges (the spectral levels' current blocks), at the lowest issue priority, in the launch's
 // dynamic LDS (>= CH_FAR_LDS bytes).  4-wave launches only (the item's 4 waves own its 64 rows).
+// The HBM stream of K-hat goes 3 chunks ahead (119 VGPRs for this path alone, within the chain
+// kernel's 128).
 constexpr size_t CH_FAR_LDS = sizeof(double) * 2 * 4 * 4 * CG_LD;
 template <int NW>
 __device__ __forceinline__ void far_tile(const StepArgs& ta, double* lds) {
@@ -877,9 +879,9 @@ __device__ __forceinline__ void far_tile(const StepArgs& ta, double* lds) {
     const CgItem it = items[idx];
     auto& xs = *reinterpret_cast<double(*)[2][4 * 4 * CG_LD]>(lds);
     switch (it.ncols > 32 ? 4 : (it.ncols > 16 ? 2 : 1)) {
-      case 4: cgemm_item<4, 4, 1, 1>(it, tseg, xs); break;
-      case 2: cgemm_item<2, 4, 1, 1>(it, tseg, xs); break;
-      default: cgemm_item<1, 4, 1, 1>(it, tseg, xs); break;
+      case 4: cgemm_item<4, 4, 3, 1>(it, tseg, xs); break;
+      case 2: cgemm_item<2, 4, 3, 1>(it, tseg, xs); break;
+      default: cgemm_item<1, 4, 3, 1>(it, tseg, xs); break;
     }
   }
 }
