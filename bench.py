@@ -154,10 +154,15 @@ def main():
                     help="every rank on device 0 (rehearsal of the N > 1 control flow on one GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
-                    help="PMC-derived HBM bytes per dominant-kernel launch (from a rocprofv3 --pmc pass)")
+    ap.add_argument("--traffic-json", default="",
+                    help="PMC-derived HBM bytes per dominant-kernel launch (from rocprofv3 --pmc passes); "
+                         "default: profiles/traffic_<config>_<ntraj>.json if present, else "
+                         "profiles/traffic_latest.json (used only when its config / ntraj / plan match)")
     args = ap.parse_args()
     refuse_experiment_env()
+    if not args.traffic_json:
+        per = os.path.join(ROOT, "profiles", "traffic_%s_%d.json" % (args.config, args.ntraj))
+        args.traffic_json = per if os.path.exists(per) else os.path.join(ROOT, "profiles", "traffic_latest.json")
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
