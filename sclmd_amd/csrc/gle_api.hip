@@ -135,6 +135,7 @@ struct Level {
   // long block never sits in front of the next small-level block on the in-order stream:
   // spectral: [segment transform] [cgemm item chunk]... [inverse transform + event]
   int ncg_chunk = 1;
+  int nfs = 1, nif = 1;        // segment / inverse transform pieces (DOF ranges of every bath)
   int npiece = 1;
   int64_t ev_seq[2] = {0, 0};      // enqueue order of ev[] (merged main-stream waits)
   int64_t pend_block = INT64_MIN;  // block whose pieces are still being issued
@@ -1675,6 +1676,7 @@ int plan_far_fused(gle_handle* h) {
       if (hipGetDeviceProperties(&prop, h->cfg.device) == hipSuccess) ncu = prop.multiProcessorCount;
       const int64_t want = (int64_t)((double)lv.fcg.size() / (h->cg_per_cu * ncu));
       lv.ncg_chunk = (int)std::max<int64_t>(lv.nsplit, want);
+      lv.nfs = lv.nif = 1;
       lv.npiece = lv.ncg_chunk + 2;
       lv.bg_split = true;
       continue;
@@ -1985,7 +1987,13 @@ int freeze(gle_handle* h) {
         const int64_t nch = gle_env("GLE_CG_CEIL") ? (int64_t)std::ceil(want - 1e-9) : (int64_t)want;
         lv.ncg_chunk = (int)std::max<int64_t>(1, std::min<int64_t>(nch, nslot));
         if (const char* e = gle_env("GLE_NO_PIECES")) lv.ncg_chunk = atoi(e) > 0 ? 1 : lv.ncg_chunk;
-        lv.npiece = lv.ncg_chunk + 2;
+        // the long levels' transforms go out as DOF-range pieces too (one piece = every bath's
+        // range j): a whole-level transform of P = 256 (2 x 2400 workgroups at C3) held the CUs
+        // of ~20 steps' chain launches at once, the slowest short windows of the phase scan
+        int fdiv = 32;
+        if (const char* e = gle_env("GLE_FFT_CHUNK")) fdiv = atoi(e) > 0 ? std::max(1, atoi(e)) : 1 << 30;
+        lv.nfs = lv.nif = std::max(1, std::min(lv.P / fdiv, 16));
+        lv.npiece = lv.nfs + lv.ncg_chunk + lv.nif;
       }
     } else {
       for (int par = 0; par < 2; ++par) {
@@ -2133,19 +2141,23 @@ int launch_level_pieces(gle_handle* h, Level& lv, int64_t k, hipStream_t s, bool
       if (h->prof && !priming) h->prof_blocks[li] += 1.0;
       continue;
     }
-    if (j == 0) {
+    // pieces: [0, nfs) segment transform DOF ranges, then ncg_chunk GEMM chunks, then [.., npiece)
+    // inverse transform DOF ranges
+    const int jg = j - lv.nfs + 1;  // 1-based GEMM chunk
+    if (j < lv.nfs) {
       for (size_t b = 0; b < h->baths.size(); ++b) {
         Bath& bb = h->baths[b];
         LevelBath& L = lv.lb[b];
         if (!L.active || (!priming && (h->dbg_skip & 2))) continue;
+        const int k0 = (int)((int64_t)bb.nc * j / lv.nfs), k1 = (int)((int64_t)bb.nc * (j + 1) / lv.nfs);
         if (launch_seg_fft(bb.d_H, bb.ldh, bb.R, (int)h->B, bb.nc, bb.ncp, lv.P, T, priming ? L.M : 1, L.d_seg,
-                           L.seg_fstride, L.ldseg, L.Rseg, h->d_cstab, lv.cstride, s))
+                           L.seg_fstride, L.ldseg, L.Rseg, h->d_cstab, lv.cstride, s, k0, k1))
           return fail(h, GLE_ERR_UNSUP, "segment transform launch failed (P = " + std::to_string(lv.P) + ")");
       }
-    } else if (j <= lv.ncg_chunk) {
+    } else if (jg <= lv.ncg_chunk) {
       // one chunk of the batched GEMM of the per-frequency products, profiled like run_op
       const int64_t n = nitems;
-      const int64_t c0 = n * (j - 1) / lv.ncg_chunk, c1 = n * j / lv.ncg_chunk;
+      const int64_t c0 = n * (jg - 1) / lv.ncg_chunk, c1 = n * jg / lv.ncg_chunk;
       if (c1 <= c0) continue;
       hipEvent_t e1 = nullptr;
       unsigned long long* ts = nullptr;
@@ -2167,13 +2179,15 @@ int launch_level_pieces(gle_handle* h, Level& lv, int64_t k, hipStream_t s, bool
         h->prof_bytes += lv.cg_bytes * frac;
       }
     } else {
+      const int ji = jg - lv.ncg_chunk - 1;  // inverse transform piece
       for (size_t b = 0; b < h->baths.size(); ++b) {
         Bath& bb = h->baths[b];
         LevelBath& L = lv.lb[b];
         if (!L.active || (!priming && (h->dbg_skip & 4))) continue;
+        const int k0 = (int)((int64_t)bb.nc * ji / lv.nif), k1 = (int)((int64_t)bb.nc * (ji + 1) / lv.nif);
         if (launch_far_ifft(L.d_Yspec, L.yfstride, (!split && lv.cg_split > 1) ? (int64_t)(lv.P + 1) * L.yfstride : 0,
                             bb.nc, (int)h->B, lv.P, L.d_out + (int64_t)par * lv.P * h->B,
-                            (int64_t)2 * lv.P * h->B, h->d_cstab, lv.cstride, s))
+                            (int64_t)2 * lv.P * h->B, h->d_cstab, lv.cstride, s, k0, k1))
           return fail(h, GLE_ERR_UNSUP, "inverse transform launch failed (P = " + std::to_string(lv.P) + ")");
       }
     }

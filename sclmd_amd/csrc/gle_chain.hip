@@ -229,6 +229,16 @@ __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave,
   if (cur >= 0) flush();
 }
 
+// DOF and S(t+1) tiles have the kernel's DRN columns (T->rn == DRN): products of that width only,
+// so the 64-column near-field variant is not instantiated beside the DOF prologue's live values
+// (it made the register allocator spill the DOF stages)
+template <int NW, int RN>
+__device__ __forceinline__ void run_products_rn(const ChTile* __restrict__ T, int64_t t, double* lds, int skip = 0) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  products<RN, NW>(T, wave, lane, t, lds, skip);
+}
+
 template <int NW>
 __device__ __forceinline__ void run_products(const ChTile* __restrict__ T, int64_t t, double* lds, int skip = 0) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -366,7 +376,7 @@ __device__ __forceinline__ void dof_A(const ChTile* __restrict__ T, const StepDe
   }
   if (T->first && threadIdx.x < Geo::NT && T->c0 + (int)threadIdx.x < B)
     *G(pmax_word(sd, 0, par ^ 1, T->c0 + threadIdx.x)) = 0ull;
-  run_products<NW>(T, t, lds);
+  run_products_rn<NW, DRN>(T, t, lds);
   __syncthreads();
   stamp(sd, 0, 2, ta);
   // ---- epilogue (md.vv id0, md.py:383-397)
@@ -497,7 +507,7 @@ __device__ __forceinline__ void dof_B(const ChTile* __restrict__ T, const StepDe
       sv[x][u] = G(bd.S)[(int64_t)par1 * bd.vs + kb];
     }
   }
-  run_products<NW>(T, t, lds);
+  run_products_rn<NW, DRN>(T, t, lds);
   __syncthreads();
   stamp(sd, 1, 2, ta);
 #pragma unroll
@@ -580,7 +590,7 @@ __device__ __forceinline__ void dof_C(const ChTile* __restrict__ T, const StepDe
     *G(pmax_word(sd, 1, par1, T->c0 + threadIdx.x)) = 0ull;
     if (harm) G(sd->qvalid)[T->c0 + threadIdx.x] = 1;
   }
-  run_products<NW>(T, t, lds);
+  run_products_rn<NW, DRN>(T, t, lds);
   __syncthreads();
   stamp(sd, 2, 2, ta);
   double dq[EPT];
@@ -695,7 +705,7 @@ __device__ __forceinline__ void dof_BC(const ChTile* __restrict__ T, const StepD
   // which potential-cache branches at q~ any trajectory of the tile takes (workgroup-uniform)
   anyhit = __syncthreads_or(anyhit);
   anymiss = __syncthreads_or(anymiss);
-  run_products<NW>(T, t, lds, (anyhit ? 0 : 1) | (anymiss ? 0 : 2));
+  run_products_rn<NW, DRN>(T, t, lds, (anyhit ? 0 : 1) | (anymiss ? 0 : 2));
   __syncthreads();
   // the words this launch reads (w1) are read above: only now may the first tile reset them
   if (T->first && threadIdx.x < Geo::NT && T->c0 + (int)threadIdx.x < B) {
@@ -809,7 +819,7 @@ __device__ __forceinline__ void sfin(const ChTile* __restrict__ T, const StepDev
     for (int l = 0; l < MAXLVL; ++l) lvs += lv[l];
     pre[x] = lvs + sn;
   }
-  run_products<NW>(T, t, lds);
+  run_products_rn<NW, DRN>(T, t, lds);
   __syncthreads();
   stamp(sd, stage, 2, ta);
 #pragma unroll
@@ -851,9 +861,12 @@ __device__ __forceinline__ void raw(const ChTile* __restrict__ T, const StepDev*
 // The HBM stream of K-hat goes 3 chunks ahead (119 VGPRs for this path alone, within the chain
 // kernel's 128).
 constexpr size_t CH_FAR_LDS = sizeof(double) * 2 * 4 * 4 * CG_LD;
+#ifndef CH_FAR_PATH
+#define CH_FAR_PATH 1
+#endif
 template <int NW>
 __device__ __forceinline__ void far_tile(const StepArgs& ta, double* lds) {
-  if constexpr (NW == 4) {
+  if constexpr (NW == 4 && CH_FAR_PATH) {
     __builtin_amdgcn_s_setprio(0);
     int j = (int)blockIdx.x - ta.nstatic;
     const CgItem* items = nullptr;

@@ -338,9 +338,11 @@ void launch_khat_pack(const double* Kf, int ml, int nks_k, double* khat, int P, 
                       int nc, int nrt2, int nks2, const double* cstab, int cstride, hipStream_t s);
 int launch_seg_fft(const double* H, int64_t ldh, int R, int B, int nc, int ncp, int P, int64_t T,
                    int nseg, double* seg, int64_t seg_fstride, int64_t ldseg, int Rseg,
-                   const double* cstab, int cstride, hipStream_t s);
+                   const double* cstab, int cstride, hipStream_t s, int k0 = 0, int k1 = -1);
+// [k0, k1): the DOF range of this launch (the background schedule issues a long level's transforms
+// as several DOF-range pieces); k1 < 0: up to nc
 int launch_far_ifft(const double* Y, int64_t yfstride, int64_t ysplit, int nc, int B, int P, double* out,
-                    int64_t ldout, const double* cstab, int cstride, hipStream_t s);
+                    int64_t ldout, const double* cstab, int cstride, hipStream_t s, int k0 = 0, int k1 = -1);
 // velocity power spectra of recorded series (functions.powerspecp): out [ngroup][B][nmd]
 int launch_power(const double* ps, int64_t nph, int B, int64_t nmd, int ngroup, const int64_t* goff,
                  const int64_t* dofs, const double* tw, double* out, hipStream_t s);

@@ -960,7 +960,7 @@ void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStre
 // thread busy in every butterfly stage), fewer for long transforms (LDS: BC/2 series of 2P points)
 template <int BC>
 __global__ __launch_bounds__(256) void seg_fft_kernel(const double* __restrict__ H, int64_t ldh, int R,
-                                                      int B, int nc, int ncp, int P, int logn,
+                                                      int B, int k0, int nk, int ncp, int P, int logn,
                                                       int64_t T, double* __restrict__ seg,
                                                       int64_t seg_fstride, int64_t ldseg, int Rseg,
                                                       const double2* __restrict__ cstab, int cstride) {
@@ -969,8 +969,8 @@ __global__ __launch_bounds__(256) void seg_fft_kernel(const double* __restrict__
   stage_twiddles(fbuf + (BC / 2) * N, N, cstab, cstride);
   const int nbc = (B + BC - 1) / BC;
   const int bc = blockIdx.x % nbc;
-  const int k = (blockIdx.x / nbc) % nc;
-  const int sidx = blockIdx.x / (nbc * nc);
+  const int k = k0 + (int)((blockIdx.x / nbc) % nk);
+  const int sidx = blockIdx.x / (nbc * nk);
   const int64_t sigma = T / P - sidx;
   const int64_t t0 = sigma * P - 2 * P + 2;
   const int b0 = bc * BC;
@@ -1045,8 +1045,8 @@ static int fft_bc(int B, int P) {
 }
 
 template <int BC>
-static int seg_fft_launch(const double* H, int64_t ldh, int R, int B, int nc, int ncp, int P, int logn, int64_t T,
-                          int nseg, double* seg, int64_t seg_fstride, int64_t ldseg, int Rseg,
+static int seg_fft_launch(const double* H, int64_t ldh, int R, int B, int k0, int nk, int ncp, int P, int logn,
+                          int64_t T, int nseg, double* seg, int64_t seg_fstride, int64_t ldseg, int Rseg,
                           const double* cstab, int cstride, hipStream_t s) {
   const size_t shmem = ((size_t)(BC / 2) * 2 * P + P) * sizeof(double2);
   if (shmem > 160 * 1024) return -2;
@@ -1054,23 +1054,28 @@ static int seg_fft_launch(const double* H, int64_t ldh, int R, int B, int nc, in
   // time on the step's critical path at block boundaries)
   if (!lds_attr_once((const void*)seg_fft_kernel<BC>)) return -3;
   const int nbc = (B + BC - 1) / BC;
-  const int64_t blocks = (int64_t)nseg * nc * nbc;
-  seg_fft_kernel<BC><<<(unsigned)blocks, 256, shmem, s>>>(H, ldh, R, B, nc, ncp, P, logn, T, seg, seg_fstride,
+  const int64_t blocks = (int64_t)nseg * nk * nbc;
+  if (blocks <= 0) return 0;
+  seg_fft_kernel<BC><<<(unsigned)blocks, 256, shmem, s>>>(H, ldh, R, B, k0, nk, ncp, P, logn, T, seg, seg_fstride,
                                                            ldseg, Rseg, (const double2*)cstab, cstride);
   return 0;
 }
 
 int launch_seg_fft(const double* H, int64_t ldh, int R, int B, int nc, int ncp, int P, int64_t T,
                    int nseg, double* seg, int64_t seg_fstride, int64_t ldseg, int Rseg,
-                   const double* cstab, int cstride, hipStream_t s) {
+                   const double* cstab, int cstride, hipStream_t s, int k0, int k1) {
+  if (k1 < 0 || k1 > nc) k1 = nc;
+  k0 = k0 < 0 ? 0 : k0;
+  const int nk = k1 - k0;
+  if (nk <= 0) return 0;
   int logn = 0;
   while ((1 << logn) < 2 * P) ++logn;
   if ((1 << logn) != 2 * P) return -1;
   switch (fft_bc(B, P)) {
-    case 64: return seg_fft_launch<64>(H, ldh, R, B, nc, ncp, P, logn, T, nseg, seg, seg_fstride, ldseg, Rseg, cstab, cstride, s);
-    case 32: return seg_fft_launch<32>(H, ldh, R, B, nc, ncp, P, logn, T, nseg, seg, seg_fstride, ldseg, Rseg, cstab, cstride, s);
-    case 16: return seg_fft_launch<16>(H, ldh, R, B, nc, ncp, P, logn, T, nseg, seg, seg_fstride, ldseg, Rseg, cstab, cstride, s);
-    default: return seg_fft_launch<8>(H, ldh, R, B, nc, ncp, P, logn, T, nseg, seg, seg_fstride, ldseg, Rseg, cstab, cstride, s);
+    case 64: return seg_fft_launch<64>(H, ldh, R, B, k0, nk, ncp, P, logn, T, nseg, seg, seg_fstride, ldseg, Rseg, cstab, cstride, s);
+    case 32: return seg_fft_launch<32>(H, ldh, R, B, k0, nk, ncp, P, logn, T, nseg, seg, seg_fstride, ldseg, Rseg, cstab, cstride, s);
+    case 16: return seg_fft_launch<16>(H, ldh, R, B, k0, nk, ncp, P, logn, T, nseg, seg, seg_fstride, ldseg, Rseg, cstab, cstride, s);
+    default: return seg_fft_launch<8>(H, ldh, R, B, k0, nk, ncp, P, logn, T, nseg, seg, seg_fstride, ldseg, Rseg, cstab, cstride, s);
   }
 }
 
@@ -1081,7 +1086,7 @@ int launch_seg_fft(const double* H, int64_t ldh, int R, int B, int nc, int ncp, 
 // Grid: DOF k x 8-trajectory chunk; two real outputs per complex inverse FFT.
 template <int BC>
 __global__ __launch_bounds__(256) void far_ifft_kernel(const double* __restrict__ Y, int64_t yfstride,
-                                                       int64_t ysplit, int nc, int B, int P, int logn,
+                                                       int64_t ysplit, int nc, int k0, int B, int P, int logn,
                                                        double* __restrict__ out, int64_t ldout,
                                                        const double2* __restrict__ cstab, int cstride) {
   extern __shared__ double2 fbuf[];  // BC/2 series of N points, then N/2 twiddles
@@ -1089,7 +1094,7 @@ __global__ __launch_bounds__(256) void far_ifft_kernel(const double* __restrict_
   stage_twiddles(fbuf + (BC / 2) * N, N, cstab, cstride);
   const int nbc = (B + BC - 1) / BC;
   const int bc = blockIdx.x % nbc;
-  const int k = blockIdx.x / nbc;
+  const int k = k0 + (int)(blockIdx.x / nbc);
   const int b0 = bc * BC;
   const int64_t pl = (int64_t)nc * B;
   for (int e = threadIdx.x; e < N * BC / 2; e += blockDim.x) {
@@ -1136,29 +1141,33 @@ __global__ __launch_bounds__(256) void far_ifft_kernel(const double* __restrict_
 }
 
 template <int BC>
-static int far_ifft_launch(const double* Y, int64_t yfstride, int64_t ysplit, int nc, int B, int P, int logn,
-                           double* out, int64_t ldout, const double* cstab, int cstride, hipStream_t s) {
+static int far_ifft_launch(const double* Y, int64_t yfstride, int64_t ysplit, int nc, int k0, int nk, int B, int P,
+                           int logn, double* out, int64_t ldout, const double* cstab, int cstride, hipStream_t s) {
   const size_t shmem = ((size_t)(BC / 2) * 2 * P + P) * sizeof(double2);
   if (shmem > 160 * 1024) return -2;
   // raise the dynamic-LDS limit once per instantiation (a per-launch attribute call costs host
   // time on the step's critical path at block boundaries)
   if (!lds_attr_once((const void*)far_ifft_kernel<BC>)) return -3;
   const int nbc = (B + BC - 1) / BC;
-  far_ifft_kernel<BC><<<(unsigned)(nc * nbc), 256, shmem, s>>>(Y, yfstride, ysplit, nc, B, P, logn, out, ldout,
+  far_ifft_kernel<BC><<<(unsigned)(nk * nbc), 256, shmem, s>>>(Y, yfstride, ysplit, nc, k0, B, P, logn, out, ldout,
                                                               (const double2*)cstab, cstride);
   return 0;
 }
 
 int launch_far_ifft(const double* Y, int64_t yfstride, int64_t ysplit, int nc, int B, int P, double* out,
-                    int64_t ldout, const double* cstab, int cstride, hipStream_t s) {
+                    int64_t ldout, const double* cstab, int cstride, hipStream_t s, int k0, int k1) {
+  if (k1 < 0 || k1 > nc) k1 = nc;
+  k0 = k0 < 0 ? 0 : k0;
+  const int nk = k1 - k0;
+  if (nk <= 0) return 0;
   int logn = 0;
   while ((1 << logn) < 2 * P) ++logn;
   if ((1 << logn) != 2 * P) return -1;
   switch (fft_bc(B, P)) {
-    case 64: return far_ifft_launch<64>(Y, yfstride, ysplit, nc, B, P, logn, out, ldout, cstab, cstride, s);
-    case 32: return far_ifft_launch<32>(Y, yfstride, ysplit, nc, B, P, logn, out, ldout, cstab, cstride, s);
-    case 16: return far_ifft_launch<16>(Y, yfstride, ysplit, nc, B, P, logn, out, ldout, cstab, cstride, s);
-    default: return far_ifft_launch<8>(Y, yfstride, ysplit, nc, B, P, logn, out, ldout, cstab, cstride, s);
+    case 64: return far_ifft_launch<64>(Y, yfstride, ysplit, nc, k0, nk, B, P, logn, out, ldout, cstab, cstride, s);
+    case 32: return far_ifft_launch<32>(Y, yfstride, ysplit, nc, k0, nk, B, P, logn, out, ldout, cstab, cstride, s);
+    case 16: return far_ifft_launch<16>(Y, yfstride, ysplit, nc, k0, nk, B, P, logn, out, ldout, cstab, cstride, s);
+    default: return far_ifft_launch<8>(Y, yfstride, ysplit, nc, k0, nk, B, P, logn, out, ldout, cstab, cstride, s);
   }
 }
 
