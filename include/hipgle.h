@@ -57,7 +57,7 @@ typedef struct gle_config {
                            8 when every bath has nc <= 512, 4 otherwise                          */
     int32_t far_mode;   /* GLE_FAR_AUTO / GLE_FAR_DIRECT / GLE_FAR_SPECTRAL                      */
     int32_t max_block;  /* largest ladder block length; 0 = auto (256 spectral, direct: L with
-                           L * ntraj >= 256, L <= 32)                                           */
+                           L * ntraj >= 256, L <= 64)                                           */
 } gle_config;
 
 /* memory sum  S(t+1) = sum_{i>=1} K_i p_{t+1-i}   as a ladder:

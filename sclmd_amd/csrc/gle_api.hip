@@ -1733,9 +1733,12 @@ int freeze(gle_handle* h) {
   } else if (spec_ok) {
     Pmax = std::max(P0, 256);
   } else {
-    // direct: enough columns per block for MFMA reuse of each streamed kernel slice
+    // direct: enough columns per block for MFMA reuse of each streamed kernel slice, and long
+    // enough blocks that the last level's kernel slices stream from HBM rarely: the last level
+    // reads (ml - 2 Pmax) slices per Pmax steps.  C2 (one trajectory, ml = 1024): Pmax 64 ran
+    // 30.8 us/step against 46.6 at 32 (128: 31.4, 256: 31.9; same box, r03)
     int L = P0;
-    while (L * B < 256 && L < 32) L *= 2;
+    while (L * B < 256 && L < 64) L *= 2;
     Pmax = L;
   }
   h->P0 = P0;

@@ -75,6 +75,17 @@ def measure(args, meta, dyn, baths):
             st.run(args.short)
             st.sync()
             reps.append(round((time.perf_counter() - t0) / args.short * 1e3, 5))
+        wins = {}
+        for K in [int(x) for x in args.windows.split(",") if x]:  # window-length sweep: t(K) = a + b K
+            ts = []
+            for _ in range(args.window_reps):
+                st.run(29)
+                st.sync()
+                t0 = time.perf_counter()
+                st.run(K)
+                st.sync()
+                ts.append((time.perf_counter() - t0) * 1e3)
+            wins[K] = round(float(np.median(ts)), 4)
         p, q, _ = st.get_state()
     finally:
         st.close()
@@ -89,7 +100,7 @@ def measure(args, meta, dyn, baths):
                  "cgemm_tflops": prof["flops"] / (ms * 1e-3) / 1e12}
     return {**extra, "ms_per_step": el / args.steps * 1e3, "short_ms_per_step": el_short / max(args.short, 1) * 1e3,
             "aligned_short_ms_per_step": el_aligned / max(args.short, 1) * 1e3, "short_reps_ms": reps,
-            "traj_steps_per_s": B * args.steps / el, "finite": bool(np.isfinite(p).all() and np.isfinite(q).all())}
+            "traj_steps_per_s": B * args.steps / el, "window_ms": wins, "finite": bool(np.isfinite(p).all() and np.isfinite(q).all())}
 
 
 def main():
@@ -104,6 +115,8 @@ def main():
     ap.add_argument("--short-reps", type=int, default=0, help="extra short windows at drifting phases")
     ap.add_argument("--profile", type=int, default=0, help="HIP-event timing of the far-field launches on")
     ap.add_argument("--chainprof", type=int, default=0, help="device stamps of the chain launches on")
+    ap.add_argument("--windows", default="", help="comma-separated window lengths: median ms per window")
+    ap.add_argument("--window-reps", type=int, default=9)
     args = ap.parse_args()
     from sclmd_amd import synthetic
 
