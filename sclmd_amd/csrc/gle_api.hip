@@ -2527,7 +2527,7 @@ int gle_create(const gle_config* cfg, gle_handle** out) {
       if (reserve > 0)
         e = hipExtStreamCreateWithCUMask(&h->bg[i], (uint32_t)cumask.size(), cumask.data());
       else
-        e = hipStreamCreateWithPriority(&h->bg[i], hipStreamNonBlocking, lo);
+        e = hipStreamCreateWithPriority(&h->bg[i], hipStreamNonBlocking, gle_env("GLE_BG_SAMEPRIO") ? hi : lo);
       if (e == hipSuccess)
         e = hipEventCreateWithFlags(&h->ev_bg[i], hipEventDisableTiming | hipEventReleaseToDevice);
     }
