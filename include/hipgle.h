@@ -279,6 +279,13 @@ int gle_set_plan_class(gle_handle* h, int32_t plan_class);
  * Requires a plan.  Any pointer may be NULL. */
 int gle_plan_detail(gle_handle* h, int32_t* plan_class, int32_t* fused_waves, double* cg_per_cu,
                     int32_t* nlevel, int64_t* dyn_dropped, int32_t* far_fused);
+/* Plan flags of the built plan: GLE_PLAN_FUSED_BC (the velocity stages B + C run as one launch),
+ * GLE_PLAN_FPOT_LAUNCH (md.potforce at q~ runs as a small launch before the fused stage, which
+ * then needs no K0 P dyn product; the large-bath plan), GLE_PLAN_FAR_FUSED.  Requires a plan. */
+#define GLE_PLAN_FUSED_BC 1
+#define GLE_PLAN_FPOT_LAUNCH 2
+#define GLE_PLAN_FAR_FUSED 4
+int gle_plan_flags(gle_handle* h, int32_t* flags);
 /* Memory-sum ladder levels: *nlevel = number of levels; for the first nmax levels the block length
  * P[l] and the blocks of that level issued since profiling was enabled (a block issued in pieces
  * counts its pieces' share).  Over a window of K steps a level in steady state issues K / P. */

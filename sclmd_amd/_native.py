@@ -32,7 +32,7 @@ EXPORTS = [
     "gle_profile_levels", "gle_step_work", "gle_reduce_current", "gle_comm_unique_id", "gle_comm_init",
     "gle_comm_destroy", "gle_record", "gle_record_zero", "gle_get_record", "gle_get_record_history",
     "gle_power_spectrum", "gle_set_record", "gle_set_record_history", "gle_noise_stream_begin",
-    "gle_noise_stream_chunk", "gle_noise_stream_end", "gle_set_plan_class", "gle_plan_detail",
+    "gle_noise_stream_chunk", "gle_noise_stream_end", "gle_set_plan_class", "gle_plan_detail", "gle_plan_flags",
     "gle_comm_allreduce", "gle_noise_stream_abort", "gle_device_mem_info",
 ]
 
@@ -100,6 +100,7 @@ _SIGS = {
     "gle_set_plan_class": (ctypes.c_int, [_P, ctypes.c_int32]),
     "gle_plan_detail": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32), _D,
                                        ctypes.POINTER(ctypes.c_int32), _I64, ctypes.POINTER(ctypes.c_int32)]),
+    "gle_plan_flags": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int32)]),
     "gle_reduce_current": (ctypes.c_int, [_P, _P, _D]),
     "gle_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
     "gle_comm_init": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p,
@@ -516,9 +517,11 @@ class Stepper:
         self._chk(self.lib.gle_plan_detail(self.h, ctypes.byref(c), ctypes.byref(w), ctypes.byref(cu),
                                            ctypes.byref(n), ctypes.byref(dd), ctypes.byref(ff)), "gle_plan_detail")
         names = {v: k for k, v in PLAN_CLASSES.items()}
+        fl = ctypes.c_int32(0)
+        self._chk(self.lib.gle_plan_flags(self.h, ctypes.byref(fl)), "gle_plan_flags")
         return {"plan_class": names.get(int(c.value), int(c.value)), "fused_waves": int(w.value),
                 "cg_per_cu": float(cu.value), "nlevel": int(n.value), "dyn_dropped": int(dd.value),
-                "far_fused": bool(ff.value)}
+                "far_fused": bool(ff.value), "fpot_launch": bool(fl.value & 2)}
 
     def profile_levels(self):
         """[(P, blocks issued since profiling was enabled)] per ladder level."""

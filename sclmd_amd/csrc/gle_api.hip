@@ -219,6 +219,14 @@ struct gle_handle {
   Chain chA[2], chB[2], chC, chNear;  // [with dyn.q]; chNear: all near-field partial tiles (priming)
   Chain chBC;                          // stages B + C fused (harmonic force, disjoint baths)
   bool fuse_bc = false;
+  // fused stage with the potential force at q~ evaluated before it (bc_fpot): a small launch between
+  // A and BC computes md.potforce at q~ for every DOF (cache rule included) and adds it to the bath
+  // rows of V, so the velocity stage needs M1.p_half + hK0.(V + Fpot_b) only (two products per bath
+  // row instead of three: no K0 P dyn product)
+  bool bc_fpot = false;
+  int32_t *d_dyn_rp = nullptr, *d_dyn_col = nullptr;  // dyn as CSR (rows of nph), for the fpot launch
+  double* d_dyn_val = nullptr;
+  int32_t* d_fpot_vb = nullptr;                       // per DOF: bath * 2^24 + bath-local row, or -1
   int ch_nw[3] = {4, 8, 4};            // chain workgroup waves per stage (A, B / fused BC, C)
   bool small_baths = false;            // every bath has nc <= 512 (the chain is latency-bound)
   bool far_fused = false;              // spectral levels ride in the chain launches (fused schedule)
@@ -1170,6 +1178,40 @@ int plan_chain(gle_handle* h) {
       }
     const char* e = gle_env("GLE_FUSE_BC");
     h->fuse_bc = h->has_dyn && disjoint && nb > 0 && !(e && atoi(e) == 0);
+    // large baths: the K0 P dyn product costs the fused stage a third of its nc x nc products, more
+    // than the extra launch (C5: 421.6 vs 432.0 us/step; C3: 52.0 vs 50.9, 3 / 2 interleaved
+    // rounds, same box, r03)
+    const char* ef = gle_env("GLE_BC_FPOT");
+    h->bc_fpot = h->fuse_bc && (ef ? atoi(ef) != 0 : !h->small_baths);
+  }
+  if (h->bc_fpot) {
+    std::vector<int32_t> rp(h->nph + 1, 0), col;
+    std::vector<double> val;
+    for (int64_t d = 0; d < h->nph; ++d) {
+      for (int64_t c2 = 0; c2 < h->nph; ++c2) {
+        const double v = h->dyn_h[(size_t)(d * h->nph + c2)];
+        if (v == 0.0) continue;
+        col.push_back((int32_t)c2);
+        val.push_back(v);
+      }
+      rp[d + 1] = (int32_t)col.size();
+    }
+    if (col.empty()) {
+      col.push_back(0);
+      val.push_back(0.0);
+    }
+    std::vector<int32_t> vb(h->nph, -1);
+    for (int j = 0; j < nb; ++j)
+      for (int64_t k = 0; k < h->baths[j].nc; ++k) vb[h->baths[j].cids[k]] = (j << 24) | (int32_t)k;
+    int rc = dalloc_n(h, &h->d_dyn_rp, rp.size());
+    if (!rc) rc = upload(h, h->d_dyn_rp, rp.data(), rp.size() * 4);
+    if (!rc) rc = dalloc_n(h, &h->d_dyn_col, col.size());
+    if (!rc) rc = upload(h, h->d_dyn_col, col.data(), col.size() * 4);
+    if (!rc) rc = dalloc_n(h, &h->d_dyn_val, val.size());
+    if (!rc) rc = upload(h, h->d_dyn_val, val.data(), val.size() * 8);
+    if (!rc) rc = dalloc_n(h, &h->d_fpot_vb, vb.size());
+    if (!rc) rc = upload(h, h->d_fpot_vb, vb.data(), vb.size() * 4);
+    if (rc) return rc;
   }
   if (h->fuse_bc) {
     for (auto& b : h->baths) {
@@ -1380,7 +1422,7 @@ int plan_chain(gle_handle* h) {
                             b.nks, 0});
     }
     segs.insert(segs.end(), qsegs.begin(), qsegs.end());
-    if (withD && h->has_dyn && stage != 2) {
+    if (withD && h->has_dyn && stage != 2 && !(stage == 3 && h->bc_fpot)) {
       int64_t o = h->dyn_tofs[rt];
       for (auto& r : h->dyn_rng[rt]) {
         segs.push_back(Seg{2 * CH_TB, h->d_dynd + o, 64, (stage == 0 ? h->d_Q : h->d_Qt) + (int64_t)4 * r.first * B,
@@ -1395,7 +1437,8 @@ int plan_chain(gle_handle* h) {
       for (int u = 0; u < nu; ++u) {  // OYB: M1.p_half + h K0.V - h (K0 Kq).q~
         const Bath& b = h->baths[ubath[u]];
         segs.push_back(Seg{CH_OYB + u, b.d_K0sqd + b.tofs[rt], 64, b.d_Xcur, (int)B, 0, 0, b.nks, 0});
-        if (b.ml >= 2)  // V = n1 - c S1 from the S(t+1) tiles
+        if (b.ml >= 2 || h->bc_fpot)  // V = n1 - c S1 from the S(t+1) tiles (+ Fpot_b: the fpot launch,
+                                      // which also forms V = n1 + Fpot_b of a bath without memory)
           segs.push_back(Seg{CH_OYB + u, b.d_hK0d + b.tofs[rt], 64, b.d_V, (int)B, 0, 0, b.nks, 0});
         else {          // no memory sum: V = noise(t+1), read from the noise ring (nc rows per slot)
           Seg sg{CH_OYB + u, b.d_hK0d + b.tofs[rt], 64, b.d_noise, (int)B, (int)h->nmd, 1, b.nks, (int)(b.nc * B)};
@@ -1405,7 +1448,7 @@ int plan_chain(gle_handle* h) {
         if (b.has_q)
           segs.push_back(Seg{CH_OYB + u, b.d_KKqd + b.tofs[rt], 64, b.d_Xq + b.vs, (int)B, 0, 0, b.nks, 0});
       }
-      for (int u = 0; u < nu; ++u) {  // OYD: -h (K0 P dyn).q~   (cache miss at q~)
+      for (int u = 0; u < nu && !h->bc_fpot; ++u) {  // OYD: -h (K0 P dyn).q~   (cache miss at q~)
         const Bath& b = h->baths[ubath[u]];
         int64_t o = b.kd_tofs[rt];
         for (auto& r : b.kd_rng[rt]) {
@@ -1415,7 +1458,7 @@ int plan_chain(gle_handle* h) {
           o += (int64_t)r.second * 64;
         }
       }
-      for (int u = 0; u < nu; ++u) {  // OYE: h K0.Fc   (cache hit at q~)
+      for (int u = 0; u < nu && !h->bc_fpot; ++u) {  // OYE: h K0.Fc   (cache hit at q~)
         const Bath& b = h->baths[ubath[u]];
         Seg sg{CH_OYE + u, b.d_hK0d + b.tofs[rt], 64, b.d_Xf, (int)B, 0, 0, b.nks, 0};
         sg.cond = CH_HIT;
@@ -2387,6 +2430,28 @@ int step_end_impl(gle_handle* h, const double* fpot_host_T) {
     if (h->host_force_step) return fail(h, GLE_ERR_STATE, "step begun with a host force must end with one");
   }
   if (h->fuse_bc && mode1 == 1) {
+    if (h->bc_fpot) {
+      FpotArgs fa{};
+      fa.nph = (int32_t)h->nph;
+      fa.B = (int32_t)h->B;
+      fa.par = (int32_t)(h->t & 1);
+      fa.rp = h->d_dyn_rp;
+      fa.col = h->d_dyn_col;
+      fa.val = h->d_dyn_val;
+      fa.vb = h->d_fpot_vb;
+      fa.Qt = h->d_Qt;
+      fa.Fc = h->d_Fc;
+      fa.Q0 = h->d_Q0;
+      fa.pmax = h->d_pmax;
+      fa.t1 = (int32_t)((h->t + 1) % h->nmd);
+      for (size_t j = 0; j < h->baths.size() && j < (size_t)MAXBATH; ++j) {
+        fa.V[j] = h->baths[j].d_V;
+        fa.noise[j] = h->baths[j].ml < 2 ? h->baths[j].d_noise : nullptr;
+        fa.nc[j] = h->baths[j].nc;
+      }
+      launch_fpot(fa, h->stream);
+      mode1 |= 4;  // the velocity stage takes Fpot(q~) from Fc, V holds V + Fpot_b
+    }
     run_chain(h, 3, h->chBC, ta, mode1, h->levels.empty(), 1);
   } else {
     run_chain(h, 1, h->chB[mode1], ta, mode1, h->levels.empty(), 1);
@@ -3484,7 +3549,7 @@ int gle_step_work(gle_handle* h, double* flops, double* bytes) {
     if (b.has_q) nprod += h->fuse_bc ? 3.0 : 2.0;    // Kq.q_t, Kq.q~ (+ K0 Kq.q~)
     fl += 2.0 * nc2 * B * nprod;
     by += 8.0 * nc2 * ((double)b.nn + (h->fuse_bc ? 1.0 : 0.0) + (b.has_q ? 2.0 : 0.0));
-    if (h->fuse_bc) {
+    if (h->fuse_bc && !h->bc_fpot) {
       fl += 2.0 * kd_nnz * B;  // (K0 P dyn).q~ on a potential-cache miss (every harmonic step)
       by += 8.0 * kd_nnz;
     }
@@ -3699,6 +3764,14 @@ int gle_plan_detail(gle_handle* h, int32_t* plan_class, int32_t* fused_waves, do
   if (nlevel) *nlevel = (int32_t)h->levels.size();
   if (dyn_dropped) *dyn_dropped = h->dyn_dropped;
   if (far_fused) *far_fused = h->far_fused ? 1 : 0;
+  return GLE_OK;
+}
+
+int gle_plan_flags(gle_handle* h, int32_t* flags) {
+  if (!h || !flags) return GLE_ERR_ARG;
+  if (!h->frozen) return fail(h, GLE_ERR_STATE, "no plan yet (gle_set_state builds it)");
+  *flags = (h->fuse_bc ? GLE_PLAN_FUSED_BC : 0) | (h->bc_fpot ? GLE_PLAN_FPOT_LAUNCH : 0) |
+           (h->far_fused ? GLE_PLAN_FAR_FUSED : 0);
   return GLE_OK;
 }
 

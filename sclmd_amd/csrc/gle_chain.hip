@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <cstddef>
+#include <vector>
 
 #include "gle_internal.h"
 #include "gle_cgemm.h"
@@ -673,6 +674,7 @@ __device__ __forceinline__ void dof_BC(const ChTile* __restrict__ T, const StepD
   const int par = (int)(t & 1), par1 = par ^ 1;
   const double dt = sd->dt;
   const bool harm = mode != 0;
+  const bool pre = (mode & 4) != 0;  // Fpot(q~) evaluated by the fpot launch: Fc / Q0 current, V + Fpot_b
   Elem E[EPT];
   double ph[EPT], qt[EPT], fc[EPT], q0[EPT];
   bool hit1[EPT];
@@ -690,7 +692,7 @@ __device__ __forceinline__ void dof_BC(const ChTile* __restrict__ T, const StepD
     cons[x] = G(sd->cmask)[E[x].ok ? E[x].d : 0];
     q0[x] = G(sd->Q0)[ii];
     const unsigned long long w1 = *G(pmax_word(sd, 1, par, E[x].ok ? E[x].b : 0));
-    hit1[x] = harm ? word_hit(w1) : true;
+    hit1[x] = (harm && !pre) ? word_hit(w1) : true;
     anyhit |= (E[x].ok && hit1[x]) ? 1 : 0;
     anymiss |= (E[x].ok && !hit1[x]) ? 1 : 0;
 #pragma unroll
@@ -979,17 +981,23 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(DRN == 
   }
 }
 
-// dynamic LDS above the 64 KiB default needs the kernel's limit raised (once per kernel and device)
+// dynamic LDS above the 64 KiB default needs the kernel's limit raised (once per kernel and device;
+// every chain_kernel instantiation has the same function type, so the record is keyed by address)
 template <class K>
 bool lds_limit(K* fn, size_t lds) {
   if (lds <= 64 * 1024) return true;
-  static thread_local int done_dev = -1;
+  struct Entry {
+    const void* fn;
+    int dev;
+  };
+  static thread_local std::vector<Entry> done;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return false;
-  if (done_dev == dev) return true;
+  for (const Entry& e : done)
+    if (e.fn == (const void*)fn && e.dev == dev) return true;
   if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
     return false;
-  done_dev = dev;
+  done.push_back({(const void*)fn, dev});
   return true;
 }
 
@@ -1028,6 +1036,51 @@ void launch_chain(int stage, int nw, int drn, size_t lds_bytes, const ChTile* ti
   else if (stage == 1) launch_st<1>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
   else if (stage == 2) launch_st<2>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
   else launch_st<3>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
+}
+
+namespace {
+__global__ __launch_bounds__(256) void fpot_kernel(FpotArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)a.nph * a.B) return;
+  const int d = (int)(i / a.B), b = (int)(i - (int64_t)d * a.B);
+  const unsigned long long w = *G(a.pmax + ((int64_t)(1 * 2 + a.par)) * a.B + b);
+  double f;
+  if (word_hit(w)) {  // md.potforce cache hit at q~ (md.py:449-450, 767-779)
+    f = G(a.Fc)[i];
+  } else {            // miss: f = -1.0*mdot(dyn, q~) and cache it (md.py:467-473)
+    double acc = 0.0;
+    const int r0 = G(a.rp)[d], r1 = G(a.rp)[d + 1];
+    for (int r = r0; r < r1; ++r) acc += G(a.val)[r] * G(a.Qt)[(int64_t)G(a.col)[r] * a.B + b];
+    f = -1.0 * acc;
+    G(a.Fc)[i] = f;
+    G(a.Q0)[i] = G(a.Qt)[i];
+  }
+  const int vb = G(a.vb)[d];
+  if (vb >= 0) {
+    double* V = a.V[0];
+    const double* nz = a.noise[0];
+    int nc = a.nc[0];
+#pragma unroll
+    for (int j = 1; j < MAXBATH; ++j)
+      if ((vb >> 24) == j) {
+        V = a.V[j];
+        nz = a.noise[j];
+        nc = a.nc[j];
+      }
+    const int k = vb & 0xFFFFFF;
+    const int64_t o = (int64_t)k * a.B + b;
+    // V = n1 - c S1 (S(t+1) tiles of stage A) or n1 (no memory sum), plus the bath rows' Fpot(q~)
+    const double v0 = nz ? G(nz)[((int64_t)a.t1 * nc + k) * a.B + b] : G(V)[o];
+    G(V)[o] = v0 + f;
+  }
+}
+}  // namespace
+
+void launch_fpot(const FpotArgs& a, hipStream_t s) {
+  const int64_t n = (int64_t)a.nph * a.B;
+  if (n <= 0) return;
+  GLE_BOUNDS_SYNC();
+  fpot_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(a);
 }
 
 void bounds_publish_chain(const BoundsTab& t) {

@@ -320,6 +320,21 @@ void launch_reduce(const RItem* items, int nitems, int max_elems, StepArgs ta,
 void launch_chain(int stage, int nw, int drn, size_t lds_bytes, const ChTile* tiles, int ntiles, const StepDev* sd,
                   StepArgs ta, int mode, hipStream_t s);
 void launch_finalize(const StepDev* sd, int B, int nmd, int nbath, hipStream_t s);
+// md.potforce at q~ for every DOF and trajectory before the fused velocity stage (bc_fpot): the
+// cache rule per trajectory (pmax word id1 of parity par), on a miss f = -dyn.q~ (CSR rows) with
+// Fc, Q0 updated; f added to the owning bath's V row (vb: bath << 24 | row, -1 outside the baths)
+struct FpotArgs {
+  int32_t nph, B, par, t1;  // t1 = (t + 1) mod nmd: noise slot of a bath without memory sum
+  const int32_t *rp, *col, *vb;
+  const double* val;
+  const double* Qt;
+  double *Fc, *Q0;
+  const unsigned long long* pmax;
+  double* V[MAXBATH];
+  const double* noise[MAXBATH];  // baths with ml < 2 (no S(t+1) tiles): V = noise(t+1) + Fpot_b
+  int32_t nc[MAXBATH];
+};
+void launch_fpot(const FpotArgs& a, hipStream_t s);
 void launch_philox_normal(double* x, int64_t nfreq, int64_t ncp, int64_t nc, int64_t B,
                           uint64_t seed, uint64_t traj_offset, hipStream_t s, int64_t w_off = 0);
 // streamed noise: a[w0 + w][row_off + r][b] = sum_k M[w][r][k] x[w][k][b] for w < nw
