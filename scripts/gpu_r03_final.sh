@@ -14,7 +14,7 @@ timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_20.j
 timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -30 $O/bench.err; exit 1; }
 timeout -k 10 300 python bench.py --config C2 --ntraj 1 --steps 256 --warmup 32 > $O/bench_c2.json 2> $O/bench_c2.err || { echo "bench c2 failed"; tail -30 $O/bench_c2.err; exit 1; }
 if [ -z "$SKIP_C5" ]; then
-timeout -k 10 400 python bench.py --config C5 --ntraj 32 --steps 64 --warmup 8 --no-cpu-baseline > $O/bench_c5.json 2> $O/bench_c5.err || { echo "bench c5 failed"; tail -30 $O/bench_c5.err; exit 1; }
+timeout -k 10 400 python bench.py --config C5 --ntraj 32 --steps ${C5_STEPS:-64} --warmup 16 --no-cpu-baseline > $O/bench_c5.json 2> $O/bench_c5.err || { echo "bench c5 failed"; tail -30 $O/bench_c5.err; exit 1; }
 fi
 python3 -c "
 import json, os
