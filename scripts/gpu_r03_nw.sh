@@ -11,3 +11,16 @@ for l in open('$O/nw.jsonl'):
     d=json.loads(l); r=d['short_reps_ms']
     print('%-20s'%d['variant'], 'long %.4f'%d['ms_per_step'], 'short %.4f'%d['short_ms_per_step'], 'reps mean %.4f'%st.mean(r), d['finite'])
 "
+# near-field partial slots 16 (plan) vs 32 / 48 (shorter near-field tiles), separate processes
+: > $O/np.jsonl
+for r in 1 2; do
+  for lib in exp np32 np48; do
+    SCLMD_AMD_LIB=sclmd_amd/_lib/libhipgle_$lib.so timeout -k 10 240 python scripts/exp_time.py --steps 512 --short-reps 6 --tag $lib >> $O/np.jsonl 2>> $O/np.err || { echo "$lib failed"; tail -20 $O/np.err; exit 1; }
+  done
+done
+python3 -c "
+import json, statistics as st
+for l in open('$O/np.jsonl'):
+    d=json.loads(l); r=d['short_reps_ms']
+    print('%-6s'%d['tag'], 'long %.4f'%d['ms_per_step'], 'short %.4f'%d['short_ms_per_step'], 'reps mean %.4f'%st.mean(r), d['finite'])
+"
