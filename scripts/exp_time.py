@@ -75,6 +75,16 @@ def measure(args, meta, dyn, baths):
             st.run(args.short)
             st.sync()
             reps.append(round((time.perf_counter() - t0) / args.short * 1e3, 5))
+        scan = []
+        if args.phase_scan:  # bench.py's scan: consecutive sync-bracketed K-step windows over the period
+            K = args.phase_scan
+            for _ in range(max(1, ptop // K)):
+                t_now = st.get_state()[2]
+                st.sync()
+                t0 = time.perf_counter()
+                st.run(K)
+                st.sync()
+                scan.append((int(t_now % ptop), round((time.perf_counter() - t0) / K * 1e3, 5)))
         wins = {}
         for K in [int(x) for x in args.windows.split(",") if x]:  # window-length sweep: t(K) = a + b K
             ts = []
@@ -100,7 +110,7 @@ def measure(args, meta, dyn, baths):
                  "cgemm_tflops": prof["flops"] / (ms * 1e-3) / 1e12}
     return {**extra, "ms_per_step": el / args.steps * 1e3, "short_ms_per_step": el_short / max(args.short, 1) * 1e3,
             "aligned_short_ms_per_step": el_aligned / max(args.short, 1) * 1e3, "short_reps_ms": reps,
-            "traj_steps_per_s": B * args.steps / el, "window_ms": wins, "finite": bool(np.isfinite(p).all() and np.isfinite(q).all())}
+            "traj_steps_per_s": B * args.steps / el, "window_ms": wins, "phase_scan": scan, "finite": bool(np.isfinite(p).all() and np.isfinite(q).all())}
 
 
 def main():
@@ -117,6 +127,7 @@ def main():
     ap.add_argument("--chainprof", type=int, default=0, help="device stamps of the chain launches on")
     ap.add_argument("--windows", default="", help="comma-separated window lengths: median ms per window")
     ap.add_argument("--window-reps", type=int, default=9)
+    ap.add_argument("--phase-scan", type=int, default=0, help="K: K-step windows over the largest period")
     args = ap.parse_args()
     from sclmd_amd import synthetic
 
