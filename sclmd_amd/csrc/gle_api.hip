@@ -1765,7 +1765,7 @@ int freeze(gle_handle* h) {
   h->small_baths = h->plan_class == GLE_PLAN_SMALL_BATHS ? true
                   : h->plan_class == GLE_PLAN_LARGE_BATHS ? false
                                                           : ncmax <= 512;
-  h->cg_per_cu = h->small_baths ? 0.5 : 4.0;
+  h->cg_per_cu = h->small_baths ? 2.0 : 4.0;
   const int P0 = h->cfg.block_len > 0 ? h->cfg.block_len : (h->small_baths ? 8 : 4);
   // fused-stage tile waves: 4 when the chain is latency-bound (C3: 53.3 vs 55.3 us/step with the
   // 1-workgroup-per-CU far-field chunks below), 8 for large baths (C5: 447 vs ~410 us at 4)
@@ -2022,12 +2022,11 @@ int freeze(gle_handle* h) {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, h->cfg.device) == hipSuccess) ncu = prop.multiProcessorCount;
         const int nslot = std::max(1, lv.P / h->P0);
-        // workgroups per CU per cgemm chunk (GLE_CG_PER_CU): with small baths and 4-wave fused
-        // tiles, chunks of ~1/2 workgroup per CU (C3: 53.3 vs 55.3 us/step at 1 vs 2; 0.5 another
-        // 1 % after the dyn roundoff drop, 3 A/B rounds; the chain finds slots sooner, the
-        // far-field launches run at a lower MFMA occupancy); 4 per CU for large baths (C5, with
-        // the fpot launch: 354 vs 400 us/step at 2, flat from 4 to 32; r03, 2 interleaved rounds)
-        double per_cu = h->small_baths ? 0.5 : 4.0;
+        // workgroups per CU per cgemm chunk (GLE_CG_PER_CU): 2 with small baths (C3, r03 with
+        // the spill-free chain and transform pieces, 3 interleaved rounds: 50.0 vs 51.1 us/step
+        // at 0.5, 20-step windows 52.6 vs 55.0; 1 and 3 in between; r02's 0.5 predates those),
+        // 4 for large baths (C5, with the fpot launch: 354 vs 400 us/step at 2, flat from 4 to 32)
+        double per_cu = h->small_baths ? 2.0 : 4.0;
         if (const char* e = gle_env("GLE_CG_PER_CU")) per_cu = std::max(0.25, atof(e));
         h->cg_per_cu = per_cu;
         const double want = (double)lv.cg.size() / (per_cu * ncu);

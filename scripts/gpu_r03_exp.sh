@@ -279,7 +279,7 @@ python3 -c "
 import json, statistics as st
 for l in open('$O/nw.jsonl'):
     d=json.loads(l); r=d['short_reps_ms']
-    print('%-20s'%d['variant'], 'long %.4f'%d['ms_per_step'], 'short %.4f'%d['short_ms_per_step'], 'reps mean %.4f'%st.mean(r), d['finite'])
+    print('%-20s'%d['variant'], 'long %.4f'%d['ms_per_step'], 'short %.4f'%d['short_ms_per_step'], 'reps mean %.4f'%st.mean(r), 'w20 %.4f'%(d['window_ms']['20']/20), d['finite'])
 "
 # near-field partial slots 16 (plan) vs 32 / 48 (shorter near-field tiles), separate processes
 : > $O/np.jsonl
@@ -371,5 +371,18 @@ for l in open('$O/kc.jsonl'):
 "
 }
 
-[ $# -gt 0 ] || { echo "experiments: kc ab1 audit batch c2p c2w c5b c5cpc c5exp c5f c5s evidence fpot interf nw ph win2 xq"; exit 2; }
+exp_c3cpc() {
+# C3 far-field chunk sizes beyond 1 workgroup per CU (0.25-1 were flat earlier this round)
+O=gpurun_out/r03c3cpc
+mkdir -p $O
+SCLMD_AMD_LIB=sclmd_amd/_lib/libhipgle_exp.so timeout -k 10 500 python scripts/exp_time.py --steps 512 --short-reps 8 --rounds 3 --windows 20 --window-reps 9 --variants ";GLE_CG_PER_CU=1;GLE_CG_PER_CU=2;GLE_CG_PER_CU=3" --tag c3cpc > $O/c3cpc.jsonl 2> $O/c3cpc.err || { echo "c3cpc failed"; tail -20 $O/c3cpc.err; exit 1; }
+python3 -c "
+import json, statistics as st
+for l in open('$O/c3cpc.jsonl'):
+    d=json.loads(l); r=d['short_reps_ms']
+    print('%-20s'%d['variant'], 'long %.4f'%d['ms_per_step'], 'short %.4f'%d['short_ms_per_step'], 'reps mean %.4f'%st.mean(r), 'w20 %.4f'%(d['window_ms']['20']/20), d['finite'])
+"
+}
+
+[ $# -gt 0 ] || { echo "experiments: c3cpc kc ab1 audit batch c2p c2w c5b c5cpc c5exp c5f c5s evidence fpot interf nw ph win2 xq"; exit 2; }
 for e in "$@"; do "exp_$e" || exit 1; done

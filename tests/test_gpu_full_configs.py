@@ -94,7 +94,7 @@ def _run_vs_oracle(config, natom, B, check, t0=37, nst=540, nmd=1024, ml=1024, s
     assert P0 == (block_len or (8 if expect_class == "small" else 4)), info
     assert detail["fused_waves"] == (4 if expect_class == "small" else 8), detail
     assert detail["fpot_launch"] == (expect_class == "large"), detail
-    assert detail["cg_per_cu"] == (0.5 if expect_class == "small" else 4.0), detail
+    assert detail["cg_per_cu"] == (2.0 if expect_class == "small" else 4.0), detail
     # every ladder level computed blocks inside the run (P = P0 ... 256 at ml = 1024)
     assert [P for P, _ in levels] == _expected_levels(P0, ml), levels
     assert all(bl >= 1.0 for _, bl in levels), levels
