@@ -384,5 +384,26 @@ for l in open('$O/c3cpc.jsonl'):
 "
 }
 
-[ $# -gt 0 ] || { echo "experiments: c3cpc kc ab1 audit batch c2p c2w c5b c5cpc c5exp c5f c5s evidence fpot interf nw ph win2 xq"; exit 2; }
+exp_lines() {
+# bench lines after the chunk-size changes: C5 cgemm FETCH / WRITE passes (per-launch traffic for the
+# new chunking), then the C3 (20/5, 512) and C5 (256-step period) lines reading the new traffic files
+O=gpurun_out/r03lines
+mkdir -p $O/pmc
+for c in FETCH_SIZE WRITE_SIZE; do
+timeout -s KILL 400 rocprofv3 --pmc $c --output-format csv -d $O/pmc/$c -o run -- python3 bench.py --config C5 --ntraj 32 --steps 256 --warmup 16 --no-cpu-baseline > $O/pmc/$c.json 2> $O/pmc/$c.err || { echo "pmc $c failed"; tail -20 $O/pmc/$c.err; exit 1; }
+done
+python3 scripts/pmc_summary.py $O/pmc $O/pmc/traffic_c5.json --kernel cgemm_kernel --config C5 --ntraj 32 || exit 1
+cp $O/pmc/traffic_c5.json profiles/traffic_C5_32.json
+timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_20.json 2> $O/bench_20.err || { echo "bench20 failed"; tail -30 $O/bench_20.err; exit 1; }
+timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -30 $O/bench.err; exit 1; }
+timeout -k 10 400 python bench.py --config C5 --ntraj 32 --steps 256 --warmup 16 --no-cpu-baseline > $O/bench_c5.json 2> $O/bench_c5.err || { echo "bench c5 failed"; tail -30 $O/bench_c5.err; exit 1; }
+python3 -c "
+import json
+for f in ['bench_20','bench','bench_c5']:
+    d=json.load(open('$O/%s.json'%f)); r=d.get('roofline',{})
+    print(f, '%.0f traj-steps/s'%d['value'], 'us/step %.1f'%(d['ms_per_step']*1e3), 'roof %s %.1f frac %.3f traffic %s algo %s'%(r.get('unit'), r.get('achieved',0), r.get('frac',0), r.get('traffic'), r.get('algorithmic_bytes_per_launch')), d.get('window_phase'))
+"
+}
+
+[ $# -gt 0 ] || { echo "experiments: lines c3cpc kc ab1 audit batch c2p c2w c5b c5cpc c5exp c5f c5s evidence fpot interf nw ph win2 xq"; exit 2; }
 for e in "$@"; do "exp_$e" || exit 1; done
