@@ -405,5 +405,18 @@ for f in ['bench_20','bench','bench_c5']:
 "
 }
 
-[ $# -gt 0 ] || { echo "experiments: lines c3cpc kc ab1 audit batch c2p c2w c5b c5cpc c5exp c5f c5s evidence fpot interf nw ph win2 xq"; exit 2; }
+exp_fftp() {
+# transform piece size (GLE_FFT_CHUNK = P per piece) and piece cadence with the 2-per-CU GEMM chunks
+O=gpurun_out/r03fftp
+mkdir -p $O
+SCLMD_AMD_LIB=sclmd_amd/_lib/libhipgle_exp.so timeout -k 10 700 python scripts/exp_time.py --steps 512 --short-reps 8 --rounds 3 --windows 20 --window-reps 9 --variants ";GLE_FFT_CHUNK=16;GLE_FFT_CHUNK=64;GLE_PIECE_STEP=2" --tag fftp > $O/fftp.jsonl 2> $O/fftp.err || { echo "fftp failed"; tail -20 $O/fftp.err; exit 1; }
+python3 -c "
+import json, statistics as st
+for l in open('$O/fftp.jsonl'):
+    d=json.loads(l); r=d['short_reps_ms']
+    print('%-20s'%d['variant'], 'long %.4f'%d['ms_per_step'], 'reps mean %.4f max %.4f'%(st.mean(r), max(r)), 'w20 %.4f'%(d['window_ms']['20']/20), d['finite'])
+"
+}
+
+[ $# -gt 0 ] || { echo "experiments: fftp lines c3cpc kc ab1 audit batch c2p c2w c5b c5cpc c5exp c5f c5s evidence fpot interf nw ph win2 xq"; exit 2; }
 for e in "$@"; do "exp_$e" || exit 1; done
