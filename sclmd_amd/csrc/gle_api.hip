@@ -1865,10 +1865,10 @@ int freeze(gle_handle* h) {
     lv.cg_rn = (int)std::min<int64_t>(4, (B + 15) / 16);
     lv.cg_split = 1;
     if (lv.spectral) {
-      // small levels: split the k range of every product in two (partial planes added by the
-      // inverse transform) so the launch has >= 2 workgroups per CU to hide the HBM latency of the
-      // K̂ stream, which is still read once (GLE_CG_NARROW: 32-column tiles instead, reading it
-      // once per 32 columns)
+      // small levels of large baths: split the k range of every product in two (partial planes
+      // added by the inverse transform) so the launch has >= 2 workgroups per CU to hide the HBM
+      // latency of the K̂ stream, which is still read once (GLE_CG_NARROW: 32-column tiles
+      // instead, reading it once per 32 columns)
       int64_t n4 = 0;
       for (auto& b : h->baths)
         if (b.ml > lv.lag0)
@@ -1876,7 +1876,11 @@ int freeze(gle_handle* h) {
       int ncu = 256;
       hipDeviceProp_t prop;
       if (hipGetDeviceProperties(&prop, h->cfg.device) == hipSuccess) ncu = prop.multiProcessorCount;
-      if (n4 < 2 * ncu) {
+      // not with small baths: with 2-workgroup-per-CU chunks the unsplit products ran 49.0 vs 50.3
+      // us/step at C3 (3 interleaved rounds, r03); GLE_CG_SPLIT=0/1 forces it off / on
+      const char* esp = gle_env("GLE_CG_SPLIT");
+      const bool want_split = esp ? atoi(esp) != 0 : !h->small_baths;
+      if (n4 < 2 * ncu && want_split) {
         if (gle_env("GLE_CG_NARROW")) lv.cg_rn = 2;
         else lv.cg_split = 2;
       }

@@ -418,5 +418,20 @@ for l in open('$O/fftp.jsonl'):
 "
 }
 
-[ $# -gt 0 ] || { echo "experiments: fftp lines c3cpc kc ab1 audit batch c2p c2w c5b c5cpc c5exp c5f c5s evidence fpot interf nw ph win2 xq"; exit 2; }
+exp_split() {
+# small spectral levels without the k-split of their products (GLE_CG_SPLIT=0), and the far-field
+# items without the XCD grouping (GLE_CG_XCD=0, read once per process: its own process)
+O=gpurun_out/r03split
+mkdir -p $O
+SCLMD_AMD_LIB=sclmd_amd/_lib/libhipgle_exp.so timeout -k 10 500 python scripts/exp_time.py --steps 512 --short-reps 8 --rounds 3 --windows 20 --window-reps 9 --variants ";GLE_CG_SPLIT=0" --tag split > $O/split.jsonl 2> $O/split.err || { echo "split failed"; tail -20 $O/split.err; exit 1; }
+GLE_CG_XCD=0 SCLMD_AMD_LIB=sclmd_amd/_lib/libhipgle_exp.so timeout -k 10 300 python scripts/exp_time.py --steps 512 --short-reps 8 --windows 20 --window-reps 9 --tag noxcd >> $O/split.jsonl 2>> $O/split.err || { echo "noxcd failed"; tail -20 $O/split.err; exit 1; }
+python3 -c "
+import json, statistics as st
+for l in open('$O/split.jsonl'):
+    d=json.loads(l); r=d['short_reps_ms']
+    print('%-8s %-16s'%(d['tag'], d['variant']), 'long %.4f'%d['ms_per_step'], 'reps mean %.4f'%st.mean(r), 'w20 %.4f'%(d['window_ms']['20']/20), d['finite'])
+"
+}
+
+[ $# -gt 0 ] || { echo "experiments: split fftp lines c3cpc kc ab1 audit batch c2p c2w c5b c5cpc c5exp c5f c5s evidence fpot interf nw ph win2 xq"; exit 2; }
 for e in "$@"; do "exp_$e" || exit 1; done
