@@ -433,5 +433,33 @@ for l in open('$O/split.jsonl'):
 "
 }
 
-[ $# -gt 0 ] || { echo "experiments: split fftp lines c3cpc kc ab1 audit batch c2p c2w c5b c5cpc c5exp c5f c5s evidence fpot interf nw ph win2 xq"; exit 2; }
+exp_final4() {
+# current code: parity suite, C3 cgemm / chain PMC passes first (traffic per launch for the current
+# chunking into profiles/traffic_C3_64.json), then the C3 / C2 bench lines and the C3 kernel trace
+O=gpurun_out/r03final4
+mkdir -p $O/prof $O/pmc
+timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo "tests failed"; grep -E "FAILED|Error" $O/gpu_tests.log | head; tail -30 $O/gpu_tests.log; exit 1; }
+tail -1 $O/gpu_tests.log
+for c in FETCH_SIZE WRITE_SIZE; do
+timeout -s KILL 300 rocprofv3 --pmc $c --output-format csv -d $O/pmc/$c -o run -- python3 bench.py --no-cpu-baseline > $O/pmc/$c.json 2> $O/pmc/$c.err || { echo "pmc $c failed"; tail -20 $O/pmc/$c.err; exit 1; }
+done
+python3 scripts/pmc_summary.py $O/pmc $O/pmc/traffic_cgemm.json --kernel cgemm_kernel --config C3 --ntraj 64 || exit 1
+python3 scripts/pmc_summary.py $O/pmc $O/pmc/traffic_chain.json --kernel chain_kernel --config C3 --ntraj 64 --last 1024 --skip-chain-window 0 || exit 1
+cp $O/pmc/traffic_cgemm.json profiles/traffic_C3_64.json
+timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_20.json 2> $O/bench_20.err || { echo "bench20 failed"; tail -30 $O/bench_20.err; exit 1; }
+timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -30 $O/bench.err; exit 1; }
+timeout -k 10 300 python bench.py --config C2 --ntraj 1 --steps 256 --warmup 32 > $O/bench_c2.json 2> $O/bench_c2.err || { echo "bench c2 failed"; tail -30 $O/bench_c2.err; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --no-cpu-baseline > $O/prof/bench.json 2> $O/prof/bench.err || { echo "prof failed"; tail -20 $O/prof/bench.err; exit 1; }
+N=$(python3 -c "import json;print(json.load(open('$O/prof/bench.json'))['roofline']['launches'])")
+python3 scripts/trace_summary.py $O/prof/run_kernel_trace.csv --steps --gaps --last cgemm $N --skip $N > $O/prof/summary.txt
+tail -4 $O/prof/summary.txt
+python3 -c "
+import json
+for f in ['bench_20','bench','bench_c2']:
+    d=json.load(open('$O/%s.json'%f)); r=d.get('roofline',{}); c=d.get('chain_roofline',{})
+    print(f, '%.0f traj-steps/s'%d['value'], 'us/step %.1f'%(d['ms_per_step']*1e3), 'roof %s %.1f frac %.3f traffic %s algo %s'%(r.get('unit'), r.get('achieved',0), r.get('frac',0), r.get('traffic'), r.get('algorithmic_bytes_per_launch')), 'chain %.1f frac %.3f'%(c.get('us_per_step',0), c.get('frac',0)), 'cpu', (d.get('cpu_baseline') or {}).get('value'), d.get('window_phase'))
+"
+}
+
+[ $# -gt 0 ] || { echo "experiments: final4 split fftp lines c3cpc kc ab1 audit batch c2p c2w c5b c5cpc c5exp c5f c5s evidence fpot interf nw ph win2 xq"; exit 2; }
 for e in "$@"; do "exp_$e" || exit 1; done
