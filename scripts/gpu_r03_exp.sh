@@ -461,5 +461,18 @@ for f in ['bench_20','bench','bench_c2']:
 "
 }
 
-[ $# -gt 0 ] || { echo "experiments: final4 split fftp lines c3cpc kc ab1 audit batch c2p c2w c5b c5cpc c5exp c5f c5s evidence fpot interf nw ph win2 xq"; exit 2; }
+exp_cpc2() {
+# C3 GEMM chunk size around 2 per CU with the unsplit small levels
+O=gpurun_out/r03cpc2
+mkdir -p $O
+SCLMD_AMD_LIB=sclmd_amd/_lib/libhipgle_exp.so timeout -k 10 600 python scripts/exp_time.py --steps 512 --short-reps 8 --rounds 3 --windows 20 --window-reps 9 --variants ";GLE_CG_PER_CU=1.5;GLE_CG_PER_CU=3" --tag cpc2 > $O/cpc2.jsonl 2> $O/cpc2.err || { echo "cpc2 failed"; tail -20 $O/cpc2.err; exit 1; }
+python3 -c "
+import json, statistics as st
+for l in open('$O/cpc2.jsonl'):
+    d=json.loads(l); r=d['short_reps_ms']
+    print('%-20s'%d['variant'], 'long %.4f'%d['ms_per_step'], 'reps mean %.4f'%st.mean(r), 'w20 %.4f'%(d['window_ms']['20']/20), d['finite'])
+"
+}
+
+[ $# -gt 0 ] || { echo "experiments: cpc2 final4 split fftp lines c3cpc kc ab1 audit batch c2p c2w c5b c5cpc c5exp c5f c5s evidence fpot interf nw ph win2 xq"; exit 2; }
 for e in "$@"; do "exp_$e" || exit 1; done
