@@ -389,7 +389,7 @@ def main():
                      "timing": "device timestamps (per-workgroup stores)",
                      "algorithmic_flops_per_launch": prof["chain_flops"] / nl})
         res["roofline"] = roof
-    if prof.get("chain_launches", 0) > 0 and plan["far_mode"] == "spectral" and not detail["far_fused"]:
+    if prof.get("chain_launches", 0) > 0 and not detail["far_fused"]:
         # the per-step chain (md.vv stages, the step's critical path) in the same window, timed by
         # its own device timestamps: algorithmic flops of its products / its kernel durations;
         # us_per_step = chain kernel time per step (beside the far field, so > its time alone)

@@ -893,7 +893,7 @@ int fill_tasks(gle_handle* h, ChTile& T, const std::vector<Seg>& segs, int nout,
         tk.slot = cur_slot;
         tk.cond = sg.cond;
         tk.xrows = (int32_t)((sg.xrows > 0 ? sg.xrows : 4 * sg.nks) - 4 * kl);
-        *flops += 2048.0 * T.rn * (double)(s1 - s0);
+        *flops += 128.0 * T.ncols * (double)(s1 - s0);  // 2 x 16 rows x 4 k x valid columns
       }
       pos += sg.nks;
     }
@@ -977,7 +977,7 @@ int fill_tasks_balanced(ChTile& T, const std::vector<Seg>& segs, int nout, Chain
       tk.slot = slot_of[w][sg.o];
       tk.cond = sg.cond;
       tk.xrows = (int32_t)((sg.xrows > 0 ? sg.xrows : 4 * sg.nks) - 4 * r.kl);
-      c.flops += 2048.0 * T.rn * (double)r.n;
+      c.flops += 128.0 * T.ncols * (double)r.n;  // 2 x 16 rows x 4 k x valid columns
     }
     T.ntw[w] = cnt;
   }

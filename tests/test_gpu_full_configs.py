@@ -2,7 +2,7 @@
 
 C3 as benched: 300-atom junction, 2 phonon baths nc = 300, ml = 1024, 64 trajectories with the
 spectral ladder plan bench.py runs (levels P = 8 ... 256 at the default first block length, and
-P = 4 ... 256 at block_len = 4; split-K cgemm items), started
+P = 4 ... 256 at block_len = 4; far-field GEMM chunks of 2 workgroups per CU), started
 at an unaligned t0 from a random nonzero history, run 540 steps so that every level's blocks are
 computed from nonzero data (the P = 256 level fires at 256 and 512).  Reduced C5: three baths (two
 phonon baths and a biased electron bath with exim, zeta1, zeta2 != 0, nc = 96-99), ml = 1024, 32
@@ -12,8 +12,9 @@ oracle (oracle.GLEBatch, pinned to the reference-shaped oracle and the reference
 the ladder plan; wrap-around is covered in test_gpu_md.py).
 
 The large-bath plan (any bath with nc > 512: first block length 4 with a direct P = 4 level, the
-8-wave fused velocity stage, 2 far-field GEMM workgroups per CU per chunk) is what bench.py runs at
-C5 (nc = 999 / 1002).  It is checked twice against the oracle: at nc = 522 (natom 522, ml = 512,
+8-wave fused velocity stage, the fpot launch, split-K far-field GEMM chunks of 4 workgroups per CU)
+is what bench.py runs at C5 (nc = 999 / 1002).  It is checked twice against the oracle: at nc = 522
+(natom 522, ml = 512,
 picked by the automatic rule), and at the reduced C5 size with the plan class forced through the
 ABI (gle_set_plan_class), so both plan classes meet the same biased three-bath junction."""
 import numpy as np
