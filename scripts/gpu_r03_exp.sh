@@ -474,5 +474,19 @@ for l in open('$O/cpc2.jsonl'):
 "
 }
 
-[ $# -gt 0 ] || { echo "experiments: cpc2 final4 split fftp lines c3cpc kc ab1 audit batch c2p c2w c5b c5cpc c5exp c5f c5s evidence fpot interf nw ph win2 xq"; exit 2; }
+exp_c5alone() {
+# C5: the chain with and without the far field (GLE_DBG_NO_LADDER=1: no ladder levels, wrong
+# numbers, timing only), chain launches device-stamped: how much the K-hat stream costs the chain.
+O=gpurun_out/r03c5alone
+mkdir -p $O
+SCLMD_AMD_LIB=sclmd_amd/_lib/libhipgle_exp.so timeout -k 10 600 python -u scripts/exp_time.py --config C5 --ntraj 32 --steps 256 --short 20 --rounds 2 --chainprof 1 --variants ";GLE_DBG_NO_LADDER=1" --tag c5alone > $O/c5alone.jsonl 2> $O/c5alone.err || { echo "c5alone failed"; tail -20 $O/c5alone.err; exit 1; }
+python3 -c "
+import json
+for l in open('$O/c5alone.jsonl'):
+    d=json.loads(l)
+    print('%-22s'%d['variant'], 'long %.4f'%d['ms_per_step'], 'chain us/step', d.get('chain_us_per_step'))
+"
+}
+
+[ $# -gt 0 ] || { echo "experiments: c5alone cpc2 final4 split fftp lines c3cpc kc ab1 audit batch c2p c2w c5b c5cpc c5exp c5f c5s evidence fpot interf nw ph win2 xq"; exit 2; }
 for e in "$@"; do "exp_$e" || exit 1; done
