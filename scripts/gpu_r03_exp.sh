@@ -488,5 +488,19 @@ for l in open('$O/c5alone.jsonl'):
 "
 }
 
-[ $# -gt 0 ] || { echo "experiments: c5alone cpc2 final4 split fftp lines c3cpc kc ab1 audit batch c2p c2w c5b c5cpc c5exp c5f c5s evidence fpot interf nw ph win2 xq"; exit 2; }
+exp_c5skip() {
+# C5 step decomposition (timing only, wrong numbers): no far-field GEMMs (GLE_DBG_SKIP=1), no
+# transforms (6), neither (7), against the plan; chain launches device-stamped.
+O=gpurun_out/r03c5skip
+mkdir -p $O
+SCLMD_AMD_LIB=sclmd_amd/_lib/libhipgle_exp.so timeout -k 10 600 python -u scripts/exp_time.py --config C5 --ntraj 32 --steps 256 --short 20 --rounds 2 --chainprof 1 --variants ";GLE_DBG_SKIP=1;GLE_DBG_SKIP=6;GLE_DBG_SKIP=7" --tag c5skip > $O/c5skip.jsonl 2> $O/c5skip.err || { echo "c5skip failed"; tail -20 $O/c5skip.err; exit 1; }
+python3 -c "
+import json
+for l in open('$O/c5skip.jsonl'):
+    d=json.loads(l)
+    print('%-22s'%d['variant'], 'long %.4f'%d['ms_per_step'], 'chain us/step', d.get('chain_us_per_step'))
+"
+}
+
+[ $# -gt 0 ] || { echo "experiments: c5skip c5alone cpc2 final4 split fftp lines c3cpc kc ab1 audit batch c2p c2w c5b c5cpc c5exp c5f c5s evidence fpot interf nw ph win2 xq"; exit 2; }
 for e in "$@"; do "exp_$e" || exit 1; done
