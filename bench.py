@@ -125,6 +125,44 @@ def refuse_experiment_env():
             bad, (" SCLMD_AMD_LIB=" + lib) if lib else ""))
 
 
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_command(nproc, argv, port):
+    """torch.distributed.run command line that starts `nproc` ranks of this script (one per GPU) on
+    the loopback rendezvous, with the parent's own arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def launch_or_check_world(args, argv):
+    """--gpus N > 1 without a torchrun environment: start the N ranks as child processes BEFORE any
+    GPU call (the parent never initialises HIP) and return their exit status; under torchrun the
+    launcher's WORLD_SIZE must equal --gpus.  Returns None when this process is a rank."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if args.gpus > 1:
+            import subprocess
+
+            env = dict(os.environ)
+            env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+            cmd = spawn_command(args.gpus, argv, _free_port())
+            log("[bench] starting %d ranks: %s" % (args.gpus, " ".join(cmd)))
+            return subprocess.call(cmd, env=env)
+        return None
+    if int(env_world) != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%s (launch one rank per GPU with "
+                         "--nproc-per-node equal to --gpus)" % (args.gpus, env_world))
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -160,6 +198,11 @@ def main():
                          "profiles/traffic_latest.json (used only when its config / ntraj / plan match)")
     args = ap.parse_args()
     refuse_experiment_env()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    rc = launch_or_check_world(args, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
     if not args.traffic_json:
         per = os.path.join(ROOT, "profiles", "traffic_%s_%d.json" % (args.config, args.ntraj))
         args.traffic_json = per if os.path.exists(per) else os.path.join(ROOT, "profiles", "traffic_latest.json")
@@ -175,8 +218,14 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if args.same_device:
             local_rank = 0
+        elif torch.cuda.device_count() < world:
+            raise SystemExit("bench.py: %d ranks but %d visible GPUs (one rank per GPU; --same-device "
+                             "rehearses the multi-rank path on one)" % (world, torch.cuda.device_count()))
         torch.cuda.set_device(local_rank)
         dist.init_process_group(args.dist_backend)
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit("bench.py: process group has %d ranks, --gpus %d" % (dist.get_world_size(), args.gpus))
+        world, rank = dist.get_world_size(), dist.get_rank()
 
     from sclmd_amd import md as MD
     from sclmd_amd import synthetic

@@ -76,8 +76,10 @@ typedef struct gle_config {
 
 /* Plan class.  AUTO picks by the largest bath: SMALL when every bath has nc <= 512 (the per-step
  * chain is latency-bound: first block length 8, 4-wave fused velocity-stage tiles, far-field GEMM
- * chunks of ~1/2 workgroup per CU), LARGE otherwise (first block length 4, 8-wave fused tiles, 2
- * workgroups per CU).  Forcing a class changes only the schedule, never the result beyond fp64
+ * chunks of 2 workgroups per CU), LARGE otherwise (first block length 4, 8-wave fused tiles, the
+ * potential force at q~ as its own small launch before the fused stage (GLE_PLAN_FPOT_LAUNCH),
+ * far-field GEMM chunks of 4 workgroups per CU).  Forcing a class changes only the schedule, never
+ * the result beyond fp64
  * rounding; tests use it to run the large-bath plan at small sizes. */
 #define GLE_PLAN_AUTO 0
 #define GLE_PLAN_SMALL_BATHS 1

@@ -2504,9 +2504,16 @@ const char* gle_last_error(const gle_handle* h) {
 
 int gle_device_mem_info(int32_t device, int64_t* free_bytes, int64_t* total_bytes) {
   if (!free_bytes || !total_bytes) return fail(nullptr, GLE_ERR_ARG, "null argument");
-  if (hipSetDevice(device) != hipSuccess) return fail(nullptr, GLE_ERR_HIP, "gle_device_mem_info: no such device");
+  // the caller's current device (e.g. torch's) is restored on every return path
+  int prev = -1;
+  if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  if (hipSetDevice(device) != hipSuccess) {
+    if (prev >= 0) (void)hipSetDevice(prev);
+    return fail(nullptr, GLE_ERR_HIP, "gle_device_mem_info: no such device");
+  }
   size_t fr = 0, tot = 0;
   const hipError_t e = hipMemGetInfo(&fr, &tot);
+  if (prev >= 0) (void)hipSetDevice(prev);
   if (e != hipSuccess) return fail(nullptr, GLE_ERR_HIP, std::string("hipMemGetInfo: ") + hipGetErrorString(e));
   *free_bytes = (int64_t)fr;
   *total_bytes = (int64_t)tot;
@@ -3557,9 +3564,11 @@ int gle_step_work(gle_handle* h, double* flops, double* bytes) {
       fl += 2.0 * kd_nnz * B;  // (K0 P dyn).q~ on a potential-cache miss (every harmonic step)
       by += 8.0 * kd_nnz;
     }
+    if (h->bc_fpot) by += 16.0 * b.nc * B;  // fpot launch: V += Fpot_b (read-modify-write of every bath row)
     by += 8.0 * 12.0 * b.nc * B;  // bath-local vectors: noise rows, S, V, gathers, ring pushes
   }
-  fl += 2.0 * dyn_nnz * B;  // dyn.q~ (the potential force at q~)
+  fl += 2.0 * dyn_nnz * B;  // dyn.q~ (the potential force at q~; the fpot launch's CSR product under bc_fpot)
+  if (h->bc_fpot) by += 4.0 * dyn_nnz + 4.0 * (h->nph + 1) + 8.0 * 3.0 * (double)h->nph * B;  // CSR columns / rows, Qt, Fc, Q0
   by += 8.0 * dyn_nnz + 8.0 * 12.0 * (double)h->nph * B;  // dyn, state vectors (p, q, p_half, q~, F, caches)
   for (const Level& lv : h->levels) {
     const double P = (double)lv.P;

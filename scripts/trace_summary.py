@@ -13,6 +13,14 @@ def short(name):
 
 
 rows = list(csv.DictReader(open(sys.argv[1])))
+
+
+def step_end_stage(rs):
+    """The chain launch that closes a step: the fused velocity stage (chain_kernel<3, ...>, plans with
+    GLE_PLAN_FUSED_BC: 2 chain launches per step) or stage C (chain_kernel<2, ...>: 3 per step)."""
+    return "chain_kernel<3" if any(r["n"].startswith("chain_kernel<3") for r in rs) else "chain_kernel<2"
+
+
 for r in rows:
     r["s"] = int(r["Start_Timestamp"])
     r["e"] = int(r["End_Timestamp"])
@@ -42,7 +50,7 @@ if "--last" in sys.argv:
 
 if "--steps" in sys.argv:
     rows.sort(key=lambda r: r["s"])
-    cs = [r for r in rows if r["n"].startswith("chain_kernel<2")]
+    cs = [r for r in rows if r["n"].startswith(step_end_stage(rows))]
     n = min(100, len(cs) - 1)
     if n > 0:
         a, b = cs[-n - 1]["e"], cs[-1]["e"]
@@ -80,7 +88,10 @@ if "--gaps" in sys.argv:
     rows.sort(key=lambda r: r["s"])
     ch = [r for r in rows if r["n"].startswith("chain_kernel")][-301:]
     gaps = [(b["s"] - a["e"]) / 1e3 for a, b in zip(ch, ch[1:])]
-    if gaps:
-        print("\nchain gaps over %d launches: total %.1f us = %.2f us/step; largest %s"
-              % (len(gaps), sum(gaps), sum(gaps) / (len(gaps) / 3.0),
+    # steps in the window = its step-closing launches (2 chain launches per step in fused plans, 3
+    # otherwise), not a fixed 3
+    nsteps = sum(1 for r in ch[1:] if r["n"].startswith(step_end_stage(ch)))
+    if gaps and nsteps:
+        print("\nchain gaps over %d launches (%d steps): total %.1f us = %.2f us/step; largest %s"
+              % (len(gaps), nsteps, sum(gaps), sum(gaps) / nsteps,
                  [round(x, 1) for x in sorted(gaps)[-8:]]))
