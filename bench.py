@@ -248,10 +248,15 @@ def main():
             b.noise = rng.standard_normal((args.ntraj, meta["nmd"], b.nc)) * 1e-3
     else:
         for i in range(len(baths)):
+            tn = time.perf_counter()
             m.gen_noise(i, 0)
+            log("[bench] rank %d noise of bath %d (%s, nc %d): %.1fs" % (rank, i, baths[i].kind, baths[i].nc,
+                                                                      time.perf_counter() - tn))
     st = m._ensure_device()
+    tp = time.perf_counter()
     m.steps(0)  # uploads assigned noise
     st.sync()
+    log("[bench] rank %d plan / first prime: %.1fs" % (rank, time.perf_counter() - tp))
     setup_s = time.perf_counter() - t_setup
     plan = st.plan_info()
     detail = st.plan_detail()

@@ -174,6 +174,12 @@ int gle_noise_generate(gle_handle* h, int32_t bath, const double* x_host, uint64
 int gle_noise_stream_begin(gle_handle* h, int32_t bath, int32_t is_complex, int64_t max_chunk);
 int gle_noise_stream_chunk(gle_handle* h, int32_t bath, int64_t w0, int64_t nw, const double* m_re,
                            const double* m_im, uint64_t seed, uint64_t traj_offset);
+/* Frequencies [w0, w0 + nw) whose factor is one shared matrix times a per-frequency scale (a
+ * spectrum A_w = s_w H: factor sqrt(s_w) H_+^(1/2), noise.py:73-84 / 171-191 at frequencies where one
+ * term is nonzero): m_re / m_im the factor of H (row-major [nc][nc]) handed over once, scale [nw] the
+ * sqrt(s_w); the same draws and products as gle_noise_stream_chunk with the scaled matrices. */
+int gle_noise_stream_shared(gle_handle* h, int32_t bath, int64_t w0, int64_t nw, const double* scale,
+                            const double* m_re, const double* m_im, uint64_t seed, uint64_t traj_offset);
 int gle_noise_stream_end(gle_handle* h, int32_t bath);
 /* Release a begun stream's scratch without generating (an error between begin and end); the bath's
  * previous noise stays.  gle_destroy releases any stream still open. */

@@ -33,7 +33,7 @@ EXPORTS = [
     "gle_comm_destroy", "gle_record", "gle_record_zero", "gle_get_record", "gle_get_record_history",
     "gle_power_spectrum", "gle_set_record", "gle_set_record_history", "gle_noise_stream_begin",
     "gle_noise_stream_chunk", "gle_noise_stream_end", "gle_set_plan_class", "gle_plan_detail", "gle_plan_flags",
-    "gle_comm_allreduce", "gle_noise_stream_abort", "gle_device_mem_info",
+    "gle_comm_allreduce", "gle_noise_stream_abort", "gle_device_mem_info", "gle_noise_stream_shared",
 ]
 
 REC_P, REC_Q, REC_F, REC_HIST = 1, 2, 4, 8
@@ -119,6 +119,8 @@ _SIGS = {
     "gle_noise_stream_chunk": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, _D, _D,
                                               ctypes.c_uint64, ctypes.c_uint64]),
     "gle_noise_stream_end": (ctypes.c_int, [_P, ctypes.c_int32]),
+    "gle_noise_stream_shared": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, _D, _D, _D,
+                                               ctypes.c_uint64, ctypes.c_uint64]),
 }
 
 _lib = None
@@ -374,6 +376,37 @@ class Stepper:
         except BaseException:
             # a failed chunk or factor generator (e.g. LinAlgError) must not leave the spectrum
             # scratch (1-2 GB per C5 bath) on the device
+            self.lib.gle_noise_stream_abort(self.h, int(bath))
+            raise
+        self._chk(self.lib.gle_noise_stream_end(self.h, int(bath)), "gle_noise_stream_end")
+
+    def noise_stream_plan(self, bath, segments, is_complex, seed, traj_offset=0, max_chunk=64):
+        """Streamed device noise from work segments (noise.stream_factor_plan): ("dense", w0, M) with
+        M (nw, nc, nc) per-frequency factors, ("shared", w0, nw, scale, F) one factor F times
+        scale[w] for frequencies [w0, w0 + nw); frequencies in no segment get no noise."""
+        self._chk(self.lib.gle_noise_stream_begin(self.h, int(bath), 1 if is_complex else 0, int(max_chunk)),
+                  "gle_noise_stream_begin")
+        sd = int(seed) & (2**64 - 1)
+        try:
+            for seg in segments:
+                if seg[0] == "dense":
+                    _, w0, m = seg
+                    for o in range(0, m.shape[0], max_chunk):
+                        mc = m[o:o + max_chunk]
+                        mre = _f64(np.real(mc))
+                        mim = _f64(np.imag(mc)) if is_complex else None
+                        self._chk(self.lib.gle_noise_stream_chunk(self.h, int(bath), int(w0 + o), int(mc.shape[0]),
+                                                                  _ptr(mre), _ptr(mim), sd, int(traj_offset)),
+                                  "gle_noise_stream_chunk")
+                else:
+                    _, w0, nw, scale, f = seg
+                    sc = _f64(scale)
+                    fre = _f64(np.real(f))
+                    fim = _f64(np.imag(f)) if is_complex else None
+                    self._chk(self.lib.gle_noise_stream_shared(self.h, int(bath), int(w0), int(nw), _ptr(sc),
+                                                               _ptr(fre), _ptr(fim), sd, int(traj_offset)),
+                              "gle_noise_stream_shared")
+        except BaseException:
             self.lib.gle_noise_stream_abort(self.h, int(bath))
             raise
         self._chk(self.lib.gle_noise_stream_end(self.h, int(bath)), "gle_noise_stream_end")

@@ -199,7 +199,9 @@ class ebath(_BathBase):
         return [("0", hermitianize((e - x).astype(complex))), ("m", hermitianize(0.5 * (x + 1j * y))),
                 ("p", hermitianize(0.5 * (x - 1j * y)))]
 
-    def _spectrum_term(self, i):
+    def _spectrum_term(self, i, matrix=True):
+        """(kind, shared key, scale, dense matrix or None) of frequency i; matrix=False classifies
+        without building the dense matrix."""
         dw = 2.0 * np.pi / self.dt / self.nmd
         delta = self.dt * self.nmd
         w = dw * i
@@ -211,6 +213,8 @@ class ebath(_BathBase):
             return "zero", None, 0.0, None
         if len(nz) == 1:
             return "shared", "0mp"[nz[0]], float(c[nz[0]]), None
+        if not matrix:
+            return "dense", None, 1.0, None
         m = c[0] * self.efric
         m = m + (-0.5 * c[0] * self.exip + 0.5 * c[1] * (self.exip + 1j * self.exim))
         m = m + (-0.5 * c[0] * self.exip + 0.5 * c[2] * (self.exip - 1j * self.exim))
@@ -357,7 +361,9 @@ class phbath(_BathBase):
         g = np.asarray(self.gamma)
         return [(0, hermitianize(g[0])), (len(g) - 1, hermitianize(g[-1]))]
 
-    def _spectrum_term(self, i):
+    def _spectrum_term(self, i, matrix=True):
+        """(kind, shared key, scale, dense matrix or None) of frequency i; matrix=False classifies
+        without building the dense matrix."""
         from .functions import flinterp, hermitianize, nearest
 
         dw = 2.0 * np.pi / self.dt / self.nmd
@@ -369,4 +375,4 @@ class phbath(_BathBase):
         n = nearest(w, self.gwl)
         if n == 0 or n == len(self.gwl) - 1:
             return "shared", (0 if n == 0 else len(self.gwl) - 1), float(c), None
-        return "dense", None, 1.0, hermitianize(c * flinterp(w, self.gwl, self.gamma))
+        return "dense", None, 1.0, hermitianize(c * flinterp(w, self.gwl, self.gamma)) if matrix else None

@@ -128,6 +128,7 @@ struct Level {
   int cg_rn = 4;
   int cg_split = 1;            // split-K halves per product (small levels: 2 workgroups per CU)
   double cg_flops = 0, cg_bytes = 0;  // algorithmic, per block
+  double cg_units = 0;                 // Gauss products of the block's items (3 per two-plane item)
   hipEvent_t ev[2] = {nullptr, nullptr};
   int64_t last_block = INT64_MIN;
   int64_t bg_block[2] = {INT64_MIN, INT64_MIN};  // block launched on the background stream
@@ -1678,18 +1679,22 @@ int plan_far_fused(gle_handle* h) {
         const int64_t a_rt = (int64_t)L.M * b.nks * 64;
         const int64_t plane = (int64_t)b.nrt * a_rt;
         const int S = L.M * b.nks;
-        for (int f = 0; f <= lv.P; ++f)
-          for (int g = 0; g < 3; ++g) {
-            if ((f == 0 || f == lv.P) && g != 0) continue;  // real spectra: planes 1, 2 stay zero
+        for (int f = 0; f <= lv.P; ++f) {
+          const bool real = f == 0 || f == lv.P;  // real spectra: T_1, T_2 stay zero
+          {
             for (int rg = 0; 4 * rg < b.nrt; ++rg)
               for (int c0 = 0; c0 < B; c0 += NT) {
                 CgItem it{};
                 it.s0 = (int32_t)((int64_t)S * sp / lv.nsplit);
                 it.ns = (int32_t)((int64_t)S * (sp + 1) / lv.nsplit) - it.s0;
                 it.accum = sp > 0 ? 1 : 0;
-                it.A = L.d_khat + (int64_t)f * L.khat_fstride + g * plane + (int64_t)4 * rg * a_rt;
-                it.X = L.d_seg + (int64_t)f * L.seg_fstride + (int64_t)g * b.ncp * L.ldseg;
-                it.out = L.d_Yspec + (int64_t)f * L.yfstride + (int64_t)g * b.nc * B + (int64_t)64 * rg * B + c0;
+                it.g3 = real ? 0 : 1;
+                it.A = L.d_khat + (int64_t)f * L.khat_fstride + (int64_t)4 * rg * a_rt;
+                it.a_pl = plane;
+                it.X = L.d_seg + (int64_t)f * L.seg_fstride;
+                it.x_pl = (int64_t)b.ncp * L.ldseg;
+                it.out = L.d_Yspec + (int64_t)f * L.yfstride + (int64_t)64 * rg * B + c0;
+                it.o_pl = (int64_t)b.nc * B;
                 it.a_rt = a_rt;
                 it.ldx = (int32_t)L.ldseg;
                 it.cs = (int32_t)B;
@@ -1705,6 +1710,7 @@ int plan_far_fused(gle_handle* h) {
                 ++nout;
               }
           }
+        }
       }
       lv.nout = nout;
     }
@@ -1813,8 +1819,8 @@ int freeze(gle_handle* h) {
       for (auto& b : h->baths) {
         if (b.ml <= lv.lag0) continue;
         const int M = (std::min(lv.lag1, b.ml) + lv.P - 1) / lv.P - 2;
-        need += (size_t)(lv.P + 1) * 3 * b.nrt * b.nks * M * 64 * 8;
-        need += (size_t)(lv.P + 1) * 3 * b.ncp * ((M + 4) * B + 512) * 8;
+        need += (size_t)(lv.P + 1) * 2 * b.nrt * b.nks * M * 64 * 8;
+        need += (size_t)(lv.P + 1) * 2 * b.ncp * ((M + 4) * B + 512) * 8;
         need += (size_t)(lv.P + 1) * 3 * b.nc * B * 8;
       }
     }
@@ -1872,7 +1878,7 @@ int freeze(gle_handle* h) {
       int64_t n4 = 0;
       for (auto& b : h->baths)
         if (b.ml > lv.lag0)
-          n4 += (int64_t)(lv.P + 1) * 3 * ((b.nrt + 3) / 4) * ((B + 16 * lv.cg_rn - 1) / (16 * lv.cg_rn));
+          n4 += (int64_t)(lv.P + 1) * ((b.nrt + 3) / 4) * ((B + 16 * lv.cg_rn - 1) / (16 * lv.cg_rn));
       int ncu = 256;
       hipDeviceProp_t prop;
       if (hipGetDeviceProperties(&prop, h->cfg.device) == hipSuccess) ncu = prop.multiProcessorCount;
@@ -1898,8 +1904,8 @@ int freeze(gle_handle* h) {
       L.M = (L.lag1 + lv.P - 1) / lv.P - 2;
       L.Rseg = L.M + 4;
       L.ldseg = (int64_t)L.Rseg * B + 512;  // ring slots addressed modulo Rseg (no mirrored copy)
-      L.khat_fstride = (int64_t)3 * b.nrt * b.nks * L.M * 64;  // the three Gauss planes
-      L.seg_fstride = (int64_t)3 * b.ncp * L.ldseg;             // Re + Im, Im, Re rows
+      L.khat_fstride = (int64_t)2 * b.nrt * b.nks * L.M * 64;  // Re, Im planes
+      L.seg_fstride = (int64_t)2 * b.ncp * L.ldseg;             // Re, Im rows
       L.yfstride = (int64_t)3 * b.nc * B;                       // T_0, T_1, T_2
       rc = dalloc_n(h, &L.d_khat, (size_t)(lv.P + 1) * L.khat_fstride);
       if (!rc) rc = dalloc_n(h, &L.d_seg, (size_t)(lv.P + 1) * L.seg_fstride, 4096);
@@ -1974,7 +1980,7 @@ int freeze(gle_handle* h) {
       // one workgroup per (bath, f, Gauss part g, 64-row group, 16 RN-column tile); items of one
       // (f, g) are adjacent, so the row groups that share an X window run together
       lv.cg.clear();  // cg_rn / cg_split were chosen with the level's buffers
-      lv.cg_flops = lv.cg_bytes = 0;
+      lv.cg_flops = lv.cg_bytes = lv.cg_units = 0;
       const int NT = 16 * lv.cg_rn;
       for (size_t j = 0; j < h->baths.size(); ++j) {
         Bath& b = h->baths[j];
@@ -1982,12 +1988,12 @@ int freeze(gle_handle* h) {
         if (!L.active) continue;
         const int64_t a_rt = (int64_t)L.M * b.nks * 64;
         const int64_t plane = (int64_t)b.nrt * a_rt;
-        for (int f = 0; f <= lv.P; ++f)
-          for (int g = 0; g < 3; ++g) {
-            // f = 0 and f = P: K-hat and X-hat are real, so Re Y = T_0 - T_1 = T_0 (X plane 1 = Im = 0)
-            // and Im Y is dropped (far_ifft realonly): planes 1 and 2 are not needed, their T
-            // planes stay zero
-            if ((f == 0 || f == lv.P) && g != 0) continue;
+        for (int f = 0; f <= lv.P; ++f) {
+          // f = 0 and f = P: K-hat and X-hat are real, so Re Y = T_0 - T_1 = T_0 = Kr Xr and Im Y is
+          // dropped (far_ifft realonly): one product, the T_1 / T_2 planes stay zero.  Otherwise one
+          // item forms all three Gauss parts from the Re / Im planes of K-hat and X-hat.
+          const bool real = f == 0 || f == lv.P;
+          {
             for (int rg = 0; 4 * rg < b.nrt; ++rg)
               for (int c0 = 0; c0 < B; c0 += NT)
                 for (int hk = 0; hk < lv.cg_split; ++hk) {
@@ -1995,10 +2001,14 @@ int freeze(gle_handle* h) {
                 const int S = L.M * b.nks;
                 it.s0 = S * hk / lv.cg_split;
                 it.ns = S * (hk + 1) / lv.cg_split - it.s0;
-                it.A = L.d_khat + (int64_t)f * L.khat_fstride + g * plane + (int64_t)4 * rg * a_rt;
-                it.X = L.d_seg + (int64_t)f * L.seg_fstride + (int64_t)g * b.ncp * L.ldseg;
+                it.g3 = real ? 0 : 1;
+                it.A = L.d_khat + (int64_t)f * L.khat_fstride + (int64_t)4 * rg * a_rt;
+                it.a_pl = plane;
+                it.X = L.d_seg + (int64_t)f * L.seg_fstride;
+                it.x_pl = (int64_t)b.ncp * L.ldseg;
                 it.out = L.d_Yspec + (int64_t)hk * (lv.P + 1) * L.yfstride + (int64_t)f * L.yfstride +
-                         (int64_t)g * b.nc * B + (int64_t)64 * rg * B + c0;
+                         (int64_t)64 * rg * B + c0;
+                it.o_pl = (int64_t)b.nc * B;
                 it.a_rt = a_rt;
                 it.ldx = (int32_t)L.ldseg;
                 it.cs = (int32_t)B;
@@ -2011,11 +2021,15 @@ int freeze(gle_handle* h) {
                 it.ldo = (int32_t)B;
                 it.col0 = c0;
                 lv.cg.push_back(it);
+                lv.cg_units += real ? 1.0 : 3.0;
               }
-            // algorithmic work of T_g(f): A read once, X window read once, T written
-            lv.cg_flops += 2.0 * b.nc * ((double)L.M * b.nc) * B;
-            lv.cg_bytes += 8.0 * ((double)b.nc * L.M * b.nc + (double)L.M * b.nc * B + (double)b.nc * B);
+            // algorithmic work of the products of f: the Gauss parts' MFMA flops;
+            // K-hat's planes read once, the X window's planes read once, the T planes written once
+            const double np = real ? 1.0 : 3.0, npl = real ? 1.0 : 2.0;
+            lv.cg_flops += np * 2.0 * b.nc * ((double)L.M * b.nc) * B;
+            lv.cg_bytes += 8.0 * (npl * (double)b.nc * L.M * b.nc + npl * (double)L.M * b.nc * B + np * (double)b.nc * B);
           }
+        }
       }
       rc = dalloc_n(h, &lv.d_cg, lv.cg.size());
       if (!rc) rc = upload(h, lv.d_cg, lv.cg.data(), lv.cg.size() * sizeof(CgItem));
@@ -2033,7 +2047,11 @@ int freeze(gle_handle* h) {
         double per_cu = h->small_baths ? 2.0 : 4.0;
         if (const char* e = gle_env("GLE_CG_PER_CU")) per_cu = std::max(0.25, atof(e));
         h->cg_per_cu = per_cu;
-        const double want = (double)lv.cg.size() / (per_cu * ncu);
+        // chunks sized in Gauss products (a two-plane item forms three): the chunk durations the
+        // per-CU rates were measured with (GLE_CG_UNITS=0: in items, i.e. workgroups)
+        const char* eu = gle_env("GLE_CG_UNITS");
+        const double units = (eu && atoi(eu) == 0) ? (double)lv.cg.size() : lv.cg_units;
+        const double want = units / (per_cu * ncu);
         const int64_t nch = gle_env("GLE_CG_CEIL") ? (int64_t)std::ceil(want - 1e-9) : (int64_t)want;
         lv.ncg_chunk = (int)std::max<int64_t>(1, std::min<int64_t>(nch, nslot));
         if (const char* e = gle_env("GLE_NO_PIECES")) lv.ncg_chunk = atoi(e) > 0 ? 1 : lv.ncg_chunk;
@@ -3312,6 +3330,40 @@ int gle_noise_stream_chunk(gle_handle* h, int32_t bath, int64_t w0, int64_t nw, 
   return GLE_OK;
 }
 
+int gle_noise_stream_shared(gle_handle* h, int32_t bath, int64_t w0, int64_t nw, const double* scale,
+                            const double* m_re, const double* m_im, uint64_t seed, uint64_t traj_offset) {
+  int rc = check_bath(h, bath);
+  if (rc) return rc;
+  Bath& b = h->baths[bath];
+  if (!b.d_sa) return fail(h, GLE_ERR_STATE, "gle_noise_stream_begin first");
+  const int64_t nf = h->nmd / 2 + 1;
+  if (!m_re || !scale || w0 < 0 || nw < 1 || w0 + nw > nf || (b.s_complex && !m_im))
+    return fail(h, GLE_ERR_ARG, "bad shared noise stream range");
+  hipSetDevice(h->cfg.device);
+  const int64_t B = h->B, nc = b.nc, rows = b.s_complex ? 2 * nc : nc;
+  const size_t nm = (size_t)nc * nc;
+  DevTmp d_sc;
+  if (tmalloc(&d_sc.p, (size_t)nw * 8) != hipSuccess) return fail(h, GLE_ERR_NOMEM, "noise stream scales");
+  // the shared factor takes the chunk matrix buffer's first slot(s): stream-ordered after the
+  // previous chunk's products that read it
+  HIPCHK(h, hipMemcpyAsync(b.d_sm, m_re, nm * 8, hipMemcpyHostToDevice, h->stream));
+  if (b.s_complex) HIPCHK(h, hipMemcpyAsync(b.d_sm + nm, m_im, nm * 8, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(d_sc.p, scale, (size_t)nw * 8, hipMemcpyHostToDevice, h->stream));
+  const double* dsc = (const double*)d_sc.p;
+  for (int64_t o = 0; o < nw; o += b.s_cap) {
+    const int64_t n = std::min<int64_t>(b.s_cap, nw - o);
+    HIPCHK(h, hipMemsetAsync(b.d_sx, 0, (size_t)n * b.ncp * B * 8, h->stream));
+    launch_philox_normal(b.d_sx, n, b.ncp, nc, B, seed, traj_offset, h->stream, w0 + o);
+    launch_noise_gemm(b.d_sm, (int)nc, (int)nc, b.d_sx, b.ncp, (int)B, b.d_sa, (int)rows, 0, w0 + o, (int)n,
+                      h->stream, 0, dsc + o);
+    if (b.s_complex)
+      launch_noise_gemm(b.d_sm + nm, (int)nc, (int)nc, b.d_sx, b.ncp, (int)B, b.d_sa, (int)rows, (int)nc, w0 + o,
+                        (int)n, h->stream, 0, dsc + o);
+  }
+  HIPCHK(h, hipStreamSynchronize(h->stream));  // the caller's host buffers and the scale scratch
+  return GLE_OK;
+}
+
 int gle_noise_stream_end(gle_handle* h, int32_t bath) {
   int rc = check_bath(h, bath);
   if (rc) return rc;
@@ -3582,7 +3634,7 @@ int gle_step_work(gle_handle* h, double* flops, double* bytes) {
       for (size_t j = 0; j < h->baths.size(); ++j)
         if (lv.lb[j].active) {
           const double ncb = (double)h->baths[j].nc * B;
-          fby += 8.0 * ncb * (N + 3.0 * (P + 1.0)) + 8.0 * ncb * (3.0 * (P + 1.0) * lv.cg_split + P);
+          fby += 8.0 * ncb * (N + 2.0 * (P + 1.0)) + 8.0 * ncb * (3.0 * (P + 1.0) * lv.cg_split + P);
         }
       fl += (lv.cg_flops + fft) / P;
       by += (lv.cg_bytes + fby) / P;

@@ -179,5 +179,153 @@ __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, doubl
   }
 }
 
+// Two-plane Gauss item (it.g3 = 1, 0 < f < P): the three real products of one output tile from
+// Khat's two planes (Kr, Ki: each fragment streamed from HBM once, 2/3 of the three-plane bytes) and
+// the segment spectra's two planes (Xr, Xi), with the Gauss sums formed in registers:
+//   T_0 += Kr (Xr + Xi),  T_1 += (Kr + Ki) Xi,  T_2 += (Ki - Kr) Xr
+// (the same fp64 sums the three-plane layout stored, so the same results bit for bit).  X moves
+// through a double-buffered LDS chunk of both planes (row stride 16 RN + 16 doubles); three
+// accumulator sets per wave.
+template <int RN, int KC>
+struct Cg3 {
+  static constexpr int NT = 16 * RN;
+  static constexpr int LD = NT + 16;
+  static constexpr int PLANE = 4 * KC * LD;      // doubles of one X plane chunk in LDS
+  static constexpr int LDS = 2 * 2 * PLANE;      // two buffers x two planes
+};
+
+template <int RN, int KC, int AD>
+__device__ __forceinline__ void cgemm_item3(const CgItem& it, int64_t tseg, double* xs) {
+  using C = Cg3<RN, KC>;
+  constexpr int NT = C::NT, LD = C::LD, PL = C::PLANE;
+  constexpr int XPT = 2 * 4 * KC * NT / 256;  // X doubles per thread per chunk (both planes)
+  constexpr int TPR = NT / XPT;                // staging threads per X row
+  static_assert(2 * 4 * KC * TPR == 256, "one X row of one plane per TPR threads, every thread stages");
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int brow = lane >> 4, bcol = lane & 15;
+  const int S = it.ns;
+  const int nch = (S + KC - 1) / KC;
+  const bool active = wave < it.nrt;
+  gdbl* Aw = (gdbl*)(it.A + (int64_t)(active ? wave : 0) * it.a_rt + (int64_t)it.s0 * 64 + lane);
+  const int64_t apl = it.a_pl;
+  const int xpl = tid / (4 * KC * TPR);                 // plane this thread stages (0: Xr, 1: Xi)
+  const int xr = (tid % (4 * KC * TPR)) / TPR, xc = (tid % TPR) * XPT;
+  const double* Xp = it.X + (xpl ? it.x_pl : 0);
+  const int tbase = (int)cg_pmod(tseg, it.Rseg);
+  double xv[XPT], ar[AD + 1][KC], ai[AD + 1][KC];
+  d4 acc[3][RN];
+#pragma unroll
+  for (int g = 0; g < 3; ++g)
+#pragma unroll
+    for (int n = 0; n < RN; ++n) acc[g][n] = d4{0.0, 0.0, 0.0, 0.0};
+#ifdef GLE_BOUNDS
+#define CG3_BCHK_X(u) GLE_BCHK(Xp + (int64_t)(4 * ks_ + (xr & 3)) * it.ldx + (int64_t)slot_ * it.cs + it.col0 + xc + (u))
+#define CG3_BCHK_A(s, o) GLE_BCHK(it.A + (int64_t)(active ? wave : 0) * it.a_rt + (int64_t)it.s0 * 64 + lane + (int64_t)(s) * 64 + (o))
+#else
+#define CG3_BCHK_X(u) ((void)0)
+#define CG3_BCHK_A(s, o) ((void)0)
+#endif
+#define CG3_LOAD_X(c)                                                                                 \
+  do {                                                                                                \
+    const int s0_ = (c) * KC + (xr >> 2);                                                          \
+    const int sc_ = it.s0 + (s0_ < S ? s0_ : S - 1);                                                  \
+    const int i_ = (int)((unsigned)sc_ / (unsigned)it.nks), ks_ = sc_ - i_ * it.nks;                  \
+    int slot_ = tbase - i_;                                                                           \
+    slot_ += slot_ < 0 ? it.Rseg : 0;                                                                 \
+    gdbl* xp_ = (gdbl*)(Xp + (int64_t)(4 * ks_ + (xr & 3)) * it.ldx + (int64_t)slot_ * it.cs + it.col0 + xc); \
+    _Pragma("unroll") for (int u = 0; u < XPT; ++u) {                                               \
+      CG3_BCHK_X(u);                                                                                  \
+      xv[u] = xp_[u];                                                                                 \
+    }                                                                                                 \
+  } while (0)
+#define CG3_STORE_X(c, buf)                                                                           \
+  do {                                                                                                \
+    const double m_ = (c) * KC + (xr >> 2) < S ? 1.0 : 0.0;                                        \
+    _Pragma("unroll") for (int u = 0; u < XPT; ++u) xs[(buf) * 2 * PL + xpl * PL + xr * LD + xc + u] = xv[u] * m_; \
+  } while (0)
+#define CG3_LOAD_A(c, R)                                                                              \
+  do {                                                                                                \
+    _Pragma("unroll") for (int u = 0; u < KC; ++u) {                                               \
+      const int s0_ = (c) * KC + u;                                                                \
+      const int64_t o_ = (int64_t)(s0_ < S ? s0_ : S - 1) * 64;                                       \
+      CG3_BCHK_A(s0_ < S ? s0_ : S - 1, 0);                                                           \
+      CG3_BCHK_A(s0_ < S ? s0_ : S - 1, apl);                                                         \
+      ar[R][u] = CG_ALOAD(&Aw[o_]);                                                                   \
+      ai[R][u] = CG_ALOAD(&Aw[o_ + apl]);                                                             \
+    }                                                                                                 \
+  } while (0)
+  CG3_LOAD_A(0, 0);
+  if (AD > 1) CG3_LOAD_A(1, 1 % (AD + 1));
+  if (AD > 2) CG3_LOAD_A(2, 2 % (AD + 1));
+  if (AD > 3) CG3_LOAD_A(3, 3 % (AD + 1));
+  static_assert(AD <= 4, "prologue covers AD <= 4");
+  CG3_LOAD_X(0);
+  CG3_STORE_X(0, 0);
+  __syncthreads();
+  for (int c0 = 0; c0 < nch; c0 += AD + 1) {
+#pragma unroll
+    for (int r = 0; r <= AD; ++r) {
+      const int c = c0 + r;
+      if (c >= nch) break;
+      CG3_LOAD_X(c + 1);
+      CG3_LOAD_A(c + AD, (r + AD) % (AD + 1));
+      const double* xb_ = xs + (c & 1) * 2 * PL + brow * LD + bcol;
+#pragma unroll
+      for (int u = 0; u < KC; ++u) {
+        const double m_ = (active && c * KC + u < S) ? 1.0 : 0.0;
+        const double kr = ar[r][u] * m_, ki = ai[r][u] * m_;
+        const double k1 = kr + ki, k2 = ki - kr;
+#pragma unroll
+        for (int n = 0; n < RN; ++n) {
+          const double xre = xb_[4 * u * LD + 16 * n], xim = xb_[PL + 4 * u * LD + 16 * n];
+          acc[0][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(kr, xre + xim, acc[0][n], 0, 0, 0);
+          acc[1][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(k1, xim, acc[1][n], 0, 0, 0);
+          acc[2][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(k2, xre, acc[2][n], 0, 0, 0);
+        }
+      }
+      CG3_STORE_X(c + 1, (c & 1) ^ 1);
+      __syncthreads();
+    }
+  }
+#undef CG3_LOAD_A
+#undef CG3_STORE_X
+#undef CG3_LOAD_X
+#undef CG3_BCHK_X
+#undef CG3_BCHK_A
+  if (active) {
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+      for (int n = 0; n < RN; ++n)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int row = 16 * wave + brow + 4 * q, col = 16 * n + bcol;
+          if (row < it.nrows && col < it.ncols) {
+            double* o = &it.out[g * it.o_pl + (int64_t)row * it.ldo + col];
+            GLE_BCHK(o);
+            *o = it.accum ? *o + acc[g][n][q] : acc[g][n][q];
+          }
+        }
+  }
+}
+
+// doubles of LDS a far-field workgroup needs for either item kind
+template <int RN, int KC>
+constexpr int cg_lds_doubles() {
+  return Cg3<RN, KC>::LDS > 2 * 4 * KC * CG_LD ? Cg3<RN, KC>::LDS : 2 * 4 * KC * CG_LD;
+}
+
+// one item of either kind (the kind is item-uniform)
+template <int RN, int KC, int AD, int XD, int DBG = 0>
+__device__ __forceinline__ void cgemm_any(const CgItem& it, int64_t tseg, double* lds) {
+  if (it.g3) {
+    // 64-column tiles: chunks of 2 k-steps (three accumulator sets of 4 tiles fit the kernel's
+    // register budget without spilling)
+    cgemm_item3<RN, (RN == 4 ? 2 : KC), (RN == 4 ? 1 : (AD < 4 ? AD : 4))>(it, tseg, lds);
+  } else {
+    cgemm_item<RN, KC, AD, XD, DBG>(it, tseg, *reinterpret_cast<double(*)[2][4 * KC * CG_LD]>(lds));
+  }
+}
 
 }  // namespace gle

@@ -111,11 +111,15 @@ struct CItem {
 };
 
 // One workgroup of a spectral level's batched GEMM (gle_kernels.hip cgemm_kernel): 64 rows x 16 RN
-// columns of T_g(f) = sum_m A_g(f, m) X_g(f, sigma - m).
+// columns of the Gauss products of Y(f) = sum_m Khat(f, m) Xhat(f, sigma - m), from the two real
+// planes of Khat (Kr, Ki) and of the segment spectra (Xr, Xi):
+//   g3 = 1 (0 < f < P)  T_0 = Kr (Xr + Xi),  T_1 = (Kr + Ki) Xi,  T_2 = (Ki - Kr) Xr   (one item, all
+//                       three parts: Kr and Ki streamed once, the Gauss sums formed in registers)
+//   g3 = 0 (f = 0, P)   T_0 = Kr Xr  (real spectra; T_1 = T_2 = 0 are never written)
 struct CgItem {
-  const double* A;   // A plane of (f, g) at row tile 4 rg, k-step 0: [rt][m][ks][64]
-  const double* X;   // segment-ring plane of (f, g), row 0
-  double* out;       // T_g(f) at row 64 rg, column col0
+  const double* A;   // Kr plane of f at row tile 4 rg, k-step 0: [rt][m][ks][64] (Ki at + a_pl)
+  const double* X;   // segment-ring Xr plane of f, row 0 (Xi at + x_pl)
+  double* out;       // T_0(f) at row 64 rg, column col0 (T_1, T_2 at + o_pl, + 2 o_pl)
   int64_t a_rt;      // doubles between row tiles of A (M nks 64)
   int32_t ldx, cs;   // X row stride, columns per ring slot (B)
   int32_t Rseg, M, nks;
@@ -125,7 +129,10 @@ struct CgItem {
   int32_t s0, ns;    // k-step range [s0, s0 + ns) of this item (split-K halves write separate planes)
   int32_t accum;     // 1: add the item's partial to out (fused schedule: the k-splits of one product
                      // run in successive launches, first one stores); 0: store
-  int32_t pad;
+  int32_t g3;        // 1: the three Gauss parts from (Kr, Ki) x (Xr, Xi); 0: T_0 = Kr Xr only
+  int64_t a_pl;      // doubles from the Kr plane to the Ki plane
+  int64_t x_pl;      // doubles from the Xr plane to the Xi plane
+  int64_t o_pl;      // doubles between the T_g planes
 };
 
 // Deterministic fixed-order sum of split partial tiles (+ optional far-field addend).
@@ -337,9 +344,11 @@ struct FpotArgs {
 void launch_fpot(const FpotArgs& a, hipStream_t s);
 void launch_philox_normal(double* x, int64_t nfreq, int64_t ncp, int64_t nc, int64_t B,
                           uint64_t seed, uint64_t traj_offset, hipStream_t s, int64_t w_off = 0);
-// streamed noise: a[w0 + w][row_off + r][b] = sum_k M[w][r][k] x[w][k][b] for w < nw
+// streamed noise: a[w0 + w][row_off + r][b] = wscale[w] sum_k M[w][r][k] x[w][k][b] for w < nw (M of
+// frequency w at M + w mstride, mstride < 0: nc kc, 0: one shared factor; wscale nullptr: 1)
 void launch_noise_gemm(const double* M, int nc, int kc, const double* x, int ncp, int B, double* a, int rows,
-                       int row_off, int64_t w0, int nw, hipStream_t s);
+                       int row_off, int64_t w0, int nw, hipStream_t s, int64_t mstride = -1,
+                       const double* wscale = nullptr);
 void launch_near_fill(const double* H, int64_t ldh, int R, int B, int ncp, double* NR, int64_t vs, int NRS,
                       int64_t t, hipStream_t s);
 void launch_ring_copy(double* H, int64_t ldh, int R, int B, int nc, int64_t tau0, int nt, double* buf,

@@ -492,17 +492,20 @@ void launch_philox_normal(double* x, int64_t nfreq, int64_t ncp, int64_t nc, int
 // imaginary part of a complex one) and x the chunk's N(0,1) draws [nw][ncp][B].  Setup work
 // (once per run), LDS-tiled fp64 FMA: 64 rows x 32 columns per block, k in steps of 32.
 constexpr int NG_R = 64, NG_C = 32, NG_K = 32;
+// mstride: doubles between the frequencies' factors (0: one shared factor for every frequency of the
+// launch); wscale (nullable): a per-frequency scale of the product (a shared factor times sqrt(s_w))
 __global__ __launch_bounds__(256) void noise_gemm_kernel(const double* __restrict__ M, int nc, int kc,
                                                          const double* __restrict__ x, int ncp, int B,
                                                          double* __restrict__ a, int rows, int row_off,
-                                                         int64_t w0) {
+                                                         int64_t w0, int64_t mstride,
+                                                         const double* __restrict__ wscale) {
   __shared__ double Ms[NG_R][NG_K + 1];
   __shared__ double Xs[NG_K][NG_C + 1];
   const int w = blockIdx.z;
   const int r0 = blockIdx.x * NG_R, c0 = blockIdx.y * NG_C;
   const int tid = threadIdx.x;
   const int ty = tid / 8, tx = tid % 8;  // rows 2 ty, 2 ty + 1; columns 4 tx .. 4 tx + 3
-  const double* Mw = M + (int64_t)w * nc * kc;
+  const double* Mw = M + (int64_t)w * mstride;
   const double* xw = x + (int64_t)w * ncp * B;
   double acc[2][4] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
   for (int k0 = 0; k0 < kc; k0 += NG_K) {
@@ -527,20 +530,22 @@ __global__ __launch_bounds__(256) void noise_gemm_kernel(const double* __restric
     }
     __syncthreads();
   }
+  const double sc = wscale ? wscale[w] : 1.0;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int r = r0 + 2 * ty + i, c = c0 + 4 * tx + j;
-      if (r < nc && c < B) a[((w0 + w) * rows + row_off + r) * (int64_t)B + c] = acc[i][j];
+      if (r < nc && c < B) a[((w0 + w) * rows + row_off + r) * (int64_t)B + c] = sc * acc[i][j];
     }
 }
 
 void launch_noise_gemm(const double* M, int nc, int kc, const double* x, int ncp, int B, double* a, int rows,
-                       int row_off, int64_t w0, int nw, hipStream_t s) {
+                       int row_off, int64_t w0, int nw, hipStream_t s, int64_t mstride, const double* wscale) {
   if (nw <= 0) return;
   const dim3 grid((unsigned)((nc + NG_R - 1) / NG_R), (unsigned)((B + NG_C - 1) / NG_C), (unsigned)nw);
-  noise_gemm_kernel<<<grid, 256, 0, s>>>(M, nc, kc, x, ncp, B, a, rows, row_off, w0);
+  noise_gemm_kernel<<<grid, 256, 0, s>>>(M, nc, kc, x, ncp, B, a, rows, row_off, w0,
+                                         mstride < 0 ? (int64_t)nc * kc : mstride, wscale);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -764,9 +769,9 @@ namespace gle {
 // cstab[q] = (cos(pi q / Pmax), sin(pi q / Pmax)), q < 2 Pmax; a level reads it with stride
 // Pmax / P, so e^{-i pi f n / P} = (cs.x, -cs.y) at q = ((f n) mod 2P) * stride.
 //
-//   Khat_m(f) = sum_i' k_m[i'] e^{-i pi f i'/P}, f = 0..P, stored as the three real planes of the
-//   Gauss 3-multiplication  g = 0: Re,  1: Re + Im,  2: Im - Re  in fragment-native order
-//   [f][g][rt][m - m0][ks][64] (a wave streams its row tile's k-steps contiguously), read straight
+//   Khat_m(f) = sum_i' k_m[i'] e^{-i pi f i'/P}, f = 0..P, stored as two real planes (Re, Im) in
+//   fragment-native order [f][Re | Im][rt][m - m0][ks][64] (a wave streams its row tile's k-steps
+//   contiguously; the Gauss sums Re + Im, Im - Re are formed in the GEMM's registers), read straight
 //   out of the fragment-native K already on the device (one-time setup).
 __global__ void khat_pack_kernel(const double* __restrict__ Kf, int ml, int nks_k,
                                  double* __restrict__ khat, int P, int m0, int M, int nc, int nrt2,
@@ -798,10 +803,9 @@ __global__ void khat_pack_kernel(const double* __restrict__ Kf, int ml, int nks_
         im -= kv * cs.y;
       }
     }
-    const int64_t o = (int64_t)f * 3 * plane + (((int64_t)rt2 * M + mm) * nks2 + ks2) * 64 + lane;
+    const int64_t o = (int64_t)f * 2 * plane + (((int64_t)rt2 * M + mm) * nks2 + ks2) * 64 + lane;
     khat[o] = re;
-    khat[o + plane] = re + im;
-    khat[o + 2 * plane] = im - re;
+    khat[o + plane] = im;
   }
 }
 
@@ -855,16 +859,16 @@ template <int RN, int KC, int AD = CG_AD, int XD = CG_XD, int DBG = 0>
 #endif
 __global__ __launch_bounds__(256, KC <= 4 ? CG_WPE : 2) void cgemm_kernel(const CgItem* __restrict__ items, int nitems, int64_t tseg,
                                                        int xcd, unsigned long long* ts) {
-  __shared__ double xs[2][4 * KC * CG_LD];
+  __shared__ double xs[cg_lds_doubles<RN, KC>()];
   if (ts && threadIdx.x == 0) atomicMin(ts, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   if (xcd) {
     const int per = gridDim.x >> 3;
     const int item = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
-    if (item < nitems) cgemm_item<RN, KC, AD, XD, DBG>(items[item], tseg, xs);
+    if (item < nitems) cgemm_any<RN, KC, AD, XD, DBG>(items[item], tseg, xs);
   } else {
     for (int item = blockIdx.x; item < nitems; item += gridDim.x) {
       const CgItem it = items[item];
-      cgemm_item<RN, KC, AD, XD, DBG>(it, tseg, xs);
+      cgemm_any<RN, KC, AD, XD, DBG>(it, tseg, xs);
       __syncthreads();
     }
   }
@@ -953,8 +957,8 @@ void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStre
 
 // Segment spectra of the nseg newest segments sigma = T/P - sidx (grid: sidx x DOF k x 8-trajectory
 // chunk): x[n] = p at time sigma*P - 2P + 2 + n (n < 2P-1), x[2P-1] = 0;
-// Xhat(f) = sum_n x[n] e^{-i pi f n / P}, f = 0..P, written into the frequency-f segment ring as the
-// Gauss planes  g = 0: Re + Im,  1: Im,  2: Re  (rows [g ncp + k], mirrored slots).  Two real series
+// Xhat(f) = sum_n x[n] e^{-i pi f n / P}, f = 0..P, written into the frequency-f segment ring as two
+// planes  g = 0: Re,  1: Im  (rows [g ncp + k]; the GEMM forms Re + Im in registers).  Two real series
 // per complex FFT.
 // BC trajectories per block: 64 for the small transforms (one block per DOF, 512 B rows, every
 // thread busy in every butterfly stage), fewer for long transforms (LDS: BC/2 series of 2P points)
@@ -1009,9 +1013,9 @@ __global__ __launch_bounds__(256) void seg_fft_kernel(const double* __restrict__
       im = -0.5 * (z.x - zc.x);
     }
     double* sf = seg + (int64_t)f * seg_fstride + b;
-    const double v[3] = {re + im, im, re};
+    const double v[2] = {re, im};
 #pragma unroll
-    for (int g = 0; g < 3; ++g) {
+    for (int g = 0; g < 2; ++g) {
       const int64_t ir = (int64_t)(g * ncp + k) * ldseg;
       sf[ir + slot * B] = v[g];  // (cgemm addresses ring slots modulo Rseg: no mirrored copy)
     }

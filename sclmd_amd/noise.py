@@ -166,6 +166,84 @@ def stream_factor_chunks(bath, chunk=64, workers=None):
             yield w, np.stack([f.result() for f in fl])
 
 
+def stream_factor_plan(bath, chunk=64, workers=None, cache=None):
+    """The streamed factors of a bath as device work segments, in frequency order:
+      ("shared", w0, nw, scale, F)  frequencies [w0, w0 + nw) whose spectrum is s_w H for one shared
+                                    H: factor F = H_+^(1/2) handed over once, scale = sqrt(s_w)
+      ("dense", w0, M)              M (nw, nc, nc) the factors of frequencies [w0, w0 + nw)
+    Frequencies whose spectrum is zero produce nothing (the device spectrum starts at zero).  Dense
+    factors are computed on a thread pool (LAPACK releases the GIL; BLAS pinned to one thread per
+    worker), two chunks ahead of the consumer.  cache: a dict that keeps the dense chunks (and the
+    shared factors) of this bath across runs -- the factors do not change between runs, only the
+    draws (md.py:569-570) -- so later runs hand over the cached factors without factorising."""
+    import os
+    from concurrent.futures import ThreadPoolExecutor
+
+    from threadpoolctl import threadpool_limits
+
+    nfreq = int(bath.nmd / 2) + 1
+    nc = bath.nc
+    dtype = complex if bath.kind == "ebath" else float
+    if cache is not None and cache.get("complete"):
+        for seg in cache["segments"]:
+            yield seg
+        return
+    terms = [bath._spectrum_term(i, matrix=False) for i in range(nfreq)]
+    # runs: (kind, key, [frequencies])
+    runs = []
+    for i, (kind, key, sc, _) in enumerate(terms):
+        if kind == "zero":
+            continue
+        if runs and runs[-1][0] == kind and runs[-1][1] == key and runs[-1][2][-1] == i - 1 and \
+                (kind == "shared" or len(runs[-1][2]) < chunk):
+            runs[-1][2].append(i)
+        else:
+            runs.append((kind, key, [i]))
+    if workers is None:
+        try:
+            workers = len(os.sched_getaffinity(0))
+        except AttributeError:  # pragma: no cover
+            workers = os.cpu_count() or 1
+        workers = max(1, min(16, workers))
+    keep = [] if cache is not None else None
+    shared = {}
+    with threadpool_limits(1, user_api="blas"), ThreadPoolExecutor(max_workers=workers) as pool:
+        need = {key for kind, key, _ in runs if kind == "shared"}
+        for key, h in bath._shared_matrices():
+            if key in need:
+                shared[key] = positive_factor(h).astype(dtype, copy=False)
+        pending = []
+
+        def emit(item):
+            kind, key, ws = item
+            if kind == "shared":
+                sc = np.sqrt(np.array([terms[i][2] for i in ws]))
+                seg = ("shared", ws[0], len(ws), sc, shared[key])
+            else:
+                seg = ("dense", ws[0], np.stack([f.result() for f in key]))
+            if keep is not None:
+                keep.append(seg)
+            return seg
+
+        for kind, key, ws in runs:
+            if kind == "dense":
+                futs = [pool.submit(lambda i=i: dense_factor(bath._spectrum_term(i)[3]).astype(dtype, copy=False))
+                        for i in ws]
+                pending.append(("dense", futs, ws))
+            else:
+                pending.append(("shared", key, ws))
+            ndense = sum(1 for p in pending if p[0] == "dense")
+            while pending and (pending[0][0] == "shared" or ndense > 2):
+                if pending[0][0] == "dense":
+                    ndense -= 1
+                yield emit(pending.pop(0))
+        for item in pending:
+            yield emit(item)
+    if cache is not None:
+        cache["segments"] = keep
+        cache["complete"] = True
+
+
 def generate(factor, dt, nmd, ntraj=1, rngs=None, seed=None, device=0):
     """Standalone device generation of ntraj realisations (ntraj, nmd, nc) for one factor."""
     st = _native.Stepper(factor.nc, ntraj, nmd, dt, device)

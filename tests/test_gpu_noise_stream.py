@@ -114,3 +114,50 @@ def test_stream_failure_releases_scratch_and_recovers():
     want = ref.get_noise(0)
     ref.close()
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("kind", ["ph", "e"])
+def test_stream_plan_equals_chunks_and_reuses_cache(kind, monkeypatch):
+    """The work-segment stream (noise.stream_factor_plan: zero frequencies skipped, shared-matrix
+    frequencies as one factor times per-frequency scales, dense factors per frequency) gives the
+    noise of the full per-frequency chunk stream for the same seed (1e-12); a second run with the
+    factor cache factorises nothing and, for the same seed, repeats the first run's noise exactly."""
+    from sclmd_amd import _native as N
+    from sclmd_amd import noise as Nz
+    from sclmd_amd import synthetic
+
+    rng = np.random.default_rng(6)
+    nmd, B = 1024, 6
+    if kind == "ph":
+        b = synthetic.make_phbath(300.0, list(range(36)), 8, nmd, rng, nw=40)
+    else:
+        b = synthetic.make_biased_ebath(300.0, list(range(30)), nmd, rng)
+    cplx = kind == "e"
+
+    def stepper():
+        st = N.Stepper(b.nc, B, nmd, synthetic.DT, 0)
+        st.add_bath(N.GLE_BATH_PHONON, np.arange(b.nc), np.zeros((1, b.nc, b.nc)))
+        return st
+
+    st = stepper()
+    st.noise_stream(0, Nz.stream_factor_chunks(b, chunk=16), cplx, seed=21, traj_offset=2, max_chunk=16)
+    want = st.get_noise(0)
+    cache = {}
+    st.noise_stream_plan(0, Nz.stream_factor_plan(b, chunk=16, cache=cache), cplx, seed=21, traj_offset=2,
+                         max_chunk=16)
+    got = st.get_noise(0)
+    kinds = {s[0] for s in cache["segments"]}
+    assert kinds == {"shared", "dense"}, kinds
+    assert rel(got, want) < 1e-12
+    calls = []
+    monkeypatch.setattr(Nz, "dense_factor", lambda a: calls.append(1) or Nz.positive_factor(a))
+    st.noise_stream_plan(0, Nz.stream_factor_plan(b, chunk=16, cache=cache), cplx, seed=21, traj_offset=2,
+                         max_chunk=16)
+    again = st.get_noise(0)
+    st.noise_stream_plan(0, Nz.stream_factor_plan(b, chunk=16, cache=cache), cplx, seed=22, traj_offset=2,
+                         max_chunk=16)
+    other = st.get_noise(0)
+    st.close()
+    assert not calls
+    assert np.array_equal(again, got)
+    assert rel(other, got) > 0.1
