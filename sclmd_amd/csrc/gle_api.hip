@@ -1057,8 +1057,27 @@ void xcd_order(gle_handle* h, Chain& c) {
   c.tiles.swap(out);
 }
 
+// Experiment (GLE_CH_ORDER=1): tiles in decreasing order of their longest wave's dependent operand
+// round trips (batches of k-steps), so the longest tiles are dispatched first.
+void lpt_order(gle_handle* h, Chain& c) {
+  const char* e = gle_env("GLE_CH_ORDER");
+  if (!e || atoi(e) == 0) return;
+  auto rts = [&](const ChTile& T) {
+    const int U = c.nw >= 16 ? (T.rn == 1 ? 16 : (T.rn == 2 ? 6 : 3)) : (T.rn == 1 ? 8 : (T.rn == 2 ? 4 : 2));
+    int best = 0;
+    for (int w = 0; w < c.nw && w < CH_NW; ++w) {
+      int n = 0;
+      for (int k = 0; k < T.ntw[w] && k < CH_TPW; ++k) n += (T.task[w][k].nks + U - 1) / U;
+      best = std::max(best, n);
+    }
+    return best;
+  };
+  std::stable_sort(c.tiles.begin(), c.tiles.end(), [&](const ChTile& a, const ChTile& b) { return rts(a) > rts(b); });
+}
+
 int upload_chain(gle_handle* h, Chain& c) {
   if (c.tiles.empty()) return GLE_OK;
+  lpt_order(h, c);
   xcd_order(h, c);
   int rc = dalloc_n(h, &c.d, c.tiles.size());
   if (!rc) rc = upload(h, c.d, c.tiles.data(), c.tiles.size() * sizeof(ChTile));
@@ -1329,7 +1348,8 @@ int plan_chain(gle_handle* h) {
     if (rc) return rc;
   }
   // near-field partial items (lags [2, nn), target t+2) per bath: sizes and slot counts
-  const int rn_raw = (int)std::min<int64_t>(4, (B + 15) / 16);
+  int rn_raw = (int)std::min<int64_t>(4, (B + 15) / 16);
+  if (const char* e = gle_env("GLE_RAW_RN")) rn_raw = std::max(1, std::min(rn_raw, atoi(e) >= 4 ? 4 : (atoi(e) >= 2 ? 2 : 1)));
   const int nt_raw = 16 * rn_raw;
   const int ncolr = (int)((B + nt_raw - 1) / nt_raw);
   const char* env = gle_env("GLE_NEAR_KS");
