@@ -310,19 +310,25 @@ __device__ __forceinline__ void cgemm_item3(const CgItem& it, int64_t tseg, doub
   }
 }
 
+// k-steps per LDS chunk of the two-plane items: 64-column tiles take chunks of 2 (three accumulator
+// sets of 4 tiles fit the kernel's register budget without spilling, and the two X planes of a
+// chunk the LDS of the one-plane item's chunk of 4)
+template <int RN, int KC>
+constexpr int cg3_kc() {
+  return RN == 4 ? 2 : KC;
+}
+
 // doubles of LDS a far-field workgroup needs for either item kind
 template <int RN, int KC>
 constexpr int cg_lds_doubles() {
-  return Cg3<RN, KC>::LDS > 2 * 4 * KC * CG_LD ? Cg3<RN, KC>::LDS : 2 * 4 * KC * CG_LD;
+  return Cg3<RN, cg3_kc<RN, KC>()>::LDS > 2 * 4 * KC * CG_LD ? Cg3<RN, cg3_kc<RN, KC>()>::LDS : 2 * 4 * KC * CG_LD;
 }
 
 // one item of either kind (the kind is item-uniform)
 template <int RN, int KC, int AD, int XD, int DBG = 0>
 __device__ __forceinline__ void cgemm_any(const CgItem& it, int64_t tseg, double* lds) {
   if (it.g3) {
-    // 64-column tiles: chunks of 2 k-steps (three accumulator sets of 4 tiles fit the kernel's
-    // register budget without spilling)
-    cgemm_item3<RN, (RN == 4 ? 2 : KC), (RN == 4 ? 1 : (AD < 4 ? AD : 4))>(it, tseg, lds);
+    cgemm_item3<RN, cg3_kc<RN, KC>(), (RN == 4 ? 1 : (AD < 4 ? AD : 4))>(it, tseg, lds);
   } else {
     cgemm_item<RN, KC, AD, XD, DBG>(it, tseg, *reinterpret_cast<double(*)[2][4 * KC * CG_LD]>(lds));
   }
