@@ -1800,7 +1800,15 @@ int freeze(gle_handle* h) {
   if (h->cfg.max_block > 0) {
     Pmax = std::max(P0, h->cfg.max_block);
   } else if (spec_ok) {
-    Pmax = std::max(P0, 256);
+    // spectral levels cost the same per step whatever their P (M = 2 partitions of P lags, K-hat read
+    // once per block of P steps), except the last one, whose M = (ml - 2P) / P grows as ml / P: the
+    // largest block is the smallest power of two >= 256 with 4P >= ml (at most 1024), so the last
+    // level has M = 2 too.  C3 (ml 1024): 256.  C5 (ml 4096): 1024, a third of the K-hat bytes per
+    // step that a last level of P = 256 with M = 14 streams.
+    int pm = 256;
+    while (4 * pm < mlmax && pm < 1024) pm *= 2;
+    if (const char* e = gle_env("GLE_PMAX_SPEC")) pm = std::max(8, atoi(e));
+    Pmax = std::max(P0, pm);
   } else {
     // direct: enough columns per block for MFMA reuse of each streamed kernel slice, and long
     // enough blocks that the last level's kernel slices stream from HBM rarely: the last level

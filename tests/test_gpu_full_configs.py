@@ -37,8 +37,13 @@ def _obath(O, b, noise, dt, nmd):
     return O.Bath("ph", b.cids, b.kernel, noise, dt, nmd)
 
 
-def _expected_levels(P0, ml, pmax=256):
-    """The ladder's block lengths: P = P0 2^l while 2P < ml, the last one at 4P >= ml or P = pmax."""
+def _expected_levels(P0, ml, pmax=None):
+    """The ladder's block lengths: P = P0 2^l while 2P < ml, the last one at 4P >= ml or P = pmax
+    (spectral plans: the smallest power of two >= 256 with 4 pmax >= ml, at most 1024)."""
+    if pmax is None:
+        pmax = 256
+        while 4 * pmax < ml and pmax < 1024:
+            pmax *= 2
     out, P = [], P0
     while 2 * P < ml:
         out.append(P)
@@ -206,11 +211,11 @@ def test_c2_bench_plan_b1_vs_oracle():
 def test_c5_full_shape_linearity_and_sampled_rows():
     """C5 as benched (VERDICT r03 missing #2): 1000 atoms, phonon baths nc = 999 / 999 with ml = 4096
     built on the device (gmem), the biased electron bath nc = 1002, nmd = 8192, 32 trajectories,
-    coloured noise streamed by frequency chunks, the large-bath plan picked automatically (7 ladder
-    levels P = 4 ... 256, the P = 256 level's last partition ragged).
+    coloured noise streamed by frequency chunks, the large-bath plan picked automatically (9 ladder
+    levels P = 4 ... 1024; the two-plane Gauss items of every spectral level).
     (i) linearity: trajectory 2 starts as trajectory 0 + trajectory 1 in state, history and noise;
-        after 2 x 256 + 30 steps from the unaligned t0 = 37 it is still their sum (state and every
-        bath's history, 1e-11);
+        after 2 x 1024 + 30 steps from the unaligned t0 = 37 (two blocks of the largest level, P =
+        1024, lags [2048, 4096)) it is still their sum (state and every bath's history, 1e-11);
     (ii) sampled rows: one more step, and the force F0 of md.vv's id0 call (md.py:383-392) implied by
          q~ on 32 DOF rows of the three baths equals a host fp64 evaluation from the device's own
          state, history and noise: -dyn q_t + noise_t - dt (K_0 p_t + sum_{i>=1} K_i p_{t-i}) on the
@@ -220,7 +225,7 @@ def test_c5_full_shape_linearity_and_sampled_rows():
     from sclmd_amd import noise as NZ
     from sclmd_amd import synthetic
 
-    B, t0, nst = 32, 37, 2 * 256 + 30
+    B, t0 = 32, 37
     dyn, _, baths, meta = synthetic.junction("C5", seed=1234, gmem_device=True)
     nph, nmd, dt, ml = meta["nph"], meta["nmd"], meta["dt"], meta["ml"]
     assert meta["nc"] == [999, 999, 1002] and ml == 4096 and nmd == 8192
@@ -251,11 +256,13 @@ def test_c5_full_shape_linearity_and_sampled_rows():
         detail = st.plan_detail()
         assert detail["plan_class"] == "large" and detail["fpot_launch"] and detail["cg_per_cu"] == 4.0, detail
         assert st.plan_info()["far_mode"] == "spectral"
+        Ps = [P for P, _ in st.profile_levels()]
+        assert Ps == [4, 8, 16, 32, 64, 128, 256, 512, 1024], Ps
+        nst = 2 * Ps[-1] + 30  # every level computes >= 2 blocks from the (random, nonzero) history
         st.profile(True)
         st.run(nst)
         levels = st.profile_levels()
         st.profile(False)
-        assert [P for P, _ in levels] == [4, 8, 16, 32, 64, 128, 256], levels
         assert all(bl >= 2.0 for _, bl in levels), levels
         pg, qg, t = st.get_state()
         assert t == t0 + nst
