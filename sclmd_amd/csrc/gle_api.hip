@@ -1848,7 +1848,7 @@ int freeze(gle_handle* h) {
         if (b.ml <= lv.lag0) continue;
         const int M = (std::min(lv.lag1, b.ml) + lv.P - 1) / lv.P - 2;
         need += (size_t)(lv.P + 1) * 2 * b.nrt * b.nks * M * 64 * 8;
-        need += (size_t)(lv.P + 1) * 2 * b.ncp * ((M + 4) * B + 512) * 8;
+        need += (size_t)(lv.P + 1) * 2 * b.ncp * ((M + 4) * B + 8) * 8;
         need += (size_t)(lv.P + 1) * 3 * b.nc * B * 8;
       }
     }
@@ -1931,7 +1931,9 @@ int freeze(gle_handle* h) {
       if (!lv.spectral) continue;
       L.M = (L.lag1 + lv.P - 1) / lv.P - 2;
       L.Rseg = L.M + 4;
-      L.ldseg = (int64_t)L.Rseg * B + 512;  // ring slots addressed modulo Rseg (no mirrored copy)
+      // ring slots addressed modulo Rseg (no mirrored copy); rows padded by 8 doubles (the 512 of
+      // earlier rounds was 73 % of a row at C5's P = 1024 level, ~7 GB per bath)
+      L.ldseg = (int64_t)L.Rseg * B + 8;
       L.khat_fstride = (int64_t)2 * b.nrt * b.nks * L.M * 64;  // Re, Im planes
       L.seg_fstride = (int64_t)2 * b.ncp * L.ldseg;             // Re, Im rows
       L.yfstride = (int64_t)3 * b.nc * B;                       // T_0, T_1, T_2
