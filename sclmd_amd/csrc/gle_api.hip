@@ -119,6 +119,11 @@ struct LevelBath {
 struct Level {
   int P = 1, lag0 = 2, lag1 = 2;
   bool spectral = false;
+  // spectral: 2 = K-hat and segment spectra as Re / Im planes, one item forming all three Gauss
+  // products (items of <= 32 columns: the HBM-bound K-hat stream of large baths, C5); 3 = the three
+  // Gauss planes, one item per product (64-column items: past the fp64 ridge, where the two-plane
+  // item's three accumulator sets leave its prefetch ring too shallow, C3)
+  int nplanes = 3;
   int cstride = 1;             // twiddle-table stride (Pspec / P)
   int sidx = 0;                // background stream
   std::vector<LevelBath> lb;   // per bath
@@ -1701,19 +1706,20 @@ int plan_far_fused(gle_handle* h) {
         const int S = L.M * b.nks;
         for (int f = 0; f <= lv.P; ++f) {
           const bool real = f == 0 || f == lv.P;  // real spectra: T_1, T_2 stay zero
-          {
+          const int ng = lv.nplanes == 2 ? 1 : (real ? 1 : 3);
+          for (int g = 0; g < ng; ++g) {
             for (int rg = 0; 4 * rg < b.nrt; ++rg)
               for (int c0 = 0; c0 < B; c0 += NT) {
                 CgItem it{};
                 it.s0 = (int32_t)((int64_t)S * sp / lv.nsplit);
                 it.ns = (int32_t)((int64_t)S * (sp + 1) / lv.nsplit) - it.s0;
                 it.accum = sp > 0 ? 1 : 0;
-                it.g3 = real ? 0 : 1;
-                it.A = L.d_khat + (int64_t)f * L.khat_fstride + (int64_t)4 * rg * a_rt;
+                it.g3 = (lv.nplanes == 2 && !real) ? 1 : 0;
+                it.A = L.d_khat + (int64_t)f * L.khat_fstride + g * plane + (int64_t)4 * rg * a_rt;
                 it.a_pl = plane;
-                it.X = L.d_seg + (int64_t)f * L.seg_fstride;
+                it.X = L.d_seg + (int64_t)f * L.seg_fstride + (int64_t)g * b.ncp * L.ldseg;
                 it.x_pl = (int64_t)b.ncp * L.ldseg;
-                it.out = L.d_Yspec + (int64_t)f * L.yfstride + (int64_t)64 * rg * B + c0;
+                it.out = L.d_Yspec + (int64_t)f * L.yfstride + (int64_t)g * b.nc * B + (int64_t)64 * rg * B + c0;
                 it.o_pl = (int64_t)b.nc * B;
                 it.a_rt = a_rt;
                 it.ldx = (int32_t)L.ldseg;
@@ -1847,8 +1853,9 @@ int freeze(gle_handle* h) {
       for (auto& b : h->baths) {
         if (b.ml <= lv.lag0) continue;
         const int M = (std::min(lv.lag1, b.ml) + lv.P - 1) / lv.P - 2;
-        need += (size_t)(lv.P + 1) * 2 * b.nrt * b.nks * M * 64 * 8;
-        need += (size_t)(lv.P + 1) * 2 * b.ncp * ((M + 4) * B + 8) * 8;
+        const int npl = B <= 32 ? 2 : 3;  // Level::nplanes
+        need += (size_t)(lv.P + 1) * npl * b.nrt * b.nks * M * 64 * 8;
+        need += (size_t)(lv.P + 1) * npl * b.ncp * ((M + 4) * B + 8) * 8;
         need += (size_t)(lv.P + 1) * 3 * b.nc * B * 8;
       }
     }
@@ -1897,6 +1904,8 @@ int freeze(gle_handle* h) {
   for (auto& lv : h->levels) {
     lv.cstride = lv.spectral ? Pspec / lv.P : 1;
     lv.cg_rn = (int)std::min<int64_t>(4, (B + 15) / 16);
+    lv.nplanes = lv.cg_rn <= 2 ? 2 : 3;
+    if (const char* e = gle_env("GLE_GAUSS_PLANES")) lv.nplanes = atoi(e) == 2 ? 2 : 3;
     lv.cg_split = 1;
     if (lv.spectral) {
       // small levels of large baths: split the k range of every product in two (partial planes
@@ -1934,15 +1943,15 @@ int freeze(gle_handle* h) {
       // ring slots addressed modulo Rseg (no mirrored copy); rows padded by 8 doubles (the 512 of
       // earlier rounds was 73 % of a row at C5's P = 1024 level, ~7 GB per bath)
       L.ldseg = (int64_t)L.Rseg * B + 8;
-      L.khat_fstride = (int64_t)2 * b.nrt * b.nks * L.M * 64;  // Re, Im planes
-      L.seg_fstride = (int64_t)2 * b.ncp * L.ldseg;             // Re, Im rows
+      L.khat_fstride = (int64_t)lv.nplanes * b.nrt * b.nks * L.M * 64;  // Re, Im | the Gauss planes
+      L.seg_fstride = (int64_t)lv.nplanes * b.ncp * L.ldseg;             // Re, Im | Re + Im, Im, Re rows
       L.yfstride = (int64_t)3 * b.nc * B;                       // T_0, T_1, T_2
       rc = dalloc_n(h, &L.d_khat, (size_t)(lv.P + 1) * L.khat_fstride);
       if (!rc) rc = dalloc_n(h, &L.d_seg, (size_t)(lv.P + 1) * L.seg_fstride, 4096);
       if (!rc) rc = dalloc_n(h, &L.d_Yspec, (size_t)lv.cg_split * (lv.P + 1) * L.yfstride, 4096);
       if (rc) return rc;
       launch_khat_pack(b.d_K, b.ml, b.nks, L.d_khat, lv.P, 2, L.M, b.nc, b.nrt, b.nks, h->d_cstab,
-                       lv.cstride, h->stream);
+                       lv.cstride, h->stream, lv.nplanes);
       HIPCHK(h, hipStreamSynchronize(h->stream));
     }
     // background stream per level group (a first level on a stream of its own measured slower)
@@ -2022,8 +2031,10 @@ int freeze(gle_handle* h) {
           // f = 0 and f = P: K-hat and X-hat are real, so Re Y = T_0 - T_1 = T_0 = Kr Xr and Im Y is
           // dropped (far_ifft realonly): one product, the T_1 / T_2 planes stay zero.  Otherwise one
           // item forms all three Gauss parts from the Re / Im planes of K-hat and X-hat.
+          // three-plane layout (nplanes = 3): one item per Gauss part g, reading plane g of K-hat and X
           const bool real = f == 0 || f == lv.P;
-          {
+          const int ng = lv.nplanes == 2 ? 1 : (real ? 1 : 3);
+          for (int g = 0; g < ng; ++g) {
             for (int rg = 0; 4 * rg < b.nrt; ++rg)
               for (int c0 = 0; c0 < B; c0 += NT)
                 for (int hk = 0; hk < lv.cg_split; ++hk) {
@@ -2031,13 +2042,13 @@ int freeze(gle_handle* h) {
                 const int S = L.M * b.nks;
                 it.s0 = S * hk / lv.cg_split;
                 it.ns = S * (hk + 1) / lv.cg_split - it.s0;
-                it.g3 = real ? 0 : 1;
-                it.A = L.d_khat + (int64_t)f * L.khat_fstride + (int64_t)4 * rg * a_rt;
+                it.g3 = (lv.nplanes == 2 && !real) ? 1 : 0;
+                it.A = L.d_khat + (int64_t)f * L.khat_fstride + g * plane + (int64_t)4 * rg * a_rt;
                 it.a_pl = plane;
-                it.X = L.d_seg + (int64_t)f * L.seg_fstride;
+                it.X = L.d_seg + (int64_t)f * L.seg_fstride + (int64_t)g * b.ncp * L.ldseg;
                 it.x_pl = (int64_t)b.ncp * L.ldseg;
                 it.out = L.d_Yspec + (int64_t)hk * (lv.P + 1) * L.yfstride + (int64_t)f * L.yfstride +
-                         (int64_t)64 * rg * B + c0;
+                         (int64_t)g * b.nc * B + (int64_t)64 * rg * B + c0;
                 it.o_pl = (int64_t)b.nc * B;
                 it.a_rt = a_rt;
                 it.ldx = (int32_t)L.ldseg;
@@ -2051,11 +2062,12 @@ int freeze(gle_handle* h) {
                 it.ldo = (int32_t)B;
                 it.col0 = c0;
                 lv.cg.push_back(it);
-                lv.cg_units += real ? 1.0 : 3.0;
+                lv.cg_units += it.g3 ? 3.0 : 1.0;
               }
-            // algorithmic work of the products of f: the Gauss parts' MFMA flops;
+            // algorithmic work of the products of (f, g): the Gauss parts' MFMA flops;
             // K-hat's planes read once, the X window's planes read once, the T planes written once
-            const double np = real ? 1.0 : 3.0, npl = real ? 1.0 : 2.0;
+            const bool two = lv.nplanes == 2 && !real;
+            const double np = two ? 3.0 : 1.0, npl = two ? 2.0 : 1.0;
             lv.cg_flops += np * 2.0 * b.nc * ((double)L.M * b.nc) * B;
             lv.cg_bytes += 8.0 * (npl * (double)b.nc * L.M * b.nc + npl * (double)L.M * b.nc * B + np * (double)b.nc * B);
           }
@@ -2209,7 +2221,7 @@ int launch_level_pieces(gle_handle* h, Level& lv, int64_t k, hipStream_t s, bool
       LevelBath& L = lv.lb[b];
       if (!L.active) continue;
       if (launch_seg_fft(bb.d_H, bb.ldh, bb.R, (int)h->B, bb.nc, bb.ncp, lv.P, T, L.M, L.d_seg, L.seg_fstride,
-                         L.ldseg, L.Rseg, h->d_cstab, lv.cstride, s))
+                         L.ldseg, L.Rseg, h->d_cstab, lv.cstride, s, 0, -1, lv.nplanes))
         return fail(h, GLE_ERR_UNSUP, "segment transform launch failed (P = " + std::to_string(lv.P) + ")");
     }
     launch_cgemm(lv.cg_rn, lv.d_cg, (int)lv.cg.size(), T / lv.P, s, 0, nullptr);
@@ -2249,7 +2261,7 @@ int launch_level_pieces(gle_handle* h, Level& lv, int64_t k, hipStream_t s, bool
         if (!L.active || (!priming && (h->dbg_skip & 2))) continue;
         const int k0 = (int)((int64_t)bb.nc * j / lv.nfs), k1 = (int)((int64_t)bb.nc * (j + 1) / lv.nfs);
         if (launch_seg_fft(bb.d_H, bb.ldh, bb.R, (int)h->B, bb.nc, bb.ncp, lv.P, T, priming ? L.M : 1, L.d_seg,
-                           L.seg_fstride, L.ldseg, L.Rseg, h->d_cstab, lv.cstride, s, k0, k1))
+                           L.seg_fstride, L.ldseg, L.Rseg, h->d_cstab, lv.cstride, s, k0, k1, lv.nplanes))
           return fail(h, GLE_ERR_UNSUP, "segment transform launch failed (P = " + std::to_string(lv.P) + ")");
       }
     } else if (jg <= lv.ncg_chunk) {
@@ -2401,7 +2413,7 @@ int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
           LevelBath& L = lv.lb[b];
           if (!L.active) continue;
           if (launch_seg_fft(bb.d_H, bb.ldh, bb.R, (int)h->B, bb.nc, bb.ncp, lv.P, t, 1, L.d_seg, L.seg_fstride,
-                             L.ldseg, L.Rseg, h->d_cstab, lv.cstride, h->stream))
+                             L.ldseg, L.Rseg, h->d_cstab, lv.cstride, h->stream, 0, -1, lv.nplanes))
             return fail(h, GLE_ERR_UNSUP, "segment transform launch failed (P = " + std::to_string(lv.P) + ")");
         }
         lv.fblock = k + 1;
@@ -3664,7 +3676,7 @@ int gle_step_work(gle_handle* h, double* flops, double* bytes) {
       for (size_t j = 0; j < h->baths.size(); ++j)
         if (lv.lb[j].active) {
           const double ncb = (double)h->baths[j].nc * B;
-          fby += 8.0 * ncb * (N + 2.0 * (P + 1.0)) + 8.0 * ncb * (3.0 * (P + 1.0) * lv.cg_split + P);
+          fby += 8.0 * ncb * (N + lv.nplanes * (P + 1.0)) + 8.0 * ncb * (3.0 * (P + 1.0) * lv.cg_split + P);
         }
       fl += (lv.cg_flops + fft) / P;
       by += (lv.cg_bytes + fby) / P;

@@ -358,11 +358,12 @@ void launch_contract_cplx(int rn, const CItem* items, int nitems, StepArgs ta, h
 // (s_memrealtime, 100 MHz): the launch's kernel duration as a kernel trace reports it
 void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStream_t s, int max_grid = 0,
                   unsigned long long* ts = nullptr);
+// nplanes: 2 (Re, Im: two-plane Gauss items) or 3 (the three Gauss planes, one item per part)
 void launch_khat_pack(const double* Kf, int ml, int nks_k, double* khat, int P, int m0, int M,
-                      int nc, int nrt2, int nks2, const double* cstab, int cstride, hipStream_t s);
+                      int nc, int nrt2, int nks2, const double* cstab, int cstride, hipStream_t s, int nplanes);
 int launch_seg_fft(const double* H, int64_t ldh, int R, int B, int nc, int ncp, int P, int64_t T,
                    int nseg, double* seg, int64_t seg_fstride, int64_t ldseg, int Rseg,
-                   const double* cstab, int cstride, hipStream_t s, int k0 = 0, int k1 = -1);
+                   const double* cstab, int cstride, hipStream_t s, int k0, int k1, int nplanes);
 // [k0, k1): the DOF range of this launch (the background schedule issues a long level's transforms
 // as several DOF-range pieces); k1 < 0: up to nc
 int launch_far_ifft(const double* Y, int64_t yfstride, int64_t ysplit, int nc, int B, int P, double* out,

@@ -769,13 +769,14 @@ namespace gle {
 // cstab[q] = (cos(pi q / Pmax), sin(pi q / Pmax)), q < 2 Pmax; a level reads it with stride
 // Pmax / P, so e^{-i pi f n / P} = (cs.x, -cs.y) at q = ((f n) mod 2P) * stride.
 //
-//   Khat_m(f) = sum_i' k_m[i'] e^{-i pi f i'/P}, f = 0..P, stored as two real planes (Re, Im) in
-//   fragment-native order [f][Re | Im][rt][m - m0][ks][64] (a wave streams its row tile's k-steps
-//   contiguously; the Gauss sums Re + Im, Im - Re are formed in the GEMM's registers), read straight
-//   out of the fragment-native K already on the device (one-time setup).
+//   Khat_m(f) = sum_i' k_m[i'] e^{-i pi f i'/P}, f = 0..P, stored in fragment-native order
+//   [f][plane][rt][m - m0][ks][64] (a wave streams its row tile's k-steps contiguously) as two real
+//   planes Re, Im (nplanes = 2: the two-plane Gauss items form Re + Im, Im - Re in registers) or as
+//   the three Gauss planes Re, Re + Im, Im - Re (nplanes = 3: one item per Gauss part), read
+//   straight out of the fragment-native K already on the device (one-time setup).
 __global__ void khat_pack_kernel(const double* __restrict__ Kf, int ml, int nks_k,
                                  double* __restrict__ khat, int P, int m0, int M, int nc, int nrt2,
-                                 int nks2, const double2* __restrict__ cstab, int cstride) {
+                                 int nks2, const double2* __restrict__ cstab, int cstride, int nplanes) {
   const int64_t total = (int64_t)(P + 1) * nrt2 * M * nks2 * 64;
   const int64_t plane = (int64_t)nrt2 * M * nks2 * 64;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
@@ -803,16 +804,21 @@ __global__ void khat_pack_kernel(const double* __restrict__ Kf, int ml, int nks_
         im -= kv * cs.y;
       }
     }
-    const int64_t o = (int64_t)f * 2 * plane + (((int64_t)rt2 * M + mm) * nks2 + ks2) * 64 + lane;
+    const int64_t o = (int64_t)f * nplanes * plane + (((int64_t)rt2 * M + mm) * nks2 + ks2) * 64 + lane;
     khat[o] = re;
-    khat[o + plane] = im;
+    if (nplanes == 2) {
+      khat[o + plane] = im;
+    } else {  // three Gauss planes Re, Re + Im, Im - Re
+      khat[o + plane] = re + im;
+      khat[o + 2 * plane] = im - re;
+    }
   }
 }
 
 void launch_khat_pack(const double* Kf, int ml, int nks_k, double* khat, int P, int m0, int M,
-                      int nc, int nrt2, int nks2, const double* cstab, int cstride, hipStream_t s) {
+                      int nc, int nrt2, int nks2, const double* cstab, int cstride, hipStream_t s, int nplanes) {
   khat_pack_kernel<<<8192, 256, 0, s>>>(Kf, ml, nks_k, khat, P, m0, M, nc, nrt2, nks2,
-                                        (const double2*)cstab, cstride);
+                                        (const double2*)cstab, cstride, nplanes);
 }
 
 // In-place radix-2 FFT of NS complex series of length N = 2^logn held bit-reversed in LDS
@@ -958,8 +964,9 @@ void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStre
 // Segment spectra of the nseg newest segments sigma = T/P - sidx (grid: sidx x DOF k x 8-trajectory
 // chunk): x[n] = p at time sigma*P - 2P + 2 + n (n < 2P-1), x[2P-1] = 0;
 // Xhat(f) = sum_n x[n] e^{-i pi f n / P}, f = 0..P, written into the frequency-f segment ring as two
-// planes  g = 0: Re,  1: Im  (rows [g ncp + k]; the GEMM forms Re + Im in registers).  Two real series
-// per complex FFT.
+// planes  g = 0: Re,  1: Im  (nplanes = 2; the two-plane GEMM items form Re + Im in registers) or the
+// three Gauss planes  g = 0: Re + Im,  1: Im,  2: Re  (nplanes = 3), rows [g ncp + k].  Two real
+// series per complex FFT.
 // BC trajectories per block: 64 for the small transforms (one block per DOF, 512 B rows, every
 // thread busy in every butterfly stage), fewer for long transforms (LDS: BC/2 series of 2P points)
 template <int BC>
@@ -967,7 +974,8 @@ __global__ __launch_bounds__(256) void seg_fft_kernel(const double* __restrict__
                                                       int B, int k0, int nk, int ncp, int P, int logn,
                                                       int64_t T, double* __restrict__ seg,
                                                       int64_t seg_fstride, int64_t ldseg, int Rseg,
-                                                      const double2* __restrict__ cstab, int cstride) {
+                                                      const double2* __restrict__ cstab, int cstride,
+                                                      int nplanes) {
   extern __shared__ double2 fbuf[];  // BC/2 series of N points, then N/2 twiddles
   const int N = 2 * P;
   stage_twiddles(fbuf + (BC / 2) * N, N, cstab, cstride);
@@ -1013,11 +1021,11 @@ __global__ __launch_bounds__(256) void seg_fft_kernel(const double* __restrict__
       im = -0.5 * (z.x - zc.x);
     }
     double* sf = seg + (int64_t)f * seg_fstride + b;
-    const double v[2] = {re, im};
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
+    // two planes Re, Im (two-plane Gauss items) or the three Gauss planes Re + Im, Im, Re
+    const double v3[3] = {re + im, im, re}, v2[2] = {re, im};
+    for (int g = 0; g < nplanes; ++g) {
       const int64_t ir = (int64_t)(g * ncp + k) * ldseg;
-      sf[ir + slot * B] = v[g];  // (cgemm addresses ring slots modulo Rseg: no mirrored copy)
+      sf[ir + slot * B] = nplanes == 2 ? v2[g] : v3[g];  // (cgemm addresses ring slots modulo Rseg: no mirrored copy)
     }
   }
 }
@@ -1051,7 +1059,7 @@ static int fft_bc(int B, int P) {
 template <int BC>
 static int seg_fft_launch(const double* H, int64_t ldh, int R, int B, int k0, int nk, int ncp, int P, int logn,
                           int64_t T, int nseg, double* seg, int64_t seg_fstride, int64_t ldseg, int Rseg,
-                          const double* cstab, int cstride, hipStream_t s) {
+                          const double* cstab, int cstride, hipStream_t s, int nplanes) {
   const size_t shmem = ((size_t)(BC / 2) * 2 * P + P) * sizeof(double2);
   if (shmem > 160 * 1024) return -2;
   // raise the dynamic-LDS limit once per instantiation (a per-launch attribute call costs host
@@ -1061,13 +1069,13 @@ static int seg_fft_launch(const double* H, int64_t ldh, int R, int B, int k0, in
   const int64_t blocks = (int64_t)nseg * nk * nbc;
   if (blocks <= 0) return 0;
   seg_fft_kernel<BC><<<(unsigned)blocks, 256, shmem, s>>>(H, ldh, R, B, k0, nk, ncp, P, logn, T, seg, seg_fstride,
-                                                           ldseg, Rseg, (const double2*)cstab, cstride);
+                                                           ldseg, Rseg, (const double2*)cstab, cstride, nplanes);
   return 0;
 }
 
 int launch_seg_fft(const double* H, int64_t ldh, int R, int B, int nc, int ncp, int P, int64_t T,
                    int nseg, double* seg, int64_t seg_fstride, int64_t ldseg, int Rseg,
-                   const double* cstab, int cstride, hipStream_t s, int k0, int k1) {
+                   const double* cstab, int cstride, hipStream_t s, int k0, int k1, int nplanes) {
   if (k1 < 0 || k1 > nc) k1 = nc;
   k0 = k0 < 0 ? 0 : k0;
   const int nk = k1 - k0;
@@ -1076,10 +1084,10 @@ int launch_seg_fft(const double* H, int64_t ldh, int R, int B, int nc, int ncp, 
   while ((1 << logn) < 2 * P) ++logn;
   if ((1 << logn) != 2 * P) return -1;
   switch (fft_bc(B, P)) {
-    case 64: return seg_fft_launch<64>(H, ldh, R, B, k0, nk, ncp, P, logn, T, nseg, seg, seg_fstride, ldseg, Rseg, cstab, cstride, s);
-    case 32: return seg_fft_launch<32>(H, ldh, R, B, k0, nk, ncp, P, logn, T, nseg, seg, seg_fstride, ldseg, Rseg, cstab, cstride, s);
-    case 16: return seg_fft_launch<16>(H, ldh, R, B, k0, nk, ncp, P, logn, T, nseg, seg, seg_fstride, ldseg, Rseg, cstab, cstride, s);
-    default: return seg_fft_launch<8>(H, ldh, R, B, k0, nk, ncp, P, logn, T, nseg, seg, seg_fstride, ldseg, Rseg, cstab, cstride, s);
+    case 64: return seg_fft_launch<64>(H, ldh, R, B, k0, nk, ncp, P, logn, T, nseg, seg, seg_fstride, ldseg, Rseg, cstab, cstride, s, nplanes);
+    case 32: return seg_fft_launch<32>(H, ldh, R, B, k0, nk, ncp, P, logn, T, nseg, seg, seg_fstride, ldseg, Rseg, cstab, cstride, s, nplanes);
+    case 16: return seg_fft_launch<16>(H, ldh, R, B, k0, nk, ncp, P, logn, T, nseg, seg, seg_fstride, ldseg, Rseg, cstab, cstride, s, nplanes);
+    default: return seg_fft_launch<8>(H, ldh, R, B, k0, nk, ncp, P, logn, T, nseg, seg, seg_fstride, ldseg, Rseg, cstab, cstride, s, nplanes);
   }
 }
 
