@@ -33,6 +33,20 @@ def ReadNetCDFVar(file, var):
         return np.array(f.variables[var].data, dtype=np.float64)
 
 
+def read_history(file, var, ml):
+    """phis / qhis of an MD{j}.nc file as (ml, nph) or (ntraj, ml, nph): the ('mem', ...) layout, or
+    the record layout md.dump uses for ensembles whose history exceeds a classic-format variable
+    (rows [0, ml) of ('nnmd', 'traj', 'nph'))."""
+    with netcdf_file(file, "r", mmap=False) as f:
+        v = f.variables[var]
+        dims = tuple(v.dimensions)
+        a = np.array(v.data, dtype=np.float64)
+    if dims and dims[0] == "nnmd":
+        a = a[:ml]
+        return np.transpose(a, (1, 0, 2)) if a.ndim == 3 else a
+    return a
+
+
 def var_dims(file, var):
     """Dimension names of one variable of an MD{j}.nc file."""
     with netcdf_file(file, "r", mmap=False) as f:

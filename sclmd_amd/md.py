@@ -477,6 +477,8 @@ class md:
     # streamed baths keep their dense factors in host memory between runs (C5: ~11 GB for the three
     # baths, against ~46 s of factorisation per run without the cache)
     noise_factor_cache = True
+    # largest fixed-size variable of an MD{j}.nc file (NetCDF classic format, scipy.io)
+    nc_var_limit = 2**31 - 4096
 
     def _noise_seed(self, i, run):
         base = 0 if self.seed is None else int(self.seed)
@@ -768,8 +770,16 @@ class md:
         C.Write2NetCDFFile(f, self.q, "q", tr + ("nph",), units="")
         C.Write2NetCDFFile(f, [self.t], "t", ("one",), units="")
         C.Write2NetCDFFile(f, [ipie], "ipie", ("one",), units="")
-        C.Write2NetCDFFile(f, self.phis, "phis", tr + ("mem", "nph"), units="")
-        C.Write2NetCDFFile(f, self.qhis, "qhis", tr + ("mem", "nph"), units="")
+        phis, qhis = np.asarray(self.phis), np.asarray(self.qhis)
+        if multi and self.ml <= self.nmd and phis.nbytes >= self.nc_var_limit:
+            # a classic-format variable holds < 2 GiB (C5: 32 x 4096 x 3000 doubles = 3.1 GB): large
+            # ensembles store the histories along the record dimension, rows [0, ml) of ('nnmd',
+            # 'traj', 'nph') -- read back by checkpoint.read_history
+            C.Write2NetCDFFile(f, np.transpose(phis, (1, 0, 2)), "phis", ("nnmd",) + tr + ("nph",), units="")
+            C.Write2NetCDFFile(f, np.transpose(qhis, (1, 0, 2)), "qhis", ("nnmd",) + tr + ("nph",), units="")
+        else:
+            C.Write2NetCDFFile(f, phis, "phis", tr + ("mem", "nph"), units="")
+            C.Write2NetCDFFile(f, qhis, "qhis", tr + ("mem", "nph"), units="")
         C.commit(f, tmp, self._ncname(id))
 
     def _read_poweratomlist(self, fn):
@@ -795,7 +805,7 @@ class md:
     def _resume(self, j):
         """The reference's per-run file logic (md.py:506-567).  Returns the last finished piece
         (-1 for a new run) or None when run j is already complete."""
-        from .checkpoint import ReadNetCDFVar
+        from .checkpoint import ReadNetCDFVar, read_history
 
         fn, fnm = self._ncname(j), self._ncname(j - 1)
         if os.path.isfile(fn):
@@ -809,7 +819,7 @@ class md:
                 self.p = ReadNetCDFVar(fn, "p")
                 self.q = ReadNetCDFVar(fn, "q")
                 self.t = int(ReadNetCDFVar(fn, "t")[0])
-                self._load_phis(ReadNetCDFVar(fn, "phis"), ReadNetCDFVar(fn, "qhis"))
+                self._load_phis(read_history(fn, "phis", self.ml), read_history(fn, "qhis", self.ml))
                 self.power = ReadNetCDFVar(fn, "power")
                 if self.atomlist is not None:
                     self.poweratomlist = self._read_poweratomlist(fn)
@@ -834,8 +844,8 @@ class md:
             self.p = ReadNetCDFVar(fnm, "p")
             self.q = ReadNetCDFVar(fnm, "q")
             self.t = int(ReadNetCDFVar(fnm, "t")[0])
-            ph = ReadNetCDFVar(fnm, "phis")
-            qh = ReadNetCDFVar(fnm, "qhis")
+            ph = read_history(fnm, "phis", self.ml)
+            qh = read_history(fnm, "qhis", self.ml)
             if ph.shape[-2:] == (self.ml, self.nph):
                 self._load_phis(ph, qh if qh.shape == ph.shape else None)
         elif j != 0:

@@ -18,13 +18,13 @@ def rel(a, b):
     return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
 
 
-def _md(nstart, nstop, npie=2, save=True):
+def _md(nstart, nstop, npie=2, save=True, ntraj=1):
     from sclmd_amd import md as MD
     from sclmd_amd import synthetic
 
     dyn, axyz, baths, meta = synthetic.junction("C3", seed=5, natom=10, ml=16, nmd=64, nw=60)
     m = MD.md(meta["dt"], meta["nmd"], meta["T"], axyz=axyz, dyn=dyn, nstart=nstart, nstop=nstop,
-              npie=npie, seed=11, noise_mode="device", verbose=False)
+              npie=npie, seed=11, noise_mode="device", verbose=False, ntraj=ntraj)
     for b in baths:
         m.AddBath(b)
     m.AddConstr([range(0, 3)])
@@ -125,3 +125,32 @@ def test_unfinished_run_needs_saveall(uninterrupted, tmp_path, monkeypatch):
     with pytest.raises(RuntimeError, match="saveall"):
         m.Run()
     m.close()
+
+
+def test_ensemble_history_record_layout_continues(tmp_path, monkeypatch):
+    """An ensemble whose p / q histories exceed a classic-format variable (C5: 32 x 4096 x 3000
+    doubles) stores them along the record dimension; continuing from that file reproduces the
+    uninterrupted run (the limit is lowered here so a small ensemble takes that layout)."""
+    from sclmd_amd import md as MD
+    from sclmd_amd.checkpoint import read_history, var_dims
+
+    monkeypatch.setattr(MD.md, "nc_var_limit", 0)
+    full = tmp_path / "full"
+    full.mkdir()
+    monkeypatch.chdir(full)
+    m = _md(0, 2, ntraj=3)
+    m.Run()
+    p, q, t, kap = _final(m)
+    ph = np.array(m.phis)
+    m.close()
+    assert var_dims(str(full / "MD0.nc"), "phis")[0] == "nnmd"
+    assert rel(read_history(str(full / "MD1.nc"), "phis", 16), ph) == 0.0
+    cont = tmp_path / "cont"
+    cont.mkdir()
+    shutil.copy(full / "MD0.nc", cont / "MD0.nc")
+    monkeypatch.chdir(cont)
+    m = _md(1, 2, ntraj=3)
+    m.Run()
+    p2, q2, t2, kap2 = _final(m)
+    m.close()
+    assert t2 == t and rel(q2, q) < 1e-10 and rel(p2, p) < 1e-10 and rel(kap2[-1], kap[-1]) < 1e-9

@@ -189,6 +189,29 @@ def test_checkpoint_netcdf_roundtrip(tmp_path):
     assert C.ReadNetCDFVar(fn, "t")[0] == 42 and C.has_var(fn, "ps") and not C.has_var(fn, "qs")
 
 
+def test_read_history_both_layouts(tmp_path):
+    """checkpoint.read_history: the ('traj', 'mem', 'nph') layout and the record layout md.dump
+    uses for ensemble histories above a classic-format variable's size give the same array."""
+    from sclmd_amd import checkpoint as C
+
+    rng = np.random.default_rng(1)
+    ph = rng.normal(size=(3, 4, 5))  # (traj, ml, nph)
+    for rec in (False, True):
+        fn = str(tmp_path / ("rec.nc" if rec else "mem.nc"))
+        f, tmp = C.open_for_write(fn)
+        f.createDimension("nnmd", None)
+        f.createDimension("nph", 5)
+        f.createDimension("mem", 4)
+        f.createDimension("traj", 3)
+        C.Write2NetCDFFile(f, rng.normal(size=(9, 5)), "ps", ("nnmd", "nph"), units="")  # 9 records > ml
+        if rec:
+            C.Write2NetCDFFile(f, np.transpose(ph, (1, 0, 2)), "phis", ("nnmd", "traj", "nph"), units="")
+        else:
+            C.Write2NetCDFFile(f, ph, "phis", ("traj", "mem", "nph"), units="")
+        C.commit(f, tmp, fn)
+        assert np.array_equal(C.read_history(fn, "phis", 4), ph), rec
+
+
 @pytest.mark.parametrize("kind", ["ph", "e_bias", "e_eq"])
 def test_streamed_noise_factors_cover_the_positive_part(kind):
     """noise.stream_factor_chunks (the C5 path: factors streamed to the device by frequency chunk)
