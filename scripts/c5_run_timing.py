@@ -44,6 +44,9 @@ def main():
     parts = collections.defaultdict(lambda: collections.defaultdict(float))
     cur = {"run": -1}
 
+    def log(*a):
+        print("[c5run %.1fs]" % (time.perf_counter() - t_all), *a, file=sys.stderr, flush=True)
+
     def timed(name, fn):
         def w(*a, **k):
             t0 = time.perf_counter()
@@ -53,6 +56,7 @@ def main():
                 if name == "dump":
                     m._st.sync()
                 parts[cur["run"]][name] += time.perf_counter() - t0
+                log("run %d %s %.2fs" % (cur["run"], name, time.perf_counter() - t0))
         return w
 
     orig_resume = m._resume
@@ -74,6 +78,7 @@ def main():
         m._st.sync()
         parts[cur["run"]]["steps"] += time.perf_counter() - t0
         parts[cur["run"]]["nsteps"] += n
+        log("run %d %d steps %.2fs" % (cur["run"], n, time.perf_counter() - t0))
 
     m.steps = steps
     m.dump = timed("dump", m.dump)
