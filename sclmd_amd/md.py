@@ -709,6 +709,14 @@ class md:
             st.set_history(i, h)
         self._reset_his = False
 
+    def _wrote_current(self, fn, ipie=None):
+        """fn is the file this process wrote last, unchanged since, at the current t (and piece)."""
+        ld = getattr(self, "_last_dump", None)
+        if ld is None or ld[0] != fn or not os.path.isfile(fn):
+            return False
+        st_ = os.stat(fn)
+        return (st_.st_mtime_ns, st_.st_size) == ld[1:3] and int(self.t) == ld[3] and (ipie is None or ipie == ld[4])
+
     def dump(self, ipie, id):
         """Write MD{id}.nc (md.py:684-764): energy, p, q, t, ipie, phis, qhis, with SaveAll the noise
         series and fhis{i} (and ps / qs with savep / saveq), with savep the power spectra.  With
@@ -780,7 +788,12 @@ class md:
         else:
             C.Write2NetCDFFile(f, phis, "phis", tr + ("mem", "nph"), units="")
             C.Write2NetCDFFile(f, qhis, "qhis", tr + ("mem", "nph"), units="")
-        C.commit(f, tmp, self._ncname(id))
+        fn = self._ncname(id)
+        C.commit(f, tmp, fn)
+        st_ = os.stat(fn)
+        # what this process wrote: the next run's start can skip reading its own file back, and an
+        # unchanged second dump of the same piece need not be rewritten
+        self._last_dump = (fn, st_.st_mtime_ns, st_.st_size, int(self.t), ipie, bool(self.savep))
 
     def _read_poweratomlist(self, fn):
         """poweratomlist (natomlist, nmd, 2) from an MD{j}.nc file in either layout: this build's
@@ -839,7 +852,12 @@ class md:
                 self.t = int(ReadNetCDFVar(fn, "t")[0])
                 return None
             raise RuntimeError("md.Run: ipie error in %s (ipie = %d)" % (fn, ipie))
-        if os.path.isfile(fnm):
+        if os.path.isfile(fnm) and self._wrote_current(fnm):
+            # the previous run's file is the one this process just wrote from the device state it
+            # still holds (same t, file unchanged): reading p, q and the histories back would only
+            # return them (C5: 6 GB of phis / qhis)
+            self._log("continuing from previous run (state on the device)")
+        elif os.path.isfile(fnm):
             self._log("reading history from previous run")
             self.p = ReadNetCDFVar(fnm, "p")
             self.q = ReadNetCDFVar(fnm, "q")
@@ -902,7 +920,10 @@ class md:
                 self.cflist = []
             if self.savep:
                 self._power(j)
-            self.dump(piece, j)
+            # "dump again, to make sure power is all right" (md.py:654): without savep nothing the
+            # file holds has changed since the piece's dump, which is then left as written
+            if self.savep or not self._wrote_current(self._ncname(j), piece):
+                self.dump(piece, j)
             cur = self._st.get_current()                      # (nbath, ntraj, nmd)
             sums = self._reduce(self._st.current_sums())      # (nbath, 3) over all ranks
             kap = sums[:, 0] / sums[:, 2] * U.curcof
