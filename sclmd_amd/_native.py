@@ -136,7 +136,9 @@ def load():
                        "`python -c 'import __graft_entry__ as g; g.build()'`" % LIB_PATH)
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in _SIGS.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:  # an older library (A/B experiments); build() checks the release one exports all
+            continue
         fn.restype = res
         fn.argtypes = args
     _lib = lib

@@ -1943,6 +1943,7 @@ int freeze(gle_handle* h) {
       // ring slots addressed modulo Rseg (no mirrored copy); rows padded by 8 doubles (the 512 of
       // earlier rounds was 73 % of a row at C5's P = 1024 level, ~7 GB per bath)
       L.ldseg = (int64_t)L.Rseg * B + 8;
+      if (const char* e = gle_env("GLE_SEG_PAD")) L.ldseg = (int64_t)L.Rseg * B + std::max(0, atoi(e));
       L.khat_fstride = (int64_t)lv.nplanes * b.nrt * b.nks * L.M * 64;  // Re, Im | the Gauss planes
       L.seg_fstride = (int64_t)lv.nplanes * b.ncp * L.ldseg;             // Re, Im | Re + Im, Im, Re rows
       L.yfstride = (int64_t)3 * b.nc * B;                       // T_0, T_1, T_2
