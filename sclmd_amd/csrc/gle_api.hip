@@ -209,6 +209,7 @@ struct gle_handle {
   bool bg_serial = false;      // GLE_BG_SERIAL=1: ladder pieces on the main stream (time-sliced, experiment)
   int piece_slack = 1;         // GLE_PIECE_SLACK: boundaries left between a block's last piece and its use
   bool merge_waits = true;     // GLE_MERGE_WAITS=0: one main-stream wait per level
+  int wait_early = 0;          // GLE_WAIT_EARLY: steps before a block's first use at which the main stream waits for it
   int64_t ev_seq_counter = 0;
   int dbg_skip = 0;            // GLE_DBG_SKIP bits (timing experiments only, wrong results):
                                // 1 cgemm, 2 seg_fft, 4 far_ifft, 8 direct level ops
@@ -1825,6 +1826,8 @@ int freeze(gle_handle* h) {
     Pmax = L;
   }
   h->P0 = P0;
+  h->wait_early = std::min(h->wait_early, P0 - 1);
+  if (h->piece_slack < 1) h->wait_early = 0;
   // pieces go out at every step (GLE_PIECE_STEP=P0: only at first-level boundaries): the same
   // long-window rate, and a short window's background work depends less on its phase (20-step
   // windows over all phases: 55-67 us/step vs 55-79 us at C3)
@@ -2457,7 +2460,12 @@ int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
         }
         if (lv.next_piece >= lv.npiece) lv.pend_block = INT64_MIN;
       }
-      if (boundary && t % lv.P == 0 && lv.bg_block[k & 1] == k) {
+      // the main stream waits for block k at the first step within wait_early steps of its first
+      // use k P (the block's last piece and event were enqueued >= piece_slack first-level blocks
+      // before k P, and wait_early < P0); wait_early = 0: at the boundary k P itself
+      const int64_t kw = floordiv(t + h->wait_early, lv.P);
+      if (lv.bg_block[kw & 1] == kw) {
+        const int64_t k = kw;
         // per background stream, waiting for the block enqueued last implies the earlier ones
         // (in-order streams): one barrier packet per stream instead of one per level
         if (h->merge_waits) {
@@ -2624,6 +2632,7 @@ int gle_create(const gle_config* cfg, gle_handle** out) {
   if (const char* e = gle_env("GLE_PIECE_SLACK")) h->piece_slack = std::max(0, atoi(e));
   if (const char* e = gle_env("GLE_BG_SERIAL")) h->bg_serial = atoi(e) != 0;
   if (const char* e = gle_env("GLE_MERGE_WAITS")) h->merge_waits = atoi(e) != 0;
+  if (const char* e = gle_env("GLE_WAIT_EARLY")) h->wait_early = std::max(0, atoi(e));
   // main stream (the latency-bound per-step chain) at the highest priority, background streams
   // (ladder blocks) at the lowest
   {
