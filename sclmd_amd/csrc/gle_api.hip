@@ -1907,8 +1907,7 @@ int freeze(gle_handle* h) {
   for (auto& lv : h->levels) {
     lv.cstride = lv.spectral ? Pspec / lv.P : 1;
     lv.cg_rn = (int)std::min<int64_t>(4, (B + 15) / 16);
-    lv.nplanes = lv.cg_rn <= 2 ? 2 : 3;
-    if (const char* e = gle_env("GLE_GAUSS_PLANES")) lv.nplanes = atoi(e) == 2 ? 2 : 3;
+    lv.nplanes = lv.cg_rn <= 2 ? 2 : 3;  // (64-column items have no two-plane kernel path)
     lv.cg_split = 1;
     if (lv.spectral) {
       // small levels of large baths: split the k range of every product in two (partial planes

@@ -325,13 +325,17 @@ constexpr int cg_lds_doubles() {
 }
 
 // one item of either kind (the kind is item-uniform)
+// (the planner gives two-plane items only to levels of <= 32-column items: the 64-column kernel
+// carries the one-plane path alone and keeps its register budget)
 template <int RN, int KC, int AD, int XD, int DBG = 0>
 __device__ __forceinline__ void cgemm_any(const CgItem& it, int64_t tseg, double* lds) {
-  if (it.g3) {
-    cgemm_item3<RN, cg3_kc<RN, KC>(), (RN == 4 ? 1 : (AD < 4 ? AD : 4))>(it, tseg, lds);
-  } else {
-    cgemm_item<RN, KC, AD, XD, DBG>(it, tseg, *reinterpret_cast<double(*)[2][4 * KC * CG_LD]>(lds));
+  if constexpr (RN <= 2) {
+    if (it.g3) {
+      cgemm_item3<RN, cg3_kc<RN, KC>(), (AD < 4 ? AD : 4)>(it, tseg, lds);
+      return;
+    }
   }
+  cgemm_item<RN, KC, AD, XD, DBG>(it, tseg, *reinterpret_cast<double(*)[2][4 * KC * CG_LD]>(lds));
 }
 
 }  // namespace gle
