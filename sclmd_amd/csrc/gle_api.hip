@@ -1671,8 +1671,12 @@ int apply_record(gle_handle* h) {
 int plan_far_fused(gle_handle* h) {
   h->far_fused = false;
   h->far_max_items = 0;
-  bool any = false;
-  for (auto& lv : h->levels) any |= lv.spectral;
+  bool any = false, two = false;
+  for (auto& lv : h->levels) {
+    any |= lv.spectral;
+    two |= lv.spectral && lv.nplanes == 2;
+  }
+  if (two) return GLE_OK;  // the chain kernel's far path runs one-plane items only
   const bool nw4 = h->chA[0].nw == 4 && h->chA[1].nw == 4 && h->chB[0].nw == 4 && h->chB[1].nw == 4 &&
                    h->chC.nw == 4 && (!h->fuse_bc || h->chBC.nw == 4);
   // measured r03 (C3, one MI355X, same box): 83 us/step fused vs 50 us background -- the items,

@@ -862,7 +862,7 @@ __device__ __forceinline__ void raw(const ChTile* __restrict__ T, const StepDev*
 // dynamic LDS (>= CH_FAR_LDS bytes).  4-wave launches only (the item's 4 waves own its 64 rows).
 // The HBM stream of K-hat goes 3 chunks ahead (119 VGPRs for this path alone, within the chain
 // kernel's 128).
-constexpr size_t CH_FAR_LDS = sizeof(double) * cg_lds_doubles<4, 4>();
+constexpr size_t CH_FAR_LDS = sizeof(double) * 2 * 4 * 4 * CG_LD;
 #ifndef CH_FAR_PATH
 #define CH_FAR_PATH 1
 #endif
@@ -892,10 +892,13 @@ __device__ __forceinline__ void far_tile(const StepArgs& ta, double* lds) {
     }
     if (!found) return;
     const CgItem it = items[idx];
+    // one-plane items only (the planner keeps two-plane levels out of the fused schedule): the
+    // two-plane path's three accumulator sets would set the whole chain kernel's register budget
+    auto& xs = *reinterpret_cast<double(*)[2][4 * 4 * CG_LD]>(lds);
     switch (it.ncols > 32 ? 4 : (it.ncols > 16 ? 2 : 1)) {
-      case 4: cgemm_any<4, 4, 3, 1>(it, tseg, lds); break;
-      case 2: cgemm_any<2, 4, 3, 1>(it, tseg, lds); break;
-      default: cgemm_any<1, 4, 3, 1>(it, tseg, lds); break;
+      case 4: cgemm_item<4, 4, 3, 1>(it, tseg, xs); break;
+      case 2: cgemm_item<2, 4, 3, 1>(it, tseg, xs); break;
+      default: cgemm_item<1, 4, 3, 1>(it, tseg, xs); break;
     }
   }
 }
