@@ -4,14 +4,15 @@ set -o pipefail
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 O=gpurun_out/${1:-r04c}
 mkdir -p $O
-timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_20.json 2> $O/bench_20.err || { tail -20 $O/bench_20.err; exit 1; }
-cut -c1-200 $O/bench_20.json
-timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
-cut -c1-200 $O/bench.json
+[ -n "$NOBENCH" ] || timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_20.json 2> $O/bench_20.err || { tail -20 $O/bench_20.err; exit 1; }
+[ -n "$NOBENCH" ] || cut -c1-200 $O/bench_20.json
+[ -n "$NOBENCH" ] || timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+[ -n "$NOBENCH" ] || cut -c1-200 $O/bench.json
 : > $O/libs.jsonl
+IFS=';' read -ra VLIST <<< "${VARS:-;GLE_WAIT_EARLY=4}"
 for r in 1 2 3; do
   for lib in exp r03; do
-    for v in "" "GLE_WAIT_EARLY=4"; do
+    for v in "${VLIST[@]}"; do
       env $v SCLMD_AMD_LIB=sclmd_amd/_lib/libhipgle_$lib.so timeout -k 10 200 python scripts/exp_time.py --tag "$lib $v" >> $O/libs.jsonl 2>> $O/libs.err || { echo "lib $lib failed"; tail -5 $O/libs.err; exit 1; }
     done
   done
