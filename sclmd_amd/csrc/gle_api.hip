@@ -1862,7 +1862,7 @@ int freeze(gle_handle* h) {
         const int M = (std::min(lv.lag1, b.ml) + lv.P - 1) / lv.P - 2;
         const int npl = B <= 32 ? 2 : 3;  // Level::nplanes
         need += (size_t)(lv.P + 1) * npl * b.nrt * b.nks * M * 64 * 8;
-        need += (size_t)(lv.P + 1) * npl * b.ncp * ((M + 4) * B + 8) * 8;
+        need += (size_t)(lv.P + 1) * npl * b.ncp * ((M + 4) * B + (npl == 2 ? 8 : 512)) * 8;
         need += (size_t)(lv.P + 1) * 3 * b.nc * B * 8;
       }
     }
@@ -1946,9 +1946,10 @@ int freeze(gle_handle* h) {
       if (!lv.spectral) continue;
       L.M = (L.lag1 + lv.P - 1) / lv.P - 2;
       L.Rseg = L.M + 4;
-      // ring slots addressed modulo Rseg (no mirrored copy); rows padded by 8 doubles (the 512 of
-      // earlier rounds was 73 % of a row at C5's P = 1024 level, ~7 GB per bath)
-      L.ldseg = (int64_t)L.Rseg * B + 8;
+      // ring slots addressed modulo Rseg (no mirrored copy); rows padded by 512 doubles for
+      // 64-column items (C3: 49.8 vs 50.2 us/step at 8, 3 interleaved rounds, r04) and by 8 for the
+      // two-plane levels (512 was 73 % of a row at C5's P = 1024 level, ~7 GB per bath)
+      L.ldseg = (int64_t)L.Rseg * B + (lv.nplanes == 2 ? 8 : 512);
       if (const char* e = gle_env("GLE_SEG_PAD")) L.ldseg = (int64_t)L.Rseg * B + std::max(0, atoi(e));
       L.khat_fstride = (int64_t)lv.nplanes * b.nrt * b.nks * L.M * 64;  // Re, Im | the Gauss planes
       L.seg_fstride = (int64_t)lv.nplanes * b.ncp * L.ldseg;             // Re, Im | Re + Im, Im, Re rows

@@ -1021,11 +1021,18 @@ __global__ __launch_bounds__(256) void seg_fft_kernel(const double* __restrict__
       im = -0.5 * (z.x - zc.x);
     }
     double* sf = seg + (int64_t)f * seg_fstride + b;
-    // two planes Re, Im (two-plane Gauss items) or the three Gauss planes Re + Im, Im, Re
-    const double v3[3] = {re + im, im, re}, v2[2] = {re, im};
-    for (int g = 0; g < nplanes; ++g) {
-      const int64_t ir = (int64_t)(g * ncp + k) * ldseg;
-      sf[ir + slot * B] = nplanes == 2 ? v2[g] : v3[g];  // (cgemm addresses ring slots modulo Rseg: no mirrored copy)
+    // two planes Re, Im (two-plane Gauss items) or the three Gauss planes Re + Im, Im, Re; straight-line
+    // stores (a register array indexed by a runtime plane number goes to scratch)
+    // (cgemm addresses ring slots modulo Rseg: no mirrored copy)
+    const int64_t pl = (int64_t)ncp * ldseg;
+    double* so = sf + (int64_t)k * ldseg + (int64_t)slot * B;
+    if (nplanes == 2) {
+      so[0] = re;
+      so[pl] = im;
+    } else {
+      so[0] = re + im;
+      so[pl] = im;
+      so[2 * pl] = re;
     }
   }
 }
