@@ -32,7 +32,6 @@ namespace {
 thread_local std::string g_create_error;
 
 struct Op {
-  bool cplx = false;   // complex items (contract_cplx_kernel)
   int rn = 1;
   int cu = 1;          // staged X columns per thread per row (contract_kernel template)
   int max_elems = 0;   // largest reduce tile
@@ -456,8 +455,6 @@ struct Gemm {
   int Kd = 0;  // true (unpadded) reduction length, for the algorithmic flop/byte count
   int tdiv = 1;
   bool lat = false;  // per-step product: minimise sequential LDS stages per item
-  bool cplx = false; // complex product: Im parts of A, X, dst at a_im, x_im, dst_im
-  int64_t a_im = 0, x_im = 0, dst_im = 0;
 };
 
 // Split policy: target ~target_items work items in total for this product, each with at least
@@ -487,7 +484,7 @@ void plan_gemm(Op& op, const Gemm& g, int target_items, int min_work) {
       if (g.ring) {
         // slice chunks are whole multiples of what one LDS window holds, so no item runs its
         // k-stages with a short remainder window
-        const int wcap = g.cplx ? CPLX_WW_CAP : std::min(LDS_WW_MAX, 256 * (op.rn >= 16 ? 3 : 4));
+        const int wcap = std::min(LDS_WW_MAX, 256 * (op.rn >= 16 ? 3 : 4));
         const int ns_cap = std::max(1, (wcap - NT) / std::max(1, g.cs) + 1);
         const int q = std::max(1, (int)((double)ni / ((double)split * ns_cap) + 0.5));
         chunk = ns_cap * q;
@@ -508,7 +505,7 @@ void plan_gemm(Op& op, const Gemm& g, int target_items, int min_work) {
   for (int gi = 0; gi < ngroups; ++gi)
     for (int ct = 0; ct < ncol; ++ct) {
       slot0s[(size_t)gi * ncol + ct] = op.partial_doubles;
-      if (use_partial) op.partial_doubles += (size_t)nsplit * (g.cplx ? 2 : 1) * 64 * NT;
+      if (use_partial) op.partial_doubles += (size_t)nsplit * 64 * NT;
     }
   for (int ct = 0; ct < ncol; ++ct) {
     const int col0 = ct * NT;
@@ -541,18 +538,14 @@ void plan_gemm(Op& op, const Gemm& g, int target_items, int min_work) {
           it.col0 = col0;
           it.ncols = ncols;
           it.nrows = nrows;
-          const size_t slot_sz = (size_t)(g.cplx ? 2 : 1) * 64 * NT;
-          it.a_im = g.a_im;
-          it.x_im = g.x_im;
+          const size_t slot_sz = (size_t)64 * NT;
           if (use_partial) {
             // offset into the op's partial buffer, fixed up in materialize()
             it.out = (double*)(uintptr_t)((slot0s[key] + (size_t)nslot[key] * slot_sz) * sizeof(double));
             it.ldo = NT;
-            it.o_im = 64 * NT;
           } else {
             it.out = g.dst + (int64_t)(64 * gi) * g.ldd + col0;
             it.ldo = (int32_t)g.ldd;
-            it.o_im = g.dst_im;
           }
           op.items.push_back(it);
           ++nslot[key];
@@ -567,27 +560,23 @@ void plan_gemm(Op& op, const Gemm& g, int target_items, int min_work) {
         const int nrows = std::min(64, g.M - 64 * gi);
         if (nrows <= 0) continue;
         const size_t key = (size_t)gi * ncol + ct;
-        for (int part = 0; part < (g.cplx ? 2 : 1); ++part) {
-          RItem r{};
-          r.dst = g.dst + part * g.dst_im + (int64_t)(64 * gi) * g.ldd + col0;
-          // offset, fixed up in materialize()
-          r.src = (const double*)(uintptr_t)((slot0s[key] + (size_t)part * 64 * NT) * sizeof(double));
-          r.ldd = (int32_t)g.ldd;
-          r.lds = NT;
-          r.nslots = nslot[key];
-          r.slot_stride = (int64_t)(g.cplx ? 2 : 1) * 64 * NT;
-          r.rows = nrows;
-          r.cols = std::min<int>(NT, g.N - col0);
-          op.ritems.push_back(r);
-        }
+        RItem r{};
+        r.dst = g.dst + (int64_t)(64 * gi) * g.ldd + col0;
+        r.src = (const double*)(uintptr_t)(slot0s[key] * sizeof(double));  // offset, fixed up in materialize()
+        r.ldd = (int32_t)g.ldd;
+        r.lds = NT;
+        r.nslots = nslot[key];
+        r.slot_stride = (int64_t)64 * NT;
+        r.rows = nrows;
+        r.cols = std::min<int>(NT, g.N - col0);
+        op.ritems.push_back(r);
       }
   // algorithmic work of this product: each kernel entry read once, X read
   // once, output written once.
   if (ni > 0) {
     const double kd = g.Kd > 0 ? g.Kd : 4.0 * g.nks_total;
-    const double cf = g.cplx ? 4.0 : 1.0, cb = g.cplx ? 2.0 : 1.0;  // complex: 4 real products
-    op.flops += cf * 2.0 * g.M * kd * g.N * ni;
-    op.bytes += cb * 8.0 * ((double)ni * g.M * kd + kd * (g.ring ? (double)(ni + (g.N + g.cs - 1) / std::max(1, g.cs) - 1) * g.cs : g.N) + (double)g.M * g.N);
+    op.flops += 2.0 * g.M * kd * g.N * ni;
+    op.bytes += 8.0 * ((double)ni * g.M * kd + kd * (g.ring ? (double)(ni + (g.N + g.cs - 1) / std::max(1, g.cs) - 1) * g.cs : g.N) + (double)g.M * g.N);
   }
 }
 
@@ -601,7 +590,7 @@ int materialize(gle_handle* h, Op& op, const std::vector<bool>& is_partial) {
     maxww = std::max(maxww, std::min(ww, LDS_WW_MAX));
   }
   const int cap = op.rn >= 16 ? 3 : 4;
-  op.cu = op.cplx ? 2 : std::max(1, std::min(cap, (maxww + 255) / 256));
+  op.cu = std::max(1, std::min(cap, (maxww + 255) / 256));
   for (const auto& r : op.ritems) op.max_elems = std::max(op.max_elems, r.rows * r.cols);
   if (op.partial_doubles) {
     int rc = dalloc_n(h, &op.partial, op.partial_doubles);
@@ -739,11 +728,8 @@ void run_op(gle_handle* h, Op& op, hipStream_t s, const StepArgs& ta, bool profi
     hipEventRecord(e0, s);
   }
   StepArgs tc = ta;
-  if (e0 && h->d_tst && !op.cplx) tc.ts = h->d_tst + 2 * h->tst_used++;  // device stamps: first start, last end
-  if (op.cplx)
-    launch_contract_cplx(op.rn, op.d_items, (int)op.items.size(), ta, s);
-  else
-    launch_contract(op.rn, op.cu, op.d_items, (int)op.items.size(), tc, s);
+  if (e0 && h->d_tst) tc.ts = h->d_tst + 2 * h->tst_used++;  // device stamps: first start, last end
+  launch_contract(op.rn, op.cu, op.d_items, (int)op.items.size(), tc, s);
   if (e1) {
     hipEventRecord(e1, s);
     h->prof_n += 1;
@@ -1097,7 +1083,7 @@ int plan_chain(gle_handle* h) {
   if (const char* e = gle_env("GLE_CHAIN_NW")) {
     int v[3] = {4, 8, 4};
     sscanf(e, "%d,%d,%d", &v[0], &v[1], &v[2]);
-    for (int i = 0; i < 3; ++i) h->ch_nw[i] = v[i] >= 16 ? 16 : (v[i] >= 8 ? 8 : 4);
+    for (int i = 0; i < 3; ++i) h->ch_nw[i] = v[i] >= 8 ? 8 : 4;  // (16-wave groups spill)
   }
   if (const char* e = gle_env("GLE_CHAIN_DRN")) h->ch_drn = atoi(e) >= 2 ? 2 : 1;
   if (const char* e = gle_env("GLE_BC_BALANCE")) h->bc_balance = atoi(e) != 0;

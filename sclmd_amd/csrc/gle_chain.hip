@@ -1021,8 +1021,7 @@ void launch_nd(int drn, size_t lds, const ChTile* tiles, int ntiles, const StepD
 template <int STAGE>
 void launch_st(int nw, int drn, size_t lds, const ChTile* tiles, int ntiles, const StepDev* sd, StepArgs ta,
                int mode, hipStream_t s) {
-  if (nw == 16) launch_nd<STAGE, 16>(drn, lds, tiles, ntiles, sd, ta, mode, s);
-  else if (nw == 8) launch_nd<STAGE, 8>(drn, lds, tiles, ntiles, sd, ta, mode, s);
+  if (nw == 8) launch_nd<STAGE, 8>(drn, lds, tiles, ntiles, sd, ta, mode, s);
   else launch_nd<STAGE, 4>(drn, lds, tiles, ntiles, sd, ta, mode, s);
 }
 

@@ -81,7 +81,6 @@ constexpr int LDS_COLS = 1000;     // padded staged row length (doubles): 8*1000
 constexpr int LDS_WW_MAX = 960;    // usable window width: roundup32(960) + 16 <= LDS_COLS
 constexpr int MAXBATH = 8;
 constexpr int MAXLVL = 12;         // levels of the memory-sum ladder
-constexpr int CPLX_WW_CAP = 512;   // contract_cplx_kernel window (doubles per staged row)
 constexpr int ROWS_PER_WG = 64;    // 4 waves x 16 rows
 
 // One workgroup's share of a contraction  out[r][c] = sum_{i in slices} sum_k A_i[r][k] X_i[k][c]
@@ -106,8 +105,6 @@ struct CItem {
   int32_t nrows;     // valid rows to store (<= 64)
   int32_t tdiv;      // ring index = floor(clock.t / tdiv) + tshift - slice (1: steps, P: segments)
   int32_t pad;
-  // complex items (contract_cplx_kernel): imaginary parts at these offsets (doubles) from A, X, out
-  int64_t a_im, x_im, o_im;
 };
 
 // One workgroup of a spectral level's batched GEMM (gle_kernels.hip cgemm_kernel): 64 rows x 16 RN
@@ -353,7 +350,6 @@ void launch_near_fill(const double* H, int64_t ldh, int R, int B, int ncp, doubl
                       int64_t t, hipStream_t s);
 void launch_ring_copy(double* H, int64_t ldh, int R, int B, int nc, int64_t tau0, int nt, double* buf,
                       int dir, hipStream_t s);
-void launch_contract_cplx(int rn, const CItem* items, int nitems, StepArgs ta, hipStream_t s);
 // ts (profiling, may be null): [0] <- min over workgroups of the start, [1] <- max of the end
 // (s_memrealtime, 100 MHz): the launch's kernel duration as a kernel trace reports it
 void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStream_t s, int max_grid = 0,

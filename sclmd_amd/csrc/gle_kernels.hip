@@ -175,159 +175,12 @@ __global__ __launch_bounds__(WG, 2) void contract_kernel(const CItem* __restrict
   }
 }
 
-// Complex contraction  (Yr + i Yi) = sum_slices sum_k (Ar + i Ai)(Xr + i Xi): each wave loads the Ar
-// and Ai fragments of its 16-row tile once and issues the four real MFMAs of the complex product;
-// the LDS stage holds 8 rows of Xr and 8 rows of Xi.  Used for the per-frequency spectral far field.
-constexpr int CPLX_WW_MAX = CPLX_WW_CAP;  // 16 rows x (512+16) doubles = 66 KB (2 WGs per CU)
-template <int RN>
-__global__ __launch_bounds__(WG, 2) void contract_cplx_kernel(const CItem* __restrict__ items,
-                                                              StepArgs ta) {
-  __shared__ double lds[2 * KROWS * (CPLX_WW_MAX + 16)];
-  constexpr int NT = 16 * RN;
-  constexpr int CU = 2;
-  const int nblk = gridDim.x;
-  const int bid = (nblk & 7) ? (int)blockIdx.x : (int)(blockIdx.x & 7) * (nblk >> 3) + (int)(blockIdx.x >> 3);
-  const CItem it = items[bid];
-  const int tid = threadIdx.x;
-  const int wave = tid >> 6;
-  const int lane = tid & 63;
-  const int64_t t = ta.t;
-
-  d4 accr[RN], acci[RN];
-#pragma unroll
-  for (int n = 0; n < RN; ++n) {
-    accr[n] = d4{0.0, 0.0, 0.0, 0.0};
-    acci[n] = d4{0.0, 0.0, 0.0, 0.0};
-  }
-  const int ns_max = it.ring ? (CPLX_WW_MAX - NT) / it.cs + 1 : 1;
-  const bool active = wave < it.nrt;
-  const double* Aw = it.A + (int64_t)wave * it.a_rt + lane;
-  const int brow = lane >> 4;
-  const int bcol = lane & 15;
-  const int nst = it.nks / KC;
-
-  for (int s0 = 0; s0 < it.ni; s0 += ns_max) {
-    const int ns = min(ns_max, it.ni - s0);
-    const int ww = (ns - 1) * it.cs + NT;
-    const int wwp = ((ww + 31) & ~31) + 16;
-    int64_t wbase = it.col0;
-    if (it.ring) {
-      const int64_t tt = it.tdiv > 1 ? t / it.tdiv : t;
-      const int64_t tau = tt + it.tshift - (int64_t)(it.ia + s0 + ns - 1);
-      wbase += pmod(tau, it.ring) * it.cs;
-    }
-    const double* xs0 = it.X + wbase;
-    const double* As0 = Aw + (int64_t)s0 * 64;
-    double xr[2 * KROWS * CU];
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int r = 0; r < KROWS; ++r)
-#pragma unroll
-        for (int u = 0; u < CU; ++u) {
-          const int c = tid + WG * u;
-          xr[(h * KROWS + r) * CU + u] = (c < ww) ? BLD(&xs0[h * it.x_im + (int64_t)r * it.ldx + c]) : 0.0;
-        }
-    for (int st = 0; st < nst; ++st) {
-      __syncthreads();
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int r = 0; r < KROWS; ++r)
-#pragma unroll
-          for (int u = 0; u < CU; ++u) {
-            const int c = tid + WG * u;
-            if (c < ww) lds[(h * KROWS + r) * wwp + c] = xr[(h * KROWS + r) * CU + u];
-          }
-      __syncthreads();
-      const double* Ak = As0 + (int64_t)(st * KC) * it.a_ks;
-      if (st + 1 < nst) {
-        const double* xs = xs0 + (int64_t)(4 * KC * (st + 1)) * it.ldx;
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-          for (int r = 0; r < KROWS; ++r)
-#pragma unroll
-            for (int u = 0; u < CU; ++u) {
-              const int c = tid + WG * u;
-              xr[(h * KROWS + r) * CU + u] = (c < ww) ? BLD(&xs[h * it.x_im + (int64_t)r * it.ldx + c]) : 0.0;
-            }
-      }
-      if (active) {
-        // Re/Im fragments of the next slice are in flight while this slice's MFMAs run
-        double ar[KC], ai[KC];
-#pragma unroll
-        for (int kk = 0; kk < KC; ++kk) {
-          ar[kk] = BLD(&Ak[kk * it.a_ks]);
-          ai[kk] = BLD(&Ak[it.a_im + kk * it.a_ks]);
-        }
-        for (int ss = 0; ss < ns; ++ss) {
-          double nr[KC], ni_[KC];
-#pragma unroll
-          for (int kk = 0; kk < KC; ++kk) {
-            nr[kk] = (ss + 1 < ns) ? BLD(&Ak[kk * it.a_ks + (ss + 1) * 64]) : 0.0;
-            ni_[kk] = (ss + 1 < ns) ? BLD(&Ak[it.a_im + kk * it.a_ks + (ss + 1) * 64]) : 0.0;
-          }
-          const int off = (ns - 1 - ss) * it.cs;
-#pragma unroll
-          for (int kk = 0; kk < KC; ++kk) {
-            const double nai = -ai[kk];
-            const double* br = lds + (kk * 4 + brow) * wwp + off + bcol;
-            const double* bi = br + KROWS * wwp;
-#pragma unroll
-            for (int n = 0; n < RN; ++n) {
-              const double vr = br[16 * n], vi = bi[16 * n];
-              accr[n] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[kk], vr, accr[n], 0, 0, 0);
-              accr[n] = __builtin_amdgcn_mfma_f64_16x16x4f64(nai, vi, accr[n], 0, 0, 0);
-              acci[n] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[kk], vr, acci[n], 0, 0, 0);
-              acci[n] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[kk], vi, acci[n], 0, 0, 0);
-            }
-          }
-#pragma unroll
-          for (int kk = 0; kk < KC; ++kk) {
-            ar[kk] = nr[kk];
-            ai[kk] = ni_[kk];
-          }
-        }
-      }
-    }
-  }
-  if (active) {
-#pragma unroll
-    for (int n = 0; n < RN; ++n) {
-      const int col = 16 * n + bcol;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wave * 16 + brow + 4 * r;
-        if (row < it.nrows && col < it.ncols) {
-          GLE_BCHK(&it.out[(int64_t)row * it.ldo + col]);
-          GLE_BCHK(&it.out[it.o_im + (int64_t)row * it.ldo + col]);
-          it.out[(int64_t)row * it.ldo + col] = accr[n][r];
-          it.out[it.o_im + (int64_t)row * it.ldo + col] = acci[n][r];
-        }
-      }
-    }
-  }
-}
-
 void bounds_publish_kernels(const BoundsTab& t) {
 #ifdef GLE_BOUNDS
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_btab), &t, sizeof(t));
 #else
   (void)t;
 #endif
-}
-
-void launch_contract_cplx(int rn, const CItem* items, int nitems, StepArgs ta, hipStream_t s) {
-  if (nitems <= 0) return;
-  GLE_BOUNDS_SYNC();
-  dim3 g(nitems), b(WG);
-  switch (rn) {
-    case 1: contract_cplx_kernel<1><<<g, b, 0, s>>>(items, ta); break;
-    case 2: contract_cplx_kernel<2><<<g, b, 0, s>>>(items, ta); break;
-    case 4: contract_cplx_kernel<4><<<g, b, 0, s>>>(items, ta); break;
-    default: contract_cplx_kernel<8><<<g, b, 0, s>>>(items, ta); break;
-  }
 }
 
 template <int RN>
