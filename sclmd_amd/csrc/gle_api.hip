@@ -206,7 +206,8 @@ struct gle_handle {
   int piece_g = 1;              // steps per piece slot (P0 once planned; GLE_PIECE_STEP=1: every step)
   bool prof_ev = false;         // gle_profile: HIP events around the dominant kernel's launches
   bool bg_serial = false;      // GLE_BG_SERIAL=1: ladder pieces on the main stream (time-sliced, experiment)
-  int piece_slack = 1;         // GLE_PIECE_SLACK: boundaries left between a block's last piece and its use
+  int piece_slack = 1;         // first-level blocks left between a block's last piece and its use (plan)
+  int piece_slack_env = -1;    // GLE_PIECE_SLACK (experiment build) overrides the plan's value
   bool merge_waits = true;     // GLE_MERGE_WAITS=0: one main-stream wait per level
   int wait_early = 0;          // GLE_WAIT_EARLY: steps before a block's first use at which the main stream waits for it
   int64_t ev_seq_counter = 0;
@@ -1788,7 +1789,13 @@ int freeze(gle_handle* h) {
   h->small_baths = h->plan_class == GLE_PLAN_SMALL_BATHS ? true
                   : h->plan_class == GLE_PLAN_LARGE_BATHS ? false
                                                           : ncmax <= 512;
-  h->cg_per_cu = h->small_baths ? 2.0 : 4.0;
+  h->cg_per_cu = h->small_baths ? 1.25 : 4.0;
+  // ladder pieces of a block spread over its whole window (slack 0, small baths: the main stream
+  // waits at the block's first use) or end one first-level block early (slack 1, large baths).  C3,
+  // with far-field chunks of 1.25 workgroups per CU, 3 interleaved rounds on each of two boxes
+  // (r04, `profiles/r04/sched_c3.jsonl`): 512-step window 48.7-48.9 vs 49.5 us/step, 20-step
+  // windows over all phases of the largest level mean 51.1 vs 52.5-52.9, max 54.6 vs 62.6-63.4
+  h->piece_slack = h->piece_slack_env >= 0 ? h->piece_slack_env : (h->small_baths ? 0 : 1);
   const int P0 = h->cfg.block_len > 0 ? h->cfg.block_len : (h->small_baths ? 8 : 4);
   // fused-stage tile waves: 4 when the chain is latency-bound (C3: 53.3 vs 55.3 us/step with the
   // 1-workgroup-per-CU far-field chunks below), 8 for large baths (C5: 447 vs ~410 us at 4)
@@ -2076,11 +2083,11 @@ int freeze(gle_handle* h) {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, h->cfg.device) == hipSuccess) ncu = prop.multiProcessorCount;
         const int nslot = std::max(1, lv.P / h->P0);
-        // workgroups per CU per cgemm chunk (GLE_CG_PER_CU): 2 with small baths (C3, r03 with
-        // the spill-free chain and transform pieces, 3 interleaved rounds: 50.0 vs 51.1 us/step
-        // at 0.5, 20-step windows 52.6 vs 55.0; 1 and 3 in between; r02's 0.5 predates those),
-        // 4 for large baths (C5, with the fpot launch: 354 vs 400 us/step at 2, flat from 4 to 32)
-        double per_cu = h->small_baths ? 2.0 : 4.0;
+        // workgroups per CU per cgemm chunk (GLE_CG_PER_CU): 1.25 with small baths and the
+        // whole-window piece schedule (C3 r04: 1 and 2.5 cost 0.5-2 us/step, 1.5-1.75 within
+        // 0.2; with slack 1, 2 was best in r03: 50.0 vs 51.1 us/step at 0.5), 4 for large baths
+        // (C5, with the fpot launch: 354 vs 400 us/step at 2, flat from 4 to 32)
+        double per_cu = h->small_baths ? 1.25 : 4.0;
         if (const char* e = gle_env("GLE_CG_PER_CU")) per_cu = std::max(0.25, atof(e));
         h->cg_per_cu = per_cu;
         // chunks sized in Gauss products (a two-plane item forms three): the chunk durations the
@@ -2619,7 +2626,7 @@ int gle_create(const gle_config* cfg, gle_handle** out) {
   if (const char* e = gle_env("GLE_FAR_AFRAC")) h->far_afrac = std::max(0.0, std::min(1.0, atof(e)));
   if (const char* e = gle_env("GLE_DBG_SKIP")) h->dbg_skip = atoi(e);
   if (const char* e = gle_env("GLE_BG_GRID")) h->bg_grid = std::max(0, atoi(e));
-  if (const char* e = gle_env("GLE_PIECE_SLACK")) h->piece_slack = std::max(0, atoi(e));
+  if (const char* e = gle_env("GLE_PIECE_SLACK")) h->piece_slack_env = std::max(0, atoi(e));
   if (const char* e = gle_env("GLE_BG_SERIAL")) h->bg_serial = atoi(e) != 0;
   if (const char* e = gle_env("GLE_MERGE_WAITS")) h->merge_waits = atoi(e) != 0;
   if (const char* e = gle_env("GLE_WAIT_EARLY")) h->wait_early = std::max(0, atoi(e));
