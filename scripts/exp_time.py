@@ -133,6 +133,11 @@ def main():
 
     dyn, _, baths, meta = synthetic.junction(args.config, seed=1234, gmem_device=True)
     variants = [v for v in args.variants.split(";")] if args.variants else [""]
+    if len(variants) > 1 and any("GLE_BG_SAMEPRIO" in v for v in variants):
+        # once a handle has created its background streams at the main stream's priority, every
+        # later handle of the process with mixed priorities ran at ~115 instead of 49 us/step (HIP's
+        # hardware-queue reuse, r04 `profiles/r04/sched_priority_mixing_trap_c3.jsonl`)
+        sys.exit("GLE_BG_SAMEPRIO changes the process's hardware-queue mapping: time it in a process of its own")
     base = {k: v for k, v in os.environ.items() if k.startswith("GLE_") or k.startswith("EXP_")}
     for r in range(args.rounds):
         for v in variants:
