@@ -1959,8 +1959,10 @@ int freeze(gle_handle* h) {
     // build): small baths {P0 .. 4 P0}, {.. 32 P0}, rest (C3: 8-32 and 64-256; 3 interleaved rounds on
     // two boxes, `profiles/r04/sched_c3.jsonl`: 20-step phase mean 50.1-50.2 vs 51.0 us/step, 512-step
     // 48.3-48.6 vs 48.6-48.8; 1,8 / 2,8 / 1,4 / 4,8 / 4,16 cost up to 3 us at 512 steps, one stream
-    // for all 8 us), large baths {.. 8 P0}, {.. 64 P0}, rest
-    int g1 = h->small_baths ? 4 : 8, g2 = h->small_baths ? 32 : 64;
+    // for all 8 us), large baths and direct plans {.. 8 P0}, {.. 64 P0}, rest (C2, direct: 30.8 vs
+    // 31.6 us/step at 512 steps with 4,32; `profiles/r04/sched_c2.jsonl`)
+    const bool g_small = h->small_baths && spec_ok;
+    int g1 = g_small ? 4 : 8, g2 = g_small ? 32 : 64;
     if (const char* e = gle_env("GLE_BG_GROUP")) sscanf(e, "%d,%d", &g1, &g2);
     lv.sidx = lv.P <= g1 * P0 ? 0 : (lv.P <= g2 * P0 ? 1 : 2);
     for (int q = 0; q < 2; ++q)
