@@ -769,11 +769,9 @@ void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStre
   }
   // GLE_CG_LDS_PAD (bytes, experiment switch): unused dynamic LDS per workgroup, capping how many
   // far-field workgroups a CU holds so the per-step chain's workgroups find room beside them
-  static int lds_pad = -1;
-  if (lds_pad < 0) {
-    const char* e = gle_env("GLE_CG_LDS_PAD");
-    lds_pad = e ? std::max(0, std::min(96 * 1024, atoi(e))) : 0;
-  }
+  // (re-read per launch like GLE_CG_RING: variants of one process switch it)
+  int lds_pad = 0;
+  if (const char* e = gle_env("GLE_CG_LDS_PAD")) lds_pad = std::max(0, std::min(96 * 1024, atoi(e)));
   const size_t shm = (size_t)lds_pad;
   const bool capped = max_grid > 0 && max_grid < nitems;
   const int xcd = (!capped && g_cg_xcd) ? 1 : 0;
