@@ -240,7 +240,7 @@ struct gle_handle {
   double far_afrac = 0.5;              // share of a step's far items in its first chain launch
   int64_t far_max_items = 0;           // most far items one chain launch can carry
   int plan_class = GLE_PLAN_AUTO;      // gle_set_plan_class: forces small_baths either way
-  double cg_per_cu = 0.5;              // far-field GEMM workgroups per CU per chunk (plan)
+  double cg_per_cu = 1.25;             // far-field GEMM workgroups per CU per chunk (set by the plan)
   int ch_drn = 1;                      // DOF-tile 16-column MFMA tiles
   int P0 = 1;          // first level block; near field = lags [1, 2 P0)
   int near_end = 1;
@@ -2086,7 +2086,7 @@ int freeze(gle_handle* h) {
       if (!rc) rc = upload(h, lv.d_cg, lv.cg.data(), lv.cg.size() * sizeof(CgItem));
       if (rc) return rc;
       {
-        // cgemm chunks of >= 2 workgroups per CU, at most one chunk per first-level boundary
+        // cgemm chunks of ~cg_per_cu workgroups per CU, at most one chunk per first-level boundary
         int ncu = 256;
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, h->cfg.device) == hipSuccess) ncu = prop.multiProcessorCount;
