@@ -190,6 +190,10 @@ def main():
                          "rehearse the multi-rank path, e.g. with --same-device on a one-GPU box)")
     ap.add_argument("--same-device", action="store_true",
                     help="every rank on device 0 (rehearsal of the N > 1 control flow on one GPU)")
+    ap.add_argument("--early-collective", action="store_true",
+                    help="one collective right after the process group is joined, before the stepper exists "
+                         "(RCCL's streams then take their hardware queues first; rehearsal of a host program "
+                         "that communicates before it builds the stepper)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--traffic-json", default="",
@@ -211,7 +215,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    # Under a launcher (WORLD_SIZE set, world 1 included) the rank joins the process group, so a
+    # world-1 `torchrun --nproc-per-node 1` run has RCCL's communicator and streams beside the
+    # stepper's (the multi-GPU path rehearsed on one GPU); a plain `python bench.py` has no group.
+    if "WORLD_SIZE" in os.environ:
         import torch
         import torch.distributed as dist
 
@@ -226,6 +233,8 @@ def main():
         if dist.get_world_size() != args.gpus:
             raise SystemExit("bench.py: process group has %d ranks, --gpus %d" % (dist.get_world_size(), args.gpus))
         world, rank = dist.get_world_size(), dist.get_rank()
+        if args.early_collective:
+            dist.barrier()
 
     from sclmd_amd import md as MD
     from sclmd_amd import synthetic
@@ -457,8 +466,11 @@ def main():
             "algorithmic_flops_per_step": prof["chain_flops"] / args.steps,
             "timing": "device timestamps (per-workgroup stores)",
             "window": "third window of the same %d steps" % args.steps}
-    kap = sums[:, 0] / sums[:, 2] * 243414.0
-    res["heat_current_nW"] = [float(x) for x in kap]
+    # The reduce runs (it is the ensemble's one collective), but its result is not reported: over a
+    # bench window the run is partly filled and not in steady state, so the mean current is neither
+    # md.Run's per-run kappa (md.py:657-664) nor tools.calTC's estimate (tools.py:191-201).
+    res["ensemble_reduce"] = {"doubles": int(sums.size), "backend": (args.dist_backend if dist is not None else "none"),
+                              "world": world}
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         noise = [st.get_noise(i)[0] for i in range(len(baths))]

@@ -89,6 +89,23 @@ def _eigh_stack(spec):
     return f
 
 
+def _digest(*arrays):
+    """Content fingerprint of the arrays a noise spectrum is built from (xxh3 over shape, dtype and
+    bytes): an array edited in place, or replaced by one that reuses a freed array's id(), changes
+    the key, so cached noise factors are never reused for a different spectrum."""
+    import xxhash
+
+    h = xxhash.xxh3_64()
+    for a in arrays:
+        if a is None:
+            h.update(b"none")
+            continue
+        a = np.ascontiguousarray(np.asarray(a))
+        h.update(repr((a.shape, a.dtype.str)).encode())
+        h.update(a.view(np.uint8).reshape(-1).data)
+    return h.hexdigest()
+
+
 class _BathBase:
     kind = None
 
@@ -180,7 +197,7 @@ class ebath(_BathBase):
 
     def _noise_key(self):
         return ("e", self.T, self.bias, self.wmax, self.dt, self.nmd, self.classical, self.zpmotion,
-                id(self.efric), id(self.exim), id(self.exip))
+                _digest(self.efric, self.exim, self.exip))
 
     def _spectrum(self):
         if not self.ebath:
@@ -346,7 +363,7 @@ class phbath(_BathBase):
 
     def _noise_key(self):
         return ("ph", self.T, self.wmax, self.dt, self.nmd, self.classical, self.zpmotion,
-                id(self.gamma), id(self.gwl))
+                _digest(self.gamma, self.gwl))
 
     def _spectrum(self):
         return _noise.phonon_spectrum(self.gamma, self.gwl, self.T, self.wmax, self.dt, self.nmd,

@@ -34,17 +34,23 @@ def ReadNetCDFVar(file, var):
 
 
 def read_history(file, var, ml):
-    """phis / qhis of an MD{j}.nc file as (ml, nph) or (ntraj, ml, nph): the ('mem', ...) layout, or
-    the record layout md.dump uses for ensembles whose history exceeds a classic-format variable
-    (rows [0, ml) of ('nnmd', 'traj', 'nph'))."""
+    """phis / qhis of an MD{j}.nc file as (ml, nph) or (ntraj, ml, nph): the ('mem', ...) layout; the
+    trajectory groups md.dump writes for ensembles whose history exceeds a classic-format variable
+    (var_g0, var_g1, ... over ('trajg{k}', 'mem', 'nph'), joined in order); or the record layout of
+    round-4 files (rows [0, ml) of ('nnmd', 'traj', 'nph'))."""
     with netcdf_file(file, "r", mmap=False) as f:
+        if var not in f.variables and (var + "_g0") in f.variables:
+            parts, k = [], 0
+            while (var + "_g%d" % k) in f.variables:
+                parts.append(np.array(f.variables[var + "_g%d" % k].data, dtype=np.float64))
+                k += 1
+            return np.concatenate(parts, axis=0)
         v = f.variables[var]
         dims = tuple(v.dimensions)
-        a = np.array(v.data, dtype=np.float64)
-    if dims and dims[0] == "nnmd":
-        a = a[:ml]
-        return np.transpose(a, (1, 0, 2)) if a.ndim == 3 else a
-    return a
+        if dims and dims[0] == "nnmd":
+            a = np.array(v.data[:ml], dtype=np.float64)
+            return np.transpose(a, (1, 0, 2)) if a.ndim == 3 else a
+        return np.array(v.data, dtype=np.float64)
 
 
 def var_dims(file, var):
@@ -69,3 +75,15 @@ def commit(f, tmp, path):
     """Close and atomically move into place (a crash never leaves a half-written checkpoint)."""
     f.close()
     os.replace(tmp, path)
+
+
+def abandon(f, tmp):
+    """A write that failed: close what can be closed and remove the partial file."""
+    try:
+        f.close()
+    except Exception:
+        pass
+    try:
+        os.remove(tmp)
+    except OSError:
+        pass

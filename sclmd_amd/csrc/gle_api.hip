@@ -2652,8 +2652,22 @@ int gle_create(const gle_config* cfg, gle_handle** out) {
     int split = 0;
     if (const char* r = gle_env("GLE_CU_SPLIT")) split = std::max(0, atoi(r));
     const char* split_main = gle_env("GLE_CU_SPLIT_MAIN");
+    // GLE_QUEUE_MODE (experiment): 1 background streams on full-CU-mask streams (dedicated hardware
+    // queues outside the per-priority pools), 2 the main stream too
+    int qmode = 0;
+    if (const char* r = gle_env("GLE_QUEUE_MODE")) qmode = atoi(r);
     std::vector<uint32_t> cumask, mainmask;
-    if (reserve > 0 || split > 0) {
+    if (qmode > 0 && reserve == 0 && split == 0) {
+      hipDeviceProp_t prop;
+      hipGetDeviceProperties(&prop, cfg->device);
+      const int ncu = prop.multiProcessorCount;
+      cumask.assign((ncu + 31) / 32, 0u);
+      for (int c = 0; c < ncu; ++c) cumask[c / 32] |= 1u << (c % 32);
+      mainmask = cumask;
+      if (qmode > 1) split = -1;  // main on the full mask (below)
+      reserve = 1;                // background on the full mask (below)
+    }
+    if (qmode == 0 && (reserve > 0 || split > 0)) {
       hipDeviceProp_t prop;
       hipGetDeviceProperties(&prop, cfg->device);
       const int ncu = prop.multiProcessorCount;
@@ -2669,11 +2683,11 @@ int gle_create(const gle_config* cfg, gle_handle** out) {
         for (int c = std::min(reserve, ncu - 8); c < ncu; ++c) cumask[c / 32] |= 1u << (c % 32);
       }
     }
-    if (split > 0 && !(split_main && atoi(split_main) == 0))
+    if ((split > 0 && !(split_main && atoi(split_main) == 0)) || split < 0)
       e = hipExtStreamCreateWithCUMask(&h->stream, (uint32_t)mainmask.size(), mainmask.data());
     else
       e = hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, hi);
-    reserve = reserve > 0 || split > 0;
+    reserve = reserve > 0 || split != 0;
     for (int i = 0; i < gle_handle::NBG && e == hipSuccess; ++i) {
       if (reserve > 0)
         e = hipExtStreamCreateWithCUMask(&h->bg[i], (uint32_t)cumask.size(), cumask.data());

@@ -710,12 +710,21 @@ class md:
         self._reset_his = False
 
     def _wrote_current(self, fn, ipie=None):
-        """fn is the file this process wrote last, unchanged since, at the current t (and piece)."""
+        """fn is the file this process wrote last, unchanged since, at the current t (and piece).  A
+        file still being written by the background dump counts as written (its snapshot is the
+        device state at that t; a write error surfaces at the next join)."""
+        pend = getattr(self, "_dump_pending", None)
+        if pend is not None and pend[0] == fn:
+            return int(self.t) == pend[1] and (ipie is None or ipie == pend[2])
         ld = getattr(self, "_last_dump", None)
         if ld is None or ld[0] != fn or not os.path.isfile(fn):
             return False
         st_ = os.stat(fn)
         return (st_.st_mtime_ns, st_.st_size) == ld[1:3] and int(self.t) == ld[3] and (ipie is None or ipie == ld[4])
+
+    # MD{j}.nc is written on a background thread from a host snapshot of the state (md.Run goes on
+    # stepping the next piece / run meanwhile); False writes it before dump returns
+    async_dump = True
 
     def dump(self, ipie, id):
         """Write MD{id}.nc (md.py:684-764): energy, p, q, t, ipie, phis, qhis, with SaveAll the noise
@@ -723,43 +732,73 @@ class md:
         ntraj > 1 a trajectory dimension is added.  Deviations: NetCDF classic format (netCDF4 is not
         installed; see sclmd_amd.checkpoint), where only the first dimension may be the unlimited
         'nnmd', so poweratomlist is stored as ('nnmd', 'atomlist', 'two') (transposed back on
-        resume)."""
-        from . import checkpoint as C
+        resume); ensemble histories above a classic-format variable's size are split into
+        trajectory groups (phis_g{k} / qhis_g{k}, checkpoint.read_history joins them).
 
+        The device state is copied to host memory here (the file holds exactly the state at this
+        call); with async_dump the file itself is written on a background thread, joined before
+        the next dump, before a checkpoint file is read or removed, at the end of Run and in
+        close() -- a write error is raised there."""
+        self._join_dump()
+        snap = self._dump_snapshot(ipie, id)
+        if not self.async_dump:
+            self._write_snapshot(snap)
+            return
+        import threading
+
+        box = {"snap": snap}
+        th = threading.Thread(target=self._write_snapshot_bg, args=(box,), name="sclmd-dump", daemon=True)
+        self._dump_pending = (snap["fn"], int(self.t), ipie, th, box)
+        th.start()
+
+    def _write_snapshot_bg(self, box):
+        try:
+            self._write_snapshot(box["snap"])
+        except BaseException as e:  # re-raised by _join_dump on the caller's thread
+            box["error"] = e
+        finally:
+            box.pop("snap", None)   # the host copy is freed as soon as the file is written
+
+    def _join_dump(self):
+        """Wait for the background MD{j}.nc write, if any, and raise its error."""
+        pend = getattr(self, "_dump_pending", None)
+        if pend is None:
+            return
+        self._dump_pending = None
+        pend[3].join()
+        if "error" in pend[4]:
+            raise RuntimeError("md.dump: writing %s failed" % pend[0]) from pend[4]["error"]
+
+    def _dump_snapshot(self, ipie, id):
+        """Host copy of everything MD{id}.nc holds: dimensions and (name, array, dims) variables."""
         multi = self.ntraj > 1
         tr = ("traj",) if multi else ()
-        f, tmp = C.open_for_write(self._ncname(id))
-        f.createDimension("nnmd", None)  # the record dimension (the classic format wants it first)
-        f.createDimension("nph", self.nph)
-        f.createDimension("one", 1)
-        f.createDimension("two", 2)
-        f.createDimension("mem", self.ml)
-        f.createDimension("nmd", self.nmd)
+        dims = [("nnmd", None), ("nph", self.nph), ("one", 1), ("two", 2), ("mem", self.ml), ("nmd", self.nmd)]
         if multi:
-            f.createDimension("traj", self.ntraj)
+            dims.append(("traj", self.ntraj))
         if self.atomlist is not None:
-            f.createDimension("atomlist", len(self.atomlist))
+            dims.append(("atomlist", len(self.atomlist)))
         for i, b in enumerate(self.baths):
-            f.createDimension("n" + str(i), b.nc)
+            dims.append(("n" + str(i), b.nc))
+        var = []
 
         def series(name, a):  # (nmd, X) or (ntraj, nmd, X) -> record dimension first
             a = np.asarray(a)
             if multi:
-                C.Write2NetCDFFile(f, np.transpose(a, (1, 0, 2)), name, ("nnmd", "traj", "nph"), units="")
+                var.append((name, np.transpose(a, (1, 0, 2)), ("nnmd", "traj", "nph")))
             else:
-                C.Write2NetCDFFile(f, a, name, ("nnmd", "nph"), units="")
+                var.append((name, a, ("nnmd", "nph")))
 
         if self.saveall:
             for i, b in enumerate(self.baths):
-                nz = np.asarray(b.noise)
+                nz = np.array(b.noise)
                 if multi and nz.ndim == 2:  # one host-injected realisation shared by every trajectory
                     nz = np.broadcast_to(nz, (self.ntraj,) + nz.shape)
                 if multi:  # (ntraj, nmd, nc) -> (nmd, ntraj, nc): the record dimension comes first
-                    f.createDimension("traj" + str(i), nz.shape[0])
-                    C.Write2NetCDFFile(f, np.transpose(nz, (1, 0, 2)), "noise" + str(i),
-                                       ("nnmd", "traj" + str(i), "n" + str(i)), units="")
+                    dims.append(("traj" + str(i), nz.shape[0]))
+                    var.append(("noise" + str(i), np.transpose(nz, (1, 0, 2)), ("nnmd", "traj" + str(i), "n" + str(i))))
                 else:
-                    C.Write2NetCDFFile(f, nz, "noise" + str(i), ("nnmd", "n" + str(i)), units="")
+                    var.append(("noise" + str(i), nz, ("nnmd", "n" + str(i))))
                 fh = self.fhis_of(i)
                 if fh is not None:
                     series("fhis" + str(i), fh)
@@ -768,32 +807,52 @@ class md:
             if self.saveq:
                 series("qs", self.qs)
         if self.savep:
-            C.Write2NetCDFFile(f, self.power, "power", ("nnmd", "two"), units="")
+            var.append(("power", np.array(self.power), ("nnmd", "two")))
             if self.atomlist is not None:
-                C.Write2NetCDFFile(f, np.transpose(self.poweratomlist, (1, 0, 2)), "poweratomlist",
-                                   ("nnmd", "atomlist", "two"), units="")
-        e = np.asarray(self.etot)
-        C.Write2NetCDFFile(f, e.T if multi else e, "energy", ("nnmd",) + tr, units="")
-        C.Write2NetCDFFile(f, self.p, "p", tr + ("nph",), units="")
-        C.Write2NetCDFFile(f, self.q, "q", tr + ("nph",), units="")
-        C.Write2NetCDFFile(f, [self.t], "t", ("one",), units="")
-        C.Write2NetCDFFile(f, [ipie], "ipie", ("one",), units="")
+                var.append(("poweratomlist", np.transpose(np.array(self.poweratomlist), (1, 0, 2)),
+                            ("nnmd", "atomlist", "two")))
+        e = np.array(self.etot)
+        var.append(("energy", e.T if multi else e, ("nnmd",) + tr))
+        var.append(("p", np.array(self.p), tr + ("nph",)))
+        var.append(("q", np.array(self.q), tr + ("nph",)))
+        var.append(("t", np.array([self.t]), ("one",)))
+        var.append(("ipie", np.array([ipie]), ("one",)))
         phis, qhis = np.asarray(self.phis), np.asarray(self.qhis)
-        if multi and self.ml <= self.nmd and phis.nbytes >= self.nc_var_limit:
-            # a classic-format variable holds < 2 GiB (C5: 32 x 4096 x 3000 doubles = 3.1 GB): large
-            # ensembles store the histories along the record dimension, rows [0, ml) of ('nnmd',
-            # 'traj', 'nph') -- read back by checkpoint.read_history
-            C.Write2NetCDFFile(f, np.transpose(phis, (1, 0, 2)), "phis", ("nnmd",) + tr + ("nph",), units="")
-            C.Write2NetCDFFile(f, np.transpose(qhis, (1, 0, 2)), "qhis", ("nnmd",) + tr + ("nph",), units="")
+        if multi and phis.nbytes >= self.nc_var_limit:
+            # a classic-format variable holds < 2 GiB (C5: 32 x 4096 x 3000 doubles = 3.1 GB): the
+            # ensemble's histories are split into fixed-size variables of whole trajectories,
+            # phis_g{k} / qhis_g{k} over ('trajg{k}', 'mem', 'nph') -- exactly ml rows each, one
+            # contiguous write per variable (checkpoint.read_history joins the groups)
+            per = max(1, int(self.nc_var_limit // max(phis[0].nbytes, 1)))
+            for k, a in enumerate(range(0, self.ntraj, per)):
+                b_ = min(self.ntraj, a + per)
+                dims.append(("trajg" + str(k), b_ - a))
+                var.append(("phis_g" + str(k), phis[a:b_], ("trajg" + str(k), "mem", "nph")))
+                var.append(("qhis_g" + str(k), qhis[a:b_], ("trajg" + str(k), "mem", "nph")))
         else:
-            C.Write2NetCDFFile(f, phis, "phis", tr + ("mem", "nph"), units="")
-            C.Write2NetCDFFile(f, qhis, "qhis", tr + ("mem", "nph"), units="")
-        fn = self._ncname(id)
+            var.append(("phis", phis, tr + ("mem", "nph")))
+            var.append(("qhis", qhis, tr + ("mem", "nph")))
+        return {"fn": self._ncname(id), "dims": dims, "vars": var, "t": int(self.t), "ipie": ipie,
+                "savep": bool(self.savep)}
+
+    def _write_snapshot(self, snap):
+        from . import checkpoint as C
+
+        fn = snap["fn"]
+        f, tmp = C.open_for_write(fn)
+        try:
+            for name, size in snap["dims"]:
+                f.createDimension(name, size)
+            for name, a, d in snap["vars"]:
+                C.Write2NetCDFFile(f, a, name, d, units="")
+        except BaseException:
+            C.abandon(f, tmp)
+            raise
         C.commit(f, tmp, fn)
         st_ = os.stat(fn)
         # what this process wrote: the next run's start can skip reading its own file back, and an
         # unchanged second dump of the same piece need not be rewritten
-        self._last_dump = (fn, st_.st_mtime_ns, st_.st_size, int(self.t), ipie, bool(self.savep))
+        self._last_dump = (fn, st_.st_mtime_ns, st_.st_size, snap["t"], snap["ipie"], snap["savep"])
 
     def _read_poweratomlist(self, fn):
         """poweratomlist (natomlist, nmd, 2) from an MD{j}.nc file in either layout: this build's
@@ -821,6 +880,9 @@ class md:
         from .checkpoint import ReadNetCDFVar, read_history
 
         fn, fnm = self._ncname(j), self._ncname(j - 1)
+        pend = getattr(self, "_dump_pending", None)
+        if pend is not None and not (pend[0] == fnm and self._wrote_current(fnm)):
+            self._join_dump()  # a file this logic may read is still being written
         if os.path.isfile(fn):
             self._log("find file: " + fn)
             ipie = int(ReadNetCDFVar(fn, "ipie")[0])
@@ -852,7 +914,7 @@ class md:
                 self.t = int(ReadNetCDFVar(fn, "t")[0])
                 return None
             raise RuntimeError("md.Run: ipie error in %s (ipie = %d)" % (fn, ipie))
-        if os.path.isfile(fnm) and self._wrote_current(fnm):
+        if (os.path.isfile(fnm) or getattr(self, "_dump_pending", None) is not None) and self._wrote_current(fnm):
             # the previous run's file is the one this process just wrote from the device state it
             # still holds (same t, file unchanged): reading p, q and the histories back would only
             # return them (C5: 6 GB of phis / qhis)
@@ -912,7 +974,10 @@ class md:
                         tt = self.t - 1
                         if traj is not None and (tt == 0 or tt % self.nstep == 0):
                             self._write_frame(traj, tt)
-                self.dump(piece, j)
+                # with savep the last piece's file is written once, after the power spectra below
+                # (the reference writes it before and again after them, md.py:596, 654: same file)
+                if piece < self.npie - 1 or not self.savep:
+                    self.dump(piece, j)
             if traj is not None:
                 traj.close()
             if self.cf:
@@ -920,10 +985,7 @@ class md:
                 self.cflist = []
             if self.savep:
                 self._power(j)
-            # "dump again, to make sure power is all right" (md.py:654): without savep nothing the
-            # file holds has changed since the piece's dump, which is then left as written
-            if self.savep or not self._wrote_current(self._ncname(j), piece):
-                self.dump(piece, j)
+                self.dump(piece, j)  # "dump again, to make sure power is all right" (md.py:654)
             cur = self._st.get_current()                      # (nbath, ntraj, nmd)
             sums = self._reduce(self._st.current_sums())      # (nbath, 3) over all ranks
             kap = sums[:, 0] / sums[:, 2] * U.curcof
@@ -937,9 +999,15 @@ class md:
                 if self.saveq:
                     self._avestructure(j)
             # every rank removes its own shard of the previous run's file (md.py:676-679)
-            if self.rmnc and os.path.exists(self._ncname(j - 1)):
-                self._log("Remove " + self._ncname(j - 1))
-                os.remove(self._ncname(j - 1))
+            if self.rmnc:
+                pend = getattr(self, "_dump_pending", None)
+                if pend is not None and pend[0] == self._ncname(j - 1):
+                    self._join_dump()
+                if os.path.exists(self._ncname(j - 1)):
+                    self._log("Remove " + self._ncname(j - 1))
+                    os.remove(self._ncname(j - 1))
+        # the last file is on disk (or its write error raised) when Run returns
+        self._join_dump()
         self._in_run = False
 
     def _write_frame(self, fh, tt):
@@ -1009,10 +1077,23 @@ class md:
                         "   " + str(ave[ip * 3 + 2]) + "\n")
 
     def close(self):
+        """Release the device stepper, the host driver pool and the host noise-factor caches of this
+        md's streamed baths; a background MD{j}.nc write is joined first (its error raised after
+        everything is released)."""
+        err = None
+        try:
+            self._join_dump()
+        except Exception as e:
+            err = e
         if getattr(self, "_pool", None) is not None:
             self._pool.shutdown(wait=True)
             self._pool = None
+        for b in self.baths:  # dense streamed factors (C5: ~11 GB of host memory)
+            if getattr(b, "_stream_cache", None) is not None:
+                b._stream_cache, b._stream_cache_key = None, None
         if self._st is not None:
             self._pull()
             self._st.close()
             self._st = None
+        if err is not None:
+            raise err

@@ -21,10 +21,31 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def dist_barrier(args):
+    if args.dist != "none":
+        import torch.distributed as dist
+
+        dist.barrier()
+
+
+def dist_init(args):
+    """A world-1 torch.distributed nccl (RCCL) group with one collective: torch's stream pools and
+    RCCL's streams exist from then on (bench.py's multi-rank path)."""
+    import torch
+    import torch.distributed as dist
+
+    if not dist.is_initialized():
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % args.port, rank=0, world_size=1)
+    dist.barrier()
+
+
 def measure(args, meta, dyn, baths):
     from sclmd_amd import _native as N
 
     B = args.ntraj
+    if args.dist == "before":
+        dist_init(args)
     st = N.Stepper(meta["nph"], B, meta["nmd"], meta["dt"], 0, int(os.environ.get("EXP_BLOCK_LEN", "0")), "auto",
                    int(os.environ.get("EXP_MAX_BLOCK", "0")))
     try:
@@ -41,15 +62,20 @@ def measure(args, meta, dyn, baths):
             st.set_history(i, None)
             st.set_noise(i, rng.standard_normal((B, meta["nmd"], b.nc)) * 1e-3)
         ptop = max([P for P, _ in st.profile_levels()] + [1])
+        if args.dist == "after":
+            dist_init(args)
         st.run(2 * ptop + 5)
         st.sync()
         if args.profile:
             st.profile(True)
         elif args.chainprof:
             st.profile(True, events=False, chain=True)
+        dist_barrier(args)
+        st.sync()
         t0 = time.perf_counter()
         st.run(args.short)
         st.sync()
+        dist_barrier(args)
         el_short = time.perf_counter() - t0
         # the same window started on a piece-slot boundary (t = 0 mod P0)
         st.run((-(2 * ptop + 5 + args.short)) % st.plan_info()["block_len"])
@@ -60,9 +86,12 @@ def measure(args, meta, dyn, baths):
         el_aligned = time.perf_counter() - t0
         st.run(64)
         st.sync()
+        dist_barrier(args)
+        st.sync()
         t0 = time.perf_counter()
         st.run(args.steps)
         st.sync()
+        dist_barrier(args)
         el = time.perf_counter() - t0
         prof = st.profile_read() if (args.profile or args.chainprof) else None
         if args.profile or args.chainprof:
@@ -71,9 +100,12 @@ def measure(args, meta, dyn, baths):
         for _ in range(args.short_reps):  # bench-like short windows: sync, K steps, sync
             st.run(37)
             st.sync()
+            dist_barrier(args)
+            st.sync()
             t0 = time.perf_counter()
             st.run(args.short)
             st.sync()
+            dist_barrier(args)
             reps.append(round((time.perf_counter() - t0) / args.short * 1e3, 5))
         scan = []
         if args.phase_scan:  # bench.py's scan: consecutive sync-bracketed K-step windows over the period
@@ -127,6 +159,10 @@ def main():
     ap.add_argument("--chainprof", type=int, default=0, help="device stamps of the chain launches on")
     ap.add_argument("--windows", default="", help="comma-separated window lengths: median ms per window")
     ap.add_argument("--window-reps", type=int, default=9)
+    ap.add_argument("--dist", default="none", choices=["none", "before", "after"],
+                    help="world-1 nccl process group joined before / after the stepper is created, windows "
+                         "bracketed by its barrier (bench.py's multi-rank timing)")
+    ap.add_argument("--port", type=int, default=29701)
     ap.add_argument("--phase-scan", type=int, default=0, help="K: K-step windows over the largest period")
     args = ap.parse_args()
     from sclmd_amd import synthetic

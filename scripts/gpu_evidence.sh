@@ -1,0 +1,106 @@
+#!/bin/bash
+# GPU-box evidence runs, one entry point (replaces the per-round gpu_r0*_*.sh launchers).
+#
+#   scripts/gpu_evidence.sh <outdir> <task> [<task> ...]
+#
+# tasks (each step bounded by its own timeout; the script stops at the first failure):
+#   tests      the -m gpu parity suite (one pytest process)
+#   lines      bench lines: C3 driver 20/5, C3 512 steps, C2 1 trajectory
+#   c5         C5 32-trajectory line over one period of the largest level (256 steps)
+#   rccl       C3 20/5 and 512-step lines plain vs world-1 torchrun/nccl (stepper first, and RCCL
+#              first via --early-collective), interleaved twice; 8-rank same-device gloo rehearsal
+#   trace      rocprofv3 kernel trace + stats of the C3 bench, summarised
+#   pmc        FETCH_SIZE / WRITE_SIZE passes over the C3 bench (cgemm and chain traffic)
+#   trace_c5 / pmc_c5   the same for the C5 line
+set -o pipefail
+export TMPDIR=/tmp PYTHONUNBUFFERED=1
+O=gpurun_out/${1:?outdir}
+shift
+mkdir -p $O
+fail() { echo "FAILED: $1"; [ -f "$2" ] && tail -30 "$2"; exit 1; }
+summ() {
+python3 - "$@" <<'PY'
+import json, sys
+for p in sys.argv[1:]:
+    try:
+        d = json.loads([l for l in open(p) if l.startswith("{")][-1])
+    except Exception as e:
+        print(p, "unreadable", e); continue
+    r = d.get("roofline", {}); c = d.get("chain_roofline", {})
+    print("%-28s %10.0f traj-steps/s %6.1f us/step  roof %.3f  chain %.1f us/step frac %.3f  n_gpus %s  phase %s" % (
+        p.split("/")[-1], d["value"], d["ms_per_step"] * 1e3, r.get("frac", 0), c.get("us_per_step", 0), c.get("frac", 0),
+        d["n_gpus"], (d.get("window_phase") or {}).get("scan_ms_per_step")))
+PY
+}
+TR="python3 -m torch.distributed.run --nnodes=1 --nproc-per-node"
+port=29611
+for task in "$@"; do
+case $task in
+tests)
+  timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 \
+    || fail tests $O/gpu_tests.log
+  tail -2 $O/gpu_tests.log ;;
+lines)
+  timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_c3_20x5.json 2> $O/bench_c3_20x5.err || fail b20 $O/bench_c3_20x5.err
+  timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_c3.json 2> $O/bench_c3.err || fail b512 $O/bench_c3.err
+  timeout -k 10 300 python bench.py --config C2 --ntraj 1 --steps 256 --warmup 32 > $O/bench_c2.json 2> $O/bench_c2.err || fail c2 $O/bench_c2.err
+  summ $O/bench_c3_20x5.json $O/bench_c3.json $O/bench_c2.json ;;
+c5)
+  timeout -k 10 600 python bench.py --config C5 --ntraj 32 --steps 256 --warmup 32 --no-cpu-baseline > $O/bench_c5.json 2> $O/bench_c5.err || fail c5 $O/bench_c5.err
+  summ $O/bench_c5.json ;;
+rccl)
+  python3 -c "import torch; print('stream priority range (least, greatest):', torch.cuda.Stream.priority_range())"
+  for r in 1 2; do
+    timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/rccl_plain20_$r.json 2> $O/rccl_plain20_$r.err || fail plain $O/rccl_plain20_$r.err
+    port=$((port+1))
+    timeout -k 10 300 $TR 1 --master-addr 127.0.0.1 --master-port $port bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > $O/rccl_nccl20_$r.json 2> $O/rccl_nccl20_$r.err || fail nccl $O/rccl_nccl20_$r.err
+    port=$((port+1))
+    timeout -k 10 300 $TR 1 --master-addr 127.0.0.1 --master-port $port bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --early-collective > $O/rccl_ncclfirst20_$r.json 2> $O/rccl_ncclfirst20_$r.err || fail ncclfirst $O/rccl_ncclfirst20_$r.err
+    timeout -k 10 300 python bench.py --no-cpu-baseline > $O/rccl_plain512_$r.json 2> $O/rccl_plain512_$r.err || fail plain512 $O/rccl_plain512_$r.err
+    port=$((port+1))
+    timeout -k 10 300 $TR 1 --master-addr 127.0.0.1 --master-port $port bench.py --gpus 1 --no-cpu-baseline > $O/rccl_nccl512_$r.json 2> $O/rccl_nccl512_$r.err || fail nccl512 $O/rccl_nccl512_$r.err
+  done
+  timeout -k 10 400 python bench.py --gpus 8 --same-device --dist-backend gloo --ntraj 8 --noise white --steps 20 --warmup 5 \
+    --no-cpu-baseline > $O/rehearsal_gloo8.json 2> $O/rehearsal_gloo8.err || fail gloo8 $O/rehearsal_gloo8.err
+  summ $O/rccl_*.json $O/rehearsal_gloo8.json ;;
+queues)
+  # hardware-queue placement of the stepper's streams (experiment build, GLE_QUEUE_MODE) against a
+  # world-1 nccl group joined before / after the stepper, one process per (mode, order), 2 rounds
+  : > $O/queues.jsonl
+  for r in 1 2; do for q in ${QMODES:-0 1 2}; do for d in none before after; do
+    port=$((port+1))
+    GLE_QUEUE_MODE=$q SCLMD_AMD_LIB=sclmd_amd/_lib/libhipgle_exp.so timeout -k 10 300 python scripts/exp_time.py \
+      --tag q$q-$d --dist $d --port $port --short-reps 16 >> $O/queues.jsonl 2>> $O/queues.err || fail "queues $q $d" $O/queues.err
+  done; done; done
+  python3 - $O/queues.jsonl <<'PY'
+import json, sys, collections
+import numpy as np
+agg = collections.defaultdict(list)
+for l in open(sys.argv[1]):
+    d = json.loads(l)
+    agg[d["tag"]].append((d["ms_per_step"] * 1e3, np.median(d["short_reps_ms"]) * 1e3))
+for k, v in agg.items():
+    print("%-12s 512-step %s   20-step median %s" % (k, " ".join("%.2f" % x[0] for x in v), " ".join("%.2f" % x[1] for x in v)))
+PY
+  ;;
+trace|trace_c5)
+  if [ $task = trace ]; then A="--no-cpu-baseline"; n=c3; else A="--config C5 --ntraj 32 --steps 256 --warmup 32 --no-cpu-baseline"; n=c5; fi
+  mkdir -p $O/prof_$n
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$n -o run -- \
+    python3 bench.py $A > $O/prof_$n/bench.json 2> $O/prof_$n/bench.err || fail trace $O/prof_$n/bench.err
+  N=$(python3 -c "import json;print(json.load(open('$O/prof_$n/bench.json'))['roofline']['launches'])")
+  python3 scripts/trace_summary.py $O/prof_$n/run_kernel_trace.csv --steps --gaps --last cgemm $N --skip $N > $O/prof_$n/summary.txt
+  tail -8 $O/prof_$n/summary.txt ;;
+pmc|pmc_c5)
+  if [ $task = pmc ]; then A="--no-cpu-baseline"; n=c3; cfg="--config C3 --ntraj 64"; else A="--config C5 --ntraj 32 --steps 256 --warmup 32 --no-cpu-baseline"; n=c5; cfg="--config C5 --ntraj 32"; fi
+  mkdir -p $O/pmc_$n
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -s KILL 600 rocprofv3 --pmc $c --output-format csv -d $O/pmc_$n/$c -o run -- \
+      python3 bench.py $A > $O/pmc_$n/$c.json 2> $O/pmc_$n/$c.err || fail "pmc $c" $O/pmc_$n/$c.err
+  done
+  python3 scripts/pmc_summary.py $O/pmc_$n $O/pmc_$n/traffic_cgemm.json --kernel cgemm_kernel $cfg
+  python3 scripts/pmc_summary.py $O/pmc_$n $O/pmc_$n/traffic_chain.json --kernel chain_kernel $cfg --last 1024 --skip-chain-window 0 ;;
+*)
+  echo "unknown task $task"; exit 2 ;;
+esac
+done

@@ -127,9 +127,44 @@ def test_unfinished_run_needs_saveall(uninterrupted, tmp_path, monkeypatch):
     m.close()
 
 
+def test_background_dump_files_identical_to_synchronous(tmp_path, monkeypatch):
+    """md.Run's MD{j}.nc written on the background thread (async_dump, the default) are byte for
+    byte the files of the synchronous writer, and a run continued from such a file reproduces the
+    uninterrupted run."""
+    from sclmd_amd import md as MD
+
+    outs = {}
+    for mode in (True, False):
+        d = tmp_path / ("async" if mode else "sync")
+        d.mkdir()
+        monkeypatch.chdir(d)
+        monkeypatch.setattr(MD.md, "async_dump", mode)
+        m = _md(0, 2, npie=2, ntraj=2)
+        m.Run()
+        outs[mode] = _final(m)
+        m.close()
+    for fn in ("MD0.nc", "MD1.nc"):
+        a = (tmp_path / "async" / fn).read_bytes()
+        b = (tmp_path / "sync" / fn).read_bytes()
+        assert a == b, fn
+    assert rel(outs[True][0], outs[False][0]) == 0.0 and rel(outs[True][1], outs[False][1]) == 0.0
+    # resume from the background-written file of run 0
+    cont = tmp_path / "cont"
+    cont.mkdir()
+    shutil.copy(tmp_path / "async" / "MD0.nc", cont / "MD0.nc")
+    monkeypatch.chdir(cont)
+    monkeypatch.setattr(MD.md, "async_dump", True)
+    m = _md(1, 2, npie=2, ntraj=2)
+    m.Run()
+    p2, q2, t2, kap2 = _final(m)
+    m.close()
+    p, q, t, kap = outs[True]
+    assert t2 == t and rel(q2, q) < 1e-10 and rel(p2, p) < 1e-10 and rel(kap2[-1], kap[-1]) < 1e-9
+
+
 def test_ensemble_history_record_layout_continues(tmp_path, monkeypatch):
     """An ensemble whose p / q histories exceed a classic-format variable (C5: 32 x 4096 x 3000
-    doubles) stores them along the record dimension; continuing from that file reproduces the
+    doubles) stores them as fixed-size trajectory groups (exactly ml rows each); continuing from that file reproduces the
     uninterrupted run (the limit is lowered here so a small ensemble takes that layout)."""
     from sclmd_amd import md as MD
     from sclmd_amd.checkpoint import read_history, var_dims
@@ -143,7 +178,12 @@ def test_ensemble_history_record_layout_continues(tmp_path, monkeypatch):
     p, q, t, kap = _final(m)
     ph = np.array(m.phis)
     m.close()
-    assert var_dims(str(full / "MD0.nc"), "phis")[0] == "nnmd"
+    # one fixed-size variable per trajectory group (the limit of 0 puts one trajectory in each)
+    from sclmd_amd.checkpoint import has_var
+
+    assert not has_var(str(full / "MD0.nc"), "phis")
+    assert [var_dims(str(full / "MD0.nc"), "phis_g%d" % k) for k in range(3)] == \
+        [("trajg%d" % k, "mem", "nph") for k in range(3)]
     assert rel(read_history(str(full / "MD1.nc"), "phis", 16), ph) == 0.0
     cont = tmp_path / "cont"
     cont.mkdir()

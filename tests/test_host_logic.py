@@ -196,20 +196,69 @@ def test_read_history_both_layouts(tmp_path):
 
     rng = np.random.default_rng(1)
     ph = rng.normal(size=(3, 4, 5))  # (traj, ml, nph)
-    for rec in (False, True):
-        fn = str(tmp_path / ("rec.nc" if rec else "mem.nc"))
+    for lay in ("mem", "rec", "groups"):
+        fn = str(tmp_path / (lay + ".nc"))
         f, tmp = C.open_for_write(fn)
         f.createDimension("nnmd", None)
         f.createDimension("nph", 5)
         f.createDimension("mem", 4)
         f.createDimension("traj", 3)
         C.Write2NetCDFFile(f, rng.normal(size=(9, 5)), "ps", ("nnmd", "nph"), units="")  # 9 records > ml
-        if rec:
+        if lay == "rec":  # round-4 files
             C.Write2NetCDFFile(f, np.transpose(ph, (1, 0, 2)), "phis", ("nnmd", "traj", "nph"), units="")
+        elif lay == "groups":  # md.dump's trajectory groups: 2 + 1 trajectories
+            for k, (a, b) in enumerate(((0, 2), (2, 3))):
+                f.createDimension("trajg%d" % k, b - a)
+                C.Write2NetCDFFile(f, ph[a:b], "phis_g%d" % k, ("trajg%d" % k, "mem", "nph"), units="")
         else:
             C.Write2NetCDFFile(f, ph, "phis", ("traj", "mem", "nph"), units="")
         C.commit(f, tmp, fn)
-        assert np.array_equal(C.read_history(fn, "phis", 4), ph), rec
+        assert np.array_equal(C.read_history(fn, "phis", 4), ph), lay
+
+
+def _cpu_md():
+    from sclmd_amd import md as MD
+    from sclmd_amd import synthetic
+
+    dyn, axyz, baths, meta = synthetic.junction("C3", seed=5, natom=4, ml=4, nmd=8, nw=20)
+    return MD.md(meta["dt"], meta["nmd"], meta["T"], axyz=axyz, dyn=dyn, verbose=False, ntraj=2)
+
+
+def test_background_dump_writes_and_raises_on_the_callers_thread(tmp_path, monkeypatch):
+    """md.dump with async_dump: the snapshot is taken on the caller's thread and written by a
+    background thread; the next join (next dump, Run end, close) sees the file, and a failed write
+    leaves no partial file and raises there."""
+    m = _cpu_md()
+    monkeypatch.chdir(tmp_path)
+    from sclmd_amd import checkpoint as C
+
+    good = {"fn": "MD0.nc", "dims": [("nnmd", None), ("nph", 3)], "t": 5, "ipie": 0, "savep": False,
+            "vars": [("ps", np.arange(12.0).reshape(4, 3), ("nnmd", "nph")), ("t", np.array([5.0]), ("nph",))]}
+    monkeypatch.setattr(m, "_dump_snapshot", lambda ipie, id: good)
+    m.dump(0, 0)
+    m._join_dump()
+    assert np.array_equal(C.ReadNetCDFVar("MD0.nc", "ps"), np.arange(12.0).reshape(4, 3))
+    bad = dict(good, fn="MD1.nc", vars=[("ps", np.zeros((2, 7)), ("nph", "nnmd"))])  # wrong shape
+    monkeypatch.setattr(m, "_dump_snapshot", lambda ipie, id: bad)
+    m.dump(0, 1)
+    with pytest.raises(RuntimeError, match="MD1.nc"):
+        m._join_dump()
+    assert not os.path.exists("MD1.nc") and not os.path.exists("MD1.nc.tmp")
+    m._join_dump()  # the error is raised once
+
+
+def test_noise_key_follows_content():
+    """The noise-factor cache key changes when a spectrum array is edited in place (an id() key
+    would not) and is equal for equal content in a different array."""
+    from sclmd_amd import synthetic
+
+    _, _, baths, _ = synthetic.junction("C3", seed=5, natom=4, ml=4, nmd=8, nw=20)
+    b = baths[0]
+    k0 = b._noise_key()
+    b.gamma = np.array(b.gamma)  # new object, same content
+    assert b._noise_key() == k0
+    b.gamma[3, 0, 0] += 1e-12
+    assert b._noise_key() != k0
 
 
 @pytest.mark.parametrize("kind", ["ph", "e_bias", "e_eq"])
