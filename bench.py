@@ -115,6 +115,21 @@ def cpu_baseline(baths_host, dyn, nph, dt, nmd, budget_s=20.0, nsample=5):
 METRIC = "GLE steps/sec/GPU, 300-atom junction, 1024-step kernel, 64-traj ensemble"
 
 
+def loaded_runtime():
+    """Paths of the HIP / HSA / RCCL runtimes mapped into this process (torch ships its own copies;
+    whichever is loaded first serves every later library that needs the same soname)."""
+    out = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                p = line.split()[-1]
+                if any(k in os.path.basename(p) for k in ("libamdhip64", "libhsa-runtime64", "librccl")):
+                    out.add(p)
+    except OSError:
+        pass
+    return sorted(out)
+
+
 def refuse_experiment_env():
     """The release library reads no environment; refuse anything that could select the experiment
     build or its switches (some of them skip work and give wrong results)."""
@@ -375,6 +390,7 @@ def main():
                    "far_schedule": "fused" if detail["far_fused"] else "background",
                    "plan_class": detail["plan_class"], "parallelism": "ensemble-dp%d" % world},
         "value_per_gpu": value / world,
+        "runtime_libs": loaded_runtime(),
         "setup_s": setup_s,
         "fill_steps": fill,
         "window_t0": int(t_now + fill + args.warmup),

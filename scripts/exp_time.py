@@ -165,6 +165,10 @@ def main():
     ap.add_argument("--port", type=int, default=29701)
     ap.add_argument("--phase-scan", type=int, default=0, help="K: K-step windows over the largest period")
     args = ap.parse_args()
+    if args.dist != "none":
+        # torch first: the library then binds to torch's HIP runtime (one runtime per process, as in
+        # bench.py's multi-rank path; the other order loads two runtimes and torch's cannot start)
+        import torch  # noqa: F401
     from sclmd_amd import synthetic
 
     dyn, _, baths, meta = synthetic.junction(args.config, seed=1234, gmem_device=True)

@@ -63,6 +63,23 @@ rccl)
   timeout -k 10 400 python bench.py --gpus 8 --same-device --dist-backend gloo --ntraj 8 --noise white --steps 20 --warmup 5 \
     --no-cpu-baseline > $O/rehearsal_gloo8.json 2> $O/rehearsal_gloo8.err || fail gloo8 $O/rehearsal_gloo8.err
   summ $O/rccl_*.json $O/rehearsal_gloo8.json ;;
+runtime)
+  # which HIP runtime the stepper runs on: plain (the library's /opt/rocm), torch imported first (torch's
+  # bundled copy), torchrun world-1 over gloo (torch first, no RCCL) and over nccl; interleaved twice
+  for r in 1 2; do for K in 20 512; do
+    W=$([ $K = 20 ] && echo 5 || echo 64)
+    timeout -k 10 300 python bench.py --steps $K --warmup $W --no-cpu-baseline > $O/rt_plain$K\_$r.json 2> $O/rt_plain$K\_$r.err || fail plain $O/rt_plain$K\_$r.err
+    timeout -k 10 300 python -c "import torch, runpy, sys; sys.argv = ['bench.py', '--steps', '$K', '--warmup', '$W', '--no-cpu-baseline']; runpy.run_path('bench.py', run_name='__main__')" > $O/rt_torchfirst$K\_$r.json 2> $O/rt_torchfirst$K\_$r.err || fail torchfirst $O/rt_torchfirst$K\_$r.err
+    port=$((port+1))
+    timeout -k 10 300 $TR 1 --master-addr 127.0.0.1 --master-port $port bench.py --gpus 1 --dist-backend gloo --steps $K --warmup $W --no-cpu-baseline > $O/rt_gloo$K\_$r.json 2> $O/rt_gloo$K\_$r.err || fail gloo $O/rt_gloo$K\_$r.err
+    port=$((port+1))
+    timeout -k 10 300 $TR 1 --master-addr 127.0.0.1 --master-port $port bench.py --gpus 1 --steps $K --warmup $W --no-cpu-baseline > $O/rt_nccl$K\_$r.json 2> $O/rt_nccl$K\_$r.err || fail nccl $O/rt_nccl$K\_$r.err
+  done; done
+  summ $O/rt_*.json
+  python3 -c "
+import json, glob
+for p in sorted(glob.glob('$O/rt_*_1.json')):
+    d = json.loads([l for l in open(p) if l.startswith('{')][-1]); print(p.split('/')[-1], d.get('runtime_libs'))" ;;
 queues)
   # hardware-queue placement of the stepper's streams (experiment build, GLE_QUEUE_MODE) against a
   # world-1 nccl group joined before / after the stepper, one process per (mode, order), 2 rounds
