@@ -13,6 +13,9 @@ comparison), --config C5 --ntraj 32.
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU, RCCL reduce)
 
+Timed window per rank: barrier + device sync, the K steps, device sync (the rank's clock stops
+there), then a closing barrier; value uses the MAX of the ranks' window times.
+
 Prints one JSON line (rank 0).  roofline: the dominant kernel (far-field memory-kernel
 contraction, cgemm_kernel) timed by its own device timestamps (first workgroup start to last
 workgroup end of every launch, s_memrealtime) over a second window of the same K steps, HIP events
@@ -290,6 +293,11 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    # RCCL sets a communicator up lazily: its first collectives cost up to ~2 ms each (profiles/r05,
+    # rt_nccl*), so two untimed ones go before the ladder fill
+    barrier()
+    barrier()
+
     levels = st.profile_levels()
     ptop = max([P for P, _ in levels] + [1])
     t_now = st.get_state()[2]
@@ -328,14 +336,19 @@ def main():
     m.steps(args.warmup)
     st.sync()
     st.profile(True, events=False)  # ladder block counts of the timed window
+    # The window: barrier + device sync, K steps, device sync; each rank's clock stops when its
+    # device has finished the K steps, the closing barrier follows, and el is the MAX over ranks
+    # (below), i.e. the time until the last rank's K steps are done.  The closing barrier itself is
+    # not timed: an RCCL barrier costs 0.1-0.4 ms (profiles/r05/rt_*.json), 10-40 % of a 20-step
+    # window, and it is not work of the K steps.
     barrier()
     st.sync()
     t0 = time.perf_counter()
     m.steps(args.steps)
     t_enq = time.perf_counter() - t0
     st.sync()
-    barrier()
     el = time.perf_counter() - t0
+    barrier()
     log("[bench] rank %d host enqueue %.3f ms of %.3f ms timed" % (rank, t_enq * 1e3, el * 1e3))
     window_levels = st.profile_levels()
     # roofline: HIP events around every launch of the dominant kernel over a second window of the

@@ -234,6 +234,7 @@ struct gle_handle {
   int32_t *d_dyn_rp = nullptr, *d_dyn_col = nullptr;  // dyn as CSR (rows of nph), for the fpot launch
   double* d_dyn_val = nullptr;
   int32_t* d_fpot_vb = nullptr;                       // per DOF: bath * 2^24 + bath-local row, or -1
+  int fpot_ew = 0;                                    // > 0: dyn held as ELL of that width (FpotArgs::ew)
   int ch_nw[3] = {4, 8, 4};            // chain workgroup waves per stage (A, B / fused BC, C)
   bool small_baths = false;            // every bath has nc <= 512 (the chain is latency-bound)
   bool far_fused = false;              // spectral levels ride in the chain launches (fused schedule)
@@ -1216,6 +1217,27 @@ int plan_chain(gle_handle* h) {
     std::vector<int32_t> vb(h->nph, -1);
     for (int j = 0; j < nb; ++j)
       for (int64_t k = 0; k < h->baths[j].nc; ++k) vb[h->baths[j].cids[k]] = (j << 24) | (int32_t)k;
+    // ELL copy when every row has at most FPOT_ELL nonzeros (the chain junctions: <= 3): slot s of
+    // row d at [s][d], padded with (d, 0.0); the kernel skips the zero slots, so the sum is the
+    // CSR row's, in the same order
+    int ew = 0;
+    for (int64_t d = 0; d < h->nph; ++d) ew = std::max(ew, rp[d + 1] - rp[d]);
+    h->fpot_ew = ew <= FPOT_ELL ? (ew <= 4 ? 4 : (ew <= 8 ? 8 : FPOT_ELL)) : 0;
+    if (h->fpot_ew > 0) {
+      const int W = h->fpot_ew;
+      std::vector<int32_t> ecol((size_t)W * h->nph);
+      std::vector<double> eval((size_t)W * h->nph, 0.0);
+      for (int64_t d = 0; d < h->nph; ++d)
+        for (int sl = 0; sl < W; ++sl) {
+          const int r = rp[d] + sl;
+          const bool real = r < rp[d + 1];
+          ecol[(size_t)sl * h->nph + d] = real ? col[r] : (int32_t)d;
+          eval[(size_t)sl * h->nph + d] = real ? val[r] : 0.0;
+        }
+      rp.assign(2, 0);  // unused
+      col.swap(ecol);
+      val.swap(eval);
+    }
     int rc = dalloc_n(h, &h->d_dyn_rp, rp.size());
     if (!rc) rc = upload(h, h->d_dyn_rp, rp.data(), rp.size() * 4);
     if (!rc) rc = dalloc_n(h, &h->d_dyn_col, col.size());
@@ -1448,7 +1470,10 @@ int plan_chain(gle_handle* h) {
       // the potential force at q~ enters through dyn.q~ only on a cache miss (md.py:449-473)
       for (auto& sg : segs)
         if (sg.o == 2 * CH_TB) sg.cond = CH_MISS;
-      for (int u = 0; u < nu; ++u) {  // OYB: M1.p_half + h K0.V - h (K0 Kq).q~
+      // GLE_EXP_BCLIGHT (experiment, timing only: wrong results): the fused stage without its M1.p_half
+      // and h K0.V products (one product per bath row left), to price moving them into stage A
+      const bool bclight = gle_env("GLE_EXP_BCLIGHT") != nullptr;
+      for (int u = 0; u < nu && !bclight; ++u) {  // OYB: M1.p_half + h K0.V - h (K0 Kq).q~
         const Bath& b = h->baths[ubath[u]];
         segs.push_back(Seg{CH_OYB + u, b.d_K0sqd + b.tofs[rt], 64, b.d_Xcur, (int)B, 0, 0, b.nks, 0});
         if (b.ml >= 2 || h->bc_fpot)  // V = n1 - c S1 from the S(t+1) tiles (+ Fpot_b: the fpot launch,
@@ -1553,11 +1578,16 @@ int plan_chain(gle_handle* h) {
         }
         std::vector<Seg> segs{Seg{0, b.d_Kn + ((int64_t)rt * b.nks * b.nn + 1) * 64, b.nn * 64, b.d_NR, (int)B,
                                   b.NRS, 0, b.nks, (int)b.vs}};
-        for (int v = 0; v < 2; ++v) {
-          int rc = fill_tasks(h, T, segs, 1, 0, b.nks, h->chA[v]);
-          if (rc) return rc;
-          h->chA[v].tiles.push_back(T);
-        }
+        // GLE_EXP_AZ=n (experiment): n extra copies of every S(t+1) tile in stage A (each writes the
+        // same values), to price stage-A tiles of one nc x nc product each
+        int ncopy = 1;
+        if (const char* e = gle_env("GLE_EXP_AZ")) ncopy += std::max(0, atoi(e));
+        for (int v = 0; v < 2; ++v)
+          for (int cp = 0; cp < ncopy; ++cp) {
+            int rc = fill_tasks(h, T, segs, 1, 0, b.nks, h->chA[v]);
+            if (rc) return rc;
+            h->chA[v].tiles.push_back(T);
+          }
       }
   }
   // near-field partial tiles (chains B and C, alternating items)
@@ -1940,9 +1970,14 @@ int freeze(gle_handle* h) {
       L.M = (L.lag1 + lv.P - 1) / lv.P - 2;
       L.Rseg = L.M + 4;
       // ring slots addressed modulo Rseg (no mirrored copy); rows padded by 512 doubles for
-      // 64-column items (C3: 49.8 vs 50.2 us/step at 8, 3 interleaved rounds, r04) and by 8 for the
-      // two-plane levels (512 was 73 % of a row at C5's P = 1024 level, ~7 GB per bath)
-      L.ldseg = (int64_t)L.Rseg * B + (lv.nplanes == 2 ? 8 : 512);
+      // 64-column items (C3: 49.8 vs 50.2 us/step at 8, 3 interleaved rounds, r04) and by 32 for the
+      // two-plane levels (512 was 73 % of a row at C5's P = 1024 level, ~7 GB per bath).  The pad
+      // also bounds the staged X loads: a 16- or 32-column item stages NT columns from col0, so for
+      // the last ring slot it reads up to NT - 1 - (B - 1) mod NT doubles past the slot (15 at B = 1);
+      // those columns (>= B) feed output columns that are never stored, and with a pad of >= 31 the
+      // reads stay inside the row (GLE_SEG_PAD below 31 lets them run into the next row or plane,
+      // harmless for the results but outside the row).
+      L.ldseg = (int64_t)L.Rseg * B + (lv.nplanes == 2 ? 32 : 512);
       if (const char* e = gle_env("GLE_SEG_PAD")) L.ldseg = (int64_t)L.Rseg * B + std::max(0, atoi(e));
       L.khat_fstride = (int64_t)lv.nplanes * b.nrt * b.nks * L.M * 64;  // Re, Im | the Gauss planes
       L.seg_fstride = (int64_t)lv.nplanes * b.ncp * L.ldseg;             // Re, Im | Re + Im, Im, Re rows
@@ -2513,6 +2548,7 @@ int step_end_impl(gle_handle* h, const double* fpot_host_T) {
       fa.nph = (int32_t)h->nph;
       fa.B = (int32_t)h->B;
       fa.par = (int32_t)(h->t & 1);
+      fa.ew = h->fpot_ew;
       fa.rp = h->d_dyn_rp;
       fa.col = h->d_dyn_col;
       fa.val = h->d_dyn_val;

@@ -170,7 +170,9 @@ __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, doubl
         const int row = 16 * wave + brow + 4 * q, col = 16 * n + bcol;
         if (row < it.nrows && col < it.ncols) {
           GLE_BCHK(&it.out[(int64_t)row * it.ldo + col]);
-          double* o = &it.out[(int64_t)row * it.ldo + col];
+          // global address space (a flat access would count on lgkmcnt: see Aw)
+          __attribute__((address_space(1))) double* o =
+              (__attribute__((address_space(1))) double*)&it.out[(int64_t)row * it.ldo + col];
           // fused schedule: later k-splits of a product add to the earlier ones' sum (one writer
           // per element per launch, splits in launch order: deterministic)
           *o = it.accum ? *o + acc[n][q] : acc[n][q];
@@ -302,7 +304,8 @@ __device__ __forceinline__ void cgemm_item3(const CgItem& it, int64_t tseg, doub
         for (int q = 0; q < 4; ++q) {
           const int row = 16 * wave + brow + 4 * q, col = 16 * n + bcol;
           if (row < it.nrows && col < it.ncols) {
-            double* o = &it.out[g * it.o_pl + (int64_t)row * it.ldo + col];
+            __attribute__((address_space(1))) double* o =
+                (__attribute__((address_space(1))) double*)&it.out[g * it.o_pl + (int64_t)row * it.ldo + col];
             GLE_BCHK(o);
             *o = it.accum ? *o + acc[g][n][q] : acc[g][n][q];
           }

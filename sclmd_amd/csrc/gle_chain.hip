@@ -251,15 +251,41 @@ __device__ __forceinline__ void run_products(const ChTile* __restrict__ T, int64
   }
 }
 
-// output o at element e of a tile with slots of ss doubles, added in slot order
+// output o at element e of a tile with slots of ss doubles, added in slot order.  An output has at
+// most one slot per wave (fill_tasks*), so the NW slot reads are issued together (clamped to the
+// output's slots, the extra ones masked): one LDS latency per output instead of one per slot.  The
+// sum is 0 + v_0 + v_1 + ... in slot order as before (a masked +0.0 leaves every partial sum
+// unchanged: none of them is -0.0), so the results are the same bits.
+template <int NW>
 __device__ __forceinline__ double out_sum(const ChTile* __restrict__ T, const double* lds, int o, int e, int ss) {
-  double v = 0.0;
-  for (int s = T->ob[o]; s < T->ob[o + 1]; ++s) v += lds[s * ss + e];
-  return v;
+  const int b0 = T->ob[o], n = T->ob[o + 1] - b0;
+  if constexpr (NW > 4) {  // 8-wave tiles (large baths): one slot at a time, within the register budget
+    double r = 0.0;
+    for (int s = 0; s < n; ++s) r += lds[(b0 + s) * ss + e];
+    return r;
+  }
+  double v[NW];
+#pragma unroll
+  for (int s = 0; s < NW; ++s) v[s] = lds[(n > 0 ? b0 + min(s, n - 1) : 0) * ss + e];  // >= 1 slot (launch_nd)
+  double r = 0.0;
+#pragma unroll
+  for (int s = 0; s < NW; ++s) r += s < n ? v[s] : 0.0;
+  return r;
 }
 
 __device__ __forceinline__ unsigned long long* pmax_word(const StepDev* sd, int id, int par, int b) {
   return sd->pmax + ((int64_t)(id * 2 + par)) * sd->B + b;
+}
+
+// atomicMax through the global address space: HIP's atomicMax on a generic pointer is a flat atomic,
+// which also counts on lgkmcnt, so the next LDS-read wait of the wave (the stamps' and the epilogue's
+// descriptor reads) waited for the atomic's round trip through L2
+__device__ __forceinline__ void gmax(unsigned long long* p, unsigned long long v) {
+#ifdef GLE_BOUNDS
+  bcheck(p, 8, __LINE__);
+#endif
+  __hip_atomic_fetch_max((__attribute__((address_space(1))) unsigned long long*)p, v, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // md.potforce's cache rule (sameq, md.py:449-450, 767-779) per trajectory: hit iff the cache is
@@ -380,15 +406,20 @@ __device__ __forceinline__ void dof_A(const ChTile* __restrict__ T, const StepDe
   run_products_rn<NW, DRN>(T, t, lds);
   __syncthreads();
   stamp(sd, 0, 2, ta);
-  // ---- epilogue (md.vv id0, md.py:383-397)
+  // ---- epilogue (md.vv id0, md.py:383-397).  Every output sum is read first (unconditionally, the
+  // masked ones are not used): their LDS reads are in flight together.
   double cur[EPT][CH_TB], ee[EPT], dq[EPT];
 #pragma unroll
   for (int x = 0; x < EPT; ++x) {
-    const int e = threadIdx.x + x * NW * 64;
+    const int e = min((int)threadIdx.x + x * NW * 64, Geo::NE - 1);
+    const double yd = out_sum<NW>(T, lds, 2 * CH_TB, e, Geo::NE);
+    double y[CH_TB];
+#pragma unroll
+    for (int u = 0; u < CH_TB; ++u) y[u] = out_sum<NW>(T, lds, u, e, Geo::NE);
     const bool hit = harm ? (qv[x] != 0 && word_hit(w0[x])) : true;
     double f = fc[x];  // potforce(q_t)
     if (!hit && E[x].in) {
-      f = -1.0 * out_sum(T, lds, 2 * CH_TB, e, Geo::NE);  // f = -1.0*mdot(dyn, q)  (md.py:467)
+      f = -1.0 * yd;  // f = -1.0*mdot(dyn, q)  (md.py:467)
       if (E[x].ok) {
         G(sd->Fc)[E[x].i] = f;
         G(sd->Q0)[E[x].i] = q[x];
@@ -403,8 +434,8 @@ __device__ __forceinline__ void dof_A(const ChTile* __restrict__ T, const StepDe
       cur[x][u] = 0.0;
       if (kk[x][u] >= 0) {
         const ChBath& bd = T->tb[u];
-        double fb = nz[x][u] - bd.c * (out_sum(T, lds, u, e, Geo::NE) + sv[x][u]);
-        if (bd.has_q) fb -= out_sum(T, lds, CH_TB + u, e, Geo::NE);
+        double fb = nz[x][u] - bd.c * (y[u] + sv[x][u]);
+        if (bd.has_q) fb -= out_sum<NW>(T, lds, CH_TB + u, e, Geo::NE);
         f += fb;                 // pf = pf + fbaths[i]  (md.py:432-434)
         cur[x][u] = fb * p[x];   // cur[t] = fbaths[i].p (md.py:397)
         if (double* rf = sd->rec_f[bd.bath])  // fhis[i][t] = fbaths[i] (md.py:398), bath rows
@@ -438,7 +469,7 @@ __device__ __forceinline__ void dof_A(const ChTile* __restrict__ T, const StepDe
     ee[x] = E[x].ok ? p[x] * p[x] : 0.0;
     dq[x] = E[x].ok ? fabs(qt - (hit ? q0[x] : q[x])) : 0.0;
   }
-  // per-trajectory sums over the tile's DOFs (fixed order): one row of the step's partial table
+  // per-trajectory sums over the tile's DOFs (fixed row order): one row of the step's partial table
   // [tile][bath | energy]; baths that miss the tile get zeros
   __syncthreads();
   double* red = lds;
@@ -453,24 +484,33 @@ __device__ __forceinline__ void dof_A(const ChTile* __restrict__ T, const StepDe
     }
   }
   __syncthreads();
-  const int c = threadIdx.x;
-  const int b = T->c0 + c;
-  if (c < Geo::NT && b < B) {
-    double* prow = sd->part + (((int64_t)tn * sd->ndblk + T->tile) * (nb + 1)) * B;
-    bool nan;
-    for (int j = 0; j < nb; ++j) {
-      int uj = -1;
+  auto prow = G(sd->part + (((int64_t)tn * sd->ndblk + T->tile) * (nb + 1)) * B);
+  {
+    // one thread per (quantity, column): the tile baths' currents, the kinetic energy, the cache
+    // distance (one column sum each, side by side instead of one after another in 16 threads)
+    static_assert((CH_TB + 2) * Geo::NT <= NW * 64, "one thread per column reduction");
+    const int qn = threadIdx.x / Geo::NT, c = threadIdx.x % Geo::NT;
+    const int b = T->c0 + c;
+    if (qn < CH_TB + 2 && b < B) {
+      bool nan;
+      const double v = col_red<NW, DRN>(red, qn, c, qn == CH_TB + 1, nan);
+      if (qn < CH_TB) {
+        const int j = T->tb[qn].bath;
+        if (j >= 0) prow[(int64_t)j * B + b] = v;
+      } else if (qn == CH_TB) {
+        prow[(int64_t)nb * B + b] = v;
+      } else if (diff1) {
+        const unsigned long long bits = nan ? 0x7FF8000000000000ull : (unsigned long long)__double_as_longlong(v);
+        gmax(pmax_word(sd, 1, par, b), bits);
+      }
+    }
+  }
+  for (int z = threadIdx.x; z < nb * Geo::NT; z += NW * 64) {  // baths that miss the tile
+    const int j = z / Geo::NT, b = T->c0 + z % Geo::NT;
+    bool meets = false;
 #pragma unroll
-      for (int u = 0; u < CH_TB; ++u)
-        if (T->tb[u].bath == j) uj = u;
-      prow[(int64_t)j * B + b] = uj >= 0 ? col_red<NW, DRN>(red, uj, c, false, nan) : 0.0;
-    }
-    prow[(int64_t)nb * B + b] = col_red<NW, DRN>(red, CH_TB, c, false, nan);
-    if (diff1) {
-      const double m = col_red<NW, DRN>(red, CH_TB + 1, c, true, nan);
-      const unsigned long long bits = nan ? 0x7FF8000000000000ull : (unsigned long long)__double_as_longlong(m);
-      atomicMax(pmax_word(sd, 1, par, b), bits);
-    }
+    for (int u = 0; u < CH_TB; ++u) meets |= T->tb[u].bath == j;
+    if (!meets && b < B) prow[(int64_t)j * B + b] = 0.0;
   }
 }
 
@@ -517,7 +557,7 @@ __device__ __forceinline__ void dof_B(const ChTile* __restrict__ T, const StepDe
     const bool hit1 = harm ? word_hit(w1[x]) : true;
     double f = fc[x];  // potforce(q~)
     if (!hit1 && E[x].in) {
-      f = -1.0 * out_sum(T, lds, 2 * CH_TB, e, Geo::NE);
+      f = -1.0 * out_sum<NW>(T, lds, 2 * CH_TB, e, Geo::NE);
       if (E[x].ok) {  // md.potforce miss at q~: evaluate and cache (md.py:472-473)
         G(sd->Fc)[E[x].i] = f;
         G(sd->Q0)[E[x].i] = qt[x];
@@ -529,9 +569,9 @@ __device__ __forceinline__ void dof_B(const ChTile* __restrict__ T, const StepDe
       if (kk[x][u] >= 0) {
         const ChBath& bd = T->tb[u];
         const int64_t kb = (int64_t)kk[x][u] * B + E[x].b;
-        double fb = nz[x][u] - bd.c * (out_sum(T, lds, u, e, Geo::NE) + sv[x][u]);
+        double fb = nz[x][u] - bd.c * (out_sum<NW>(T, lds, u, e, Geo::NE) + sv[x][u]);
         if (bd.has_q) {
-          const double yq = out_sum(T, lds, CH_TB + u, e, Geo::NE);
+          const double yq = out_sum<NW>(T, lds, CH_TB + u, e, Geo::NE);
           fb -= yq;
           G(bd.Yq)[kb] = yq;  // Kq.q~ is the same in both id1 calls
         }
@@ -603,7 +643,7 @@ __device__ __forceinline__ void dof_C(const ChTile* __restrict__ T, const StepDe
     for (int u = 0; u < CH_TB; ++u) {
       if (kk[x][u] >= 0) {
         const ChBath& bd = T->tb[u];
-        f += nz[x][u] - bd.c * (out_sum(T, lds, u, e, Geo::NE) + sv[x][u]) - yq[x][u];
+        f += nz[x][u] - bd.c * (out_sum<NW>(T, lds, u, e, Geo::NE) + sv[x][u]) - yq[x][u];
       }
     }
     double p2 = ph[x] + dt * f / 2.0;  // md.py:404
@@ -648,7 +688,7 @@ __device__ __forceinline__ void dof_C(const ChTile* __restrict__ T, const StepDe
       bool nan;
       const double m = col_red<NW, DRN>(lds, 0, c, true, nan);
       const unsigned long long bits = nan ? 0x7FF8000000000000ull : (unsigned long long)__double_as_longlong(m);
-      atomicMax(pmax_word(sd, 0, par1, b), bits);
+      gmax(pmax_word(sd, 0, par1, b), bits);
     }
   }
 }
@@ -718,10 +758,18 @@ __device__ __forceinline__ void dof_BC(const ChTile* __restrict__ T, const StepD
   double dq[EPT];
 #pragma unroll
   for (int x = 0; x < EPT; ++x) {
-    const int e = threadIdx.x + x * NW * 64;
+    const int e = min((int)threadIdx.x + x * NW * 64, Geo::NE - 1);
+    // the output sums first, unconditionally (their LDS reads in flight together)
+    const double yd = out_sum<NW>(T, lds, 2 * CH_TB, e, Geo::NE);
+    double yb[CH_TB], ye[CH_TB];
+#pragma unroll
+    for (int u = 0; u < CH_TB; ++u) {
+      yb[u] = out_sum<NW>(T, lds, CH_OYB + u, e, Geo::NE);
+      ye[u] = out_sum<NW>(T, lds, (hit1[x] ? CH_OYE : CH_OYD) + u, e, Geo::NE);
+    }
     double fpot = fc[x];  // potforce(q~)
     if (!hit1[x] && E[x].in) {
-      fpot = -1.0 * out_sum(T, lds, 2 * CH_TB, e, Geo::NE);
+      fpot = -1.0 * yd;
       if (E[x].ok) {  // md.potforce miss at q~: evaluate and cache (md.py:472-473)
         G(sd->Fc)[E[x].i] = fpot;
         G(sd->Q0)[E[x].i] = qt[x];
@@ -733,9 +781,8 @@ __device__ __forceinline__ void dof_BC(const ChTile* __restrict__ T, const StepD
       if (kk[x][u] >= 0) {
         const ChBath& bd = T->tb[u];
         f2 += nz[x][u] - bd.c * sv[x][u];
-        if (bd.has_q) f2 -= out_sum(T, lds, CH_TB + u, e, Geo::NE);
-        const double k0p1 = out_sum(T, lds, CH_OYB + u, e, Geo::NE) +
-                            (hit1[x] ? out_sum(T, lds, CH_OYE + u, e, Geo::NE) : out_sum(T, lds, CH_OYD + u, e, Geo::NE));
+        if (bd.has_q) f2 -= out_sum<NW>(T, lds, CH_TB + u, e, Geo::NE);
+        const double k0p1 = yb[u] + ye[u];
         f2 -= bd.c * k0p1;
       }
     double p2 = ph[x] + dt * f2 / 2.0;  // md.py:404
@@ -778,7 +825,7 @@ __device__ __forceinline__ void dof_BC(const ChTile* __restrict__ T, const StepD
       bool nan;
       const double m = col_red<NW, DRN>(lds, 0, c, true, nan);
       const unsigned long long bits = nan ? 0x7FF8000000000000ull : (unsigned long long)__double_as_longlong(m);
-      atomicMax(pmax_word(sd, 0, par1, b), bits);
+      gmax(pmax_word(sd, 0, par1, b), bits);
     }
   }
 }
@@ -794,7 +841,7 @@ __device__ __forceinline__ void sfin(const ChTile* __restrict__ T, const StepDev
   const ChSfin& sf = T->sf;
   constexpr int NT = 16 * DRN, NE = 16 * NT;  // S(t+1) tiles have the DOF tiles' width
   constexpr int EPT = (NE + NW * 64 - 1) / (NW * 64);
-  double pre[EPT];
+  double pre[EPT], nzv[EPT];
   int64_t kb[EPT];
   bool ok[EPT];
 #pragma unroll
@@ -814,6 +861,8 @@ __device__ __forceinline__ void sfin(const ChTile* __restrict__ T, const StepDev
 #pragma unroll
     for (int l = 0; l < MAXLVL; ++l)
       lv[l] = G(sf.lvl[l])[(ok[x] ? (int64_t)k * sf.lvl_ld[l] + b : 0) + ta.lvl_off[l]];
+    // fused B+C: noise(t+1) of the V row, loaded with the prologue (not after the products)
+    nzv[x] = sf.V ? G(sf.noise)[(ok[x] ? ((int64_t)((t + 1) % sd->nmd) * sf.nc + k) * B + b : 0)] : 0.0;
     double sn = 0.0, lvs = 0.0;
 #pragma unroll
     for (int q = 0; q < CH_NPMAX; ++q) sn += (q < sf.nqn) ? v[q] : 0.0;
@@ -828,13 +877,10 @@ __device__ __forceinline__ void sfin(const ChTile* __restrict__ T, const StepDev
   for (int x = 0; x < EPT; ++x) {
     const int e = threadIdx.x + x * NW * 64;
     if (ok[x]) {
-      const double s1 = out_sum(T, lds, 0, e, NE) + pre[x];
+      const double s1 = out_sum<NW>(T, lds, 0, e, NE) + pre[x];
       G(sf.S)[(int64_t)par1 * sf.vs + kb[x]] = s1;
-      if (sf.V) {  // fused B+C: V = noise(t+1) - c S(t+1), the bath part of F1 that K0 acts on
-        const int t1 = (int)((t + 1) % sd->nmd);
-        const int k = (int)(kb[x] / B), b = (int)(kb[x] - (int64_t)k * B);
-        G(sf.V)[kb[x]] = G(sf.noise)[((int64_t)t1 * sf.nc + k) * B + b] - sf.c * s1;
-      }
+      if (sf.V)  // fused B+C: V = noise(t+1) - c S(t+1), the bath part of F1 that K0 acts on
+        G(sf.V)[kb[x]] = nzv[x] - sf.c * s1;
     }
   }
 }
@@ -849,11 +895,16 @@ __device__ __forceinline__ void raw(const ChTile* __restrict__ T, const StepDev*
   stamp(sd, stage, 2, ta);
   const int NT = 16 * T->rn;
   double* dst = T->dst + ((t + T->par_shift) & 1) * T->par_stride;
-  for (int e = threadIdx.x; e < 16 * NT; e += NW * 64) {
-    double v = 0.0;
-    for (int s = T->ob[0]; s < T->ob[1]; ++s) v += lds[s * 16 * NT + e];
+  // every element's slot reads in flight together (at most 16 x 64 elements per tile)
+  constexpr int EMAX = (16 * 64 + NW * 64 - 1) / (NW * 64);
+  double v[EMAX];
+#pragma unroll
+  for (int x = 0; x < EMAX; ++x) v[x] = out_sum<NW>(T, lds, 0, min((int)threadIdx.x + x * NW * 64, 16 * NT - 1), 16 * NT);
+#pragma unroll
+  for (int x = 0; x < EMAX; ++x) {
+    const int e = threadIdx.x + x * NW * 64;
     const int row = e / NT, col = e - row * NT;
-    if (row < T->nrows && col < T->ncols) G(dst)[(int64_t)row * T->ldd + col] = v;
+    if (e < 16 * NT && row < T->nrows && col < T->ncols) G(dst)[(int64_t)row * T->ldd + col] = v[x];
   }
 }
 
@@ -1009,6 +1060,8 @@ void launch_nd(int drn, size_t lds, const ChTile* tiles, int ntiles, const StepD
   int grid = ntiles;
   for (int r = 0; r < ta.nfar; ++r) grid += ta.far[r].count;
   if (ta.nfar > 0) lds = std::max(lds, CH_FAR_LDS);
+  // at least one 64-column partial slot: the epilogues' masked slot reads stay inside the launch's LDS
+  lds = std::max(lds, (size_t)16 * 64 * sizeof(double));
   if (drn == 2) {
     lds_limit(chain_kernel<STAGE, NW, 2>, lds);
     chain_kernel<STAGE, NW, 2><<<grid, NW * 64, lds, s>>>(tiles, sd, ta, mode);
@@ -1040,40 +1093,60 @@ void launch_chain(int stage, int nw, int drn, size_t lds_bytes, const ChTile* ti
 }
 
 namespace {
+// md.potforce at q~ for every (DOF, trajectory) before the fused velocity stage.  With dyn as ELL
+// (EW > 0 nonzeros per row, slot-major) every load of a thread goes out in two rounds: the cache
+// word, Fc, q~, the bath row and the row's column / value slots first, then the q~ gathers and the
+// V row; CSR (EW = 0) keeps the row-pointer round trip.
+template <int EW>
 __global__ __launch_bounds__(256) void fpot_kernel(FpotArgs a) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= (int64_t)a.nph * a.B) return;
   const int d = (int)(i / a.B), b = (int)(i - (int64_t)d * a.B);
   const unsigned long long w = *G(a.pmax + ((int64_t)(1 * 2 + a.par)) * a.B + b);
+  const double fc = G(a.Fc)[i], qt = G(a.Qt)[i];
+  const int vb = G(a.vb)[d];
+  int cl[EW > 0 ? EW : 1];
+  double vl[EW > 0 ? EW : 1];
+#pragma unroll
+  for (int k = 0; k < EW; ++k) {
+    cl[k] = G(a.col)[(int64_t)k * a.nph + d];
+    vl[k] = G(a.val)[(int64_t)k * a.nph + d];
+  }
+  // the V row (or the noise row of a bath without memory sum), loaded beside the gathers
+  double* V = a.V[0];
+  const double* nz = a.noise[0];
+  int nc = a.nc[0];
+#pragma unroll
+  for (int j = 1; j < MAXBATH; ++j)
+    if ((vb >> 24) == j) {
+      V = a.V[j];
+      nz = a.noise[j];
+      nc = a.nc[j];
+    }
+  const int k = vb & 0xFFFFFF;
+  const int64_t o = vb >= 0 ? (int64_t)k * a.B + b : 0;
+  const double v0 = vb < 0 ? 0.0 : (nz ? G(nz)[((int64_t)a.t1 * nc + k) * a.B + b] : G(V)[o]);
   double f;
   if (word_hit(w)) {  // md.potforce cache hit at q~ (md.py:449-450, 767-779)
-    f = G(a.Fc)[i];
+    f = fc;
   } else {            // miss: f = -1.0*mdot(dyn, q~) and cache it (md.py:467-473)
     double acc = 0.0;
-    const int r0 = G(a.rp)[d], r1 = G(a.rp)[d + 1];
-    for (int r = r0; r < r1; ++r) acc += G(a.val)[r] * G(a.Qt)[(int64_t)G(a.col)[r] * a.B + b];
+    if constexpr (EW > 0) {
+      double x[EW];
+#pragma unroll
+      for (int s = 0; s < EW; ++s) x[s] = G(a.Qt)[(int64_t)cl[s] * a.B + b];
+#pragma unroll
+      for (int s = 0; s < EW; ++s) acc = vl[s] != 0.0 ? fma(vl[s], x[s], acc) : acc;  // padding: val 0.0
+    } else {
+      const int r0 = G(a.rp)[d], r1 = G(a.rp)[d + 1];
+      for (int r = r0; r < r1; ++r) acc += G(a.val)[r] * G(a.Qt)[(int64_t)G(a.col)[r] * a.B + b];
+    }
     f = -1.0 * acc;
     G(a.Fc)[i] = f;
-    G(a.Q0)[i] = G(a.Qt)[i];
+    G(a.Q0)[i] = qt;
   }
-  const int vb = G(a.vb)[d];
-  if (vb >= 0) {
-    double* V = a.V[0];
-    const double* nz = a.noise[0];
-    int nc = a.nc[0];
-#pragma unroll
-    for (int j = 1; j < MAXBATH; ++j)
-      if ((vb >> 24) == j) {
-        V = a.V[j];
-        nz = a.noise[j];
-        nc = a.nc[j];
-      }
-    const int k = vb & 0xFFFFFF;
-    const int64_t o = (int64_t)k * a.B + b;
-    // V = n1 - c S1 (S(t+1) tiles of stage A) or n1 (no memory sum), plus the bath rows' Fpot(q~)
-    const double v0 = nz ? G(nz)[((int64_t)a.t1 * nc + k) * a.B + b] : G(V)[o];
-    G(V)[o] = v0 + f;
-  }
+  // V = n1 - c S1 (S(t+1) tiles of stage A) or n1 (no memory sum), plus the bath rows' Fpot(q~)
+  if (vb >= 0) G(V)[o] = v0 + f;
 }
 }  // namespace
 
@@ -1081,7 +1154,11 @@ void launch_fpot(const FpotArgs& a, hipStream_t s) {
   const int64_t n = (int64_t)a.nph * a.B;
   if (n <= 0) return;
   GLE_BOUNDS_SYNC();
-  fpot_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(a);
+  const unsigned g = (unsigned)((n + 255) / 256);
+  if (a.ew <= 0) fpot_kernel<0><<<g, 256, 0, s>>>(a);
+  else if (a.ew <= 4) fpot_kernel<4><<<g, 256, 0, s>>>(a);
+  else if (a.ew <= 8) fpot_kernel<8><<<g, 256, 0, s>>>(a);
+  else fpot_kernel<FPOT_ELL><<<g, 256, 0, s>>>(a);
 }
 
 void bounds_publish_chain(const BoundsTab& t) {

@@ -327,8 +327,12 @@ void launch_finalize(const StepDev* sd, int B, int nmd, int nbath, hipStream_t s
 // md.potforce at q~ for every DOF and trajectory before the fused velocity stage (bc_fpot): the
 // cache rule per trajectory (pmax word id1 of parity par), on a miss f = -dyn.q~ (CSR rows) with
 // Fc, Q0 updated; f added to the owning bath's V row (vb: bath << 24 | row, -1 outside the baths)
+// dyn is held as ELL when its rows have at most FPOT_ELL nonzeros (ew > 0: col / val [ew][nph],
+// slot-major, padded with (row, 0.0)), as CSR (rp, col, val) otherwise (ew = 0)
+constexpr int FPOT_ELL = 16;
 struct FpotArgs {
   int32_t nph, B, par, t1;  // t1 = (t + 1) mod nmd: noise slot of a bath without memory sum
+  int32_t ew;               // ELL width, 0: CSR
   const int32_t *rp, *col, *vb;
   const double* val;
   const double* Qt;

@@ -12,6 +12,12 @@
 #   trace      rocprofv3 kernel trace + stats of the C3 bench, summarised
 #   pmc        FETCH_SIZE / WRITE_SIZE passes over the C3 bench (cgemm and chain traffic)
 #   trace_c5 / pmc_c5   the same for the C5 line
+#   c5run      md.Run wall time per run at C5 (scripts/c5_run_timing.py: noise, stepping, MD{j}.nc)
+#   negf       GLE ensemble current vs the NEGF Landauer current (tests/test_gpu_negf.py)
+#   ab         experiment libraries x GLE_* variants, interleaved (LIBS, VARIANTS, ROUNDS, EXPARGS,
+#              TIMELINES=1 for per-workgroup chain timelines); build them with make experiments
+#              EXPNAME=.. EXPFLAGS=.. or scripts/build_variant.sh <name> <git-rev>
+#   runtime / queues   the HIP runtime and hardware-queue studies of round 5 (profiles/r05)
 set -o pipefail
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 O=gpurun_out/${1:?outdir}
@@ -45,6 +51,12 @@ lines)
   timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_c3.json 2> $O/bench_c3.err || fail b512 $O/bench_c3.err
   timeout -k 10 300 python bench.py --config C2 --ntraj 1 --steps 256 --warmup 32 > $O/bench_c2.json 2> $O/bench_c2.err || fail c2 $O/bench_c2.err
   summ $O/bench_c3_20x5.json $O/bench_c3.json $O/bench_c2.json ;;
+c5run)
+  timeout -k 10 900 python scripts/c5_run_timing.py --runs ${RUNS:-3} > $O/c5_run_timing.json 2> $O/c5_run_timing.log || fail c5run $O/c5_run_timing.log
+  cat $O/c5_run_timing.json ;;
+negf)
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_negf.py -x -q -m gpu --timeout 200 --timeout-method thread > $O/negf.log 2>&1 || fail negf $O/negf.log
+  tail -3 $O/negf.log ;;
 c5)
   timeout -k 10 600 python bench.py --config C5 --ntraj 32 --steps 256 --warmup 32 --no-cpu-baseline > $O/bench_c5.json 2> $O/bench_c5.err || fail c5 $O/bench_c5.err
   summ $O/bench_c5.json ;;
@@ -80,6 +92,31 @@ runtime)
 import json, glob
 for p in sorted(glob.glob('$O/rt_*_1.json')):
     d = json.loads([l for l in open(p) if l.startswith('{')][-1]); print(p.split('/')[-1], d.get('runtime_libs'))" ;;
+ab)
+  # experiment libraries (LIBS, e.g. "base cur": scripts/build_variant.sh / make experiments) x
+  # GLE_* VARIANTS, one process per (lib, variant), ROUNDS interleaved; then chain timelines per lib
+  : > $O/ab.jsonl
+  for r in $(seq 1 ${ROUNDS:-3}); do for lib in ${LIBS:?}; do
+    SCLMD_AMD_LIB=sclmd_amd/_lib/libhipgle_$lib.so timeout -k 10 300 python scripts/exp_time.py --tag $lib \
+      --variants "${VARIANTS:-}" --short-reps 16 ${EXPARGS:-} >> $O/ab.jsonl 2>> $O/ab.err || fail "ab $lib" $O/ab.err
+  done; done
+  python3 - $O/ab.jsonl <<'PY'
+import json, sys, collections
+import numpy as np
+agg = collections.defaultdict(list)
+for l in open(sys.argv[1]):
+    if l.startswith("{"):
+        d = json.loads(l)
+        agg[(d["tag"], d["variant"])].append((d["ms_per_step"] * 1e3, np.median(d["short_reps_ms"]) * 1e3))
+for k, v in agg.items():
+    print("%-8s %-36s 512-step %s | 20-step median %s" % (k[0], k[1] or "(default)", " ".join("%.2f" % x[0] for x in v),
+                                                      " ".join("%.2f" % x[1] for x in v)))
+PY
+  if [ -n "$TIMELINES" ]; then for lib in $LIBS; do for v in "GLE_DBG_NO_LADDER=1" "GLE_PIECE_SLACK=0"; do
+    env $v GLE_CHAIN_DBG=700 SCLMD_AMD_LIB=sclmd_amd/_lib/libhipgle_$lib.so timeout -k 10 200 python scripts/exp_time.py \
+      --tag "$lib $v" --steps 256 > $O/tl.$lib.$v.json 2> $O/tl.$lib.$v.err || fail "tl $lib" $O/tl.$lib.$v.err
+    echo "== $lib $v"; grep "chain dbg" $O/tl.$lib.$v.err
+  done; done; fi ;;
 queues)
   # hardware-queue placement of the stepper's streams (experiment build, GLE_QUEUE_MODE) against a
   # world-1 nccl group joined before / after the stepper, one process per (mode, order), 2 rounds
@@ -94,6 +131,8 @@ import json, sys, collections
 import numpy as np
 agg = collections.defaultdict(list)
 for l in open(sys.argv[1]):
+    if not l.startswith("{"):
+        continue  # RCCL's version banner
     d = json.loads(l)
     agg[d["tag"]].append((d["ms_per_step"] * 1e3, np.median(d["short_reps_ms"]) * 1e3))
 for k, v in agg.items():

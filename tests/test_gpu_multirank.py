@@ -87,3 +87,45 @@ def test_bench_gpus2_spawns_two_ranks(tmp_path):
     assert res["n_gpus"] == 2 and res["config"]["ntraj_total"] == 128, res
     assert res["config"]["parallelism"] == "ensemble-dp2"
     assert res["value"] > 0 and np.isfinite(res["value"])
+
+
+def _bench_line(r):
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_world1_nccl_under_torchrun(tmp_path):
+    """The driver's multi-GPU launch shape on one GPU: `torchrun --nproc-per-node 1 bench.py --gpus 1`
+    joins a world-1 nccl (RCCL) process group, so RCCL's communicator and torch's stream pools exist
+    beside the stepper's streams, and the window is bracketed by RCCL barriers.  The line must report
+    the group and stay at the plain run's rate: the bound (70 us/step at C3, 20 steps) sits between
+    the plain line (~50 us) and the hardware-queue sharing trap of profiles/r04 (~115 us)."""
+    env = _env(HSA_ENABLE_IPC_MODE_LEGACY="0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "1", "--steps", "20", "--warmup", "5", "--no-cpu-baseline", "--noise", "white"]
+    res = _bench_line(subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=400, cwd=str(tmp_path)))
+    assert res["n_gpus"] == 1 and res["config"]["ntraj_total"] == 64
+    assert res["ensemble_reduce"]["backend"] == "nccl" and res["ensemble_reduce"]["world"] == 1
+    assert res["ms_per_step"] < 0.070, res["ms_per_step"]
+
+
+def test_bench_eight_ranks_same_device_gloo(tmp_path):
+    """The 8-GPU ensemble's control flow rehearsed on one GPU: 8 ranks of 8 trajectories on device 0
+    over gloo report the live group (n_gpus 8, 64 trajectories in all) and one line."""
+    env = _env()
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    env["OMP_NUM_THREADS"] = "2"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--same-device",
+                        "--dist-backend", "gloo", "--ntraj", "8", "--noise", "white", "--steps", "8", "--warmup", "2",
+                        "--fill", "16", "--no-cpu-baseline"], env=env, capture_output=True, text=True, timeout=600,
+                       cwd=str(tmp_path))
+    res = _bench_line(r)
+    assert res["n_gpus"] == 8 and res["config"]["ntraj_total"] == 64, res
+    assert res["config"]["parallelism"] == "ensemble-dp8"
+    assert res["value"] > 0 and np.isfinite(res["value"])
