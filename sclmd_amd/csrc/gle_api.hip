@@ -211,6 +211,7 @@ struct gle_handle {
   bool merge_waits = true;     // GLE_MERGE_WAITS=0: one main-stream wait per level
   int wait_early = 0;          // GLE_WAIT_EARLY: steps before a block's first use at which the main stream waits for it
   int64_t ev_seq_counter = 0;
+  bool dbg_no_chain = false;   // GLE_DBG_NO_CHAIN (experiment): no chain launches
   int dbg_skip = 0;            // GLE_DBG_SKIP bits (timing experiments only, wrong results):
                                // 1 cgemm, 2 seg_fft, 4 far_ifft, 8 direct level ops
   int dbg_ntile = 0;
@@ -792,7 +793,10 @@ void run_chain(gle_handle* h, int stage, Chain& c, const StepArgs& ta, int mode,
     h->ctst_n.push_back((int)(c.tiles.size() + nfar));
     h->prof_ch_flops += c.flops + far_flops;
   }
-  launch_chain(stage, c.nw, h->ch_drn, c.lds, c.d, (int)c.tiles.size(), h->d_sd, tc, mode, h->stream);
+  // GLE_DBG_NO_CHAIN (experiment, timing only: wrong results): the ladder without the per-step chain,
+  // to time the far-field launches isolated against the same launches beside the chain
+  if (!h->dbg_no_chain)
+    launch_chain(stage, c.nw, h->ch_drn, c.lds, c.d, (int)c.tiles.size(), h->d_sd, tc, mode, h->stream);
   if (e1) {
     hipEventRecord(e1, h->stream);
     h->prof_n += 1;
@@ -2669,6 +2673,7 @@ int gle_create(const gle_config* cfg, gle_handle** out) {
   h->dbg_no_ladder = gle_env("GLE_DBG_NO_LADDER") != nullptr;
   if (const char* e = gle_env("GLE_FAR_AFRAC")) h->far_afrac = std::max(0.0, std::min(1.0, atof(e)));
   if (const char* e = gle_env("GLE_DBG_SKIP")) h->dbg_skip = atoi(e);
+  h->dbg_no_chain = gle_env("GLE_DBG_NO_CHAIN") != nullptr;
   if (const char* e = gle_env("GLE_BG_GRID")) h->bg_grid = std::max(0, atoi(e));
   if (const char* e = gle_env("GLE_PIECE_SLACK")) h->piece_slack_env = std::max(0, atoi(e));
   if (const char* e = gle_env("GLE_BG_SERIAL")) h->bg_serial = atoi(e) != 0;

@@ -748,6 +748,9 @@ void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStre
                   unsigned long long* ts) {
   if (nitems <= 0) return;
   GLE_BOUNDS_SYNC();
+#ifdef GLE_EXPERIMENTS
+  g_cg_xcd = -1;  // re-read per launch: variants of one process (scripts/exp_time.py --variants) switch them
+#endif
   if (g_cg_xcd < 0) {
     const char* e = gle_env("GLE_CG_XCD");
     g_cg_xcd = (e && atoi(e) == 0) ? 0 : 1;

@@ -107,10 +107,13 @@ agg = collections.defaultdict(list)
 for l in open(sys.argv[1]):
     if l.startswith("{"):
         d = json.loads(l)
-        agg[(d["tag"], d["variant"])].append((d["ms_per_step"] * 1e3, np.median(d["short_reps_ms"]) * 1e3))
+        agg[(d["tag"], d["variant"])].append((d["ms_per_step"] * 1e3, np.median(d["short_reps_ms"]) * 1e3,
+                                              d.get("cgemm_tflops", 0.0), d.get("cgemm_avg_us", 0.0)))
 for k, v in agg.items():
-    print("%-8s %-36s 512-step %s | 20-step median %s" % (k[0], k[1] or "(default)", " ".join("%.2f" % x[0] for x in v),
-                                                      " ".join("%.2f" % x[1] for x in v)))
+    print("%-8s %-36s 512-step %s | 20-step median %s%s" % (k[0], k[1] or "(default)", " ".join("%.2f" % x[0] for x in v),
+          " ".join("%.2f" % x[1] for x in v),
+          (" | cgemm TF/s %s avg us %s" % (" ".join("%.1f" % x[2] for x in v), " ".join("%.1f" % x[3] for x in v)))
+          if v[0][2] else ""))
 PY
   if [ -n "$TIMELINES" ]; then for lib in $LIBS; do for v in "GLE_DBG_NO_LADDER=1" "GLE_PIECE_SLACK=0"; do
     env $v GLE_CHAIN_DBG=700 SCLMD_AMD_LIB=sclmd_amd/_lib/libhipgle_$lib.so timeout -k 10 200 python scripts/exp_time.py \
