@@ -684,6 +684,27 @@ class md:
             out[:, :n] = qh[:, :n]
         return out[0] if self.ntraj == 1 else out
 
+    def _histories(self):
+        """(phis, qhis) as md.phis / md.qhis return them, with one device read of the recorded
+        histories for both (the properties read them once each and copy them into zeroed arrays:
+        C5's 2 x 3.1 GB, most of a dump's time)."""
+        st = self._ensure_device()
+        if not ((getattr(self, "_rec_applied", 0) or 0) & _native.REC_HIST):
+            return np.asarray(self.phis), np.asarray(self.qhis)
+        ph, qh = st.get_record_history()                 # (ntraj, ml_r, nph) each, fresh arrays
+        if ph.shape[1] != self.ml:
+            out_p = np.zeros((self.ntraj, self.ml, self.nph))
+            out_q = np.zeros((self.ntraj, self.ml, self.nph))
+            n = min(self.ml, ph.shape[1])
+            out_p[:, :n], out_q[:, :n] = ph[:, :n], qh[:, :n]
+            ph, qh = out_p, out_q
+        for i, b in enumerate(self.baths):                # the bath rings the friction reads
+            h = st.get_history(i)                         # (ntraj, ml_b, nc_b)
+            ph[:, : h.shape[1], np.asarray(b.cids)] = h
+        if self.ntraj == 1:
+            return ph[0], qh[0]
+        return ph, qh
+
     def _load_phis(self, phis, qhis=None):
         st = self._ensure_device()
         self._push_state()  # history slots are relative to the device's t: set p, q, t first
@@ -817,7 +838,7 @@ class md:
         var.append(("q", np.array(self.q), tr + ("nph",)))
         var.append(("t", np.array([self.t]), ("one",)))
         var.append(("ipie", np.array([ipie]), ("one",)))
-        phis, qhis = np.asarray(self.phis), np.asarray(self.qhis)
+        phis, qhis = self._histories()
         if multi and phis.nbytes >= self.nc_var_limit:
             # a classic-format variable holds < 2 GiB (C5: 32 x 4096 x 3000 doubles = 3.1 GB): the
             # ensemble's histories are split into fixed-size variables of whole trajectories,
