@@ -212,7 +212,6 @@ struct gle_handle {
   int wait_early = 0;          // GLE_WAIT_EARLY: steps before a block's first use at which the main stream waits for it
   int64_t ev_seq_counter = 0;
   bool dbg_no_chain = false;   // GLE_DBG_NO_CHAIN (experiment): no chain launches
-  bool small_batch = false;    // B < 16: chain kernels with deeper one-column operand batches (GLE_SMALL_BATCH=0: off)
   int dbg_skip = 0;            // GLE_DBG_SKIP bits (timing experiments only, wrong results):
                                // 1 cgemm, 2 seg_fft, 4 far_ifft, 8 direct level ops
   int dbg_ntile = 0;
@@ -797,7 +796,7 @@ void run_chain(gle_handle* h, int stage, Chain& c, const StepArgs& ta, int mode,
   // GLE_DBG_NO_CHAIN (experiment, timing only: wrong results): the ladder without the per-step chain,
   // to time the far-field launches isolated against the same launches beside the chain
   if (!h->dbg_no_chain)
-    launch_chain(stage, c.nw, h->ch_drn, c.lds, c.d, (int)c.tiles.size(), h->d_sd, tc, mode, h->stream, h->small_batch);
+    launch_chain(stage, c.nw, h->ch_drn, c.lds, c.d, (int)c.tiles.size(), h->d_sd, tc, mode, h->stream);
   if (e1) {
     hipEventRecord(e1, h->stream);
     h->prof_n += 1;
@@ -2675,10 +2674,6 @@ int gle_create(const gle_config* cfg, gle_handle** out) {
   if (const char* e = gle_env("GLE_FAR_AFRAC")) h->far_afrac = std::max(0.0, std::min(1.0, atof(e)));
   if (const char* e = gle_env("GLE_DBG_SKIP")) h->dbg_skip = atoi(e);
   h->dbg_no_chain = gle_env("GLE_DBG_NO_CHAIN") != nullptr;
-  {
-    const char* e = gle_env("GLE_SMALL_BATCH");
-    h->small_batch = h->B < 16 && !(e && atoi(e) == 0);
-  }
   if (const char* e = gle_env("GLE_BG_GRID")) h->bg_grid = std::max(0, atoi(e));
   if (const char* e = gle_env("GLE_PIECE_SLACK")) h->piece_slack_env = std::max(0, atoi(e));
   if (const char* e = gle_env("GLE_BG_SERIAL")) h->bg_serial = atoi(e) != 0;

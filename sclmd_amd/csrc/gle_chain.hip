@@ -95,15 +95,9 @@ __device__ __forceinline__ int64_t cmod(int64_t a, int64_t m) {
 #ifndef CH_DB
 #define CH_DB 0
 #endif
-// SB: a plan of fewer than 16 trajectories (C2): its launches hold few tiles, so the one-column
-// tasks take batches of CH_USB k-steps (fewer round trips per task) at the cost of registers
-#ifndef CH_USB
-#define CH_USB 16
-#endif
-template <int RN, int NW, int SB = 0>
+template <int RN, int NW>
 struct Batch {
-  static constexpr int U = (SB && RN == 1) ? CH_USB
-                         : NW >= 16 ? (RN == 1 ? 16 : (RN == 2 ? 6 : 3)) : (RN == 1 ? CH_U1 : (RN == 2 ? CH_U2 : CH_U4));
+  static constexpr int U = NW >= 16 ? (RN == 1 ? 16 : (RN == 2 ? 6 : 3)) : (RN == 1 ? CH_U1 : (RN == 2 ? CH_U2 : CH_U4));
 };
 
 // GLE_CHAIN_DBG timeline: stamp 0 entry, 1 descriptor read, 2 products done, 3 end (100 MHz)
@@ -128,10 +122,10 @@ __device__ __forceinline__ void stamp(const StepDev* __restrict__ sd, int stage,
 #ifndef CH_NA
 #define CH_NA 1
 #endif
-template <int RN, int NW, int SB>
+template <int RN, int NW>
 __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave, int lane, int64_t t,
                                          double* lds, int skip) {
-  constexpr int U = Batch<RN, NW, SB>::U;
+  constexpr int U = Batch<RN, NW>::U;
   constexpr int NT = 16 * RN;
   constexpr int NA = (CH_NA / RN) > 1 ? (CH_NA / RN) : 1;  // independent accumulators: NA * RN
   static_assert(U % NA == 0, "a batch fills every accumulator set equally");
@@ -239,21 +233,21 @@ __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave,
 // DOF and S(t+1) tiles have the kernel's DRN columns (T->rn == DRN): products of that width only,
 // so the 64-column near-field variant is not instantiated beside the DOF prologue's live values
 // (it made the register allocator spill the DOF stages)
-template <int NW, int RN, int SB>
+template <int NW, int RN>
 __device__ __forceinline__ void run_products_rn(const ChTile* __restrict__ T, int64_t t, double* lds, int skip = 0) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  products<RN, NW, SB>(T, wave, lane, t, lds, skip);
+  products<RN, NW>(T, wave, lane, t, lds, skip);
 }
 
-template <int NW, int SB>
+template <int NW>
 __device__ __forceinline__ void run_products(const ChTile* __restrict__ T, int64_t t, double* lds, int skip = 0) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   switch (T->rn) {
-    case 1: products<1, NW, SB>(T, wave, lane, t, lds, skip); break;
-    case 2: products<2, NW, SB>(T, wave, lane, t, lds, skip); break;
-    default: products<4, NW, SB>(T, wave, lane, t, lds, skip); break;
+    case 1: products<1, NW>(T, wave, lane, t, lds, skip); break;
+    case 2: products<2, NW>(T, wave, lane, t, lds, skip); break;
+    default: products<4, NW>(T, wave, lane, t, lds, skip); break;
   }
 }
 
@@ -369,7 +363,7 @@ __device__ __forceinline__ double col_red(const double* red, int q, int c, bool 
 }
 
 // stage A, DOF tile
-template <int NW, int DRN, int SB>
+template <int NW, int DRN>
 __device__ __forceinline__ void dof_A(const ChTile* __restrict__ T, const StepDev* __restrict__ sd,
                                       const StepArgs& ta, int mode, double* lds) {
   using Geo = DofGeo<NW, DRN>;
@@ -409,7 +403,7 @@ __device__ __forceinline__ void dof_A(const ChTile* __restrict__ T, const StepDe
   }
   if (T->first && threadIdx.x < Geo::NT && T->c0 + (int)threadIdx.x < B)
     *G(pmax_word(sd, 0, par ^ 1, T->c0 + threadIdx.x)) = 0ull;
-  run_products_rn<NW, DRN, SB>(T, t, lds);
+  run_products_rn<NW, DRN>(T, t, lds);
   __syncthreads();
   stamp(sd, 0, 2, ta);
   // ---- epilogue (md.vv id0, md.py:383-397).  Every output sum is read first (unconditionally, the
@@ -521,7 +515,7 @@ __device__ __forceinline__ void dof_A(const ChTile* __restrict__ T, const StepDe
 }
 
 // stage B, DOF tile
-template <int NW, int DRN, int SB>
+template <int NW, int DRN>
 __device__ __forceinline__ void dof_B(const ChTile* __restrict__ T, const StepDev* __restrict__ sd,
                                       const StepArgs& ta, int mode, double* lds) {
   using Geo = DofGeo<NW, DRN>;
@@ -554,7 +548,7 @@ __device__ __forceinline__ void dof_B(const ChTile* __restrict__ T, const StepDe
       sv[x][u] = G(bd.S)[(int64_t)par1 * bd.vs + kb];
     }
   }
-  run_products_rn<NW, DRN, SB>(T, t, lds);
+  run_products_rn<NW, DRN>(T, t, lds);
   __syncthreads();
   stamp(sd, 1, 2, ta);
 #pragma unroll
@@ -598,7 +592,7 @@ __device__ __forceinline__ void dof_B(const ChTile* __restrict__ T, const StepDe
 }
 
 // stage C, DOF tile
-template <int NW, int DRN, int SB>
+template <int NW, int DRN>
 __device__ __forceinline__ void dof_C(const ChTile* __restrict__ T, const StepDev* __restrict__ sd,
                                       const StepArgs& ta, int mode, double* lds) {
   using Geo = DofGeo<NW, DRN>;
@@ -637,7 +631,7 @@ __device__ __forceinline__ void dof_C(const ChTile* __restrict__ T, const StepDe
     *G(pmax_word(sd, 1, par1, T->c0 + threadIdx.x)) = 0ull;
     if (harm) G(sd->qvalid)[T->c0 + threadIdx.x] = 1;
   }
-  run_products_rn<NW, DRN, SB>(T, t, lds);
+  run_products_rn<NW, DRN>(T, t, lds);
   __syncthreads();
   stamp(sd, 2, 2, ta);
   double dq[EPT];
@@ -709,7 +703,7 @@ __device__ __forceinline__ void dof_C(const ChTile* __restrict__ T, const StepDe
 // so every product reads only stage A's outputs: one dependent launch instead of two, and three
 // nc x nc products per bath row instead of the six of B + C.  K0 p1 is re-associated (rounding
 // only).  Products of the branch no trajectory of the tile takes are skipped.
-template <int NW, int DRN, int SB>
+template <int NW, int DRN>
 __device__ __forceinline__ void dof_BC(const ChTile* __restrict__ T, const StepDev* __restrict__ sd,
                                        const StepArgs& ta, int mode, double* lds) {
   using Geo = DofGeo<NW, DRN>;
@@ -753,7 +747,7 @@ __device__ __forceinline__ void dof_BC(const ChTile* __restrict__ T, const StepD
   // which potential-cache branches at q~ any trajectory of the tile takes (workgroup-uniform)
   anyhit = __syncthreads_or(anyhit);
   anymiss = __syncthreads_or(anymiss);
-  run_products_rn<NW, DRN, SB>(T, t, lds, (anyhit ? 0 : 1) | (anymiss ? 0 : 2));
+  run_products_rn<NW, DRN>(T, t, lds, (anyhit ? 0 : 1) | (anymiss ? 0 : 2));
   __syncthreads();
   // the words this launch reads (w1) are read above: only now may the first tile reset them
   if (T->first && threadIdx.x < Geo::NT && T->c0 + (int)threadIdx.x < B) {
@@ -838,7 +832,7 @@ __device__ __forceinline__ void dof_BC(const ChTile* __restrict__ T, const StepD
 
 // S(t+1) of bath rows [row0, row0+16) x 16 rn columns: K_1.p_t (the products) + near-field
 // partials + levels
-template <int NW, int DRN, int SB>
+template <int NW, int DRN>
 __device__ __forceinline__ void sfin(const ChTile* __restrict__ T, const StepDev* __restrict__ sd,
                                      const StepArgs& ta, double* lds, int stage) {
   const int B = sd->B;
@@ -876,7 +870,7 @@ __device__ __forceinline__ void sfin(const ChTile* __restrict__ T, const StepDev
     for (int l = 0; l < MAXLVL; ++l) lvs += lv[l];
     pre[x] = lvs + sn;
   }
-  run_products_rn<NW, DRN, SB>(T, t, lds);
+  run_products_rn<NW, DRN>(T, t, lds);
   __syncthreads();
   stamp(sd, stage, 2, ta);
 #pragma unroll
@@ -892,11 +886,11 @@ __device__ __forceinline__ void sfin(const ChTile* __restrict__ T, const StepDev
 }
 
 // near-field partial tile: rows [0, nrows) x columns [0, ncols) of the parity buffer of t + par_shift
-template <int NW, int SB>
+template <int NW>
 __device__ __forceinline__ void raw(const ChTile* __restrict__ T, const StepDev* __restrict__ sd, const StepArgs& ta,
                                     double* lds, int stage) {
   const int64_t t = ta.t;
-  run_products<NW, SB>(T, t, lds);
+  run_products<NW>(T, t, lds);
   __syncthreads();
   stamp(sd, stage, 2, ta);
   const int NT = 16 * T->rn;
@@ -960,8 +954,8 @@ __device__ __forceinline__ void far_tile(const StepArgs& ta, double* lds) {
   }
 }
 
-template <int STAGE, int NW, int DRN, int SB = 0>
-__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(SB ? 2 : (DRN == 1 && NW <= 8 ? CH_WPE : 1), 8))) void chain_kernel(const ChTile* __restrict__ tiles, const StepDev* sd,
+template <int STAGE, int NW, int DRN>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(DRN == 1 && NW <= 8 ? CH_WPE : 1, 8))) void chain_kernel(const ChTile* __restrict__ tiles, const StepDev* sd,
                                                         StepArgs ta, int mode) {
   extern __shared__ double lds[];
   if ((int)blockIdx.x >= ta.nstatic) {  // far-field item (fused schedule), launch-uniform ranges
@@ -1021,14 +1015,14 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(SB ? 2 
 #endif
   stamp(sd, STAGE, 1, ta);
   if (kind == CH_DOF) {
-    if (STAGE == 0) dof_A<NW, DRN, SB>(T, sd, ta, mode, lds);
-    else if (STAGE == 1) dof_B<NW, DRN, SB>(T, sd, ta, mode, lds);
-    else if (STAGE == 2) dof_C<NW, DRN, SB>(T, sd, ta, mode, lds);
-    else dof_BC<NW, DRN, SB>(T, sd, ta, mode, lds);
+    if (STAGE == 0) dof_A<NW, DRN>(T, sd, ta, mode, lds);
+    else if (STAGE == 1) dof_B<NW, DRN>(T, sd, ta, mode, lds);
+    else if (STAGE == 2) dof_C<NW, DRN>(T, sd, ta, mode, lds);
+    else dof_BC<NW, DRN>(T, sd, ta, mode, lds);
   } else if (kind == CH_SFIN) {
-    sfin<NW, DRN, SB>(T, sd, ta, lds, STAGE);
+    sfin<NW, DRN>(T, sd, ta, lds, STAGE);
   } else {
-    raw<NW, SB>(T, sd, ta, lds, STAGE);
+    raw<NW>(T, sd, ta, lds, STAGE);
   }
   stamp(sd, STAGE, 3, ta);
   if (ta.ts) {  // launch-uniform
@@ -1062,7 +1056,7 @@ bool lds_limit(K* fn, size_t lds) {
 
 template <int STAGE, int NW>
 void launch_nd(int drn, size_t lds, const ChTile* tiles, int ntiles, const StepDev* sd, StepArgs ta, int mode,
-               hipStream_t s, bool small) {
+               hipStream_t s) {
   int grid = ntiles;
   for (int r = 0; r < ta.nfar; ++r) grid += ta.far[r].count;
   if (ta.nfar > 0) lds = std::max(lds, CH_FAR_LDS);
@@ -1071,9 +1065,6 @@ void launch_nd(int drn, size_t lds, const ChTile* tiles, int ntiles, const StepD
   if (drn == 2) {
     lds_limit(chain_kernel<STAGE, NW, 2>, lds);
     chain_kernel<STAGE, NW, 2><<<grid, NW * 64, lds, s>>>(tiles, sd, ta, mode);
-  } else if (small && NW == 4) {
-    lds_limit(chain_kernel<STAGE, 4, 1, 1>, lds);
-    chain_kernel<STAGE, 4, 1, 1><<<grid, NW * 64, lds, s>>>(tiles, sd, ta, mode);
   } else {
     lds_limit(chain_kernel<STAGE, NW, 1>, lds);
     chain_kernel<STAGE, NW, 1><<<grid, NW * 64, lds, s>>>(tiles, sd, ta, mode);
@@ -1082,23 +1073,23 @@ void launch_nd(int drn, size_t lds, const ChTile* tiles, int ntiles, const StepD
 
 template <int STAGE>
 void launch_st(int nw, int drn, size_t lds, const ChTile* tiles, int ntiles, const StepDev* sd, StepArgs ta,
-               int mode, hipStream_t s, bool small) {
-  if (nw == 8) launch_nd<STAGE, 8>(drn, lds, tiles, ntiles, sd, ta, mode, s, small);
-  else launch_nd<STAGE, 4>(drn, lds, tiles, ntiles, sd, ta, mode, s, small);
+               int mode, hipStream_t s) {
+  if (nw == 8) launch_nd<STAGE, 8>(drn, lds, tiles, ntiles, sd, ta, mode, s);
+  else launch_nd<STAGE, 4>(drn, lds, tiles, ntiles, sd, ta, mode, s);
 }
 
 }  // namespace
 
 void launch_chain(int stage, int nw, int drn, size_t lds_bytes, const ChTile* tiles, int ntiles, const StepDev* sd,
-                  StepArgs ta, int mode, hipStream_t s, bool small) {
+                  StepArgs ta, int mode, hipStream_t s) {
   if (ntiles <= 0) return;
   GLE_BOUNDS_SYNC();
   ta.nstatic = ntiles;
   if (nw != 4) ta.nfar = 0;  // far items need 4-wave workgroups (the planner never gives them others)
-  if (stage == 0) launch_st<0>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s, small);
-  else if (stage == 1) launch_st<1>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s, small);
-  else if (stage == 2) launch_st<2>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s, small);
-  else launch_st<3>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s, small);
+  if (stage == 0) launch_st<0>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
+  else if (stage == 1) launch_st<1>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
+  else if (stage == 2) launch_st<2>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
+  else launch_st<3>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
 }
 
 namespace {

@@ -321,9 +321,8 @@ void launch_reduce(const RItem* items, int nitems, int max_elems, StepArgs ta,
 // stage 0/1/2 = A/B/C.  mode: A: 1 = harmonic id0 potential with md.potforce's cache rule (YD = dyn.q_t
 // present), 0 = potential force at q_t already in Fc; bit 1: write the id1 cache distance.
 // B / C: 1 = harmonic force at q~ (B computes YD = dyn.q~), 0 = host force in Fc.
-// small: fewer than 16 trajectories (one column tile): deeper operand batches (gle_chain.hip Batch)
 void launch_chain(int stage, int nw, int drn, size_t lds_bytes, const ChTile* tiles, int ntiles, const StepDev* sd,
-                  StepArgs ta, int mode, hipStream_t s, bool small = false);
+                  StepArgs ta, int mode, hipStream_t s);
 void launch_finalize(const StepDev* sd, int B, int nmd, int nbath, hipStream_t s);
 // md.potforce at q~ for every DOF and trajectory before the fused velocity stage (bc_fpot): the
 // cache rule per trajectory (pmax word id1 of parity par), on a miss f = -dyn.q~ (CSR rows) with
