@@ -77,7 +77,7 @@ typedef struct gle_config {
 /* Plan class.  AUTO picks by the largest bath: SMALL when every bath has nc <= 512 (the per-step
  * chain is latency-bound: first block length 8, 4-wave fused velocity-stage tiles, far-field GEMM
  * chunks of 1.25 workgroups per CU, a block's ladder pieces spread over its whole window), LARGE
- * otherwise (first block length 4, 8-wave fused tiles, the
+ * otherwise (first block length 4, the
  * potential force at q~ as its own small launch before the fused stage (GLE_PLAN_FPOT_LAUNCH),
  * far-field GEMM chunks of 4 workgroups per CU).  Forcing a class changes only the schedule, never
  * the result beyond fp64

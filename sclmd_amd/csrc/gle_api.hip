@@ -1831,9 +1831,12 @@ int freeze(gle_handle* h) {
   // windows over all phases of the largest level mean 51.1 vs 52.5-52.9, max 54.6 vs 62.6-63.4
   h->piece_slack = h->piece_slack_env >= 0 ? h->piece_slack_env : (h->small_baths ? 0 : 1);
   const int P0 = h->cfg.block_len > 0 ? h->cfg.block_len : (h->small_baths ? 8 : 4);
-  // fused-stage tile waves: 4 when the chain is latency-bound (C3: 53.3 vs 55.3 us/step with the
-  // 1-workgroup-per-CU far-field chunks below), 8 for large baths (C5: 447 vs ~410 us at 4)
-  h->ch_nw[1] = h->small_baths ? 4 : 8;
+  // fused-stage tile waves: 4 (C3: 53.3 vs 55.3 us/step at 8, r02).  Large baths took 8 until round
+  // 5 (C5 r02: 447 vs ~410 us at 4); with the two-plane far field and the ELL potential-force launch
+  // 4 waves are faster there too: 255 vs 263.5 us/step (512 steps), 253.4 vs 259.1 (20-step
+  // windows), 3 interleaved rounds on one box (`profiles/r05/c5_fused_waves.jsonl`) -- an 8-wave
+  // workgroup needs two free wave slots on every SIMD beside the far-field chunks of 4 per CU
+  h->ch_nw[1] = 4;
   int Pmax;
   if (h->cfg.max_block > 0) {
     Pmax = std::max(P0, h->cfg.max_block);

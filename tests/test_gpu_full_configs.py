@@ -13,7 +13,7 @@ oracle (oracle.GLEBatch, pinned to the reference-shaped oracle and the reference
 the ladder plan; wrap-around is covered in test_gpu_md.py).
 
 The large-bath plan (any bath with nc > 512: first block length 4 with a direct P = 4 level, the
-8-wave fused velocity stage, the fpot launch, split-K far-field GEMM chunks of 4 workgroups per CU)
+fpot launch, split-K far-field GEMM chunks of 4 workgroups per CU)
 is what bench.py runs at C5 (nc = 999 / 1002).  It is checked twice against the oracle: at nc = 522
 (natom 522, ml = 512,
 picked by the automatic rule), and at the reduced C5 size with the plan class forced through the
@@ -99,7 +99,7 @@ def _run_vs_oracle(config, natom, B, check, t0=37, nst=540, nmd=1024, ml=1024, s
     assert detail["plan_class"] == expect_class, detail
     P0 = info["block_len"]
     assert P0 == (block_len or (8 if expect_class == "small" else 4)), info
-    assert detail["fused_waves"] == (4 if expect_class == "small" else 8), detail
+    assert detail["fused_waves"] == 4, detail  # both plan classes (round 5: C5 faster at 4)
     assert detail["fpot_launch"] == (expect_class == "large"), detail
     assert detail["cg_per_cu"] == (1.25 if expect_class == "small" else 4.0), detail
     # every ladder level computed blocks inside the run (P = P0 ... 256 at ml = 1024)
@@ -132,8 +132,8 @@ def test_c5_reduced_biased_vs_oracle():
 
 
 def test_c5_reduced_large_plan_forced_vs_oracle():
-    """The large-bath plan at nc ~ 96: P0 = 4 (direct P = 4 level, spectral P = 8 ... 256), 8-wave
-    fused stage, the fpot launch (potential force at q~ before the fused stage), far-field GEMM
+    """The large-bath plan at nc ~ 96: P0 = 4 (direct P = 4 level, spectral P = 8 ... 256), the fpot
+    launch (potential force at q~ before the fused stage), far-field GEMM
     chunks of 4 workgroups per CU."""
     sim = _run_vs_oracle("C5", 96, 32, [0, 17, 31], plan_class="large", expect_class="large")
     assert sum(b.biased() for b in sim.baths) == 1
