@@ -3197,6 +3197,28 @@ int gle_set_history(gle_handle* h, int32_t bath, const double* phis) {
   return GLE_OK;
 }
 
+// Trajectory-major copy of a ring into host memory, in chunks of trajectories through a device
+// buffer of at most ~256 MB (C5's histories are GBs beside ~280 GB of resident plan): the transpose
+// runs on the device, each chunk lands in its place in the caller's array.
+static int hist_to_host(gle_handle* h, const double* src, int64_t ks, int64_t ss, int R, int64_t tau0, int nt,
+                        int nk, double* out) {
+  const int64_t per = (int64_t)nt * nk;
+  if (per <= 0) return GLE_OK;
+  const int64_t nbc = std::max<int64_t>(1, std::min<int64_t>(h->B, (256ll << 20) / (per * 8)));
+  double* d_tmp = nullptr;
+  HIPCHK(h, tmalloc((void**)&d_tmp, (size_t)(nbc * per * 8)));
+  hipError_t e = hipSuccess;
+  for (int64_t b0 = 0; b0 < h->B && e == hipSuccess; b0 += nbc) {
+    const int nb = (int)std::min<int64_t>(nbc, h->B - b0);
+    launch_hist_out(src, ks, ss, R, tau0, nt, nk, (int)b0, nb, d_tmp, h->stream);
+    e = hipMemcpyAsync(out + b0 * per, d_tmp, (size_t)nb * per * 8, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  }
+  tfree(d_tmp);
+  if (e != hipSuccess) return fail(h, GLE_ERR_HIP, std::string("history copy: ") + hipGetErrorString(e));
+  return GLE_OK;
+}
+
 int gle_get_history(gle_handle* h, int32_t bath, double* phis) {
   int rc = check_bath(h, bath);
   if (rc) return rc;
@@ -3204,20 +3226,8 @@ int gle_get_history(gle_handle* h, int32_t bath, double* phis) {
   if (!h->frozen) return fail(h, GLE_ERR_STATE, "no state yet");
   hipSetDevice(h->cfg.device);
   Bath& b = h->baths[bath];
-  const int64_t B = h->B;
-  std::vector<double> buf((size_t)b.ml * b.nc * B);
-  double* d_tmp = nullptr;
-  HIPCHK(h, tmalloc((void**)&d_tmp, buf.size() * 8));
-  launch_ring_copy(b.d_H, b.ldh, b.R, (int)B, b.nc, h->t - 1, b.ml, d_tmp, 1, h->stream);
-  hipMemcpyAsync(buf.data(), d_tmp, buf.size() * 8, hipMemcpyDeviceToHost, h->stream);
-  hipError_t e = hipStreamSynchronize(h->stream);
-  tfree(d_tmp);
-  if (e != hipSuccess) return fail(h, GLE_ERR_HIP, std::string("get_history: ") + hipGetErrorString(e));
-  for (int64_t j = 0; j < B; ++j)
-    for (int64_t i = 0; i < b.ml; ++i)
-      for (int64_t k = 0; k < b.nc; ++k)
-        phis[((size_t)j * b.ml + i) * b.nc + k] = buf[((size_t)i * b.nc + k) * B + j];
-  return GLE_OK;
+  // row i (newest first) = time t-1-i of the ring (both mirror copies hold it)
+  return hist_to_host(h, b.d_H, b.ldh, h->B, b.R, h->t - 1, b.ml, b.nc, phis);
 }
 
 int gle_get_force(gle_handle* h, double* f) {
@@ -3825,18 +3835,12 @@ int gle_get_record_history(gle_handle* h, double* phis, double* qhis, int64_t* m
   if (!h->d_rec_hp) return fail(h, GLE_ERR_STATE, "histories were never recorded (gle_record GLE_REC_HIST)");
   hipSetDevice(h->cfg.device);
   const int64_t B = h->B, n = h->nph, R = h->rec_ml;
-  std::vector<double> buf((size_t)R * n * B);
+  // row i (newest first) = time t-1-i = ring slot (t-1-i) mod R
   for (int k = 0; k < 2; ++k) {
     double* out = k == 0 ? phis : qhis;
     if (!out) continue;
-    int rc = download(h, buf.data(), k == 0 ? h->d_rec_hp : h->d_rec_hq, buf.size() * 8);
+    int rc = hist_to_host(h, k == 0 ? h->d_rec_hp : h->d_rec_hq, B, n * B, (int)R, h->t - 1, (int)R, (int)n, out);
     if (rc) return rc;
-    // row i (newest first) = time t-1-i = ring slot (t-1-i) mod R
-    for (int64_t i = 0; i < R; ++i) {
-      const int64_t slot = ((h->t - 1 - i) % R + R) % R;
-      for (int64_t b = 0; b < B; ++b)
-        for (int64_t d = 0; d < n; ++d) out[((size_t)b * R + i) * n + d] = buf[((size_t)slot * n + d) * B + b];
-    }
   }
   return GLE_OK;
 }

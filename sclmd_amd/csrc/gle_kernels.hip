@@ -590,6 +590,30 @@ void launch_ring_copy(double* H, int64_t ldh, int R, int B, int nc, int64_t tau0
   ring_copy_kernel<<<(unsigned)blocks, 256, 0, s>>>(H, ldh, R, B, nc, tau0, nt, buf, dir);
 }
 
+// Trajectory-major copy of nt ring slots for trajectories [b0, b0 + nb): out[bb][i][k] =
+// src[k ks + ((tau0 - i) mod R) ss + b0 + bb] (i = 0 is time tau0).  Bath rings: ks = ldh, ss = B;
+// the recorded full-DOF rings [slot][d][b]: ks = B, ss = nph B.  The host getters copy the chunks
+// straight into the caller's arrays (no host-side transpose).
+__global__ void hist_out_kernel(const double* __restrict__ src, int64_t ks, int64_t ss, int R, int64_t tau0,
+                                int nt, int nk, int b0, int nb, double* __restrict__ out) {
+  const int64_t n = (int64_t)nb * nt * nk;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = e % nk;
+    const int64_t i = (e / nk) % nt;
+    const int64_t bb = e / ((int64_t)nk * nt);
+    out[e] = src[k * ks + pmod(tau0 - i, R) * ss + b0 + bb];
+  }
+}
+
+void launch_hist_out(const double* src, int64_t ks, int64_t ss, int R, int64_t tau0, int nt, int nk, int b0, int nb,
+                     double* out, hipStream_t s) {
+  const int64_t n = (int64_t)nb * nt * nk;
+  if (n <= 0) return;
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 8192);
+  hist_out_kernel<<<(unsigned)blocks, 256, 0, s>>>(src, ks, ss, R, tau0, nt, nk, b0, nb, out);
+}
+
 // near ring (slot-major [NRS][vs], the chain's compact copy of the newest p): slots of times
 // t, t-1, ..., t-NRS+1 from the history ring
 __global__ void near_fill_kernel(const double* __restrict__ H, int64_t ldh, int R, int B, int ncp,
