@@ -393,11 +393,12 @@ class Stepper:
             for seg in segments:
                 if seg[0] == "dense":
                     _, w0, m = seg
-                    for o in range(0, m.shape[0], max_chunk):
-                        mc = m[o:o + max_chunk]
-                        mre = _f64(np.real(mc))
-                        mim = _f64(np.imag(mc)) if is_complex else None
-                        self._chk(self.lib.gle_noise_stream_chunk(self.h, int(bath), int(w0 + o), int(mc.shape[0]),
+                    # complex factors arrive as (Re, Im) planes (noise.stream_factor_plan) or complex
+                    mr, mi = m if isinstance(m, tuple) else (np.real(m), np.imag(m) if is_complex else None)
+                    for o in range(0, mr.shape[0], max_chunk):
+                        mre = _f64(mr[o:o + max_chunk])
+                        mim = _f64(mi[o:o + max_chunk]) if is_complex else None
+                        self._chk(self.lib.gle_noise_stream_chunk(self.h, int(bath), int(w0 + o), int(mre.shape[0]),
                                                                   _ptr(mre), _ptr(mim), sd, int(traj_offset)),
                                   "gle_noise_stream_chunk")
                 else:

@@ -170,7 +170,8 @@ def stream_factor_plan(bath, chunk=64, workers=None, cache=None):
     """The streamed factors of a bath as device work segments, in frequency order:
       ("shared", w0, nw, scale, F)  frequencies [w0, w0 + nw) whose spectrum is s_w H for one shared
                                     H: factor F = H_+^(1/2) handed over once, scale = sqrt(s_w)
-      ("dense", w0, M)              M (nw, nc, nc) the factors of frequencies [w0, w0 + nw)
+      ("dense", w0, M)              M (nw, nc, nc) the factors of frequencies [w0, w0 + nw); complex
+                                    factors as a pair (Re M, Im M) of contiguous planes
     Frequencies whose spectrum is zero produce nothing (the device spectrum starts at zero).  Dense
     factors are computed on a thread pool (LAPACK releases the GIL; BLAS pinned to one thread per
     worker), two chunks ahead of the consumer.  cache: a dict that keeps the dense chunks (and the
@@ -220,7 +221,11 @@ def stream_factor_plan(bath, chunk=64, workers=None, cache=None):
                 sc = np.sqrt(np.array([terms[i][2] for i in ws]))
                 seg = ("shared", ws[0], len(ws), sc, shared[key])
             else:
-                seg = ("dense", ws[0], np.stack([f.result() for f in key]))
+                m = np.stack([f.result() for f in key])
+                if np.iscomplexobj(m):  # the device takes real and imaginary planes: split once (and
+                    # cache the split), not at every run's hand-over (C5's electron bath: 2 x 4 GB)
+                    m = (np.ascontiguousarray(m.real), np.ascontiguousarray(m.imag))
+                seg = ("dense", ws[0], m)
             if keep is not None:
                 keep.append(seg)
             return seg
