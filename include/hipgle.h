@@ -185,6 +185,17 @@ int gle_noise_stream_end(gle_handle* h, int32_t bath);
 /* Release a begun stream's scratch without generating (an error between begin and end); the bath's
  * previous noise stays.  gle_destroy releases any stream still open. */
 int gle_noise_stream_abort(gle_handle* h, int32_t bath);
+/* Keep the factors of the next complete streamed plan of `bath` (every chunk and shared segment
+ * from begin to end) in device memory, so that each later run (md.Run draws new noise per run from
+ * the same spectrum, md.py:569-570) replays them with new draws instead of handing them over PCIe
+ * again (C5: ~11 GB of dense factors per run).  retain = 0 frees them.  A plan that does not fit
+ * beside the resident state is streamed as without retention and nothing is kept. */
+int gle_noise_stream_retain(gle_handle* h, int32_t bath, int32_t retain);
+/* *bytes = device bytes of the retained complete plan of `bath`, 0 when none is retained. */
+int gle_noise_stream_retained(gle_handle* h, int32_t bath, int64_t* bytes);
+/* New noise of `bath` from its retained plan: the same result as streaming that plan again with
+ * this seed / traj_offset (GLE_ERR_STATE when no plan is retained). */
+int gle_noise_stream_replay(gle_handle* h, int32_t bath, uint64_t seed, uint64_t traj_offset);
 
 /* ---- stepping (md.vv, md.py:367-411) -------------------------------------------------- */
 /* Phase A of one step: F0 = Fpot(q_t) + sum_b bforce_b(t, id=0), current, half kick, drift.
@@ -226,6 +237,17 @@ int gle_get_record(gle_handle* h, int32_t what, int32_t bath, double* out);
 /* md.phis / md.qhis on every DOF, newest first: [ntraj][ml][nph] (rows of times before the
  * recording started read as zeros); *ml = the ring length (max over baths of ml). */
 int gle_get_record_history(gle_handle* h, double* phis, double* qhis, int64_t* ml);
+/* md.phis / md.qhis as MD{j}.nc stores them (md.py:346-349, 717-731): [ntraj][ml][nph] each, newest
+ * first.  p and q rows come from the full-DOF recording (GLE_REC_HIST; rows past its length, and
+ * every row when it is not recording, read zero); the p rows i < ml_b of each bath's DOFs come from
+ * that bath's own history ring, the friction's operand (baths in order: a later bath's ring wins on
+ * shared DOFs).  Either output may be NULL.  The transposes run on the device; page-locked outputs
+ * (gle_host_alloc) are written at the link's rate. */
+int gle_get_full_history(gle_handle* h, int64_t ml, double* phis, double* qhis);
+/* Page-locked host memory (hipHostMalloc) for large device reads such as a checkpoint's histories;
+ * errors: gle_last_error(NULL). */
+int gle_host_alloc(int64_t bytes, void** p);
+int gle_host_free(void* p);
 /* Restore recordings (a resumed run, md.py:513-534): in has gle_get_record's / _history's layout. */
 int gle_set_record(gle_handle* h, int32_t what, int32_t bath, const double* in);
 int gle_set_record_history(gle_handle* h, const double* phis, const double* qhis);

@@ -34,6 +34,8 @@ EXPORTS = [
     "gle_power_spectrum", "gle_set_record", "gle_set_record_history", "gle_noise_stream_begin",
     "gle_noise_stream_chunk", "gle_noise_stream_end", "gle_set_plan_class", "gle_plan_detail", "gle_plan_flags",
     "gle_comm_allreduce", "gle_noise_stream_abort", "gle_device_mem_info", "gle_noise_stream_shared",
+    "gle_noise_stream_retain", "gle_noise_stream_retained", "gle_noise_stream_replay", "gle_get_full_history",
+    "gle_host_alloc", "gle_host_free",
 ]
 
 REC_P, REC_Q, REC_F, REC_HIST = 1, 2, 4, 8
@@ -121,6 +123,12 @@ _SIGS = {
     "gle_noise_stream_end": (ctypes.c_int, [_P, ctypes.c_int32]),
     "gle_noise_stream_shared": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, _D, _D, _D,
                                                ctypes.c_uint64, ctypes.c_uint64]),
+    "gle_get_full_history": (ctypes.c_int, [_P, ctypes.c_int64, _D, _D]),
+    "gle_host_alloc": (ctypes.c_int, [ctypes.c_int64, ctypes.POINTER(_P)]),
+    "gle_host_free": (ctypes.c_int, [_P]),
+    "gle_noise_stream_retain": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32]),
+    "gle_noise_stream_retained": (ctypes.c_int, [_P, ctypes.c_int32, _I64]),
+    "gle_noise_stream_replay": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint64]),
 }
 
 _lib = None
@@ -166,6 +174,28 @@ def device_mem_info(device=0):
     if rc != 0:
         raise GLEError("gle_device_mem_info failed: %s" % lib.gle_last_error(None).decode())
     return int(fr.value), int(tot.value)
+
+
+class HostBuffer:
+    """Page-locked host memory (gle_host_alloc) viewed as a float64 numpy array of `shape`: device
+    reads into it run at the link's rate.  free() releases it; no view of .array may outlive that."""
+
+    def __init__(self, shape):
+        lib = load()
+        n = int(np.prod(shape))
+        p = _P()
+        if lib.gle_host_alloc(n * 8, ctypes.byref(p)) != 0:
+            raise GLEError("gle_host_alloc(%d bytes) failed: %s" % (n * 8, lib.gle_last_error(None).decode()))
+        self._lib, self._p = lib, p.value
+        self.array = np.ctypeslib.as_array((ctypes.c_double * max(n, 1)).from_address(self._p))[:n].reshape(shape)
+
+    def free(self):
+        if getattr(self, "_p", None):
+            self.array = None
+            self._lib.gle_host_free(self._p)
+            self._p = None
+
+    __del__ = free
 
 
 def device_count():
@@ -414,6 +444,21 @@ class Stepper:
             raise
         self._chk(self.lib.gle_noise_stream_end(self.h, int(bath)), "gle_noise_stream_end")
 
+    def noise_stream_retain(self, bath, retain=True):
+        """Keep the next complete streamed plan's factors on the device (False frees them)."""
+        self._chk(self.lib.gle_noise_stream_retain(self.h, int(bath), 1 if retain else 0), "gle_noise_stream_retain")
+
+    def noise_stream_retained(self, bath):
+        """Device bytes of the retained complete plan of `bath` (0: none)."""
+        n = ctypes.c_int64(0)
+        self._chk(self.lib.gle_noise_stream_retained(self.h, int(bath), ctypes.byref(n)), "gle_noise_stream_retained")
+        return n.value
+
+    def noise_stream_replay(self, bath, seed, traj_offset=0):
+        """New noise from the retained plan (= streaming that plan again with this seed)."""
+        self._chk(self.lib.gle_noise_stream_replay(self.h, int(bath), int(seed) & (2**64 - 1), int(traj_offset)),
+                  "gle_noise_stream_replay")
+
     # --------------------------------------------------------------------------- stepping
     def step_begin(self, fpot=None, want_qt=True):
         f = None if fpot is None else _f64(fpot, (self.ntraj, self.nph))
@@ -471,6 +516,21 @@ class Stepper:
         self._chk(self.lib.gle_get_record_history(self.h, _ptr(ph), _ptr(qh), ctypes.byref(ml)),
                   "gle_get_record_history")
         return ph, qh
+
+    def get_full_history(self, ml, out_p=None, out_q=None):
+        """(phis, qhis) as MD{j}.nc stores them: (ntraj, ml, nph) each, recorded rows with the baths'
+        own rings on their DOFs (gle_get_full_history); written into out_p / out_q when given
+        (C-contiguous float64 of that shape, e.g. HostBuffer arrays)."""
+        shp = (self.ntraj, int(ml), self.nph)
+        outs = []
+        for o in (out_p, out_q):
+            if o is None:
+                o = np.empty(shp)
+            elif o.shape != shp or o.dtype != np.float64 or not o.flags.c_contiguous:
+                raise ValueError("history output must be C-contiguous float64 %s" % (shp,))
+            outs.append(o)
+        self._chk(self.lib.gle_get_full_history(self.h, int(ml), _ptr(outs[0]), _ptr(outs[1])), "gle_get_full_history")
+        return outs[0], outs[1]
 
     def set_record(self, what, arr, bath=0):
         cols = self.bath_nc[bath] if what == REC_F else self.nph

@@ -13,12 +13,40 @@ import numpy as np
 from scipy.io import netcdf_file
 
 
+# fixed-size variables at least this large take the fast fill (parallel byte swap, no second copy)
+FAST_FILL_BYTES = 64 << 20
+
+
+class _WriteView(np.ndarray):
+    """A variable's big-endian buffer whose tobytes() is a view of itself: scipy's classic-format
+    writer (fp.write(var.data.tobytes())) then writes the filled buffer without copying GBs again."""
+
+    def tobytes(self, order="C"):
+        return memoryview(self.view(np.ndarray)).cast("B")
+
+
+def _fill_big_endian(dst, src, workers=8):
+    """dst[...] = src (little- to big-endian) on a thread pool (numpy's casting copy releases the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    d, s_ = dst.reshape(-1), np.ascontiguousarray(src).reshape(-1)
+    edges = np.linspace(0, d.size, workers + 1).astype(np.int64)
+    with ThreadPoolExecutor(max_workers=workers) as ex:
+        list(ex.map(lambda k: np.copyto(d[edges[k]:edges[k + 1]], s_[edges[k]:edges[k + 1]]), range(workers)))
+
+
 def Write2NetCDFFile(ncfile, var, varLabel, dimensions, units=None, description=None):
-    """Create a float64 variable and fill it (md.py:768-775)."""
+    """Create a float64 variable and fill it (md.py:768-775).  Large fixed-size variables (C5's
+    history groups, 3 GB) are byte-swapped into the file's buffer on a thread pool and written
+    from it without scipy's second whole-array copy (same bytes on disk)."""
     v = np.asarray(var, dtype=np.float64)
     tmp = ncfile.createVariable(varLabel, "d", tuple(dimensions))
     if len(dimensions) and ncfile.dimensions.get(dimensions[0]) is None:
         tmp[: v.shape[0]] = v  # record (unlimited) dimension
+    elif v.nbytes >= FAST_FILL_BYTES and tmp.data.shape == v.shape:
+        buf = np.empty(v.shape, dtype=">f8").view(_WriteView)
+        _fill_big_endian(buf, v)
+        tmp.__dict__["data"] = buf
     else:
         tmp[:] = v
     if units:

@@ -100,6 +100,19 @@ struct Bath {
   double *d_sa = nullptr, *d_sx = nullptr, *d_sm = nullptr;
   int64_t s_cap = 0;
   bool s_complex = false;
+  // factors of the last complete streamed plan kept on the device (gle_noise_stream_retain): a
+  // later run replays them with new draws (gle_noise_stream_replay) instead of handing GBs of
+  // factors over PCIe again.  s_ret_ok: every segment of the plan in progress found room.
+  struct RetSeg {
+    bool shared;
+    int64_t w0, nw;
+    double* d_m;   // factor planes (Re then Im): nw x nc x nc per dense chunk, one nc x nc when shared
+    double* d_sc;  // shared: per-frequency scales (inside d_m's allocation)
+  };
+  std::vector<RetSeg> s_ret;
+  bool s_retain = false, s_ret_ok = false, s_ret_complete = false, s_ret_complex = false;
+  int64_t s_ret_cap = 0;
+  size_t s_ret_bytes = 0;
 };
 
 // One level of the memory-sum ladder for one bath.
@@ -161,6 +174,8 @@ struct Level {
   int64_t fT = 0;                // first step of its window
 };
 
+void free_retained(Bath& b, hipStream_t s);  // retained streamed-noise factors (gle_noise_stream_*)
+
 }  // namespace
 
 struct gle_handle {
@@ -191,6 +206,10 @@ struct gle_handle {
   unsigned long long* d_dbg = nullptr;  // GLE_CHAIN_DBG stamps
   double* d_zero = nullptr;            // zero row (chain S(t+1) tiles' unused level slots)
   bool dbg_no_ladder = false;  // GLE_DBG_NO_LADDER: skip the ladder blocks (timing experiments only)
+  // GLE_EXP_ONE=n (timing only, wrong results): one chain launch per step -- stage A's DOF tiles carry
+  // n extra nc x nc products per tile bath, its S(t+1) tiles a second product, no velocity-stage
+  // launch -- to price a one-launch step built from composed operators
+  int exp_one = 0;
   int bg_grid = 0;             // GLE_BG_GRID: cap of the far-field GEMM grid (grid-stride over items)
   // device timestamps of the profiled far-field launches ([start, end] pairs, s_memrealtime)
   unsigned long long* d_tst = nullptr;
@@ -1457,6 +1476,9 @@ int plan_chain(gle_handle* h) {
         y.X = b.d_Xcur + (stage == 2 ? b.vs : 0);
       }
       if (stage != 3) segs.push_back(y);  // the fused stage needs K0.p1 only (CH_OYB + CH_OYD / CH_OYE)
+      if (stage == 0)
+        for (int x = 0; x < h->exp_one; ++x)  // GLE_EXP_ONE (timing only)
+          segs.push_back(Seg{u, b.d_K0d + b.tofs[rt], 64, b.d_Xcur, (int)B, 0, 0, b.nks, 0});
       if (b.has_q && stage != 2)
         qsegs.push_back(Seg{CH_TB + u, b.d_Kqd + b.tofs[rt], 64, b.d_Xq + (stage == 0 ? 0 : b.vs), (int)B, 0, 0,
                             b.nks, 0});
@@ -1582,13 +1604,14 @@ int plan_chain(gle_handle* h) {
         }
         std::vector<Seg> segs{Seg{0, b.d_Kn + ((int64_t)rt * b.nks * b.nn + 1) * 64, b.nn * 64, b.d_NR, (int)B,
                                   b.NRS, 0, b.nks, (int)b.vs}};
+        if (h->exp_one) segs.push_back(segs[0]);  // GLE_EXP_ONE: K_2 p_t beside K_1 p_t (timing only)
         // GLE_EXP_AZ=n (experiment): n extra copies of every S(t+1) tile in stage A (each writes the
         // same values), to price stage-A tiles of one nc x nc product each
         int ncopy = 1;
         if (const char* e = gle_env("GLE_EXP_AZ")) ncopy += std::max(0, atoi(e));
         for (int v = 0; v < 2; ++v)
           for (int cp = 0; cp < ncopy; ++cp) {
-            int rc = fill_tasks(h, T, segs, 1, 0, b.nks, h->chA[v]);
+            int rc = fill_tasks(h, T, segs, 1, 0, (int64_t)segs.size() * b.nks, h->chA[v]);
             if (rc) return rc;
             h->chA[v].tiles.push_back(T);
           }
@@ -2549,7 +2572,9 @@ int step_end_impl(gle_handle* h, const double* fpot_host_T) {
     if (!h->has_dyn) return fail(h, GLE_ERR_STATE, "no potential force at q~");
     if (h->host_force_step) return fail(h, GLE_ERR_STATE, "step begun with a host force must end with one");
   }
-  if (h->fuse_bc && mode1 == 1) {
+  if (h->exp_one && mode1 == 1) {
+    // GLE_EXP_ONE: no velocity-stage launch (timing only)
+  } else if (h->fuse_bc && mode1 == 1) {
     if (h->bc_fpot) {
       FpotArgs fa{};
       fa.nph = (int32_t)h->nph;
@@ -2674,6 +2699,7 @@ int gle_create(const gle_config* cfg, gle_handle** out) {
   h->dt = cfg->dt;
   h->nphp = rup(h->nph, 8);
   h->dbg_no_ladder = gle_env("GLE_DBG_NO_LADDER") != nullptr;
+  if (const char* e = gle_env("GLE_EXP_ONE")) h->exp_one = std::max(0, atoi(e));
   if (const char* e = gle_env("GLE_FAR_AFRAC")) h->far_afrac = std::max(0.0, std::min(1.0, atof(e)));
   if (const char* e = gle_env("GLE_DBG_SKIP")) h->dbg_skip = atoi(e);
   h->dbg_no_chain = gle_env("GLE_DBG_NO_CHAIN") != nullptr;
@@ -2833,7 +2859,10 @@ int gle_destroy(gle_handle* h) {
     if (h->bg[i]) hipStreamSynchronize(h->bg[i]);
   if (h->stream) hipStreamSynchronize(h->stream);
   // streamed-noise scratch (tmalloc, not in allocs) of a stream that was begun and never ended
-  for (int j = 0; j < (int)h->baths.size(); ++j) gle_noise_stream_abort(h, j);
+  for (int j = 0; j < (int)h->baths.size(); ++j) {
+    gle_noise_stream_abort(h, j);
+    free_retained(h->baths[j], h->stream);
+  }
   for (void* p : h->allocs) {
     bounds_del(p);
     hipFree(p);
@@ -3397,6 +3426,91 @@ void free_stream(Bath& b) {
   }
   b.s_cap = 0;
 }
+
+// retained factors are read by products already queued on `s`: wait for them before freeing
+void free_retained(Bath& b, hipStream_t s) {
+  if (!b.s_ret.empty()) hipStreamSynchronize(s);
+  for (auto& r : b.s_ret) tfree(r.d_m);
+  b.s_ret.clear();
+  b.s_ret_bytes = 0;
+  b.s_ret_complete = false;
+}
+
+// device memory for one retained segment of `nd` doubles, or nullptr (then nothing of the plan in
+// progress is retained: the stream goes on through the chunk buffer)
+double* retain_alloc(gle_handle* h, Bath& b, size_t nd) {
+  if (!b.s_retain || !b.s_ret_ok) return nullptr;
+  double* p = nullptr;
+  if (tmalloc(&p, nd * 8) != hipSuccess) {
+    (void)hipGetLastError();
+    b.s_ret_ok = false;
+    free_retained(b, h->stream);
+    return nullptr;
+  }
+  b.s_ret_bytes += nd * 8;
+  return p;
+}
+
+// spectrum rows a_w += M_w x_w for frequencies [w0, w0 + nw) from device factors (one dense chunk,
+// nw <= s_cap), draws keyed by (frequency, DOF, global trajectory)
+void stream_dense(gle_handle* h, Bath& b, int64_t w0, int64_t nw, const double* dm, uint64_t seed, uint64_t toff) {
+  const int64_t B = h->B, nc = b.nc, rows = b.s_complex ? 2 * nc : nc;
+  const size_t nm = (size_t)nw * nc * nc;
+  hipMemsetAsync(b.d_sx, 0, (size_t)nw * b.ncp * B * 8, h->stream);
+  launch_philox_normal(b.d_sx, nw, b.ncp, nc, B, seed, toff, h->stream, w0);
+  launch_noise_gemm(dm, (int)nc, (int)nc, b.d_sx, b.ncp, (int)B, b.d_sa, (int)rows, 0, w0, (int)nw, h->stream);
+  if (b.s_complex)
+    launch_noise_gemm(dm + nm, (int)nc, (int)nc, b.d_sx, b.ncp, (int)B, b.d_sa, (int)rows, (int)nc, w0, (int)nw,
+                      h->stream);
+}
+
+// the same for nw frequencies sharing one factor F (dm: Re F then Im F) times scale dsc[w]
+void stream_shared(gle_handle* h, Bath& b, int64_t w0, int64_t nw, const double* dm, const double* dsc,
+                   uint64_t seed, uint64_t toff) {
+  const int64_t B = h->B, nc = b.nc, rows = b.s_complex ? 2 * nc : nc;
+  const size_t nm = (size_t)nc * nc;
+  for (int64_t o = 0; o < nw; o += b.s_cap) {
+    const int64_t n = std::min<int64_t>(b.s_cap, nw - o);
+    hipMemsetAsync(b.d_sx, 0, (size_t)n * b.ncp * B * 8, h->stream);
+    launch_philox_normal(b.d_sx, n, b.ncp, nc, B, seed, toff, h->stream, w0 + o);
+    launch_noise_gemm(dm, (int)nc, (int)nc, b.d_sx, b.ncp, (int)B, b.d_sa, (int)rows, 0, w0 + o, (int)n, h->stream,
+                      0, dsc + o);
+    if (b.s_complex)
+      launch_noise_gemm(dm + nm, (int)nc, (int)nc, b.d_sx, b.ncp, (int)B, b.d_sa, (int)rows, (int)nc, w0 + o, (int)n,
+                        h->stream, 0, dsc + o);
+  }
+}
+
+// spectrum / draw scratch of one stream (the factor chunk buffer only when factors arrive from the host)
+int stream_scratch(gle_handle* h, Bath& b, bool is_complex, int64_t cap, bool chunk_buffer) {
+  free_stream(b);
+  const int64_t nf = h->nmd / 2 + 1, B = h->B;
+  const int64_t rows = is_complex ? 2 * b.nc : b.nc;
+  b.s_complex = is_complex;
+  b.s_cap = std::min(cap, nf);
+  const size_t na = (size_t)nf * rows * B, nx = (size_t)b.s_cap * b.ncp * B,
+               nm = chunk_buffer ? (size_t)b.s_cap * b.nc * b.nc * (is_complex ? 2 : 1) : 0;
+  if (tmalloc((void**)&b.d_sa, na * 8) != hipSuccess || tmalloc((void**)&b.d_sx, nx * 8) != hipSuccess ||
+      (nm && tmalloc((void**)&b.d_sm, nm * 8) != hipSuccess)) {
+    free_stream(b);
+    return fail(h, GLE_ERR_NOMEM, "noise stream buffers (" + std::to_string((na + nx + nm) >> 17) + " MiB)");
+  }
+  HIPCHK(h, hipMemsetAsync(b.d_sa, 0, na * 8, h->stream));
+  return GLE_OK;
+}
+
+// mirror + FFT of the accumulated spectrum into the bath's noise; releases the scratch
+int stream_finish(gle_handle* h, Bath& b) {
+  const double scale = 1.0 / (h->dt * (double)h->nmd);  // dw/2pi (functions.py:51)
+  const int frc = launch_fft_noise(b.d_sa, b.d_noise, h->d_tw, h->nmd, b.nc, b.s_complex ? 2 * b.nc : b.nc, h->B,
+                                   b.s_complex ? 1 : 0, scale, h->stream);
+  const hipError_t e = hipStreamSynchronize(h->stream);
+  free_stream(b);
+  if (frc) return fail(h, GLE_ERR_UNSUP, "device noise FFT needs nmd a power of two <= 8192");
+  if (e != hipSuccess) return fail(h, GLE_ERR_HIP, std::string("noise stream: ") + hipGetErrorString(e));
+  b.noise_set = true;
+  return GLE_OK;
+}
 }  // namespace
 
 int gle_noise_stream_abort(gle_handle* h, int32_t bath) {
@@ -3404,7 +3518,9 @@ int gle_noise_stream_abort(gle_handle* h, int32_t bath) {
   if (rc) return rc;
   hipSetDevice(h->cfg.device);
   HIPCHK(h, hipStreamSynchronize(h->stream));  // chunks in flight read the scratch
-  free_stream(h->baths[bath]);
+  Bath& b = h->baths[bath];
+  if (b.d_sa && !b.s_ret_complete) free_retained(b, h->stream);  // a plan cut short is not kept
+  free_stream(b);
   return GLE_OK;
 }
 
@@ -3414,20 +3530,10 @@ int gle_noise_stream_begin(gle_handle* h, int32_t bath, int32_t is_complex, int6
   if (max_chunk < 1) return fail(h, GLE_ERR_ARG, "max_chunk must be >= 1");
   hipSetDevice(h->cfg.device);
   Bath& b = h->baths[bath];
-  free_stream(b);
-  const int64_t nf = h->nmd / 2 + 1, B = h->B;
-  const int64_t rows = is_complex ? 2 * b.nc : b.nc;
-  b.s_complex = is_complex != 0;
-  b.s_cap = std::min(max_chunk, nf);
-  const size_t na = (size_t)nf * rows * B, nx = (size_t)b.s_cap * b.ncp * B,
-               nm = (size_t)b.s_cap * b.nc * b.nc * (is_complex ? 2 : 1);
-  if (tmalloc((void**)&b.d_sa, na * 8) != hipSuccess || tmalloc((void**)&b.d_sx, nx * 8) != hipSuccess ||
-      tmalloc((void**)&b.d_sm, nm * 8) != hipSuccess) {
-    free_stream(b);
-    return fail(h, GLE_ERR_NOMEM, "noise stream buffers (" + std::to_string((na + nx + nm) >> 17) + " MiB)");
-  }
-  HIPCHK(h, hipMemsetAsync(b.d_sa, 0, na * 8, h->stream));
-  return GLE_OK;
+  free_retained(b, h->stream);  // a new plan replaces the retained one
+  b.s_ret_ok = b.s_retain;
+  b.s_ret_cap = max_chunk;
+  return stream_scratch(h, b, is_complex != 0, max_chunk, true);
 }
 
 int gle_noise_stream_chunk(gle_handle* h, int32_t bath, int64_t w0, int64_t nw, const double* m_re,
@@ -3440,17 +3546,13 @@ int gle_noise_stream_chunk(gle_handle* h, int32_t bath, int64_t w0, int64_t nw, 
   if (!m_re || w0 < 0 || nw < 1 || nw > b.s_cap || w0 + nw > nf || (b.s_complex && !m_im))
     return fail(h, GLE_ERR_ARG, "bad noise stream chunk");
   hipSetDevice(h->cfg.device);
-  const int64_t B = h->B, nc = b.nc, rows = b.s_complex ? 2 * nc : nc;
-  const size_t nm = (size_t)nw * nc * nc;
-  // the previous chunk's products read d_sx / d_sm: the copies below are stream-ordered after them
-  HIPCHK(h, hipMemcpyAsync(b.d_sm, m_re, nm * 8, hipMemcpyHostToDevice, h->stream));
-  if (b.s_complex) HIPCHK(h, hipMemcpyAsync(b.d_sm + nm, m_im, nm * 8, hipMemcpyHostToDevice, h->stream));
-  HIPCHK(h, hipMemsetAsync(b.d_sx, 0, (size_t)nw * b.ncp * B * 8, h->stream));
-  launch_philox_normal(b.d_sx, nw, b.ncp, nc, B, seed, traj_offset, h->stream, w0);
-  launch_noise_gemm(b.d_sm, (int)nc, (int)nc, b.d_sx, b.ncp, (int)B, b.d_sa, (int)rows, 0, w0, (int)nw, h->stream);
-  if (b.s_complex)
-    launch_noise_gemm(b.d_sm + nm, (int)nc, (int)nc, b.d_sx, b.ncp, (int)B, b.d_sa, (int)rows, (int)nc, w0, (int)nw,
-                      h->stream);
+  const size_t nm = (size_t)nw * b.nc * b.nc;
+  double* dm = retain_alloc(h, b, nm * (b.s_complex ? 2 : 1));
+  if (dm) b.s_ret.push_back({false, w0, nw, dm, nullptr});
+  else dm = b.d_sm;  // the previous chunk's products read it: the copies are stream-ordered after them
+  HIPCHK(h, hipMemcpyAsync(dm, m_re, nm * 8, hipMemcpyHostToDevice, h->stream));
+  if (b.s_complex) HIPCHK(h, hipMemcpyAsync(dm + nm, m_im, nm * 8, hipMemcpyHostToDevice, h->stream));
+  stream_dense(h, b, w0, nw, dm, seed, traj_offset);
   HIPCHK(h, hipStreamSynchronize(h->stream));  // the caller reuses its host chunk buffers
   return GLE_OK;
 }
@@ -3465,26 +3567,22 @@ int gle_noise_stream_shared(gle_handle* h, int32_t bath, int64_t w0, int64_t nw,
   if (!m_re || !scale || w0 < 0 || nw < 1 || w0 + nw > nf || (b.s_complex && !m_im))
     return fail(h, GLE_ERR_ARG, "bad shared noise stream range");
   hipSetDevice(h->cfg.device);
-  const int64_t B = h->B, nc = b.nc, rows = b.s_complex ? 2 * nc : nc;
-  const size_t nm = (size_t)nc * nc;
+  const size_t nm = (size_t)b.nc * b.nc, np = nm * (b.s_complex ? 2 : 1);
   DevTmp d_sc;
-  if (tmalloc(&d_sc.p, (size_t)nw * 8) != hipSuccess) return fail(h, GLE_ERR_NOMEM, "noise stream scales");
-  // the shared factor takes the chunk matrix buffer's first slot(s): stream-ordered after the
-  // previous chunk's products that read it
-  HIPCHK(h, hipMemcpyAsync(b.d_sm, m_re, nm * 8, hipMemcpyHostToDevice, h->stream));
-  if (b.s_complex) HIPCHK(h, hipMemcpyAsync(b.d_sm + nm, m_im, nm * 8, hipMemcpyHostToDevice, h->stream));
-  HIPCHK(h, hipMemcpyAsync(d_sc.p, scale, (size_t)nw * 8, hipMemcpyHostToDevice, h->stream));
-  const double* dsc = (const double*)d_sc.p;
-  for (int64_t o = 0; o < nw; o += b.s_cap) {
-    const int64_t n = std::min<int64_t>(b.s_cap, nw - o);
-    HIPCHK(h, hipMemsetAsync(b.d_sx, 0, (size_t)n * b.ncp * B * 8, h->stream));
-    launch_philox_normal(b.d_sx, n, b.ncp, nc, B, seed, traj_offset, h->stream, w0 + o);
-    launch_noise_gemm(b.d_sm, (int)nc, (int)nc, b.d_sx, b.ncp, (int)B, b.d_sa, (int)rows, 0, w0 + o, (int)n,
-                      h->stream, 0, dsc + o);
-    if (b.s_complex)
-      launch_noise_gemm(b.d_sm + nm, (int)nc, (int)nc, b.d_sx, b.ncp, (int)B, b.d_sa, (int)rows, (int)nc, w0 + o,
-                        (int)n, h->stream, 0, dsc + o);
+  double* dm = retain_alloc(h, b, np + nw);
+  double* dsc = nullptr;
+  if (dm) {
+    dsc = dm + np;
+    b.s_ret.push_back({true, w0, nw, dm, dsc});
+  } else {
+    if (tmalloc(&d_sc.p, (size_t)nw * 8) != hipSuccess) return fail(h, GLE_ERR_NOMEM, "noise stream scales");
+    dm = b.d_sm;  // the shared factor takes the chunk buffer's first slot(s), stream-ordered
+    dsc = (double*)d_sc.p;
   }
+  HIPCHK(h, hipMemcpyAsync(dm, m_re, nm * 8, hipMemcpyHostToDevice, h->stream));
+  if (b.s_complex) HIPCHK(h, hipMemcpyAsync(dm + nm, m_im, nm * 8, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(dsc, scale, (size_t)nw * 8, hipMemcpyHostToDevice, h->stream));
+  stream_shared(h, b, w0, nw, dm, dsc, seed, traj_offset);
   HIPCHK(h, hipStreamSynchronize(h->stream));  // the caller's host buffers and the scale scratch
   return GLE_OK;
 }
@@ -3495,15 +3593,47 @@ int gle_noise_stream_end(gle_handle* h, int32_t bath) {
   Bath& b = h->baths[bath];
   if (!b.d_sa) return fail(h, GLE_ERR_STATE, "gle_noise_stream_begin first");
   hipSetDevice(h->cfg.device);
-  const double scale = 1.0 / (h->dt * (double)h->nmd);  // dw/2pi (functions.py:51)
-  const int frc = launch_fft_noise(b.d_sa, b.d_noise, h->d_tw, h->nmd, b.nc, b.s_complex ? 2 * b.nc : b.nc, h->B,
-                                   b.s_complex ? 1 : 0, scale, h->stream);
-  const hipError_t e = hipStreamSynchronize(h->stream);
-  free_stream(b);
-  if (frc) return fail(h, GLE_ERR_UNSUP, "device noise FFT needs nmd a power of two <= 8192");
-  if (e != hipSuccess) return fail(h, GLE_ERR_HIP, std::string("noise stream: ") + hipGetErrorString(e));
-  b.noise_set = true;
+  if (b.s_retain && b.s_ret_ok) {
+    b.s_ret_complete = true;
+    b.s_ret_complex = b.s_complex;
+  } else {
+    free_retained(b, h->stream);
+  }
+  return stream_finish(h, b);
+}
+
+int gle_noise_stream_retain(gle_handle* h, int32_t bath, int32_t retain) {
+  int rc = check_bath(h, bath);
+  if (rc) return rc;
+  hipSetDevice(h->cfg.device);
+  Bath& b = h->baths[bath];
+  b.s_retain = retain != 0;
+  if (!b.s_retain) free_retained(b, h->stream);
   return GLE_OK;
+}
+
+int gle_noise_stream_retained(gle_handle* h, int32_t bath, int64_t* bytes) {
+  int rc = check_bath(h, bath);
+  if (rc) return rc;
+  if (!bytes) return fail(h, GLE_ERR_ARG, "null output");
+  const Bath& b = h->baths[bath];
+  *bytes = b.s_ret_complete ? (int64_t)b.s_ret_bytes : 0;
+  return GLE_OK;
+}
+
+int gle_noise_stream_replay(gle_handle* h, int32_t bath, uint64_t seed, uint64_t traj_offset) {
+  int rc = check_bath(h, bath);
+  if (rc) return rc;
+  Bath& b = h->baths[bath];
+  if (!b.s_ret_complete) return fail(h, GLE_ERR_STATE, "no retained noise plan (gle_noise_stream_retain)");
+  hipSetDevice(h->cfg.device);
+  rc = stream_scratch(h, b, b.s_ret_complex, b.s_ret_cap, false);
+  if (rc) return rc;
+  for (const auto& r : b.s_ret) {
+    if (r.shared) stream_shared(h, b, r.w0, r.nw, r.d_m, r.d_sc, seed, traj_offset);
+    else stream_dense(h, b, r.w0, r.nw, r.d_m, seed, traj_offset);
+  }
+  return stream_finish(h, b);
 }
 
 int gle_step_begin(gle_handle* h, const double* fpot, double* q_tilde_out) {
@@ -3842,6 +3972,57 @@ int gle_get_record_history(gle_handle* h, double* phis, double* qhis, int64_t* m
     int rc = hist_to_host(h, k == 0 ? h->d_rec_hp : h->d_rec_hq, B, n * B, (int)R, h->t - 1, (int)R, (int)n, out);
     if (rc) return rc;
   }
+  return GLE_OK;
+}
+
+int gle_get_full_history(gle_handle* h, int64_t ml, double* phis, double* qhis) {
+  if (!h || ml < 0) return GLE_ERR_ARG;
+  if (!phis && !qhis) return GLE_OK;
+  if (!h->frozen) return fail(h, GLE_ERR_STATE, "no state yet");
+  hipSetDevice(h->cfg.device);
+  const int64_t B = h->B, n = h->nph, per = ml * n;
+  if (per == 0) return GLE_OK;
+  // trajectory chunks through a <= 256 MB device buffer; the copies and the next chunk's kernels
+  // are ordered on the handle's stream (one wait at the end)
+  const int64_t nbc = std::max<int64_t>(1, std::min<int64_t>(B, (256ll << 20) / (per * 8)));
+  double* d_tmp = nullptr;
+  HIPCHK(h, tmalloc((void**)&d_tmp, (size_t)(nbc * per * 8)));
+  const bool rec = (h->rec_flags & GLE_REC_HIST) && h->d_rec_hp;
+  hipError_t e = hipSuccess;
+  for (int k = 0; k < 2 && e == hipSuccess; ++k) {
+    double* out = k == 0 ? phis : qhis;
+    if (!out) continue;
+    for (int64_t b0 = 0; b0 < B && e == hipSuccess; b0 += nbc) {
+      const int nb = (int)std::min<int64_t>(nbc, B - b0);
+      launch_hist_full(rec ? (k == 0 ? h->d_rec_hp : h->d_rec_hq) : nullptr, (int)B, h->rec_ml, h->t - 1, (int)ml,
+                       (int)n, (int)b0, nb, d_tmp, h->stream);
+      if (k == 0)  // the friction's own rings win on bath DOFs, later baths over earlier ones
+        for (const Bath& b : h->baths)
+          launch_hist_overlay(b.d_H, b.ldh, (int)B, b.R, h->t - 1, b.d_inv, (int)std::min<int64_t>(ml, b.ml), (int)n,
+                              (int)b0, nb, (int)ml, d_tmp, h->stream);
+      e = hipMemcpyAsync(out + b0 * per, d_tmp, (size_t)nb * per * 8, hipMemcpyDeviceToHost, h->stream);
+    }
+  }
+  const hipError_t es = hipStreamSynchronize(h->stream);
+  tfree(d_tmp);
+  if (e == hipSuccess) e = es;
+  if (e != hipSuccess) return fail(h, GLE_ERR_HIP, std::string("full history copy: ") + hipGetErrorString(e));
+  return GLE_OK;
+}
+
+int gle_host_alloc(int64_t bytes, void** p) {
+  if (!p || bytes < 0) return GLE_ERR_ARG;
+  *p = nullptr;
+  const hipError_t e = hipHostMalloc(p, (size_t)std::max<int64_t>(bytes, 8), hipHostMallocDefault);
+  if (e != hipSuccess) {
+    *p = nullptr;
+    return fail(nullptr, GLE_ERR_NOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+  }
+  return GLE_OK;
+}
+
+int gle_host_free(void* p) {
+  if (p && hipHostFree(p) != hipSuccess) return GLE_ERR_HIP;
   return GLE_OK;
 }
 

@@ -354,6 +354,10 @@ void launch_near_fill(const double* H, int64_t ldh, int R, int B, int ncp, doubl
                       int64_t t, hipStream_t s);
 void launch_ring_copy(double* H, int64_t ldh, int R, int B, int nc, int64_t tau0, int nt, double* buf,
                       int dir, hipStream_t s);
+void launch_hist_full(const double* rec, int B, int R, int64_t tau0, int nt, int nph, int b0, int nb, double* out,
+                      hipStream_t s);
+void launch_hist_overlay(const double* H, int64_t ldh, int B, int R, int64_t tau0, const int32_t* inv, int nrow,
+                         int nph, int b0, int nb, int nt, double* out, hipStream_t s);
 void launch_hist_out(const double* src, int64_t ks, int64_t ss, int R, int64_t tau0, int nt, int nk, int b0, int nb,
                      double* out, hipStream_t s);
 // ts (profiling, may be null): [0] <- min over workgroups of the start, [1] <- max of the end

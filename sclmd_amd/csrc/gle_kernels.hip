@@ -614,6 +614,54 @@ void launch_hist_out(const double* src, int64_t ks, int64_t ss, int R, int64_t t
   hist_out_kernel<<<(unsigned)blocks, 256, 0, s>>>(src, ks, ss, R, tau0, nt, nk, b0, nb, out);
 }
 
+// md.phis / md.qhis rows (newest first) of trajectories [b0, b0 + nb) into out [nb][nt][nph]: row i
+// = slot (tau0 - i) mod R of the full-DOF recording ring rec [R][nph][B] for i < R, zero past the
+// ring (or everywhere when rec is null)
+__global__ void hist_full_kernel(const double* __restrict__ rec, int B, int R, int64_t tau0, int nt, int nph, int b0,
+                                 int nb, double* __restrict__ out) {
+  const int64_t n = (int64_t)nb * nt * nph;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = e % nph;
+    const int64_t i = (e / nph) % nt;
+    const int64_t bb = e / ((int64_t)nph * nt);
+    out[e] = (rec && i < R) ? rec[(pmod(tau0 - i, R) * nph + k) * B + b0 + bb] : 0.0;
+  }
+}
+
+// the bath DOFs' rows i < nrow of the same output from the bath's history ring H (row k of the bath
+// at H[k * ldh + slot * B + b]); inv: DOF -> bath row or -1
+__global__ void hist_overlay_kernel(const double* __restrict__ H, int64_t ldh, int B, int R, int64_t tau0,
+                                    const int32_t* __restrict__ inv, int nrow, int nph, int b0, int nb, int nt,
+                                    double* __restrict__ out) {
+  const int64_t n = (int64_t)nb * nrow * nph;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = e % nph;
+    const int k = inv[c];
+    if (k < 0) continue;
+    const int64_t i = (e / nph) % nrow;
+    const int64_t bb = e / ((int64_t)nph * nrow);
+    out[(bb * nt + i) * nph + c] = H[k * ldh + pmod(tau0 - i, R) * B + b0 + bb];
+  }
+}
+
+void launch_hist_full(const double* rec, int B, int R, int64_t tau0, int nt, int nph, int b0, int nb, double* out,
+                      hipStream_t s) {
+  const int64_t n = (int64_t)nb * nt * nph;
+  if (n <= 0) return;
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 8192);
+  hist_full_kernel<<<(unsigned)blocks, 256, 0, s>>>(rec, B, R, tau0, nt, nph, b0, nb, out);
+}
+
+void launch_hist_overlay(const double* H, int64_t ldh, int B, int R, int64_t tau0, const int32_t* inv, int nrow,
+                         int nph, int b0, int nb, int nt, double* out, hipStream_t s) {
+  const int64_t n = (int64_t)nb * nrow * nph;
+  if (n <= 0) return;
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 8192);
+  hist_overlay_kernel<<<(unsigned)blocks, 256, 0, s>>>(H, ldh, B, R, tau0, inv, nrow, nph, b0, nb, nt, out);
+}
+
 // near ring (slot-major [NRS][vs], the chain's compact copy of the newest p): slots of times
 // t, t-1, ..., t-NRS+1 from the history ring
 __global__ void near_fill_kernel(const double* __restrict__ H, int64_t ldh, int R, int B, int ncp,

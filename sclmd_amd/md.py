@@ -11,6 +11,7 @@ trajectory axis is added.
 """
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -474,8 +475,9 @@ class md:
     # factors above this size are streamed to the device by frequency chunk instead of being held
     # there whole (C5: 4097 x 1000^2 doubles per bath beside ~200 GB of spectral kernels)
     noise_stream_bytes = 4 << 30
-    # streamed baths keep their dense factors in host memory between runs (C5: ~11 GB for the three
-    # baths, against ~46 s of factorisation per run without the cache)
+    # streamed baths keep their dense factors between runs (C5: ~11 GB for the three baths, against
+    # ~46 s of factorisation per run without them): in device memory beside the plan when they fit
+    # (gle_noise_stream_retain / _replay: no factor crosses PCIe after the first run), else on the host
     noise_factor_cache = True
     # largest fixed-size variable of an MD{j}.nc file (NetCDF classic format, scipy.io)
     nc_var_limit = 2**31 - 4096
@@ -494,15 +496,27 @@ class md:
         fac_bytes = nfreq * b.nc * b.nc * 8 * (2 if b.kind == "ebath" else 1)
         if self.noise_mode == "device" and fac_bytes > self.noise_stream_bytes:
             # zero frequencies skipped, shared-matrix frequencies as one factor and scales, dense
-            # factors computed once and kept for the following runs (only the draws change per run)
-            cache = None
-            if self.noise_factor_cache:
+            # factors computed once and kept for the following runs (only the draws change per run,
+            # md.py:569-570): on the device when they fit there (the stepper replays them with new
+            # draws), else in host memory
+            seed = self._noise_seed(i, run)
+            if not self.noise_factor_cache:
+                st.noise_stream_plan(i, _noise.stream_factor_plan(b), b.kind == "ebath", seed, self.traj_offset)
+            else:
                 key = b._noise_key()
-                if getattr(b, "_stream_cache_key", None) != key:
-                    b._stream_cache, b._stream_cache_key = {}, key
-                cache = b._stream_cache
-            st.noise_stream_plan(i, _noise.stream_factor_plan(b, cache=cache), b.kind == "ebath",
-                                 self._noise_seed(i, run), self.traj_offset)
+                dev = st.__dict__.setdefault("noise_plan_keys", {})  # bath -> key of its retained plan
+                if dev.get(i) == key and st.noise_stream_retained(i):
+                    st.noise_stream_replay(i, seed, self.traj_offset)
+                else:
+                    dev.pop(i, None)
+                    if getattr(b, "_stream_cache_key", None) != key:
+                        b._stream_cache, b._stream_cache_key = {}, key
+                    st.noise_stream_retain(i, True)
+                    st.noise_stream_plan(i, _noise.stream_factor_plan(b, cache=b._stream_cache), b.kind == "ebath",
+                                         seed, self.traj_offset)
+                    if st.noise_stream_retained(i):
+                        dev[i] = key
+                        b._stream_cache, b._stream_cache_key = None, None  # the device copy serves
             b._noise_src = (st, i)
             b._noise_version = getattr(b, "_noise_version", 0) + 1
             self._noise_versions[i] = b._noise_version
@@ -684,26 +698,32 @@ class md:
             out[:, :n] = qh[:, :n]
         return out[0] if self.ntraj == 1 else out
 
-    def _histories(self):
-        """(phis, qhis) as md.phis / md.qhis return them, with one device read of the recorded
-        histories for both (the properties read them once each and copy them into zeroed arrays:
-        C5's 2 x 3.1 GB, most of a dump's time)."""
+    def _histories(self, pinned=False):
+        """(phis, qhis) as md.phis / md.qhis return them, in one device read (gle_get_full_history:
+        the recorded histories with the baths' own rings on their DOFs, transposed on the device).
+        pinned: into this md's page-locked snapshot buffers (reused by every dump; C5: 2 x 3.1 GB
+        at the link's rate instead of pageable copies)."""
         st = self._ensure_device()
-        if not ((getattr(self, "_rec_applied", 0) or 0) & _native.REC_HIST):
-            return np.asarray(self.phis), np.asarray(self.qhis)
-        ph, qh = st.get_record_history()                 # (ntraj, ml_r, nph) each, fresh arrays
-        if ph.shape[1] != self.ml:
-            out_p = np.zeros((self.ntraj, self.ml, self.nph))
-            out_q = np.zeros((self.ntraj, self.ml, self.nph))
-            n = min(self.ml, ph.shape[1])
-            out_p[:, :n], out_q[:, :n] = ph[:, :n], qh[:, :n]
-            ph, qh = out_p, out_q
-        for i, b in enumerate(self.baths):                # the bath rings the friction reads
-            h = st.get_history(i)                         # (ntraj, ml_b, nc_b)
-            ph[:, : h.shape[1], np.asarray(b.cids)] = h
+        t0 = time.perf_counter()
+        outs = (None, None)
+        if pinned:
+            shp = (self.ntraj, self.ml, self.nph)
+            bufs = getattr(self, "_snap_bufs", None)
+            if bufs is None or bufs[0].array.shape != shp:
+                self._free_snap_bufs()
+                bufs = self._snap_bufs = (_native.HostBuffer(shp), _native.HostBuffer(shp))
+            outs = (bufs[0].array, bufs[1].array)
+        ph, qh = st.get_full_history(self.ml, *outs)
+        self._tick("dump_histories", time.perf_counter() - t0)
         if self.ntraj == 1:
             return ph[0], qh[0]
         return ph, qh
+
+    def _free_snap_bufs(self):
+        """Release the dump's page-locked buffers (the background writer must be joined first)."""
+        for b in getattr(self, "_snap_bufs", None) or ():
+            b.free()
+        self._snap_bufs = None
 
     def _load_phis(self, phis, qhis=None):
         st = self._ensure_device()
@@ -760,8 +780,12 @@ class md:
         call); with async_dump the file itself is written on a background thread, joined before
         the next dump, before a checkpoint file is read or removed, at the end of Run and in
         close() -- a write error is raised there."""
+        t0 = time.perf_counter()
         self._join_dump()
+        t1 = time.perf_counter()
         snap = self._dump_snapshot(ipie, id)
+        self._tick("dump_join", t1 - t0)
+        self._tick("dump_snapshot", time.perf_counter() - t1)
         if not self.async_dump:
             self._write_snapshot(snap)
             return
@@ -838,7 +862,7 @@ class md:
         var.append(("q", np.array(self.q), tr + ("nph",)))
         var.append(("t", np.array([self.t]), ("one",)))
         var.append(("ipie", np.array([ipie]), ("one",)))
-        phis, qhis = self._histories()
+        phis, qhis = self._histories(pinned=True)
         if multi and phis.nbytes >= self.nc_var_limit:
             # a classic-format variable holds < 2 GiB (C5: 32 x 4096 x 3000 doubles = 3.1 GB): the
             # ensemble's histories are split into fixed-size variables of whole trajectories,
@@ -859,6 +883,7 @@ class md:
     def _write_snapshot(self, snap):
         from . import checkpoint as C
 
+        t0 = time.perf_counter()
         fn = snap["fn"]
         f, tmp = C.open_for_write(fn)
         try:
@@ -874,6 +899,12 @@ class md:
         # what this process wrote: the next run's start can skip reading its own file back, and an
         # unchanged second dump of the same piece need not be rewritten
         self._last_dump = (fn, st_.st_mtime_ns, st_.st_size, snap["t"], snap["ipie"], snap["savep"])
+        self._tick("dump_write", time.perf_counter() - t0)
+
+    def _tick(self, name, dt):
+        """Wall time of the named host phase, accumulated (md.phase_times: where a Run's time goes)."""
+        pt = self.__dict__.setdefault("phase_times", {})
+        pt[name] = pt.get(name, 0.0) + dt
 
     def _read_poweratomlist(self, fn):
         """poweratomlist (natomlist, nmd, 2) from an MD{j}.nc file in either layout: this build's
@@ -1112,6 +1143,7 @@ class md:
         for b in self.baths:  # dense streamed factors (C5: ~11 GB of host memory)
             if getattr(b, "_stream_cache", None) is not None:
                 b._stream_cache, b._stream_cache_key = None, None
+        self._free_snap_bufs()  # after the join above: the writer reads them
         if self._st is not None:
             self._pull()
             self._st.close()

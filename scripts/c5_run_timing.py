@@ -55,6 +55,7 @@ def main():
             finally:
                 if name == "dump":
                     m._st.sync()
+                    phases()
                 parts[cur["run"]][name] += time.perf_counter() - t0
                 log("run %d %s %.2fs" % (cur["run"], name, time.perf_counter() - t0))
         return w
@@ -82,9 +83,20 @@ def main():
 
     m.steps = steps
     m.dump = timed("dump", m.dump)
+    seen = {}
+
+    def phases():  # md.phase_times accumulated since the last call, per run
+        pt = dict(getattr(m, "phase_times", {}))
+        for k, v in pt.items():
+            d = v - seen.get(k, 0.0)
+            if d:
+                parts[cur["run"]]["phase_" + k] += d
+        seen.update(pt)
+
     t_run = time.perf_counter()
     m.Run()
     t_end = time.perf_counter()
+    phases()
     kappa = [list(map(float, k)) for k in m.kappa_runs]
     m.close()
     os.chdir(cwd)

@@ -194,3 +194,34 @@ def test_ensemble_history_record_layout_continues(tmp_path, monkeypatch):
     p2, q2, t2, kap2 = _final(m)
     m.close()
     assert t2 == t and rel(q2, q) < 1e-10 and rel(p2, p) < 1e-10 and rel(kap2[-1], kap[-1]) < 1e-9
+
+
+def test_full_history_getter_matches_host_composition(tmp_path, monkeypatch):
+    """gle_get_full_history (the dump's one device read: recorded p / q histories with every bath's
+    own ring on its DOFs, transposed on the device, optionally into page-locked buffers) equals the
+    host composition md.phis / md.qhis make from gle_get_record_history and gle_get_history --
+    before md.Run (no recording: bath rings only), and after it (recorded), with an extra bath of
+    shorter memory overlapping another's DOFs (the later bath wins on its rows)."""
+    from sclmd_amd import synthetic
+
+    monkeypatch.chdir(tmp_path)
+    m = _md(0, 1, npie=1, ntraj=3)
+    b0 = m.baths[0]
+    extra = synthetic.make_phbath(m.T, sorted({int(c) for c in b0.cids[:6]} | {0, 1}), 4, m.nmd, np.random.default_rng(3),
+                                  dt=m.dt, nw=60)
+    m.AddBath(extra)
+    m.initialise()
+    m.ResetHis()
+    for i in range(len(m.baths)):
+        m.gen_noise(i, 0)
+    m.steps(40)
+    for pinned in (False, True):
+        ph, qh = m._histories(pinned=pinned)
+        assert np.array_equal(ph, m.phis) and np.array_equal(qh, m.qhis)
+    assert np.abs(qh).max() == 0.0 and np.abs(ph).max() > 0.0
+    m.Run()
+    for pinned in (False, True):
+        ph, qh = m._histories(pinned=pinned)
+        assert np.array_equal(ph, m.phis) and np.array_equal(qh, m.qhis)
+    assert np.abs(qh).max() > 0.0
+    m.close()

@@ -161,3 +161,75 @@ def test_stream_plan_equals_chunks_and_reuses_cache(kind, monkeypatch):
     assert not calls
     assert np.array_equal(again, got)
     assert rel(other, got) > 0.1
+
+
+@pytest.mark.parametrize("kind", ["ph", "e"])
+def test_retained_plan_replay_equals_stream(kind, monkeypatch):
+    """Device-retained factors (gle_noise_stream_retain / _replay): replaying the retained plan with a
+    seed gives exactly the noise of streaming the plan again with that seed; md.gen_noise's later runs
+    replay (no factorisation, no host factor cache kept) and give the noise a fresh stream gives."""
+    from sclmd_amd import _native as N
+    from sclmd_amd import md as MD
+    from sclmd_amd import noise as Nz
+    from sclmd_amd import synthetic
+
+    rng = np.random.default_rng(9)
+    nmd, B = 1024, 6
+    if kind == "ph":
+        b = synthetic.make_phbath(300.0, list(range(36)), 8, nmd, rng, nw=40)
+    else:
+        b = synthetic.make_biased_ebath(300.0, list(range(30)), nmd, rng)
+    cplx = kind == "e"
+
+    def stepper():
+        st = N.Stepper(b.nc, B, nmd, synthetic.DT, 0)
+        st.add_bath(N.GLE_BATH_PHONON, np.arange(b.nc), np.zeros((1, b.nc, b.nc)))
+        return st
+
+    ref = stepper()
+    want = {}
+    for sd in (31, 32):
+        ref.noise_stream_plan(0, Nz.stream_factor_plan(b, chunk=16), cplx, seed=sd, traj_offset=4, max_chunk=16)
+        want[sd] = ref.get_noise(0)
+    ref.close()
+    st = stepper()
+    assert st.noise_stream_retained(0) == 0
+    with pytest.raises(N.GLEError):
+        st.noise_stream_replay(0, 31, 4)
+    st.noise_stream_retain(0, True)
+    st.noise_stream_plan(0, Nz.stream_factor_plan(b, chunk=16), cplx, seed=31, traj_offset=4, max_chunk=16)
+    assert np.array_equal(st.get_noise(0), want[31])
+    assert st.noise_stream_retained(0) > 0
+    st.noise_stream_replay(0, 32, 4)
+    assert np.array_equal(st.get_noise(0), want[32])
+    st.noise_stream_replay(0, 31, 4)
+    assert np.array_equal(st.get_noise(0), want[31])
+    st.noise_stream_retain(0, False)
+    assert st.noise_stream_retained(0) == 0
+    st.close()
+
+    # md: the second run's noise comes from the retained plan
+    dyn, axyz, baths, meta = synthetic.junction("C5", natom=12, ml=8, nmd=nmd, nw=60, seed=8)
+    m = MD.md(meta["dt"], meta["nmd"], meta["T"], axyz=axyz, dyn=dyn, ntraj=B, seed=3, noise_mode="device",
+              verbose=False)
+    m.noise_stream_bytes = 0  # force the streamed path
+    for bb in baths:
+        m.AddBath(bb)
+    m.initialise()
+    i = [k for k, bb in enumerate(baths) if (bb.kind == "ebath") == cplx][0]
+    bi = baths[i]
+    m.gen_noise(i, 0)
+    assert m._st.noise_stream_retained(i) > 0 and getattr(bi, "_stream_cache", None) is None
+    calls = []
+    monkeypatch.setattr(Nz, "dense_factor", lambda a: calls.append(1) or Nz.positive_factor(a))
+    m.gen_noise(i, 1)
+    got = m._st.get_noise(i)
+    seed1 = m._noise_seed(i, 1)
+    m.close()
+    assert not calls
+    monkeypatch.undo()
+    fresh = N.Stepper(bi.nc, B, nmd, meta["dt"], 0)
+    fresh.add_bath(N.GLE_BATH_PHONON, np.arange(bi.nc), np.zeros((1, bi.nc, bi.nc)))
+    fresh.noise_stream_plan(0, Nz.stream_factor_plan(bi), cplx, seed=seed1, traj_offset=0)
+    assert np.array_equal(got, fresh.get_noise(0))
+    fresh.close()
