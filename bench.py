@@ -401,7 +401,10 @@ def main():
                    "ntraj_per_gpu": args.ntraj, "ntraj_total": world * args.ntraj,
                    "block_len": plan["block_len"], "far_mode": plan["far_mode"],
                    "far_schedule": "fused" if detail["far_fused"] else "background",
-                   "plan_class": detail["plan_class"], "parallelism": "ensemble-dp%d" % world},
+                   "plan_class": detail["plan_class"],
+                   "chain_launches_per_step": 1 if detail.get("composed_step") else (
+                       2 + (1 if detail.get("fpot_launch") else 0)),
+                   "parallelism": "ensemble-dp%d" % world},
         "value_per_gpu": value / world,
         "runtime_libs": loaded_runtime(),
         "setup_s": setup_s,
@@ -487,7 +490,8 @@ def main():
         # us_per_step = chain kernel time per step (beside the far field, so > its time alone)
         cms = prof["chain_ms"]
         res["chain_roofline"] = {
-            "kernel": "chain_kernel (per-step md.vv stages: A and the fused velocity stage)",
+            "kernel": "chain_kernel (per-step md.vv: %s)" % (
+                "one composed launch" if detail.get("composed_step") else "stage A and the fused velocity stage"),
             "bound": "mfma", "achieved": prof["chain_flops"] / (cms * 1e-3) / 1e12,
             "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": prof["chain_flops"] / (cms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS,

@@ -316,7 +316,20 @@ int gle_plan_detail(gle_handle* h, int32_t* plan_class, int32_t* fused_waves, do
 #define GLE_PLAN_FUSED_BC 1
 #define GLE_PLAN_FPOT_LAUNCH 2
 #define GLE_PLAN_FAR_FUSED 4
+/* GLE_PLAN_COMPOSED_STEP: gle_run steps with one chain launch per step (small-bath harmonic plans
+ * without a biased electron bath): md.vv is linear in (p_t, q_t) and the bath vectors, so p_{t+1}
+ * is one product of composed operators (precomputed at plan time) and q_{t+1} = q~ follows from the
+ * step's own K0.p_t and dyn.q_t (same result to fp64 rounding; steps with a host force, gle_step_begin
+ * / gle_step_end, keep the two-launch path).  The potential force at q~ is evaluated fresh: the
+ * reference's md.potforce reuses the force at q0 when 0 < max|q~ - q0| < 1e-9 (md.py:767-779); such
+ * steps are counted, see gle_cache_audit. */
+#define GLE_PLAN_COMPOSED_STEP 8
 int gle_plan_flags(gle_handle* h, int32_t* flags);
+/* Composed steps (GLE_PLAN_COMPOSED_STEP) at which md.potforce's cache rule (sameq, md.py:767-779)
+ * would have reused a force at a point within 1e-9 but not equal to the evaluation point: counts[0]
+ * at q~ (0 < max|q~ - q_t| < 1e-9 for some trajectory), counts[1] at q_{t+1} after a constraint; the
+ * composed step evaluated the force fresh there (a difference below dyn x 1e-9).  Cumulative. */
+int gle_cache_audit(gle_handle* h, int64_t* counts);
 /* Memory-sum ladder levels: *nlevel = number of levels; for the first nmax levels the block length
  * P[l] and the blocks of that level issued since profiling was enabled (a block issued in pieces
  * counts its pieces' share).  Over a window of K steps a level in steady state issues K / P. */

@@ -35,7 +35,7 @@ EXPORTS = [
     "gle_noise_stream_chunk", "gle_noise_stream_end", "gle_set_plan_class", "gle_plan_detail", "gle_plan_flags",
     "gle_comm_allreduce", "gle_noise_stream_abort", "gle_device_mem_info", "gle_noise_stream_shared",
     "gle_noise_stream_retain", "gle_noise_stream_retained", "gle_noise_stream_replay", "gle_get_full_history",
-    "gle_host_alloc", "gle_host_free",
+    "gle_host_alloc", "gle_host_free", "gle_cache_audit",
 ]
 
 REC_P, REC_Q, REC_F, REC_HIST = 1, 2, 4, 8
@@ -126,6 +126,7 @@ _SIGS = {
     "gle_get_full_history": (ctypes.c_int, [_P, ctypes.c_int64, _D, _D]),
     "gle_host_alloc": (ctypes.c_int, [ctypes.c_int64, ctypes.POINTER(_P)]),
     "gle_host_free": (ctypes.c_int, [_P]),
+    "gle_cache_audit": (ctypes.c_int, [_P, _I64]),
     "gle_noise_stream_retain": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32]),
     "gle_noise_stream_retained": (ctypes.c_int, [_P, ctypes.c_int32, _I64]),
     "gle_noise_stream_replay": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint64]),
@@ -617,7 +618,15 @@ class Stepper:
         self._chk(self.lib.gle_plan_flags(self.h, ctypes.byref(fl)), "gle_plan_flags")
         return {"plan_class": names.get(int(c.value), int(c.value)), "fused_waves": int(w.value),
                 "cg_per_cu": float(cu.value), "nlevel": int(n.value), "dyn_dropped": int(dd.value),
-                "far_fused": bool(ff.value), "fpot_launch": bool(fl.value & 2)}
+                "far_fused": bool(ff.value), "fpot_launch": bool(fl.value & 2),
+                "composed_step": bool(fl.value & 8)}
+
+    def cache_audit(self):
+        """(at q~, at q_{t+1} after a constraint): composed steps at which md.potforce's cache rule
+        would have reused a force within 1e-9 of a different point (gle_cache_audit)."""
+        c = (ctypes.c_int64 * 2)()
+        self._chk(self.lib.gle_cache_audit(self.h, c), "gle_cache_audit")
+        return int(c[0]), int(c[1])
 
     def profile_levels(self):
         """[(P, blocks issued since profiling was enabled)] per ladder level."""

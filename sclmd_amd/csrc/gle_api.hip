@@ -86,6 +86,10 @@ struct Bath {
   int nqn = 0;
   double* d_NR = nullptr;  // near ring [NRS][vs]: p of the newest NRS steps (slot t mod NRS)
   int NRS = 2;
+  // composed one-launch step: V0 = n_t - c S(t) and W1 = n_{t+1} - c R(t+1) parity buffers [2][vs],
+  // near-field partials of lags [3, nn) [2][nqn3][vs]
+  double *d_V0 = nullptr, *d_W1 = nullptr, *d_NP3 = nullptr;
+  int nqn3 = 0;
   int64_t vs = 0;          // doubles per bath-local [ncp][B] buffer (with slack)
   int64_t ldh = 0;
   int R = 1;
@@ -246,6 +250,16 @@ struct gle_handle {
   Chain chA[2], chB[2], chC, chNear;  // [with dyn.q]; chNear: all near-field partial tiles (priming)
   Chain chBC;                          // stages B + C fused (harmonic force, disjoint baths)
   bool fuse_bc = false;
+  // composed one-launch step (STAGE 4, gle_internal.h): small-bath harmonic plans; variant t & 1
+  // reads state buffer t & 1 (d_P / d_Q or d_P2 / d_Q2) and writes the other; between gle_run calls
+  // the state is in d_P / d_Q.  x_live: V0 / W1 / NP3 hold step t's values (else x_prime first);
+  // std_stale: the two-launch path's S / NP buffers are behind (composed steps ran since)
+  bool xstep = false, x_live = false, std_stale = false;
+  Chain chX[2], chNear3;
+  double *d_P2 = nullptr, *d_Q2 = nullptr;
+  double* d_xfrag = nullptr;           // composed-operator DOF-tile fragments
+  unsigned long long* d_guard = nullptr;
+  double x_alg_flops = 0, x_alg_bytes = 0;  // algorithmic chain work per composed step
   // fused stage with the potential force at q~ evaluated before it (bc_fpot): a small launch between
   // A and BC computes md.potforce at q~ for every DOF (cache rule included) and adds it to the bath
   // rows of V, so the velocity stage needs M1.p_half + hK0.(V + Fpot_b) only (two products per bath
@@ -1823,6 +1837,425 @@ int plan_far_fused(gle_handle* h) {
   return GLE_OK;
 }
 
+// ---- composed one-launch step (STAGE 4): planning -------------------------------------------
+// Dense host composition of the step's operators (gle_internal.h, "Composed one-launch step"):
+// small-bath plans only (nph <= 4096, every bath nc <= 512), so n^2 matrices and the zero-skipping
+// products below stay at a few hundred ms of host fp64 work at C3.
+struct Dense {
+  int64_t n = 0;
+  std::vector<double> a;
+  explicit Dense(int64_t n_ = 0) : n(n_), a((size_t)(n_ * n_), 0.0) {}
+  double& at(int64_t r, int64_t c) { return a[(size_t)(r * n + c)]; }
+  double at(int64_t r, int64_t c) const { return a[(size_t)(r * n + c)]; }
+};
+
+// A B, skipping zero entries of A and the zero columns of B's rows
+Dense dmul(const Dense& A, const Dense& Bm) {
+  const int64_t n = A.n;
+  Dense C(n);
+  std::vector<std::vector<int32_t>> nzc((size_t)n);
+  for (int64_t r = 0; r < n; ++r)
+    for (int64_t c = 0; c < n; ++c)
+      if (Bm.at(r, c) != 0.0) nzc[(size_t)r].push_back((int32_t)c);
+  for (int64_t r = 0; r < n; ++r) {
+    double* cr = &C.a[(size_t)(r * n)];
+    for (int64_t k = 0; k < n; ++k) {
+      const double v = A.at(r, k);
+      if (v == 0.0) continue;
+      const double* bk = &Bm.a[(size_t)(k * n)];
+      for (int32_t c : nzc[(size_t)k]) cr[c] += v * bk[c];
+    }
+  }
+  return C;
+}
+
+// Y += alpha X
+void daxpy(Dense& Y, double alpha, const Dense& X) {
+  for (size_t i = 0; i < Y.a.size(); ++i) Y.a[i] += alpha * X.a[i];
+}
+
+// bath-local slice i of a bath's kernel, [nc][nc], from the device's compact near-field copy
+int host_slice(gle_handle* h, const Bath& b, int i, std::vector<double>& out) {
+  out.assign((size_t)b.nc * b.nc, 0.0);
+  if (i >= b.nn) return GLE_OK;  // past the kernel: zero
+  const int64_t nfrag = (int64_t)b.nrt * b.nks;
+  std::vector<double> f((size_t)nfrag * 64);
+  HIPCHK(h, hipMemcpy2DAsync(f.data(), 64 * 8, b.d_Kn + (int64_t)i * 64, (size_t)b.nn * 64 * 8, 64 * 8, (size_t)nfrag,
+                             hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  for (int rt = 0; rt < b.nrt; ++rt)
+    for (int ks = 0; ks < b.nks; ++ks)
+      for (int l = 0; l < 64; ++l) {
+        const int64_t r = 16 * rt + (l & 15), c = 4 * ks + (l >> 4);
+        if (r < b.nc && c < b.nc) out[(size_t)(r * b.nc + c)] = f[((size_t)rt * b.nks + ks) * 64 + l];
+      }
+  return GLE_OK;
+}
+
+// Rows [16 rt, 16 rt + 16) of an nph x ncols operand (element e(d, k)) as runs of nonzero 16 x 4
+// blocks (at most two per tile, merged across the smallest gap), fragments appended to frag:
+// (first k-step, k-steps, fragment offset) per run; nnz counts the operand's nonzero entries.
+struct XRun {
+  int ks0, nks;
+  int64_t off;
+};
+template <class E>
+std::vector<XRun> pack_runs(int64_t nph, int64_t ncols, int rt, const E& e, std::vector<double>& frag, double& nnz) {
+  const int nks = (int)((ncols + 3) / 4);
+  std::vector<std::pair<int, int>> rg;
+  for (int ks = 0; ks < nks; ++ks) {
+    bool nz = false;
+    for (int r = 0; r < 16; ++r) {
+      const int64_t d = 16 * (int64_t)rt + r;
+      if (d >= nph) break;
+      for (int64_t c = 4 * ks; c < 4 * ks + 4 && c < ncols; ++c)
+        if (e(d, c) != 0.0) {
+          nz = true;
+          nnz += 1.0;
+        }
+    }
+    if (!nz) continue;
+    if (!rg.empty() && rg.back().first + rg.back().second == ks) ++rg.back().second;
+    else rg.push_back({ks, 1});
+  }
+  while (rg.size() > 2) {
+    size_t bi = 0;
+    int bg = INT32_MAX;
+    for (size_t i = 0; i + 1 < rg.size(); ++i) {
+      const int gap = rg[i + 1].first - (rg[i].first + rg[i].second);
+      if (gap < bg) {
+        bg = gap;
+        bi = i;
+      }
+    }
+    rg[bi].second = rg[bi + 1].first + rg[bi + 1].second - rg[bi].first;
+    rg.erase(rg.begin() + bi + 1);
+  }
+  std::vector<XRun> out;
+  for (auto& r : rg) {
+    out.push_back({r.first, r.second, (int64_t)frag.size()});
+    for (int ks = r.first; ks < r.first + r.second; ++ks)
+      for (int l = 0; l < 64; ++l) {
+        const int64_t d = 16 * (int64_t)rt + (l & 15), c = 4 * ks + (l >> 4);
+        frag.push_back(d < nph && c < ncols ? e(d, c) : 0.0);
+      }
+  }
+  return out;
+}
+
+// Plan the composed one-launch step when the plan allows it (harmonic potential with disjoint baths,
+// small baths, no biased electron bath, first block length >= 2, no fused far-field schedule); any
+// planning failure leaves the two-launch plan alone.
+int plan_xstep(gle_handle* h) {
+  h->xstep = false;
+  const int nb = (int)h->baths.size();
+  const int64_t nph = h->nph, B = h->B;
+  if (const char* e = gle_env("GLE_XSTEP"))
+    if (atoi(e) == 0) return GLE_OK;
+  bool ok = h->fuse_bc && !h->bc_fpot && h->small_baths && !h->far_fused && h->P0 >= 2 && nb > 0 && nph <= 4096 &&
+            h->exp_one == 0;
+  for (const Bath& b : h->baths) ok = ok && !b.has_q && b.nc <= 512;
+  if (!ok) return GLE_OK;
+  const double dt = h->dt, hh = dt / 2.0, h2 = hh * hh, h3 = h2 * hh, dt22 = dt * dt / 2.0;
+  // ---- operators
+  Dense I(nph), Ck(nph), C1(nph), D(nph);
+  for (int64_t d = 0; d < nph; ++d) I.at(d, d) = 1.0;
+  D.a = h->dyn_h;
+  std::vector<std::vector<double>> K1(nb), K2(nb);
+  for (int j = 0; j < nb; ++j) {
+    Bath& b = h->baths[j];
+    int rc = host_slice(h, b, 1, K1[j]);
+    if (!rc) rc = host_slice(h, b, 2, K2[j]);
+    if (rc) return rc;
+    for (int64_t r = 0; r < b.nc; ++r)
+      for (int64_t c = 0; c < b.nc; ++c) {
+        Ck.at(b.cids[r], b.cids[c]) = b.c * b.K0[(size_t)(r * b.nc + c)];
+        C1.at(b.cids[r], b.cids[c]) = b.c * K1[j][(size_t)(r * b.nc + c)];
+      }
+  }
+  const Dense Ck2 = dmul(Ck, Ck), Ck3 = dmul(Ck2, Ck), CkD = dmul(Ck, D), DCk = dmul(D, Ck);
+  const Dense CkDCk = dmul(CkD, Ck), D2 = dmul(D, D), CkD2 = dmul(Ck, D2), Ck2D = dmul(Ck, CkD), CkC1 = dmul(Ck, C1);
+  // Mpp = I - 2hCk + 2h^2 Ck^2 - h^3 Ck^3 - dt (hD - h^2 CkD) + (dt^2/2)(hDCk - h^2 CkDCk) - (hC1 - h^2 CkC1)
+  Dense Mpp = I;
+  daxpy(Mpp, -2.0 * hh, Ck);
+  daxpy(Mpp, 2.0 * h2, Ck2);
+  daxpy(Mpp, -h3, Ck3);
+  daxpy(Mpp, -dt * hh, D);
+  daxpy(Mpp, dt * h2, CkD);
+  daxpy(Mpp, dt22 * hh, DCk);
+  daxpy(Mpp, -dt22 * h2, CkDCk);
+  daxpy(Mpp, -hh, C1);
+  daxpy(Mpp, h2, CkC1);
+  // Mpq = -h (D - hCkD + h^2 Ck^2 D) - (hD - h^2 CkD) + (dt^2/2)(hD^2 - h^2 CkD^2)
+  Dense Mpq(nph);
+  daxpy(Mpq, -2.0 * hh, D);
+  daxpy(Mpq, 2.0 * h2, CkD);
+  daxpy(Mpq, -h3, Ck2D);
+  daxpy(Mpq, dt22 * hh, D2);
+  daxpy(Mpq, -dt22 * h2, CkD2);
+  // Up = h (I - hCk + h^2 Ck^2) - (dt^2/2)(hD - h^2 CkD)   (acts on P V0)
+  Dense Up(nph);
+  daxpy(Up, hh, I);
+  daxpy(Up, -h2, Ck);
+  daxpy(Up, h3, Ck2);
+  daxpy(Up, -dt22 * hh, D);
+  daxpy(Up, dt22 * h2, CkD);
+  // Wp = hI - h^2 Ck  (acts on P W1)
+  Dense Wp(nph);
+  daxpy(Wp, hh, I);
+  daxpy(Wp, -h2, Ck);
+  // ---- buffers
+  int rc = 0;
+  const size_t nst = (size_t)h->nphp * B, nsl = (size_t)64 * B + 1024;
+  if (!h->d_P2) rc = dalloc_n(h, &h->d_P2, nst, nsl);
+  if (!rc && !h->d_Q2) rc = dalloc_n(h, &h->d_Q2, nst, nsl);
+  for (int j = 0; j < nb && !rc; ++j) {
+    Bath& b = h->baths[j];
+    rc = dalloc_n(h, &b.d_V0, (size_t)2 * b.vs);
+    if (!rc) rc = dalloc_n(h, &b.d_W1, (size_t)2 * b.vs);
+  }
+  if (rc) return rc;
+  // near-field partials of lags [3, nn) for target t+3 (the S tiles of the next launch sum them)
+  int rn_raw = (int)std::min<int64_t>(4, (B + 15) / 16);
+  const int nt_raw = 16 * rn_raw;
+  const int ncolr = (int)((B + nt_raw - 1) / nt_raw);
+  const int raw_ks = 24;
+  for (auto& b : h->baths) {
+    b.nqn3 = 0;
+    if (b.nn > 3) {
+      const int64_t W = (int64_t)(b.nn - 3) * b.nks;
+      int q = (int)std::min<int64_t>(CH_NPMAX, (W + raw_ks - 1) / raw_ks);
+      q = std::max(q, (b.nn - 3 + 4 * (CH_TPW - 1) - 1) / (4 * (CH_TPW - 1)));
+      q = std::max(1, std::min<int>(q, (int)W));
+      if (q > CH_NPMAX) return GLE_OK;
+      b.nqn3 = q;
+      rc = dalloc_n(h, &b.d_NP3, (size_t)2 * q * b.vs, 4096);
+      if (rc) return rc;
+    }
+  }
+  // ---- DOF-tile fragments: Mpp (X = p), Mpq (X = q), Up / Wp restricted to each bath's columns
+  // (X = V0 / W1 of that bath); the runs are shared by both state-buffer variants
+  const int ntile = h->ndblk;
+  std::vector<double> frag;
+  double nnz = 0.0;
+  struct TileOps {
+    std::vector<XRun> pp, pq;
+    std::vector<std::vector<XRun>> up, wp;
+  };
+  std::vector<TileOps> ops((size_t)ntile);
+  for (int rt = 0; rt < ntile; ++rt) {
+    TileOps& o = ops[(size_t)rt];
+    o.pp = pack_runs(nph, nph, rt, [&](int64_t d, int64_t c) { return Mpp.at(d, c); }, frag, nnz);
+    o.pq = pack_runs(nph, nph, rt, [&](int64_t d, int64_t c) { return Mpq.at(d, c); }, frag, nnz);
+    o.up.resize(nb);
+    o.wp.resize(nb);
+    for (int j = 0; j < nb; ++j) {
+      const Bath& b = h->baths[j];
+      o.up[j] = pack_runs(nph, b.nc, rt, [&](int64_t d, int64_t k) { return Up.at(d, b.cids[k]); }, frag, nnz);
+      o.wp[j] = pack_runs(nph, b.nc, rt, [&](int64_t d, int64_t k) { return Wp.at(d, b.cids[k]); }, frag, nnz);
+    }
+  }
+  if (frag.empty()) frag.assign(64, 0.0);
+  rc = dalloc_n(h, &h->d_xfrag, frag.size());
+  if (!rc) rc = upload(h, h->d_xfrag, frag.data(), frag.size() * 8);
+  if (!rc) rc = dalloc_n(h, &h->d_guard, 2);
+  if (rc) return rc;
+  // algorithmic work per step: the composed operators, K0 / K1 / K2 and the near lags [3, nn) on the
+  // bath rows, dyn (F0), every matrix entry read once
+  double knn = 0.0;
+  for (const Bath& b : h->baths) knn += (double)b.nc * b.nc * (double)std::max(0, std::min(b.nn, 3) + std::max(0, b.nn - 3));
+  double dyn_nnz = 0.0;
+  for (double v : h->dyn_h) dyn_nnz += v != 0.0 ? 1.0 : 0.0;
+  h->x_alg_flops = 2.0 * B * (nnz + knn + dyn_nnz);
+  h->x_alg_bytes = 8.0 * (nnz + knn + dyn_nnz) + 8.0 * 16.0 * (double)nph * B;
+  // ---- tiles
+  const int drn = h->ch_drn;
+  const int ncol1 = (int)((B + 16 * drn - 1) / (16 * drn));
+  auto err_off = [&](int code) {  // a plan the chain cannot hold: keep the two-launch plan
+    h->err.clear();
+    (void)code;
+    return GLE_OK;
+  };
+  for (int v = 0; v < 2; ++v) {
+    Chain& c = h->chX[v];
+    c.tiles.clear();
+    c.flops = 0;
+    c.nw = 4;
+    c.lds = (size_t)6 * 256 * drn * 8;  // the DOF epilogue reduces 6 quantities over the tile
+    double* pin = v == 0 ? h->d_P : h->d_P2;
+    double* qin = v == 0 ? h->d_Q : h->d_Q2;
+    double* pout = v == 0 ? h->d_P2 : h->d_P;
+    double* qout = v == 0 ? h->d_Q2 : h->d_Q;
+    for (int rt = 0; rt < ntile; ++rt)
+      for (int ct = 0; ct < ncol1; ++ct) {
+        ChTile T{};
+        T.kind = CH_DOF;
+        T.rn = drn;
+        T.row0 = 16 * rt;
+        T.c0 = 16 * drn * ct;
+        T.tile = rt;
+        T.nrows = (int)std::min<int64_t>(16, nph - 16 * rt);
+        T.ncols = (int)std::min<int64_t>(16 * drn, B - T.c0);
+        T.first = rt == 0 ? 1 : 0;
+        T.xp_in = pin;
+        T.xq_in = qin;
+        T.xp_out = pout;
+        T.xq_out = qout;
+        for (int u = 0; u < CH_TB; ++u) {
+          ChBath& cb = T.tb[u];
+          cb.bath = -1;
+          cb.noise = cb.S = cb.Yq = cb.V = h->d_zero;
+        }
+        std::vector<Seg> segs;
+        int nu = 0;
+        for (int j = 0; j < nb; ++j) {
+          Bath& b = h->baths[j];
+          uint32_t m = 0;
+          bool affine = true;
+          int off = 0;
+          for (int r = 0; r < 16; ++r) {
+            const int64_t d = 16 * rt + r;
+            if (d >= nph || b.inv[d] < 0) continue;
+            const int o2 = b.inv[d] - (int)d;
+            if (m == 0) off = o2;
+            else if (o2 != off) affine = false;
+            m |= 1u << r;
+          }
+          if (!m) continue;
+          if (nu == CH_TB) return err_off(0);
+          const int u = nu++;
+          ChBath& cb = T.tb[u];
+          cb.noise = b.d_noise;
+          cb.S = b.d_S ? b.d_S : h->d_zero;
+          cb.Xcur = b.d_Xcur;
+          cb.Xq = b.d_Xq;
+          cb.Yq = h->d_zero;
+          cb.H = b.d_H;
+          cb.NR = b.d_NR;
+          cb.inv = b.d_inv;
+          cb.c = b.c;
+          cb.vs = b.vs;
+          cb.nc = b.nc;
+          cb.ldh = (int32_t)b.ldh;
+          cb.R = b.R;
+          cb.NRS = b.NRS;
+          cb.has_q = 0;
+          cb.bath = j;
+          cb.bmask = m;
+          cb.boff = affine ? off : CH_INV;
+          cb.V = b.d_V0;
+          // K0.p_t on the tile's bath rows (X: the near ring's slot t)
+          segs.push_back(Seg{u, b.d_K0d + b.tofs[rt], 64, b.d_NR, (int)B, b.NRS, 0, b.nks, (int)b.vs});
+        }
+        {  // dyn.q_t
+          int64_t o = h->dyn_tofs[rt];
+          for (auto& r : h->dyn_rng[rt]) {
+            segs.push_back(Seg{2 * CH_TB, h->d_dynd + o, 64, qin + (int64_t)4 * r.first * B, (int)B, 0, 0, r.second, 0});
+            o += (int64_t)r.second * 64;
+          }
+        }
+        const TileOps& o = ops[(size_t)rt];
+        for (const XRun& r : o.pp)
+          segs.push_back(Seg{CH_OYB, h->d_xfrag + r.off, 64, pin + (int64_t)4 * r.ks0 * B, (int)B, 0, 0, r.nks, 0});
+        for (const XRun& r : o.pq)
+          segs.push_back(Seg{CH_OYB, h->d_xfrag + r.off, 64, qin + (int64_t)4 * r.ks0 * B, (int)B, 0, 0, r.nks, 0});
+        for (int j = 0; j < nb; ++j) {
+          const Bath& b = h->baths[j];
+          for (const XRun& r : o.up[j])
+            segs.push_back(Seg{CH_OYB, h->d_xfrag + r.off, 64, b.d_V0 + (int64_t)v * b.vs + (int64_t)4 * r.ks0 * B,
+                               (int)B, 0, 0, r.nks, 0});
+          for (const XRun& r : o.wp[j])
+            segs.push_back(Seg{CH_OYB, h->d_xfrag + r.off, 64, b.d_W1 + (int64_t)v * b.vs + (int64_t)4 * r.ks0 * B,
+                               (int)B, 0, 0, r.nks, 0});
+        }
+        int64_t W = 0;
+        for (auto& sg : segs) W += sg.nks;
+        if (fill_tasks(h, T, segs, CH_NOUT, 0, W, c)) return err_off(0);
+        c.tiles.push_back(T);
+      }
+    // S tiles: V0(t+1), W1(t+1) per bath row tile
+    for (int j = 0; j < nb; ++j) {
+      Bath& b = h->baths[j];
+      for (int rt = 0; rt < b.nrt; ++rt)
+        for (int ct = 0; ct < ncol1; ++ct) {
+          ChTile T{};
+          T.kind = CH_SFIN;
+          T.rn = drn;
+          T.row0 = 16 * rt;
+          T.c0 = 16 * drn * ct;
+          T.tile = j;
+          T.nrows = std::min(16, b.nc - 16 * rt);
+          T.ncols = (int)std::min<int64_t>(16 * drn, B - T.c0);
+          ChSfin& sf = T.sf;
+          sf.NP = b.nqn3 ? b.d_NP3 : h->d_zero;
+          sf.S = nullptr;
+          sf.vs = b.vs;
+          sf.nqn = b.nqn3;
+          sf.nc = b.nc;
+          sf.noise = b.d_noise;
+          sf.V = b.d_V0;
+          sf.W1 = b.d_W1;
+          sf.c = b.c;
+          for (int l = 0; l < MAXLVL; ++l) {
+            const bool act = l < (int)h->levels.size() && h->levels[l].lb[j].active;
+            sf.lvl[l] = act ? h->levels[l].lb[j].d_out : h->d_zero;
+            sf.lvl_ld[l] = act ? 2 * h->levels[l].P * (int32_t)B : 0;
+          }
+          std::vector<Seg> segs;
+          for (int i = 1; i <= 2 && i < b.nn; ++i)
+            segs.push_back(Seg{i - 1, b.d_Kn + ((int64_t)rt * b.nks * b.nn + i) * 64, b.nn * 64, b.d_NR, (int)B, b.NRS, 0,
+                               b.nks, (int)b.vs});
+          int64_t W = 0;
+          for (auto& sg : segs) W += sg.nks;
+          if (fill_tasks(h, T, segs, 2, 0, W, c)) return err_off(0);
+          c.tiles.push_back(T);
+        }
+    }
+  }
+  // near-field partial tiles (lags [3, nn), target t+3): in both variants, and alone for priming
+  h->chNear3.tiles.clear();
+  h->chNear3.nw = 4;
+  h->chNear3.lds = 0;
+  for (auto& b : h->baths) {
+    if (b.nqn3 == 0) continue;
+    const int64_t W = (int64_t)(b.nn - 3) * b.nks;
+    for (int rt = 0; rt < b.nrt; ++rt) {
+      std::vector<Seg> segs;
+      for (int i = 3; i < b.nn; ++i)
+        segs.push_back(Seg{0, b.d_Kn + ((int64_t)rt * b.nks * b.nn + i) * 64, b.nn * 64, b.d_NR, (int)B, b.NRS, 3 - i,
+                           b.nks, (int)b.vs});
+      for (int ct = 0; ct < ncolr; ++ct)
+        for (int q = 0; q < b.nqn3; ++q) {
+          ChTile T{};
+          T.kind = CH_RAW;
+          T.rn = rn_raw;
+          T.row0 = 16 * rt;
+          T.c0 = nt_raw * ct;
+          T.tile = (int)(&b - h->baths.data());
+          T.nrows = std::min(16, b.nc - 16 * rt);
+          T.ncols = (int)std::min<int64_t>(nt_raw, B - T.c0);
+          T.par_shift = 3;
+          T.par_stride = (int64_t)b.nqn3 * b.vs;
+          T.dst = b.d_NP3 + (int64_t)q * b.vs + (int64_t)16 * rt * B + T.c0;
+          T.ldd = (int)B;
+          for (Chain* c : {&h->chX[0], &h->chX[1], &h->chNear3}) {
+            ChTile Tc = T;
+            if (fill_tasks(h, Tc, segs, 1, W * q / b.nqn3, W * (q + 1) / b.nqn3, *c)) return err_off(0);
+            c->tiles.push_back(Tc);
+          }
+        }
+    }
+  }
+  for (Chain* c : {&h->chX[0], &h->chX[1], &h->chNear3}) {
+    if (c->tiles.empty()) continue;
+    rc = upload_chain(h, *c);
+    if (rc) return rc;
+  }
+  h->xstep = true;
+  h->x_live = false;
+  return GLE_OK;
+}
+
 int freeze(gle_handle* h) {
   if (h->frozen) return GLE_OK;
   const int64_t B = h->B;
@@ -2212,6 +2645,8 @@ int freeze(gle_handle* h) {
   if (rc) return rc;
   rc = plan_far_fused(h);
   if (rc) return rc;
+  rc = plan_xstep(h);
+  if (rc) return rc;
   // device step descriptor
   StepDev sd{};
   sd.nph = (int32_t)h->nph;
@@ -2232,6 +2667,7 @@ int freeze(gle_handle* h) {
   sd.part = h->d_part;
   sd.cmask = h->d_cmask;
   sd.ndblk = h->ndblk;
+  sd.guard = h->d_guard;
   if (const char* dbg = gle_env("GLE_CHAIN_DBG")) {
     size_t n = 0;
     for (Chain* c : {&h->chA[0], &h->chA[1], &h->chB[1], &h->chC, &h->chBC}) n = std::max(n, c->tiles.size());
@@ -2442,6 +2878,8 @@ int prime(gle_handle* h) {
   return GLE_OK;
 }
 
+int ladder_step(gle_handle* h, int early);
+
 int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
   if (!h->state_set) return fail(h, GLE_ERR_STATE, "gle_set_state has not been called");
   bounds_table_sync();
@@ -2450,10 +2888,38 @@ int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
   if (fpot_host_T == nullptr && !h->has_dyn)
     return fail(h, GLE_ERR_STATE, "no potential force: pass fpot or call gle_set_dyn (md.py:468-470)");
   int rc = 0;
+  if (h->std_stale) {
+    // composed steps ran since the two-launch path's buffers were current: rebuild S(t), the near
+    // partials and the blocks from the history, and forget the potential cache (its words held the
+    // composed step's audit distances)
+    h->std_stale = false;
+    h->need_prime = true;
+    h->pot_cache_exact = false;
+    HIPCHK(h, hipMemsetAsync(h->d_qvalid, 0, (size_t)h->B * sizeof(int32_t), h->stream));
+    HIPCHK(h, hipMemsetAsync(h->d_pmax, 0, (size_t)4 * h->B * sizeof(unsigned long long), h->stream));
+  }
+  h->x_live = false;  // this step does not maintain the composed step's V0 / W1 / NP3
   if (h->need_prime) {
     rc = prime(h);
     if (rc) return rc;
   }
+  rc = ladder_step(h, 0);
+  if (rc) return rc;
+  const bool need_pot = (fpot_host_T == nullptr) && !h->pot_cache_exact;
+  const StepArgs ta = step_args(h);
+  if (fpot_host_T)
+    HIPCHK(h, hipMemcpyAsync(h->d_Fc, fpot_host_T, (size_t)h->nph * h->B * 8, hipMemcpyHostToDevice, h->stream));
+  if (h->d_dbg && h->t == h->dbg_t) h->dbg_a = need_pot ? 1 : 0;  // GLE_CHAIN_DBG: the stage-A variant recorded
+  run_chain(h, 0, h->chA[need_pot ? 1 : 0], ta, (need_pot ? 1 : 0) | (fpot_host_T ? 0 : 2), h->levels.empty(), 0);
+  h->host_force_step = fpot_host_T != nullptr;
+  return GLE_OK;
+}
+
+// The ladder's work at the start of step t (before its chain launches): fused levels' transforms,
+// the background blocks' pieces, and the main stream's waits for the blocks its launches read --
+// target t+1 (early = 0) or also target t+2 (early = 1: the composed step's S tiles)
+int ladder_step(gle_handle* h, int early) {
+  int rc = 0;
   const int64_t t = h->t;
   // ladder: at each block boundary T = kP, start block k+1 (targets T+P+1..T+2P, data up to T) on
   // the level's background stream once step T-1 has closed; consume block k from this step on
@@ -2533,7 +2999,7 @@ int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
       // the main stream waits for block k at the first step within wait_early steps of its first
       // use k P (the block's last piece and event were enqueued >= piece_slack first-level blocks
       // before k P, and wait_early < P0); wait_early = 0: at the boundary k P itself
-      const int64_t kw = floordiv(t + h->wait_early, lv.P);
+      const int64_t kw = floordiv(t + h->wait_early + early, lv.P);
       if (lv.bg_block[kw & 1] == kw) {
         const int64_t k = kw;
         // per background stream, waiting for the block enqueued last implies the earlier ones
@@ -2552,14 +3018,7 @@ int step_begin_impl(gle_handle* h, const double* fpot_host_T) {
     for (int i = 0; i < gle_handle::NBG; ++i)
       if (wait_ev[i]) HIPCHK(h, hipStreamWaitEvent(h->stream, wait_ev[i], 0));
   }
-  const bool need_pot = (fpot_host_T == nullptr) && !h->pot_cache_exact;
-  const StepArgs ta = step_args(h);
-  if (fpot_host_T)
-    HIPCHK(h, hipMemcpyAsync(h->d_Fc, fpot_host_T, (size_t)h->nph * h->B * 8, hipMemcpyHostToDevice, h->stream));
-  if (h->d_dbg && t == h->dbg_t) h->dbg_a = need_pot ? 1 : 0;  // GLE_CHAIN_DBG: the stage-A variant recorded
-  run_chain(h, 0, h->chA[need_pot ? 1 : 0], ta, (need_pot ? 1 : 0) | (fpot_host_T ? 0 : 2), h->levels.empty(), 0);
-  h->host_force_step = fpot_host_T != nullptr;
-  return GLE_OK;
+  return rc;
 }
 
 int step_end_impl(gle_handle* h, const double* fpot_host_T) {
@@ -2607,6 +3066,85 @@ int step_end_impl(gle_handle* h, const double* fpot_host_T) {
   if (!h->levels.empty() && (h->t + 1) % h->P0 == 0) HIPCHK(h, hipEventRecord(h->ev_step, h->stream));
   h->t += 1;
   h->pot_cache_exact = (fpot_host_T == nullptr) && h->constr.empty();
+  HIPCHK(h, hipGetLastError());
+  return GLE_OK;
+}
+
+// Composed one-launch step (STAGE 4): V0[t & 1], W1[t & 1] and the near partials of lags >= 3 for
+// target t+2 from the two-launch path's state at step t (S(t), near partials of target t+1, the
+// level blocks of target t+1); the caller's ladder_step has made the main stream wait for them.
+int x_prime_buffers(gle_handle* h) {
+  const StepArgs ta = step_args(h);
+  for (auto& b : h->baths) {
+    XPrimeArgs a{};
+    a.noise = b.d_noise;
+    a.S = b.ml > 1 ? b.d_S : nullptr;
+    a.NP = b.nqn ? b.d_NP : nullptr;
+    a.nqn = b.nqn;
+    const int j = (int)(&b - h->baths.data());
+    for (size_t l = 0; l < h->levels.size() && l < (size_t)MAXLVL; ++l) {
+      const LevelBath& L = h->levels[l].lb[j];
+      a.lvl[l] = L.active ? L.d_out : nullptr;
+      a.lvl_ld[l] = 2 * h->levels[l].P * (int32_t)h->B;
+      a.lvl_off[l] = ta.lvl_off[l];
+    }
+    a.V0 = b.d_V0;
+    a.W1 = b.d_W1;
+    a.c = b.c;
+    a.vs = b.vs;
+    a.t = h->t;
+    a.nc = b.nc;
+    a.B = (int32_t)h->B;
+    a.nmd = (int32_t)h->nmd;
+    launch_xprime(a, h->stream);
+  }
+  if (!h->chNear3.tiles.empty())
+    launch_chain(4, h->chNear3.nw, h->ch_drn, h->chNear3.lds, h->chNear3.d, (int)h->chNear3.tiles.size(), h->d_sd,
+                 step_args(h, h->t - 1), 0, h->stream);
+  HIPCHK(h, hipMemsetAsync(h->d_pmax, 0, (size_t)4 * h->B * sizeof(unsigned long long), h->stream));
+  h->x_live = true;
+  return GLE_OK;
+}
+
+int run_xstep(gle_handle* h, int64_t nsteps) {
+  if (!h->state_set) return fail(h, GLE_ERR_STATE, "gle_set_state has not been called");
+  bounds_table_sync();
+  for (size_t j = 0; j < h->baths.size(); ++j)
+    if (!h->baths[j].noise_set) return fail(h, GLE_ERR_STATE, "bath " + std::to_string(j) + " has no noise");
+  if (nsteps == 0) return GLE_OK;
+  int rc = 0;
+  if (!h->x_live && h->std_stale) h->need_prime = true;  // e.g. new noise after composed steps
+  if (h->need_prime) {
+    h->x_live = false;
+    rc = prime(h);
+    if (rc) return rc;
+    h->std_stale = false;
+  }
+  const size_t nst = (size_t)h->nphp * h->B * 8;
+  if (h->t & 1) {  // step t reads state buffer t & 1
+    HIPCHK(h, hipMemcpyAsync(h->d_P2, h->d_P, nst, hipMemcpyDeviceToDevice, h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->d_Q2, h->d_Q, nst, hipMemcpyDeviceToDevice, h->stream));
+  }
+  for (int64_t s = 0; s < nsteps; ++s) {
+    rc = ladder_step(h, 1);
+    if (rc) return rc;
+    if (!h->x_live) {
+      rc = x_prime_buffers(h);
+      if (rc) return rc;
+    }
+    StepArgs ta = step_args(h);
+    const StepArgs t2 = step_args(h, h->t + 1);  // the S tiles read the levels at target t+2
+    for (int l = 0; l < MAXLVL; ++l) ta.lvl_off[l] = t2.lvl_off[l];
+    run_chain(h, 4, h->chX[h->t & 1], ta, 0, h->levels.empty(), 0);
+    h->std_stale = true;
+    if (!h->levels.empty() && (h->t + 1) % h->P0 == 0) HIPCHK(h, hipEventRecord(h->ev_step, h->stream));
+    h->t += 1;
+  }
+  if (h->t & 1) {  // the state lives in d_P / d_Q between calls
+    HIPCHK(h, hipMemcpyAsync(h->d_P, h->d_P2, nst, hipMemcpyDeviceToDevice, h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->d_Q, h->d_Q2, nst, hipMemcpyDeviceToDevice, h->stream));
+  }
+  h->pot_cache_exact = false;
   HIPCHK(h, hipGetLastError());
   return GLE_OK;
 }
@@ -2815,7 +3353,8 @@ static void dump_chain_dbg(gle_handle* h) {
   if (hipMemcpy(st.data(), h->d_dbg, st.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
   const char* kn[3] = {"DOF", "SFIN", "RAW"};
   for (int g = 0; g < 3; ++g) {
-    const Chain& c = g == 0 ? h->chA[h->dbg_a] : (g == 1 ? h->chB[1] : (h->fuse_bc ? h->chBC : h->chC));
+    const Chain& c = g == 0 ? h->chA[h->dbg_a]
+                            : (g == 1 ? h->chB[1] : (h->xstep ? h->chX[h->dbg_t & 1] : (h->fuse_bc ? h->chBC : h->chC)));
     unsigned long long t0 = ~0ull, t1 = 0;
     for (size_t i = 0; i < c.tiles.size(); ++i) {
       const unsigned long long* r = &st[((size_t)g * n + i) * 4];
@@ -3283,6 +3822,7 @@ int gle_set_noise(gle_handle* h, int32_t bath, const double* noise) {
   rc = upload(h, b.d_noise, buf.data(), buf.size() * 8);
   if (rc) return rc;
   b.noise_set = true;
+  h->x_live = false;  // V0 / W1 carry the noise
   return GLE_OK;
 }
 
@@ -3415,6 +3955,7 @@ int gle_noise_generate(gle_handle* h, int32_t bath, const double* x_host, uint64
   }
   cleanup();
   b.noise_set = true;
+  h->x_live = false;  // V0 / W1 carry the noise
   return GLE_OK;
 }
 
@@ -3509,6 +4050,7 @@ int stream_finish(gle_handle* h, Bath& b) {
   if (frc) return fail(h, GLE_ERR_UNSUP, "device noise FFT needs nmd a power of two <= 8192");
   if (e != hipSuccess) return fail(h, GLE_ERR_HIP, std::string("noise stream: ") + hipGetErrorString(e));
   b.noise_set = true;
+  h->x_live = false;  // V0 / W1 carry the noise
   return GLE_OK;
 }
 }  // namespace
@@ -3674,6 +4216,7 @@ int gle_step_end(gle_handle* h, const double* fpot_qt) {
 int gle_run(gle_handle* h, int64_t nsteps) {
   if (!h || nsteps < 0) return GLE_ERR_ARG;
   hipSetDevice(h->cfg.device);
+  if (h->xstep && h->frozen) return run_xstep(h, nsteps);
   for (int64_t s = 0; s < nsteps; ++s) {
     int rc = step_begin_impl(h, nullptr);
     if (rc) return rc;
@@ -4136,7 +4679,20 @@ int gle_plan_flags(gle_handle* h, int32_t* flags) {
   if (!h || !flags) return GLE_ERR_ARG;
   if (!h->frozen) return fail(h, GLE_ERR_STATE, "no plan yet (gle_set_state builds it)");
   *flags = (h->fuse_bc ? GLE_PLAN_FUSED_BC : 0) | (h->bc_fpot ? GLE_PLAN_FPOT_LAUNCH : 0) |
-           (h->far_fused ? GLE_PLAN_FAR_FUSED : 0);
+           (h->far_fused ? GLE_PLAN_FAR_FUSED : 0) | (h->xstep ? GLE_PLAN_COMPOSED_STEP : 0);
+  return GLE_OK;
+}
+
+int gle_cache_audit(gle_handle* h, int64_t* counts) {
+  if (!h || !counts) return GLE_ERR_ARG;
+  counts[0] = counts[1] = 0;
+  if (!h->d_guard) return GLE_OK;
+  hipSetDevice(h->cfg.device);
+  unsigned long long v[2] = {0, 0};
+  const int rc = download(h, v, h->d_guard, sizeof(v));
+  if (rc) return rc;
+  counts[0] = (int64_t)v[0];
+  counts[1] = (int64_t)v[1];
   return GLE_OK;
 }
 

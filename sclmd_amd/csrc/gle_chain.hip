@@ -102,7 +102,7 @@ struct Batch {
 
 // GLE_CHAIN_DBG timeline: stamp 0 entry, 1 descriptor read, 2 products done, 3 end (100 MHz)
 __device__ __forceinline__ void stamp(const StepDev* __restrict__ sd, int stage, int k, const StepArgs& ta) {
-  if (stage > 2) stage = 2;  // the fused B+C stage records into stage C's rows
+  if (stage > 2) stage = 2;  // the fused B+C and composed stages record into stage C's rows
   if (ta.dbg && threadIdx.x == 0 && (int)blockIdx.x < sd->dbg_ntile)
     G(sd->dbg)[((int64_t)stage * sd->dbg_ntile + blockIdx.x) * 4 + k] = __builtin_amdgcn_s_memrealtime();
 }
@@ -830,6 +830,213 @@ __device__ __forceinline__ void dof_BC(const ChTile* __restrict__ T, const StepD
   }
 }
 
+// stage 4 (composed one-launch step, gle_internal.h), DOF tile: p_{t+1} is the composed product
+// (output CH_OYB); K0.p_t (u), Kq.q_t (CH_TB + u) and dyn.q_t (2 CH_TB) give md.vv's id0 phase for the
+// tile's elements: F0, heat current, kinetic energy, recordings, q_{t+1} = q~ (md.py:383-398);
+// constraints zero p_{t+1} and q_{t+1} (md.py:407-408); history push of p_{t+1}.
+template <int NW, int DRN>
+__device__ __forceinline__ void dof_X(const ChTile* __restrict__ T, const StepDev* __restrict__ sd,
+                                      const StepArgs& ta, double* lds) {
+  using Geo = DofGeo<NW, DRN>;
+  constexpr int EPT = Geo::EPT;
+  const int B = sd->B, nb = sd->nbath;
+  const int64_t t = ta.t;
+  const int tn = (int)(t % sd->nmd);
+  const int par = (int)(t & 1), par1 = par ^ 1;
+  const double dt = sd->dt, dt2 = dt * dt;
+  // ---- loads that do not depend on the products
+  Elem E[EPT];
+  double p[EPT], q[EPT];
+  int cons[EPT];
+  int kk[EPT][CH_TB];
+  double v0[EPT][CH_TB];
+#pragma unroll
+  for (int x = 0; x < EPT; ++x) {
+    E[x] = elem_of<NW, DRN>(T, sd, x);
+    const int64_t ii = E[x].ok ? E[x].i : 0;
+    p[x] = G(T->xp_in)[ii];
+    q[x] = G(T->xq_in)[ii];
+    cons[x] = G(sd->cmask)[E[x].ok ? E[x].d : 0];
+#pragma unroll
+    for (int u = 0; u < CH_TB; ++u) {
+      const ChBath& bd = T->tb[u];
+      kk[x][u] = bath_row(bd, E[x]);
+      v0[x][u] = G(bd.V)[(int64_t)par * bd.vs + bath_idx(E[x], kk[x][u], B)];
+    }
+  }
+  // md.potforce cache audit of the previous step (its words at parity par1): the first row tile of
+  // each column tile counts the trajectories whose cache rule would have reused a force at a point
+  // within 1e-9 but not equal, and zeroes the words for step t + 1
+  if (T->first && threadIdx.x < 2 * Geo::NT) {
+    const int id = threadIdx.x / Geo::NT, b = T->c0 + (int)threadIdx.x % Geo::NT;
+    if (b < B) {
+      unsigned long long* w = pmax_word(sd, id, par1, b);
+      const unsigned long long v = *G(w);
+      if (v != 0ull && word_hit(v))
+        __hip_atomic_fetch_add((__attribute__((address_space(1))) unsigned long long*)(sd->guard + id), 1ull,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *G(w) = 0ull;
+    }
+  }
+  run_products_rn<NW, DRN>(T, t, lds);
+  __syncthreads();
+  stamp(sd, 4, 2, ta);
+  double cur[EPT][CH_TB], ee[EPT], d1[EPT], d0[EPT];
+#pragma unroll
+  for (int x = 0; x < EPT; ++x) {
+    const int e = min((int)threadIdx.x + x * NW * 64, Geo::NE - 1);
+    const double yd = out_sum<NW>(T, lds, 2 * CH_TB, e, Geo::NE);
+    const double xp = out_sum<NW>(T, lds, CH_OYB, e, Geo::NE);
+    double y[CH_TB];
+#pragma unroll
+    for (int u = 0; u < CH_TB; ++u) y[u] = out_sum<NW>(T, lds, u, e, Geo::NE);
+    double f = -1.0 * yd;  // potforce(q_t) = -1.0*mdot(dyn, q) (md.py:467)
+#pragma unroll
+    for (int u = 0; u < CH_TB; ++u) {
+      cur[x][u] = 0.0;
+      if (kk[x][u] >= 0) {
+        const ChBath& bd = T->tb[u];
+        double fb = v0[x][u] - bd.c * y[u];  // noise - c (K0.p + S(t))
+        if (bd.has_q) fb -= out_sum<NW>(T, lds, CH_TB + u, e, Geo::NE);
+        f += fb;                 // md.py:432-434
+        cur[x][u] = fb * p[x];   // md.py:397
+        if (double* rf = sd->rec_f[bd.bath])  // md.py:398
+          G(rf)[((int64_t)tn * bd.nc + kk[x][u]) * B + E[x].b] = fb;
+      }
+    }
+    const double ph = p[x] + f * dt / 2.0;               // md.py:391
+    const double qt = q[x] + p[x] * dt + f * dt2 / 2.0;  // md.py:392
+    double p2 = xp, qn = qt;
+    if (cons[x] != 0) {  // ApplyConstraint (md.py:407-408, 782-794)
+      p2 = 0.0;
+      qn = 0.0;
+    }
+    if (E[x].ok) {
+      G(T->xp_out)[E[x].i] = p2;
+      G(T->xq_out)[E[x].i] = qn;
+      G(sd->Flast)[E[x].i] = (xp - ph) * (2.0 / dt);  // F1(p1): p2 = p_half + dt F1(p1) / 2 (md.py:403-404)
+      const int64_t rs = (int64_t)tn * sd->nph * B + E[x].i;
+      if (sd->rec_p) G(sd->rec_p)[rs] = p[x];
+      if (sd->rec_q) G(sd->rec_q)[rs] = q[x];
+      if (sd->rec_hp) {
+        const int64_t hs = (int64_t)(t % sd->rec_ml) * sd->nph * B + E[x].i;
+        G(sd->rec_hp)[hs] = p[x];
+        G(sd->rec_hq)[hs] = q[x];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < CH_TB; ++u) {
+      if (kk[x][u] >= 0) {
+        const ChBath& bd = T->tb[u];
+        const int64_t kb = (int64_t)kk[x][u] * B + E[x].b;
+        const int64_t slot = cmod(t + 1, bd.R);  // history push of p_{t+1} (md.py:386-387)
+        auto hh = G(bd.H + (int64_t)kk[x][u] * bd.ldh + E[x].b);
+        hh[slot * B] = p2;
+        hh[(slot + bd.R) * B] = p2;
+        G(bd.NR)[cmod(t + 1, bd.NRS) * bd.vs + kb] = p2;
+        if (bd.has_q) G(bd.Xq)[(int64_t)par1 * bd.vs + kb] = qn;
+      }
+    }
+    ee[x] = E[x].ok ? p[x] * p[x] : 0.0;
+    d1[x] = E[x].ok ? fabs(qt - q[x]) : 0.0;   // |q~ - q0| of the id1 call (q0 = q_t)
+    d0[x] = E[x].ok ? fabs(qn - qt) : 0.0;     // |q_{t+1} - q0| of the next id0 call (q0 = q~)
+  }
+  // per-trajectory sums over the tile's DOFs (fixed row order): currents and energy into the step's
+  // partial table, the two cache distances as maxima into the parity-par words
+  __syncthreads();
+  double* red = lds;
+#pragma unroll
+  for (int x = 0; x < EPT; ++x) {
+    const int e = threadIdx.x + x * NW * 64;
+    if (E[x].in) {
+#pragma unroll
+      for (int u = 0; u < CH_TB; ++u) red[u * Geo::NE + e] = cur[x][u];
+      red[CH_TB * Geo::NE + e] = ee[x];
+      red[(CH_TB + 1) * Geo::NE + e] = d1[x];
+      red[(CH_TB + 2) * Geo::NE + e] = d0[x];
+    }
+  }
+  __syncthreads();
+  auto prow = G(sd->part + (((int64_t)tn * sd->ndblk + T->tile) * (nb + 1)) * B);
+  {
+    static_assert((CH_TB + 3) * Geo::NT <= NW * 64, "one thread per column reduction");
+    const int qn = threadIdx.x / Geo::NT, c = threadIdx.x % Geo::NT;
+    const int b = T->c0 + c;
+    if (qn < CH_TB + 3 && b < B) {
+      bool nan;
+      const double v = col_red<NW, DRN>(red, qn, c, qn > CH_TB, nan);
+      if (qn < CH_TB) {
+        const int j = T->tb[qn].bath;
+        if (j >= 0) prow[(int64_t)j * B + b] = v;
+      } else if (qn == CH_TB) {
+        prow[(int64_t)nb * B + b] = v;
+      } else {
+        const unsigned long long bits = nan ? 0x7FF8000000000000ull : (unsigned long long)__double_as_longlong(v);
+        gmax(pmax_word(sd, qn - CH_TB - 1, par, b), bits);
+      }
+    }
+  }
+  for (int z = threadIdx.x; z < nb * Geo::NT; z += NW * 64) {  // baths that miss the tile
+    const int j = z / Geo::NT, b = T->c0 + z % Geo::NT;
+    bool meets = false;
+#pragma unroll
+    for (int u = 0; u < CH_TB; ++u) meets |= T->tb[u].bath == j;
+    if (!meets && b < B) prow[(int64_t)j * B + b] = 0.0;
+  }
+}
+
+// stage 4 S tile, bath rows [row0, row0+16): V0(t+1) = W1(t) - c K1.p_t and W1(t+1) = n_{t+2} -
+// c (K2.p_t + near partials (lags >= 3, written by launch t-1) + levels at target t+2)
+template <int NW, int DRN>
+__device__ __forceinline__ void sfin_X(const ChTile* __restrict__ T, const StepDev* __restrict__ sd,
+                                       const StepArgs& ta, double* lds) {
+  const int B = sd->B;
+  const int64_t t = ta.t;
+  const int par = (int)(t & 1), par1 = par ^ 1;  // target t+2 has parity par
+  const ChSfin& sf = T->sf;
+  constexpr int NT = 16 * DRN, NE = 16 * NT;
+  constexpr int EPT = (NE + NW * 64 - 1) / (NW * 64);
+  double pre[EPT], nz2[EPT], w1[EPT];
+  int64_t kb[EPT];
+  bool ok[EPT];
+  const int t2 = (int)((t + 2) % sd->nmd);
+#pragma unroll
+  for (int x = 0; x < EPT; ++x) {
+    const int e = threadIdx.x + x * NW * 64;
+    const int k = T->row0 + e / NT;
+    const int b = T->c0 + e % NT;
+    ok[x] = e < NE && k < sf.nc && b < B;
+    kb[x] = (int64_t)k * B + b;
+    double v[CH_NPMAX], lv[MAXLVL];
+    auto np = G(sf.NP + (sf.nqn > 0 ? (int64_t)par * sf.nqn * sf.vs + (ok[x] ? kb[x] : 0) : 0));
+#pragma unroll
+    for (int q = 0; q < CH_NPMAX; ++q) v[q] = np[(int64_t)min(q, max(sf.nqn - 1, 0)) * sf.vs];
+#pragma unroll
+    for (int l = 0; l < MAXLVL; ++l)
+      lv[l] = G(sf.lvl[l])[(ok[x] ? (int64_t)k * sf.lvl_ld[l] + b : 0) + ta.lvl_off[l]];
+    nz2[x] = G(sf.noise)[ok[x] ? ((int64_t)t2 * sf.nc + k) * B + b : 0];
+    w1[x] = G(sf.W1)[(int64_t)par * sf.vs + (ok[x] ? kb[x] : 0)];
+    double sn = 0.0, lvs = 0.0;
+#pragma unroll
+    for (int q = 0; q < CH_NPMAX; ++q) sn += (q < sf.nqn) ? v[q] : 0.0;
+#pragma unroll
+    for (int l = 0; l < MAXLVL; ++l) lvs += lv[l];
+    pre[x] = lvs + sn;
+  }
+  run_products_rn<NW, DRN>(T, t, lds);
+  __syncthreads();
+  stamp(sd, 4, 2, ta);
+#pragma unroll
+  for (int x = 0; x < EPT; ++x) {
+    const int e = threadIdx.x + x * NW * 64;
+    if (ok[x]) {
+      const double y1 = out_sum<NW>(T, lds, 0, e, NE), y2 = out_sum<NW>(T, lds, 1, e, NE);
+      G(sf.V)[(int64_t)par1 * sf.vs + kb[x]] = w1[x] - sf.c * y1;              // n_{t+1} - c S(t+1)
+      G(sf.W1)[(int64_t)par1 * sf.vs + kb[x]] = nz2[x] - sf.c * (y2 + pre[x]);  // n_{t+2} - c R(t+2)
+    }
+  }
+}
+
 // S(t+1) of bath rows [row0, row0+16) x 16 rn columns: K_1.p_t (the products) + near-field
 // partials + levels
 template <int NW, int DRN>
@@ -1018,9 +1225,11 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(DRN == 
     if (STAGE == 0) dof_A<NW, DRN>(T, sd, ta, mode, lds);
     else if (STAGE == 1) dof_B<NW, DRN>(T, sd, ta, mode, lds);
     else if (STAGE == 2) dof_C<NW, DRN>(T, sd, ta, mode, lds);
-    else dof_BC<NW, DRN>(T, sd, ta, mode, lds);
+    else if (STAGE == 3) dof_BC<NW, DRN>(T, sd, ta, mode, lds);
+    else dof_X<NW, DRN>(T, sd, ta, lds);
   } else if (kind == CH_SFIN) {
-    sfin<NW, DRN>(T, sd, ta, lds, STAGE);
+    if (STAGE == 4) sfin_X<NW, DRN>(T, sd, ta, lds);
+    else sfin<NW, DRN>(T, sd, ta, lds, STAGE);
   } else {
     raw<NW>(T, sd, ta, lds, STAGE);
   }
@@ -1089,7 +1298,8 @@ void launch_chain(int stage, int nw, int drn, size_t lds_bytes, const ChTile* ti
   if (stage == 0) launch_st<0>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
   else if (stage == 1) launch_st<1>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
   else if (stage == 2) launch_st<2>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
-  else launch_st<3>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
+  else if (stage == 3) launch_st<3>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
+  else launch_st<4>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
 }
 
 namespace {

@@ -188,10 +188,27 @@ struct StepDev {
   double* rec_hq;         //   rec_ml holds p_t / q_t, md.py:386-387)
   double* rec_f[MAXBATH]; // md.fhis[i] bath-local [nmd][nc][B] (md.py:398)
   int32_t rec_ml, rec_pad;
+  // composed one-launch step (stage 4): [0] steps whose md.potforce cache would have hit at q~ with
+  // q~ != q0 (0 < max|q~ - q_t| < 1e-9, the reference then reuses the force at q_t), [1] the same at
+  // q_{t+1} after a constraint (0 < max|q_{t+1} - q~_t| < 1e-9); per-trajectory maxima in pmax
+  unsigned long long* guard;
   BathDev bath[MAXBATH];
 };
 
 // ---- per-step chain (gle_chain.hip) ------------------------------------------------------
+// Composed one-launch step (STAGE 4, small-bath harmonic plans): md.vv is linear in (p_t, q_t) and
+// the bath vectors V0 = n_t - c S(t), W1 = n_{t+1} - c R(t+1), R(t+1) = sum_{i>=2} K_i p_{t+1-i}, so
+// with Ck = c K0, C1 = c K1, Dq = dyn + Kq (bath blocks scattered), h = dt/2, A1 = I - hCk + h^2 Ck^2,
+// A2 = hI - h^2 Ck:
+//   p_{t+1} = Mpp p_t + Mpq q_t + Up P V0 + A2 P W1,                     (DOF tiles, output CH_OYB)
+//     Mpp = A1 (I - hCk) - dt A2 Dq + (dt^2/2) A2 Dq Ck - A2 C1,
+//     Mpq = -h A1 Dq - A2 Dq + (dt^2/2) A2 Dq^2,   Up = h A1 - (dt^2/2) A2 Dq
+//   q_{t+1} = q_t + dt p_t + (dt^2/2) F0, F0 = -dyn q_t + P (V0 - c K0 p_t - Kq q_t)   (md.py:392)
+// The DOF tiles also form K0 p_t, Kq q_t, dyn q_t for F0 (current, energy, recordings), the
+// S tiles V0(t+1) = W1(t) - c K1 p_t and W1(t+1) = n_{t+2} - c (K2 p_t + near(t+2) + levels), the
+// near tiles the partials of lags >= 3 for target t+3.  One dependent launch per step instead of
+// two (A, BC); the potential force is evaluated fresh at q~ (md.potforce's 1e-9 cache reuse is
+// counted by StepDev::guard when it would have applied with q~ != q0).
 // One md.vv is three launches A, B, C.  Every workgroup is one ChTile: a 16-row x 16*rn-column
 // output tile whose products are split over the 4 waves by k-steps (each wave's run of tasks
 // accumulates into an LDS partial slot; the epilogue adds the slots of an output in fixed order),
@@ -264,6 +281,7 @@ struct ChSfin {
   double* S;
   const double* noise;  // fused B+C: V = noise(t+1) - c S(t+1) into V (nullptr: not fused)
   double* V;
+  double* W1;           // stage 4: W1 parity buffers [2][vs] (read t & 1, written (t + 1) & 1); V holds V0
   double c;
   const double* lvl[MAXLVL];
   int32_t lvl_ld[MAXLVL];
@@ -283,6 +301,11 @@ struct ChTile {
   double* dst;       // CH_RAW: row 0, column 0 of the tile in parity buffer 0
   int32_t ldd;
   int32_t first;     // CH_DOF: the tile that zeroes the other-parity cache words
+  // stage 4 CH_DOF: the state buffers it reads (p_t, q_t) and writes (p_{t+1}, q_{t+1})
+  const double* xp_in;
+  const double* xq_in;
+  double* xp_out;
+  double* xq_out;
   int32_t ntw[CH_NW]; // tasks of wave w (32-bit: read with scalar loads)
   int32_t ob[CH_NOUT + 1];  // output o adds LDS slots [ob[o], ob[o+1]); outputs: Y of tile bath u
                             // (u < CH_TB), YQ of tile bath u (CH_TB + u), YD (2 CH_TB);
@@ -343,6 +366,22 @@ struct FpotArgs {
   int32_t nc[MAXBATH];
 };
 void launch_fpot(const FpotArgs& a, hipStream_t s);
+// composed one-launch step, priming one bath from the two-launch path's state at step t:
+// V0[t & 1] = n_t - c S[t & 1] (S: nullptr for a bath without memory sum), W1[t & 1] = n_{t+1} -
+// c (sum of the nqn near partials of target t+1 at parity (t + 1) & 1 + the levels at target t+1)
+struct XPrimeArgs {
+  const double* noise;
+  const double* S;
+  const double* NP;
+  const double* lvl[MAXLVL];
+  int32_t lvl_ld[MAXLVL];
+  int64_t lvl_off[MAXLVL];
+  double *V0, *W1;
+  double c;
+  int64_t vs, t;
+  int32_t nc, B, nmd, nqn;
+};
+void launch_xprime(const XPrimeArgs& a, hipStream_t s);
 void launch_philox_normal(double* x, int64_t nfreq, int64_t ncp, int64_t nc, int64_t B,
                           uint64_t seed, uint64_t traj_offset, hipStream_t s, int64_t w_off = 0);
 // streamed noise: a[w0 + w][row_off + r][b] = wscale[w] sum_k M[w][r][k] x[w][k][b] for w < nw (M of

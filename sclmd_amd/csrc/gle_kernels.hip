@@ -614,6 +614,30 @@ void launch_hist_out(const double* src, int64_t ks, int64_t ss, int R, int64_t t
   hist_out_kernel<<<(unsigned)blocks, 256, 0, s>>>(src, ks, ss, R, tau0, nt, nk, b0, nb, out);
 }
 
+__global__ void xprime_kernel(XPrimeArgs a) {
+  const int64_t n = (int64_t)a.nc * a.B;
+  const int64_t t = a.t;
+  const int par = (int)(t & 1), par1 = par ^ 1;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = e / a.B, b = e % a.B;
+    const double n0 = a.noise[((t % a.nmd) * a.nc + k) * a.B + b];
+    const double n1 = a.noise[(((t + 1) % a.nmd) * a.nc + k) * a.B + b];
+    const double S = a.S ? a.S[(int64_t)par * a.vs + e] : 0.0;
+    double r = 0.0;
+    for (int l = 0; l < MAXLVL; ++l)
+      if (a.lvl[l]) r += a.lvl[l][k * a.lvl_ld[l] + b + a.lvl_off[l]];
+    for (int q = 0; q < a.nqn; ++q) r += a.NP[((int64_t)par1 * a.nqn + q) * a.vs + e];
+    a.V0[(int64_t)par * a.vs + e] = n0 - a.c * S;
+    a.W1[(int64_t)par * a.vs + e] = n1 - a.c * r;
+  }
+}
+
+void launch_xprime(const XPrimeArgs& a, hipStream_t s) {
+  const int64_t n = (int64_t)a.nc * a.B;
+  if (n <= 0) return;
+  xprime_kernel<<<(unsigned)std::min<int64_t>((n + 255) / 256, 4096), 256, 0, s>>>(a);
+}
+
 // md.phis / md.qhis rows (newest first) of trajectories [b0, b0 + nb) into out [nb][nt][nph]: row i
 // = slot (tau0 - i) mod R of the full-DOF recording ring rec [R][nph][B] for i < R, zero past the
 // ring (or everywhere when rec is null)

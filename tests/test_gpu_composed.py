@@ -1,0 +1,145 @@
+"""The composed one-launch step (GLE_PLAN_COMPOSED_STEP, gle_internal.h): small-bath harmonic plans
+run md.vv (md.py:367-411) as ONE chain launch per step -- p_{t+1} from precomputed composed operators,
+q_{t+1} = q~ from the step's own K0.p_t and dyn.q_t.  Checked against the batched oracle
+(oracle.GLEBatch, pinned to the reference-shaped oracle and the reference's fixtures) at 1e-10 on q,
+p and the heat currents, across the switches the plan has to survive: steps with a host force in
+between (the two-launch path, then back), a new noise realisation mid-run, constraints, and a history
+ring / ladder that every level fires on.  md.potforce's 1e-9 cache reuse (md.py:767-779) is counted
+by gle_cache_audit: zero on these runs, nonzero on a system at rest."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-10
+
+
+def rel(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
+
+
+def _setup(B, natom=40, ml=96, nmd=256, seed=3, constr=None):
+    from oracle import sclmd_oracle as O
+    from sclmd_amd import _native as N
+    from sclmd_amd import synthetic
+
+    dyn, _, baths, meta = synthetic.junction("C3", natom=natom, ml=ml, nmd=nmd, nw=60, seed=seed)
+    nph, dt = meta["nph"], meta["dt"]
+    st = N.Stepper(nph, B, nmd, dt, 0)
+    for b in baths:
+        st.add_bath(N.GLE_BATH_PHONON, b.cids, b.kernel)
+    st.set_dyn(dyn)
+    if constr is not None:
+        st.set_constraint(constr)
+    rng = np.random.default_rng(seed)
+    p = rng.normal(size=(B, nph)) * 1e-2
+    q = rng.normal(size=(B, nph)) * 1e-2
+    noise = [rng.normal(size=(B, nmd, b.nc)) * 1e-3 for b in baths]
+    hist = [rng.normal(size=(B, b.kernel.shape[0], b.nc)) * 1e-2 for b in baths]
+    st.set_state(p, q, 0)
+    for i in range(len(baths)):
+        st.set_history(i, hist[i])
+        st.set_noise(i, noise[i])
+    ob = [O.Bath("ph", b.cids, b.kernel, noise[i], dt, nmd) for i, b in enumerate(baths)]
+    sim = O.GLEBatch(nph, dt, nmd, ob, dyn, ntr=B,
+                     constr=None if constr is None else [range(int(c), int(c) + 1) for c in constr])
+    sim.p, sim.q = p.T.copy(), q.T.copy()
+    for i in range(len(baths)):
+        sim.set_history(i, hist[i])
+    return st, sim, baths, ob, meta, dyn, rng
+
+
+def _check(st, sim, nst_total):
+    p, q, t = st.get_state()
+    assert t == nst_total
+    assert rel(q, sim.q.T) < TOL and rel(p, sim.p.T) < TOL, (rel(q, sim.q.T), rel(p, sim.p.T))
+    cur = st.get_current()[:, :, :nst_total]
+    want = np.stack([c[:, :nst_total] for c in sim.cur])
+    assert rel(cur, want) < 1e-9
+
+
+def test_composed_plan_is_the_c3_bench_plan():
+    """The benched C3 shape (B = 64, spectral ladder) plans the composed step."""
+    from sclmd_amd import _native as N
+    from sclmd_amd import synthetic
+
+    dyn, _, baths, meta = synthetic.junction("C3")
+    st = N.Stepper(meta["nph"], 64, meta["nmd"], meta["dt"], 0)
+    for b in baths:
+        st.add_bath(N.GLE_BATH_PHONON, b.cids, b.kernel)
+    st.set_dyn(dyn)
+    st.set_state(np.zeros((64, meta["nph"])), np.zeros((64, meta["nph"])), 0)
+    d = st.plan_detail()
+    st.close()
+    assert d["composed_step"] and d["plan_class"] == "small"
+
+
+@pytest.mark.parametrize("B", [8, 3])
+def test_composed_vs_oracle_with_path_switches(B):
+    """Composed steps, then steps with a host force (the two-launch path), then composed steps again,
+    a new noise realisation, more composed steps: every segment against the oracle.  B = 8 plans a
+    spectral ladder, B = 3 a direct one."""
+    st, sim, baths, ob, meta, dyn, rng = _setup(B)
+    assert st.plan_detail()["composed_step"]
+    nst = 0
+    st.run(37)
+    for _ in range(37):
+        sim.step()
+    nst += 37
+    _check(st, sim, nst)
+    for _ in range(5):  # host driver steps: md.potforce evaluated on the host (-dyn.q)
+        qt = st.step_begin(-(st.get_state()[1] @ dyn.T))
+        st.step_end(-(qt @ dyn.T))
+        sim.step()
+    nst += 5
+    _check(st, sim, nst)
+    st.run(70)  # crosses level boundaries (P up to 32 at ml = 96)
+    for _ in range(70):
+        sim.step()
+    nst += 70
+    _check(st, sim, nst)
+    for i, b in enumerate(baths):  # a new run's noise (md.py:569-570)
+        n = rng.normal(size=(B, meta["nmd"], b.nc)) * 1e-3
+        st.set_noise(i, n)
+        ob[i].noise = n
+    st.run(41)
+    for _ in range(41):
+        sim.step()
+    nst += 41
+    _check(st, sim, nst)
+    assert st.cache_audit() == (0, 0)
+    st.close()
+
+
+def test_composed_with_constraints_vs_oracle():
+    """ApplyConstraint (md.py:407-408, 782-794) inside the composed step."""
+    st, sim, *_ = _setup(8, constr=[0, 1, 2, 60, 61])
+    assert st.plan_detail()["composed_step"]
+    st.run(120)
+    for _ in range(120):
+        sim.step()
+    _check(st, sim, 120)
+    st.close()
+
+
+def test_cache_audit_counts_reuse_at_rest():
+    """A system at rest with noise of 1e-16: |q~ - q| stays below md.potforce's 1e-9, where the
+    reference reuses the force at q_t; the composed step counts those steps."""
+    from sclmd_amd import _native as N
+    from sclmd_amd import synthetic
+
+    dyn, _, baths, meta = synthetic.junction("C3", natom=40, ml=96, nmd=256, nw=60, seed=3)
+    B = 8
+    st = N.Stepper(meta["nph"], B, meta["nmd"], meta["dt"], 0)
+    for b in baths:
+        st.add_bath(N.GLE_BATH_PHONON, b.cids, b.kernel)
+    st.set_dyn(dyn)
+    st.set_state(np.zeros((B, meta["nph"])), np.zeros((B, meta["nph"])), 0)
+    for i, b in enumerate(baths):
+        st.set_history(i, None)
+        st.set_noise(i, np.full((B, meta["nmd"], b.nc), 1e-16))
+    st.run(10)
+    st.sync()
+    assert st.cache_audit()[0] > 0
+    st.close()
