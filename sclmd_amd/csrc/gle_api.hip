@@ -2019,7 +2019,8 @@ int plan_xstep(gle_handle* h) {
   int rn_raw = (int)std::min<int64_t>(4, (B + 15) / 16);
   const int nt_raw = 16 * rn_raw;
   const int ncolr = (int)((B + nt_raw - 1) / nt_raw);
-  const int raw_ks = 24;
+  int raw_ks = 24;
+  if (const char* e = gle_env("GLE_NEAR3_KS")) raw_ks = std::max(4, atoi(e));
   for (auto& b : h->baths) {
     b.nqn3 = 0;
     if (b.nn > 3) {
@@ -2081,6 +2082,7 @@ int plan_xstep(gle_handle* h) {
     c.tiles.clear();
     c.flops = 0;
     c.nw = 4;
+    if (const char* e = gle_env("GLE_XSTEP_NW")) c.nw = atoi(e) >= 8 ? 8 : 4;
     c.lds = (size_t)6 * 256 * drn * 8;  // the DOF epilogue reduces 6 quantities over the tile
     double* pin = v == 0 ? h->d_P : h->d_P2;
     double* qin = v == 0 ? h->d_Q : h->d_Q2;
@@ -2214,7 +2216,7 @@ int plan_xstep(gle_handle* h) {
   }
   // near-field partial tiles (lags [3, nn), target t+3): in both variants, and alone for priming
   h->chNear3.tiles.clear();
-  h->chNear3.nw = 4;
+  h->chNear3.nw = h->chX[0].nw;
   h->chNear3.lds = 0;
   for (auto& b : h->baths) {
     if (b.nqn3 == 0) continue;
@@ -2670,7 +2672,8 @@ int freeze(gle_handle* h) {
   sd.guard = h->d_guard;
   if (const char* dbg = gle_env("GLE_CHAIN_DBG")) {
     size_t n = 0;
-    for (Chain* c : {&h->chA[0], &h->chA[1], &h->chB[1], &h->chC, &h->chBC}) n = std::max(n, c->tiles.size());
+    for (Chain* c : {&h->chA[0], &h->chA[1], &h->chB[1], &h->chC, &h->chBC, &h->chX[0], &h->chX[1]})
+      n = std::max(n, c->tiles.size());
     sd.dbg_ntile = (int32_t)n;
     sd.dbg_t = atoll(dbg);
     rc = dalloc_n(h, &h->d_dbg, (size_t)3 * n * 4);
@@ -4312,7 +4315,8 @@ int gle_profile(gle_handle* h, int32_t enable) {
   }
   if ((enable & GLE_PROFILE_CHAIN) && !h->d_ctst) {
     size_t n = 0;
-    for (Chain* c : {&h->chA[0], &h->chA[1], &h->chB[0], &h->chB[1], &h->chC, &h->chBC}) n = std::max(n, c->tiles.size());
+    for (Chain* c : {&h->chA[0], &h->chA[1], &h->chB[0], &h->chB[1], &h->chC, &h->chBC, &h->chX[0], &h->chX[1]})
+      n = std::max(n, c->tiles.size());
     n += (size_t)h->far_max_items;  // far items of the fused schedule ride in the same grids
     h->ctst_tiles = n;
     if (n > 0) {
@@ -4420,6 +4424,10 @@ int gle_step_work(gle_handle* h, double* flops, double* bytes) {
   fl += 2.0 * dyn_nnz * B;  // dyn.q~ (the potential force at q~; the fpot launch's CSR product under bc_fpot)
   if (h->bc_fpot) by += 4.0 * dyn_nnz + 4.0 * (h->nph + 1) + 8.0 * 3.0 * (double)h->nph * B;  // CSR columns / rows, Qt, Fc, Q0
   by += 8.0 * dyn_nnz + 8.0 * 12.0 * (double)h->nph * B;  // dyn, state vectors (p, q, p_half, q~, F, caches)
+  if (h->xstep) {  // composed step: its operators' nonzeros, K0 / K1 / K2, the near lags, dyn (plan_xstep)
+    fl = h->x_alg_flops;
+    by = h->x_alg_bytes;
+  }
   for (const Level& lv : h->levels) {
     const double P = (double)lv.P;
     if (lv.spectral) {

@@ -16,9 +16,13 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 
 
 def step_end_stage(rs):
-    """The chain launch that closes a step: the fused velocity stage (chain_kernel<3, ...>, plans with
-    GLE_PLAN_FUSED_BC: 2 chain launches per step) or stage C (chain_kernel<2, ...>: 3 per step)."""
-    return "chain_kernel<3" if any(r["n"].startswith("chain_kernel<3") for r in rs) else "chain_kernel<2"
+    """The chain launch that closes a step: the composed step (chain_kernel<4, ...>, plans with
+    GLE_PLAN_COMPOSED_STEP: one chain launch per step), the fused velocity stage (chain_kernel<3, ...>,
+    plans with GLE_PLAN_FUSED_BC: 2 per step) or stage C (chain_kernel<2, ...>: 3 per step)."""
+    for k in ("chain_kernel<4", "chain_kernel<3"):
+        if any(r["n"].startswith(k) for r in rs):
+            return k
+    return "chain_kernel<2"
 
 
 for r in rows:
@@ -88,8 +92,8 @@ if "--gaps" in sys.argv:
     rows.sort(key=lambda r: r["s"])
     ch = [r for r in rows if r["n"].startswith("chain_kernel")][-301:]
     gaps = [(b["s"] - a["e"]) / 1e3 for a, b in zip(ch, ch[1:])]
-    # steps in the window = its step-closing launches (2 chain launches per step in fused plans, 3
-    # otherwise), not a fixed 3
+    # steps in the window = its step-closing launches (1 chain launch per step in composed plans, 2 in
+    # fused plans, 3 otherwise), not a fixed 3
     nsteps = sum(1 for r in ch[1:] if r["n"].startswith(step_end_stage(ch)))
     if gaps and nsteps:
         print("\nchain gaps over %d launches (%d steps): total %.1f us = %.2f us/step; largest %s"
