@@ -2456,13 +2456,14 @@ int freeze(gle_handle* h) {
       HIPCHK(h, hipStreamSynchronize(h->stream));
     }
     // background stream per level group, bounds in units of P0 (GLE_BG_GROUP=g1,g2 in the experiment
-    // build): small baths {P0 .. 4 P0}, {.. 32 P0}, rest (C3: 8-32 and 64-256; 3 interleaved rounds on
-    // two boxes, `profiles/r04/sched_c3.jsonl`: 20-step phase mean 50.1-50.2 vs 51.0 us/step, 512-step
-    // 48.3-48.6 vs 48.6-48.8; 1,8 / 2,8 / 1,4 / 4,8 / 4,16 cost up to 3 us at 512 steps, one stream
-    // for all 8 us), large baths and direct plans {.. 8 P0}, {.. 64 P0}, rest (C2, direct: 30.8 vs
-    // 31.6 us/step at 512 steps with 4,32; `profiles/r04/sched_c2.jsonl`)
+    // build): small baths {P0}, {.. 8 P0}, rest (C3: 8 | 16-64 | 128-256: each level's pieces are a
+    // chain of small dependent launches, so the ladder is bound by its streams' serial latency, and
+    // the first level, due every P0 steps, gets a stream of its own; round 5 with the composed step:
+    // 42.4-42.9 vs 46.0 us/step, `profiles/r05/composed/sched_ab_c3.jsonl`; round 4's 4,32 was best
+    // beside the two-launch chain), large baths and direct plans {.. 8 P0}, {.. 64 P0}, rest (C2,
+    // direct: 30.8 vs 31.6 us/step at 512 steps with 4,32; `profiles/r04/sched_c2.jsonl`)
     const bool g_small = h->small_baths && spec_ok;
-    int g1 = g_small ? 4 : 8, g2 = g_small ? 32 : 64;
+    int g1 = g_small ? 1 : 8, g2 = g_small ? 8 : 64;
     if (const char* e = gle_env("GLE_BG_GROUP")) sscanf(e, "%d,%d", &g1, &g2);
     lv.sidx = lv.P <= g1 * P0 ? 0 : (lv.P <= g2 * P0 ? 1 : 2);
     for (int q = 0; q < 2; ++q)
@@ -2768,15 +2769,46 @@ int launch_level_pieces(gle_handle* h, Level& lv, int64_t k, hipStream_t s, bool
     // inverse transform DOF ranges
     const int jg = j - lv.nfs + 1;  // 1-based GEMM chunk
     if (j < lv.nfs) {
+      // every bath's DOF range j in one launch (up to MAXFB baths per launch)
+      FftBaths fb{};
+      auto flush = [&]() {
+        if (fb.n && launch_seg_fft_multi(fb, (int)h->B, lv.P, T, priming ? lv.lb[0].M : 1, h->d_cstab, lv.cstride, s,
+                                         lv.nplanes))
+          return fail(h, GLE_ERR_UNSUP, "segment transform launch failed (P = " + std::to_string(lv.P) + ")");
+        fb.n = 0;
+        return GLE_OK;
+      };
       for (size_t b = 0; b < h->baths.size(); ++b) {
         Bath& bb = h->baths[b];
         LevelBath& L = lv.lb[b];
         if (!L.active || (!priming && (h->dbg_skip & 2))) continue;
         const int k0 = (int)((int64_t)bb.nc * j / lv.nfs), k1 = (int)((int64_t)bb.nc * (j + 1) / lv.nfs);
-        if (launch_seg_fft(bb.d_H, bb.ldh, bb.R, (int)h->B, bb.nc, bb.ncp, lv.P, T, priming ? L.M : 1, L.d_seg,
-                           L.seg_fstride, L.ldseg, L.Rseg, h->d_cstab, lv.cstride, s, k0, k1, lv.nplanes))
-          return fail(h, GLE_ERR_UNSUP, "segment transform launch failed (P = " + std::to_string(lv.P) + ")");
+        if (priming && L.M != lv.lb[0].M) {  // (priming transforms all M segments: one bath per launch)
+          if (launch_seg_fft(bb.d_H, bb.ldh, bb.R, (int)h->B, bb.nc, bb.ncp, lv.P, T, L.M, L.d_seg, L.seg_fstride,
+                             L.ldseg, L.Rseg, h->d_cstab, lv.cstride, s, k0, k1, lv.nplanes))
+            return fail(h, GLE_ERR_UNSUP, "segment transform launch failed (P = " + std::to_string(lv.P) + ")");
+          continue;
+        }
+        FftBath& e = fb.b[fb.n++];
+        e = FftBath{};
+        e.H = bb.d_H;
+        e.ldh = bb.ldh;
+        e.R = bb.R;
+        e.nc = bb.nc;
+        e.ncp = bb.ncp;
+        e.k0 = k0;
+        e.nk = k1 - k0;
+        e.seg = L.d_seg;
+        e.seg_fstride = L.seg_fstride;
+        e.ldseg = L.ldseg;
+        e.Rseg = L.Rseg;
+        if (fb.n == MAXFB) {
+          int rc = flush();
+          if (rc) return rc;
+        }
       }
+      int rc = flush();
+      if (rc) return rc;
     } else if (jg <= lv.ncg_chunk) {
       // one chunk of the batched GEMM of the per-frequency products, profiled like run_op
       const int64_t n = nitems;
@@ -2802,17 +2834,36 @@ int launch_level_pieces(gle_handle* h, Level& lv, int64_t k, hipStream_t s, bool
         h->prof_bytes += lv.cg_bytes * frac;
       }
     } else {
-      const int ji = jg - lv.ncg_chunk - 1;  // inverse transform piece
+      const int ji = jg - lv.ncg_chunk - 1;  // inverse transform piece: every bath's range in one launch
+      FftBaths fb{};
+      auto flush = [&]() {
+        if (fb.n && launch_far_ifft_multi(fb, (int)h->B, lv.P, h->d_cstab, lv.cstride, s))
+          return fail(h, GLE_ERR_UNSUP, "inverse transform launch failed (P = " + std::to_string(lv.P) + ")");
+        fb.n = 0;
+        return GLE_OK;
+      };
       for (size_t b = 0; b < h->baths.size(); ++b) {
         Bath& bb = h->baths[b];
         LevelBath& L = lv.lb[b];
         if (!L.active || (!priming && (h->dbg_skip & 4))) continue;
         const int k0 = (int)((int64_t)bb.nc * ji / lv.nif), k1 = (int)((int64_t)bb.nc * (ji + 1) / lv.nif);
-        if (launch_far_ifft(L.d_Yspec, L.yfstride, (!split && lv.cg_split > 1) ? (int64_t)(lv.P + 1) * L.yfstride : 0,
-                            bb.nc, (int)h->B, lv.P, L.d_out + (int64_t)par * lv.P * h->B,
-                            (int64_t)2 * lv.P * h->B, h->d_cstab, lv.cstride, s, k0, k1))
-          return fail(h, GLE_ERR_UNSUP, "inverse transform launch failed (P = " + std::to_string(lv.P) + ")");
+        FftBath& e = fb.b[fb.n++];
+        e = FftBath{};
+        e.Y = L.d_Yspec;
+        e.yfstride = L.yfstride;
+        e.ysplit = (!split && lv.cg_split > 1) ? (int64_t)(lv.P + 1) * L.yfstride : 0;
+        e.nc = bb.nc;
+        e.k0 = k0;
+        e.nk = k1 - k0;
+        e.out = L.d_out + (int64_t)par * lv.P * h->B;
+        e.ldout = (int64_t)2 * lv.P * h->B;
+        if (fb.n == MAXFB) {
+          int rc = flush();
+          if (rc) return rc;
+        }
       }
+      int rc = flush();
+      if (rc) return rc;
     }
   }
   if (j1 >= lv.npiece) {

@@ -406,6 +406,29 @@ void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStre
 // nplanes: 2 (Re, Im: two-plane Gauss items) or 3 (the three Gauss planes, one item per part)
 void launch_khat_pack(const double* Kf, int ml, int nks_k, double* khat, int P, int m0, int M,
                       int nc, int nrt2, int nks2, const double* cstab, int cstride, hipStream_t s, int nplanes);
+// One bath's operands of a ladder level's transform launch: the baths of a piece go out as ONE
+// launch (blocks [blk0, next bath's blk0) are this bath's), not one launch per bath
+struct FftBath {
+  const double* H;       // seg_fft: history ring, row stride ldh, R slots
+  int64_t ldh;
+  int32_t R, nc, ncp, k0, nk, Rseg;
+  double* seg;           // seg_fft: segment-spectra ring
+  int64_t seg_fstride, ldseg;
+  const double* Y;       // far_ifft: Gauss products, block output out (row stride ldout)
+  int64_t yfstride, ysplit;
+  double* out;
+  int64_t ldout;
+  int64_t blk0;
+};
+constexpr int MAXFB = 4;
+struct FftBaths {
+  FftBath b[MAXFB];
+  int32_t n, pad;
+};
+// the baths' transforms of one level piece in one launch (nbath <= MAXFB; k ranges per bath)
+int launch_seg_fft_multi(FftBaths fb, int B, int P, int64_t T, int nseg, const double* cstab, int cstride,
+                         hipStream_t s, int nplanes);
+int launch_far_ifft_multi(FftBaths fb, int B, int P, const double* cstab, int cstride, hipStream_t s);
 int launch_seg_fft(const double* H, int64_t ldh, int R, int B, int nc, int ncp, int P, int64_t T,
                    int nseg, double* seg, int64_t seg_fstride, int64_t ldseg, int Rseg,
                    const double* cstab, int cstride, hipStream_t s, int k0, int k1, int nplanes);

@@ -919,20 +919,32 @@ void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStre
 // series per complex FFT.
 // BC trajectories per block: 64 for the small transforms (one block per DOF, 512 B rows, every
 // thread busy in every butterfly stage), fewer for long transforms (LDS: BC/2 series of 2P points)
+__device__ __forceinline__ FftBath pick_bath(const FftBaths& fb, int64_t blk) {
+  FftBath r = fb.b[0];
+#pragma unroll
+  for (int j = 1; j < MAXFB; ++j)
+    if (j < fb.n && blk >= fb.b[j].blk0) r = fb.b[j];
+  return r;
+}
+
 template <int BC>
-__global__ __launch_bounds__(256) void seg_fft_kernel(const double* __restrict__ H, int64_t ldh, int R,
-                                                      int B, int k0, int nk, int ncp, int P, int logn,
-                                                      int64_t T, double* __restrict__ seg,
-                                                      int64_t seg_fstride, int64_t ldseg, int Rseg,
+__global__ __launch_bounds__(256) void seg_fft_kernel(FftBaths fb, int B, int P, int logn, int64_t T,
                                                       const double2* __restrict__ cstab, int cstride,
                                                       int nplanes) {
   extern __shared__ double2 fbuf[];  // BC/2 series of N points, then N/2 twiddles
+  const FftBath bt = pick_bath(fb, blockIdx.x);
+  const int64_t blk = (int64_t)blockIdx.x - bt.blk0;
+  const double* __restrict__ H = bt.H;
+  const int64_t ldh = bt.ldh;
+  const int R = bt.R, nk = bt.nk, ncp = bt.ncp, Rseg = bt.Rseg;
+  double* __restrict__ seg = bt.seg;
+  const int64_t seg_fstride = bt.seg_fstride, ldseg = bt.ldseg;
   const int N = 2 * P;
   stage_twiddles(fbuf + (BC / 2) * N, N, cstab, cstride);
   const int nbc = (B + BC - 1) / BC;
-  const int bc = blockIdx.x % nbc;
-  const int k = k0 + (int)((blockIdx.x / nbc) % nk);
-  const int sidx = blockIdx.x / (nbc * nk);
+  const int bc = (int)(blk % nbc);
+  const int k = bt.k0 + (int)((blk / nbc) % nk);
+  const int sidx = (int)(blk / ((int64_t)nbc * nk));
   const int64_t sigma = T / P - sidx;
   const int64_t t0 = sigma * P - 2 * P + 2;
   const int b0 = bc * BC;
@@ -1014,20 +1026,36 @@ static int fft_bc(int B, int P) {
 }
 
 template <int BC>
-static int seg_fft_launch(const double* H, int64_t ldh, int R, int B, int k0, int nk, int ncp, int P, int logn,
-                          int64_t T, int nseg, double* seg, int64_t seg_fstride, int64_t ldseg, int Rseg,
-                          const double* cstab, int cstride, hipStream_t s, int nplanes) {
+static int seg_fft_launch(const FftBaths& fb, int B, int P, int logn, int64_t T, const double* cstab, int cstride,
+                          hipStream_t s, int nplanes, int64_t blocks) {
   const size_t shmem = ((size_t)(BC / 2) * 2 * P + P) * sizeof(double2);
   if (shmem > 160 * 1024) return -2;
   // raise the dynamic-LDS limit once per instantiation (a per-launch attribute call costs host
   // time on the step's critical path at block boundaries)
   if (!lds_attr_once((const void*)seg_fft_kernel<BC>)) return -3;
-  const int nbc = (B + BC - 1) / BC;
-  const int64_t blocks = (int64_t)nseg * nk * nbc;
   if (blocks <= 0) return 0;
-  seg_fft_kernel<BC><<<(unsigned)blocks, 256, shmem, s>>>(H, ldh, R, B, k0, nk, ncp, P, logn, T, seg, seg_fstride,
-                                                           ldseg, Rseg, (const double2*)cstab, cstride, nplanes);
+  seg_fft_kernel<BC><<<(unsigned)blocks, 256, shmem, s>>>(fb, B, P, logn, T, (const double2*)cstab, cstride, nplanes);
   return 0;
+}
+
+int launch_seg_fft_multi(FftBaths fb, int B, int P, int64_t T, int nseg, const double* cstab, int cstride,
+                         hipStream_t s, int nplanes) {
+  int logn = 0;
+  while ((1 << logn) < 2 * P) ++logn;
+  if ((1 << logn) != 2 * P) return -1;
+  const int bc = fft_bc(B, P);
+  const int nbc = (B + bc - 1) / bc;
+  int64_t blocks = 0;
+  for (int j = 0; j < fb.n; ++j) {
+    fb.b[j].blk0 = blocks;
+    blocks += (int64_t)nseg * std::max(0, fb.b[j].nk) * nbc;
+  }
+  switch (bc) {
+    case 64: return seg_fft_launch<64>(fb, B, P, logn, T, cstab, cstride, s, nplanes, blocks);
+    case 32: return seg_fft_launch<32>(fb, B, P, logn, T, cstab, cstride, s, nplanes, blocks);
+    case 16: return seg_fft_launch<16>(fb, B, P, logn, T, cstab, cstride, s, nplanes, blocks);
+    default: return seg_fft_launch<8>(fb, B, P, logn, T, cstab, cstride, s, nplanes, blocks);
+  }
 }
 
 int launch_seg_fft(const double* H, int64_t ldh, int R, int B, int nc, int ncp, int P, int64_t T,
@@ -1035,17 +1063,22 @@ int launch_seg_fft(const double* H, int64_t ldh, int R, int B, int nc, int ncp, 
                    const double* cstab, int cstride, hipStream_t s, int k0, int k1, int nplanes) {
   if (k1 < 0 || k1 > nc) k1 = nc;
   k0 = k0 < 0 ? 0 : k0;
-  const int nk = k1 - k0;
-  if (nk <= 0) return 0;
-  int logn = 0;
-  while ((1 << logn) < 2 * P) ++logn;
-  if ((1 << logn) != 2 * P) return -1;
-  switch (fft_bc(B, P)) {
-    case 64: return seg_fft_launch<64>(H, ldh, R, B, k0, nk, ncp, P, logn, T, nseg, seg, seg_fstride, ldseg, Rseg, cstab, cstride, s, nplanes);
-    case 32: return seg_fft_launch<32>(H, ldh, R, B, k0, nk, ncp, P, logn, T, nseg, seg, seg_fstride, ldseg, Rseg, cstab, cstride, s, nplanes);
-    case 16: return seg_fft_launch<16>(H, ldh, R, B, k0, nk, ncp, P, logn, T, nseg, seg, seg_fstride, ldseg, Rseg, cstab, cstride, s, nplanes);
-    default: return seg_fft_launch<8>(H, ldh, R, B, k0, nk, ncp, P, logn, T, nseg, seg, seg_fstride, ldseg, Rseg, cstab, cstride, s, nplanes);
-  }
+  if (k1 - k0 <= 0) return 0;
+  FftBaths fb{};
+  fb.n = 1;
+  FftBath& b = fb.b[0];
+  b.H = H;
+  b.ldh = ldh;
+  b.R = R;
+  b.nc = nc;
+  b.ncp = ncp;
+  b.k0 = k0;
+  b.nk = k1 - k0;
+  b.seg = seg;
+  b.seg_fstride = seg_fstride;
+  b.ldseg = ldseg;
+  b.Rseg = Rseg;
+  return launch_seg_fft_multi(fb, B, P, T, nseg, cstab, cstride, s, nplanes);
 }
 
 // Block output out(kP + 1 + j) = y[j + P - 1] (j < P) of the real inverse transform of the
@@ -1054,16 +1087,20 @@ int launch_seg_fft(const double* H, int64_t ldh, int R, int B, int nc, int ncp, 
 //   y[n] = (1/2P) sum_{f<2P} Y(f) e^{+i pi f n / P},  Y(2P - f) = conj Y(f).
 // Grid: DOF k x 8-trajectory chunk; two real outputs per complex inverse FFT.
 template <int BC>
-__global__ __launch_bounds__(256) void far_ifft_kernel(const double* __restrict__ Y, int64_t yfstride,
-                                                       int64_t ysplit, int nc, int k0, int B, int P, int logn,
-                                                       double* __restrict__ out, int64_t ldout,
+__global__ __launch_bounds__(256) void far_ifft_kernel(FftBaths fb, int B, int P, int logn,
                                                        const double2* __restrict__ cstab, int cstride) {
   extern __shared__ double2 fbuf[];  // BC/2 series of N points, then N/2 twiddles
+  const FftBath bt = pick_bath(fb, blockIdx.x);
+  const int64_t blk = (int64_t)blockIdx.x - bt.blk0;
+  const double* __restrict__ Y = bt.Y;
+  const int64_t yfstride = bt.yfstride, ysplit = bt.ysplit, ldout = bt.ldout;
+  double* __restrict__ out = bt.out;
+  const int nc = bt.nc;
   const int N = 2 * P;
   stage_twiddles(fbuf + (BC / 2) * N, N, cstab, cstride);
   const int nbc = (B + BC - 1) / BC;
-  const int bc = blockIdx.x % nbc;
-  const int k = k0 + (int)(blockIdx.x / nbc);
+  const int bc = (int)(blk % nbc);
+  const int k = bt.k0 + (int)(blk / nbc);
   const int b0 = bc * BC;
   const int64_t pl = (int64_t)nc * B;
   for (int e = threadIdx.x; e < N * BC / 2; e += blockDim.x) {
@@ -1110,34 +1147,54 @@ __global__ __launch_bounds__(256) void far_ifft_kernel(const double* __restrict_
 }
 
 template <int BC>
-static int far_ifft_launch(const double* Y, int64_t yfstride, int64_t ysplit, int nc, int k0, int nk, int B, int P,
-                           int logn, double* out, int64_t ldout, const double* cstab, int cstride, hipStream_t s) {
+static int far_ifft_launch(const FftBaths& fb, int B, int P, int logn, const double* cstab, int cstride, hipStream_t s,
+                           int64_t blocks) {
   const size_t shmem = ((size_t)(BC / 2) * 2 * P + P) * sizeof(double2);
   if (shmem > 160 * 1024) return -2;
   // raise the dynamic-LDS limit once per instantiation (a per-launch attribute call costs host
   // time on the step's critical path at block boundaries)
   if (!lds_attr_once((const void*)far_ifft_kernel<BC>)) return -3;
-  const int nbc = (B + BC - 1) / BC;
-  far_ifft_kernel<BC><<<(unsigned)(nk * nbc), 256, shmem, s>>>(Y, yfstride, ysplit, nc, k0, B, P, logn, out, ldout,
-                                                              (const double2*)cstab, cstride);
+  if (blocks <= 0) return 0;
+  far_ifft_kernel<BC><<<(unsigned)blocks, 256, shmem, s>>>(fb, B, P, logn, (const double2*)cstab, cstride);
   return 0;
+}
+
+int launch_far_ifft_multi(FftBaths fb, int B, int P, const double* cstab, int cstride, hipStream_t s) {
+  int logn = 0;
+  while ((1 << logn) < 2 * P) ++logn;
+  if ((1 << logn) != 2 * P) return -1;
+  const int bc = fft_bc(B, P);
+  const int nbc = (B + bc - 1) / bc;
+  int64_t blocks = 0;
+  for (int j = 0; j < fb.n; ++j) {
+    fb.b[j].blk0 = blocks;
+    blocks += (int64_t)std::max(0, fb.b[j].nk) * nbc;
+  }
+  switch (bc) {
+    case 64: return far_ifft_launch<64>(fb, B, P, logn, cstab, cstride, s, blocks);
+    case 32: return far_ifft_launch<32>(fb, B, P, logn, cstab, cstride, s, blocks);
+    case 16: return far_ifft_launch<16>(fb, B, P, logn, cstab, cstride, s, blocks);
+    default: return far_ifft_launch<8>(fb, B, P, logn, cstab, cstride, s, blocks);
+  }
 }
 
 int launch_far_ifft(const double* Y, int64_t yfstride, int64_t ysplit, int nc, int B, int P, double* out,
                     int64_t ldout, const double* cstab, int cstride, hipStream_t s, int k0, int k1) {
   if (k1 < 0 || k1 > nc) k1 = nc;
   k0 = k0 < 0 ? 0 : k0;
-  const int nk = k1 - k0;
-  if (nk <= 0) return 0;
-  int logn = 0;
-  while ((1 << logn) < 2 * P) ++logn;
-  if ((1 << logn) != 2 * P) return -1;
-  switch (fft_bc(B, P)) {
-    case 64: return far_ifft_launch<64>(Y, yfstride, ysplit, nc, k0, nk, B, P, logn, out, ldout, cstab, cstride, s);
-    case 32: return far_ifft_launch<32>(Y, yfstride, ysplit, nc, k0, nk, B, P, logn, out, ldout, cstab, cstride, s);
-    case 16: return far_ifft_launch<16>(Y, yfstride, ysplit, nc, k0, nk, B, P, logn, out, ldout, cstab, cstride, s);
-    default: return far_ifft_launch<8>(Y, yfstride, ysplit, nc, k0, nk, B, P, logn, out, ldout, cstab, cstride, s);
-  }
+  if (k1 - k0 <= 0) return 0;
+  FftBaths fb{};
+  fb.n = 1;
+  FftBath& b = fb.b[0];
+  b.Y = Y;
+  b.yfstride = yfstride;
+  b.ysplit = ysplit;
+  b.nc = nc;
+  b.k0 = k0;
+  b.nk = k1 - k0;
+  b.out = out;
+  b.ldout = ldout;
+  return launch_far_ifft_multi(fb, B, P, cstab, cstride, s);
 }
 
 }  // namespace gle
