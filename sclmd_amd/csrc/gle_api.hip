@@ -2072,6 +2072,7 @@ int plan_xstep(gle_handle* h) {
   // ---- tiles
   const int drn = h->ch_drn;
   const int ncol1 = (int)((B + 16 * drn - 1) / (16 * drn));
+  const bool xsplit = gle_env("GLE_XSPLIT") != nullptr;
   auto err_off = [&](int code) {  // a plan the chain cannot hold: keep the two-launch plan
     h->err.clear();
     (void)code;
@@ -2169,6 +2170,23 @@ int plan_xstep(gle_handle* h) {
           for (const XRun& r : o.wp[j])
             segs.push_back(Seg{CH_OYB, h->d_xfrag + r.off, 64, b.d_W1 + (int64_t)v * b.vs + (int64_t)4 * r.ks0 * B,
                                (int)B, 0, 0, r.nks, 0});
+        }
+        if (xsplit) {
+          // GLE_XSPLIT (experiment): the composed p_{t+1} products in one workgroup, the id0 phase
+          // (K0.p_t, dyn.q_t) and q_{t+1} in another (F1 of md.f is not formed)
+          std::vector<Seg> sp, sq;
+          for (auto& sg : segs) (sg.o == CH_OYB ? sp : sq).push_back(sg);
+          for (int part = 1; part <= 2; ++part) {
+            ChTile Tp = T;
+            Tp.xpart = part;
+            Tp.first = part == 2 ? T.first : 0;
+            const auto& ss = part == 1 ? sp : sq;
+            int64_t W = 0;
+            for (auto& sg : ss) W += sg.nks;
+            if (fill_tasks(h, Tp, ss, CH_NOUT, 0, W, c)) return err_off(0);
+            c.tiles.push_back(Tp);
+          }
+          continue;
         }
         int64_t W = 0;
         for (auto& sg : segs) W += sg.nks;

@@ -867,7 +867,8 @@ __device__ __forceinline__ void dof_X(const ChTile* __restrict__ T, const StepDe
   // md.potforce cache audit of the previous step (its words at parity par1): the first row tile of
   // each column tile counts the trajectories whose cache rule would have reused a force at a point
   // within 1e-9 but not equal, and zeroes the words for step t + 1
-  if (T->first && threadIdx.x < 2 * Geo::NT) {
+  const int part = T->xpart;  // 1: p_{t+1} only, 2: id0 phase and q_{t+1} only, 0: both
+  if (T->first && part != 1 && threadIdx.x < 2 * Geo::NT) {
     const int id = threadIdx.x / Geo::NT, b = T->c0 + (int)threadIdx.x % Geo::NT;
     if (b < B) {
       unsigned long long* w = pmax_word(sd, id, par1, b);
@@ -911,10 +912,11 @@ __device__ __forceinline__ void dof_X(const ChTile* __restrict__ T, const StepDe
       p2 = 0.0;
       qn = 0.0;
     }
-    if (E[x].ok) {
-      G(T->xp_out)[E[x].i] = p2;
-      G(T->xq_out)[E[x].i] = qn;
+    if (E[x].ok && part != 2) G(T->xp_out)[E[x].i] = p2;
+    if (E[x].ok && part == 0)
       G(sd->Flast)[E[x].i] = (xp - ph) * (2.0 / dt);  // F1(p1): p2 = p_half + dt F1(p1) / 2 (md.py:403-404)
+    if (E[x].ok && part != 1) {
+      G(T->xq_out)[E[x].i] = qn;
       const int64_t rs = (int64_t)tn * sd->nph * B + E[x].i;
       if (sd->rec_p) G(sd->rec_p)[rs] = p[x];
       if (sd->rec_q) G(sd->rec_q)[rs] = q[x];
@@ -930,17 +932,20 @@ __device__ __forceinline__ void dof_X(const ChTile* __restrict__ T, const StepDe
         const ChBath& bd = T->tb[u];
         const int64_t kb = (int64_t)kk[x][u] * B + E[x].b;
         const int64_t slot = cmod(t + 1, bd.R);  // history push of p_{t+1} (md.py:386-387)
-        auto hh = G(bd.H + (int64_t)kk[x][u] * bd.ldh + E[x].b);
-        hh[slot * B] = p2;
-        hh[(slot + bd.R) * B] = p2;
-        G(bd.NR)[cmod(t + 1, bd.NRS) * bd.vs + kb] = p2;
-        if (bd.has_q) G(bd.Xq)[(int64_t)par1 * bd.vs + kb] = qn;
+        if (part != 2) {
+          auto hh = G(bd.H + (int64_t)kk[x][u] * bd.ldh + E[x].b);
+          hh[slot * B] = p2;
+          hh[(slot + bd.R) * B] = p2;
+          G(bd.NR)[cmod(t + 1, bd.NRS) * bd.vs + kb] = p2;
+        }
+        if (bd.has_q && part != 1) G(bd.Xq)[(int64_t)par1 * bd.vs + kb] = qn;
       }
     }
     ee[x] = E[x].ok ? p[x] * p[x] : 0.0;
     d1[x] = E[x].ok ? fabs(qt - q[x]) : 0.0;   // |q~ - q0| of the id1 call (q0 = q_t)
     d0[x] = E[x].ok ? fabs(qn - qt) : 0.0;     // |q_{t+1} - q0| of the next id0 call (q0 = q~)
   }
+  if (part == 1) return;  // the p_{t+1} half of a split tile: no reductions
   // per-trajectory sums over the tile's DOFs (fixed row order): currents and energy into the step's
   // partial table, the two cache distances as maxima into the parity-par words
   __syncthreads();

@@ -306,6 +306,8 @@ struct ChTile {
   const double* xq_in;
   double* xp_out;
   double* xq_out;
+  int32_t xpart;     // stage 4 CH_DOF: 0 the whole tile, 1 p_{t+1} only, 2 the id0 phase and q_{t+1} only
+  int32_t xpad;
   int32_t ntw[CH_NW]; // tasks of wave w (32-bit: read with scalar loads)
   int32_t ob[CH_NOUT + 1];  // output o adds LDS slots [ob[o], ob[o+1]); outputs: Y of tile bath u
                             // (u < CH_TB), YQ of tile bath u (CH_TB + u), YD (2 CH_TB);
