@@ -324,10 +324,6 @@ int gle_plan_detail(gle_handle* h, int32_t* plan_class, int32_t* fused_waves, do
  * reference's md.potforce reuses the force at q0 when 0 < max|q~ - q0| < 1e-9 (md.py:767-779); such
  * steps are counted, see gle_cache_audit. */
 #define GLE_PLAN_COMPOSED_STEP 8
-/* GLE_PLAN_KHAT_SYM: every memory kernel of a spectral level is exactly symmetric (K_i == K_i^T,
- * checked on the device), so the far field stores and streams only the blocks of K-hat(f) on and
- * above the diagonal (half the bytes; the same sums in the same order) */
-#define GLE_PLAN_KHAT_SYM 16
 int gle_plan_flags(gle_handle* h, int32_t* flags);
 /* Composed steps (GLE_PLAN_COMPOSED_STEP) at which md.potforce's cache rule (sameq, md.py:767-779)
  * would have reused a force at a point within 1e-9 but not equal to the evaluation point: counts[0]

@@ -90,7 +90,6 @@ struct Bath {
   // near-field partials of lags [3, nn) [2][nqn3][vs]
   double *d_V0 = nullptr, *d_W1 = nullptr, *d_NP3 = nullptr;
   int nqn3 = 0;
-  int ksym = -1;  // every slice K_i exactly symmetric (1), not (0), not yet checked (-1)
   int64_t vs = 0;          // doubles per bath-local [ncp][B] buffer (with slack)
   int64_t ldh = 0;
   int R = 1;
@@ -129,7 +128,6 @@ struct LevelBath {
   int M = 0, Rseg = 0;
   int64_t ldseg = 0, khat_fstride = 0, seg_fstride = 0, yfstride = 0;
   double *d_khat = nullptr, *d_seg = nullptr, *d_Yspec = nullptr;
-  int sym = 0;          // K-hat in the symmetric layout (every K_i of the bath exactly symmetric)
 };
 
 // Level l of the ladder: block length P; lags [2P, lag1).  Block k (targets kP+1..kP+P) only needs
@@ -1767,7 +1765,7 @@ int plan_far_fused(gle_handle* h) {
         LevelBath& L = lv.lb[j];
         if (!L.active) continue;
         const int64_t a_rt = (int64_t)L.M * b.nks * 64;
-        const int64_t plane = khat_plane_doubles(b.nrt, b.nks, L.M, L.sym);
+        const int64_t plane = (int64_t)b.nrt * a_rt;
         const int S = L.M * b.nks;
         for (int f = 0; f <= lv.P; ++f) {
           const bool real = f == 0 || f == lv.P;  // real spectra: T_1, T_2 stay zero
@@ -1780,11 +1778,8 @@ int plan_far_fused(gle_handle* h) {
                 it.ns = (int32_t)((int64_t)S * (sp + 1) / lv.nsplit) - it.s0;
                 it.accum = sp > 0 ? 1 : 0;
                 it.g3 = (lv.nplanes == 2 && !real) ? 1 : 0;
-                it.A = L.d_khat + (int64_t)f * L.khat_fstride + g * plane + (L.sym ? 0 : (int64_t)4 * rg * a_rt);
+                it.A = L.d_khat + (int64_t)f * L.khat_fstride + g * plane + (int64_t)4 * rg * a_rt;
                 it.a_pl = plane;
-                it.sym = L.sym;
-                it.rt0 = 4 * rg;
-                it.nksS = 4 * b.nrt;
                 it.X = L.d_seg + (int64_t)f * L.seg_fstride + (int64_t)g * b.ncp * L.ldseg;
                 it.x_pl = (int64_t)b.ncp * L.ldseg;
                 it.out = L.d_Yspec + (int64_t)f * L.yfstride + (int64_t)g * b.nc * B + (int64_t)64 * rg * B + c0;
@@ -2467,28 +2462,7 @@ int freeze(gle_handle* h) {
       // harmless for the results but outside the row).
       L.ldseg = (int64_t)L.Rseg * B + (lv.nplanes == 2 ? 32 : 512);
       if (const char* e = gle_env("GLE_SEG_PAD")) L.ldseg = (int64_t)L.Rseg * B + std::max(0, atoi(e));
-      // symmetric kernels (every K_i equal to its transpose up to 64 ulps of its largest entry,
-      // checked on the device once per bath: phbath.gmem's numpy products leave ~1e-20 between
-      // K_i[r][c] and K_i[c][r], the device construction none): K-hat(f) is complex symmetric, so only
-      // its blocks on and above the diagonal are stored and streamed (half the far field's HBM
-      // stream, gle_cgemm.h khat_sym_off); the blocks below read their mirror, a change within the
-      // kernel's own rounding (as gle_set_dyn's drop of dyn's eigen-reconstruction roundoff)
-      if (b.ksym < 0) {
-        double* d_mx = nullptr;
-        HIPCHK(h, tmalloc(&d_mx, (size_t)2 * b.ml * sizeof(double)));
-        std::vector<double> mx((size_t)2 * b.ml, 1.0);
-        launch_sym_check(b.d_K, b.ml, b.nc, b.nks, d_mx, h->stream);
-        hipError_t e = hipMemcpyAsync(mx.data(), d_mx, mx.size() * 8, hipMemcpyDeviceToHost, h->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
-        tfree(d_mx);
-        if (e != hipSuccess) return fail(h, GLE_ERR_HIP, std::string("kernel symmetry check: ") + hipGetErrorString(e));
-        b.ksym = 1;
-        for (int i = 0; i < b.ml; ++i)
-          if (!(mx[2 * i + 1] <= std::ldexp(mx[2 * i], -46))) b.ksym = 0;
-      }
-      L.sym = b.ksym == 1 ? 1 : 0;
-      if (const char* e = gle_env("GLE_KHAT_SYM")) L.sym = atoi(e) != 0 ? L.sym : 0;
-      L.khat_fstride = (int64_t)lv.nplanes * khat_plane_doubles(b.nrt, b.nks, L.M, L.sym);  // Re, Im | the Gauss planes
+      L.khat_fstride = (int64_t)lv.nplanes * b.nrt * b.nks * L.M * 64;  // Re, Im | the Gauss planes
       L.seg_fstride = (int64_t)lv.nplanes * b.ncp * L.ldseg;             // Re, Im | Re + Im, Im, Re rows
       L.yfstride = (int64_t)3 * b.nc * B;                       // T_0, T_1, T_2
       rc = dalloc_n(h, &L.d_khat, (size_t)(lv.P + 1) * L.khat_fstride);
@@ -2496,7 +2470,7 @@ int freeze(gle_handle* h) {
       if (!rc) rc = dalloc_n(h, &L.d_Yspec, (size_t)lv.cg_split * (lv.P + 1) * L.yfstride, 4096);
       if (rc) return rc;
       launch_khat_pack(b.d_K, b.ml, b.nks, L.d_khat, lv.P, 2, L.M, b.nc, b.nrt, b.nks, h->d_cstab,
-                       lv.cstride, h->stream, lv.nplanes, L.sym);
+                       lv.cstride, h->stream, lv.nplanes);
       HIPCHK(h, hipStreamSynchronize(h->stream));
     }
     // background stream per level group, bounds in units of P0 (GLE_BG_GROUP=g1,g2 in the experiment
@@ -2580,7 +2554,7 @@ int freeze(gle_handle* h) {
         LevelBath& L = lv.lb[j];
         if (!L.active) continue;
         const int64_t a_rt = (int64_t)L.M * b.nks * 64;
-        const int64_t plane = khat_plane_doubles(b.nrt, b.nks, L.M, L.sym);
+        const int64_t plane = (int64_t)b.nrt * a_rt;
         for (int f = 0; f <= lv.P; ++f) {
           // f = 0 and f = P: K-hat and X-hat are real, so Re Y = T_0 - T_1 = T_0 = Kr Xr and Im Y is
           // dropped (far_ifft realonly): one product, the T_1 / T_2 planes stay zero.  Otherwise one
@@ -2597,11 +2571,8 @@ int freeze(gle_handle* h) {
                 it.s0 = S * hk / lv.cg_split;
                 it.ns = S * (hk + 1) / lv.cg_split - it.s0;
                 it.g3 = (lv.nplanes == 2 && !real) ? 1 : 0;
-                it.A = L.d_khat + (int64_t)f * L.khat_fstride + g * plane + (L.sym ? 0 : (int64_t)4 * rg * a_rt);
+                it.A = L.d_khat + (int64_t)f * L.khat_fstride + g * plane + (int64_t)4 * rg * a_rt;
                 it.a_pl = plane;
-                it.sym = L.sym;
-                it.rt0 = 4 * rg;
-                it.nksS = 4 * b.nrt;
                 it.X = L.d_seg + (int64_t)f * L.seg_fstride + (int64_t)g * b.ncp * L.ldseg;
                 it.x_pl = (int64_t)b.ncp * L.ldseg;
                 it.out = L.d_Yspec + (int64_t)hk * (lv.P + 1) * L.yfstride + (int64_t)f * L.yfstride +
@@ -2626,11 +2597,7 @@ int freeze(gle_handle* h) {
             const bool two = lv.nplanes == 2 && !real;
             const double np = two ? 3.0 : 1.0, npl = two ? 2.0 : 1.0;
             lv.cg_flops += np * 2.0 * b.nc * ((double)L.M * b.nc) * B;
-            // (symmetric layout: K-hat's stored blocks, about half)
-            const double kfrac = L.sym ? (double)khat_plane_doubles(b.nrt, b.nks, L.M, 1) /
-                                             (double)khat_plane_doubles(b.nrt, b.nks, L.M, 0) : 1.0;
-            lv.cg_bytes += 8.0 * (npl * kfrac * (double)b.nc * L.M * b.nc + npl * (double)L.M * b.nc * B +
-                                  np * (double)b.nc * B);
+            lv.cg_bytes += 8.0 * (npl * (double)b.nc * L.M * b.nc + npl * (double)L.M * b.nc * B + np * (double)b.nc * B);
           }
         }
       }
@@ -4790,9 +4757,6 @@ int gle_plan_flags(gle_handle* h, int32_t* flags) {
   if (!h->frozen) return fail(h, GLE_ERR_STATE, "no plan yet (gle_set_state builds it)");
   *flags = (h->fuse_bc ? GLE_PLAN_FUSED_BC : 0) | (h->bc_fpot ? GLE_PLAN_FPOT_LAUNCH : 0) |
            (h->far_fused ? GLE_PLAN_FAR_FUSED : 0) | (h->xstep ? GLE_PLAN_COMPOSED_STEP : 0);
-  for (const Level& lv : h->levels)
-    for (const LevelBath& L : lv.lb)
-      if (L.active && L.sym) *flags |= GLE_PLAN_KHAT_SYM;
   return GLE_OK;
 }
 

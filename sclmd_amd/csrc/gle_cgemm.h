@@ -27,23 +27,6 @@ constexpr int CG_LD = 80;  // LDS row stride (doubles): 64 columns + 16, ds_read
 
 typedef const __attribute__((address_space(1))) double gdbl;
 
-// K-hat fragment offset (doubles, lane included) of row tile rt at k-step ks of partition m in the
-// symmetric layout (CgItem::sym): row tile I holds the 16 x 16 blocks I..nrt-1 of every partition,
-// k-steps [4I, nksS), so a fragment on or above the diagonal is read as stored; one below it is the
-// transpose of its mirror block (I = ks / 4, column k-steps 4 rt .. 4 rt + 3): the lane's element
-// A[16 rt + (l & 15)][4 ks + (l >> 4)] = K-hat[4 ks + (l >> 4)][16 rt + (l & 15)] sits in fragment
-// (l & 15) / 4 of that block at lane (4 (ks & 3) + (l >> 4)) | ((l & 3) << 4).  The four k-steps of
-// a block read its 2 KB once between them (L1 / L2 serve the scattered lanes).
-__device__ __forceinline__ int64_t khat_sym_off(const CgItem& it, int rt, int m, int ks, int lane) {
-  const int nS = it.nksS;
-  const bool up = ks >= 4 * rt;
-  const int I = up ? rt : (ks >> 2);
-  const int64_t offr = 64ll * it.M * ((int64_t)I * nS - 2ll * I * (I - 1));
-  const int col = up ? ks - 4 * rt : 4 * (rt - I) + ((lane & 15) >> 2);
-  const int ln = up ? lane : ((4 * (ks & 3) + (lane >> 4)) | ((lane & 3) << 4));
-  return offr + ((int64_t)m * (nS - 4 * I) + col) * 64 + ln;
-}
-
 // The far-field operand K-hat (GBs, each fragment read once per block) streams through with
 // non-temporal loads, so it does not evict the per-step chain's matrices (~2 MB per XCD with the
 // XCD-aware chain tile order) from the L2s.  CG_NT=0: default cache policy.
@@ -67,7 +50,7 @@ __device__ __forceinline__ int64_t khat_sym_off(const CgItem& it, int rt, int m,
 #ifndef CG_XD
 #define CG_XD 1
 #endif
-template <int RN, int KC, int AD, int XD, int DBG = 0, bool SYM = false>
+template <int RN, int KC, int AD, int XD, int DBG = 0>
 __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, double (&xs)[2][4 * KC * CG_LD]) {
   static_assert(XD == 1 || XD == 2, "X ring of one or two chunks");
   static_assert((AD + 1) % XD == 0, "the A ring period carries the X ring's");
@@ -83,18 +66,7 @@ __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, doubl
   const bool active = wave < it.nrt;
   // global address space: flat loads would also count on lgkmcnt, and every LDS-read wait before an
   // MFMA would then drain the HBM prefetches in flight
-  gdbl* Aw = SYM ? (gdbl*)it.A : (gdbl*)(it.A + (int64_t)(active ? wave : 0) * it.a_rt + (int64_t)it.s0 * 64 + lane);
-  const int rtw = it.rt0 + (active ? wave : 0);
-  // offset of the item's k-step s (clamped) from Aw
-  auto a_idx = [&](int s) -> int64_t {
-    if constexpr (SYM) {
-      const int sa = it.s0 + s;
-      const int m = (int)((unsigned)sa / (unsigned)it.nks);
-      return khat_sym_off(it, rtw, m, sa - m * it.nks, lane);
-    } else {
-      return (int64_t)s * 64;
-    }
-  };
+  gdbl* Aw = (gdbl*)(it.A + (int64_t)(active ? wave : 0) * it.a_rt + (int64_t)it.s0 * 64 + lane);
   const int xr = tid / TPR, xc = (tid % TPR) * XPT;
   const int tbase = (int)cg_pmod(tseg, it.Rseg);  // ring slot of segment tseg (32-bit from here on)
   // Loads are branch-free (clamped address, zero by multiplication): a branch around a load makes
@@ -106,7 +78,8 @@ __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, doubl
 #ifdef GLE_BOUNDS
 #define CG_BCHK_X(u)                                                                                  \
   GLE_BCHK(it.X + (int64_t)(4 * ks_ + (xr & 3)) * it.ldx + (int64_t)slot_ * it.cs + it.col0 + xc + (u))
-#define CG_BCHK_A(s) GLE_BCHK((const double*)Aw + a_idx(s))
+#define CG_BCHK_A(s)                                                                                  \
+  GLE_BCHK(it.A + (int64_t)(active ? wave : 0) * it.a_rt + (int64_t)it.s0 * 64 + lane + (int64_t)(s) * 64)
 #else
 #define CG_BCHK_X(u) ((void)0)
 #define CG_BCHK_A(s) ((void)0)
@@ -136,7 +109,7 @@ __device__ __forceinline__ void cgemm_item(const CgItem& it, int64_t tseg, doubl
     _Pragma("unroll") for (int u = 0; u < KC; ++u) {                                               \
       const int s0_ = (c) * KC + u;                                                                \
       CG_BCHK_A(s0_ < S ? s0_ : S - 1);                                                               \
-      AV[u] = (DBG & 1) ? 1e-3 * (s0_ + 1) : CG_ALOAD(&Aw[a_idx(s0_ < S ? s0_ : S - 1)]); /* masked */ \
+      AV[u] = (DBG & 1) ? 1e-3 * (s0_ + 1) : CG_ALOAD(&Aw[(int64_t)(s0_ < S ? s0_ : S - 1) * 64]); /* masked */ \
     }                                                                                                 \
   } while (0)
   // chunk c (ring position r = c mod (AD + 1), a compile-time constant inside the unrolled period):
@@ -223,7 +196,7 @@ struct Cg3 {
   static constexpr int LDS = 2 * 2 * PLANE;      // two buffers x two planes
 };
 
-template <int RN, int KC, int AD, bool SYM = false>
+template <int RN, int KC, int AD>
 __device__ __forceinline__ void cgemm_item3(const CgItem& it, int64_t tseg, double* xs) {
   using C = Cg3<RN, KC>;
   constexpr int NT = C::NT, LD = C::LD, PL = C::PLANE;
@@ -236,17 +209,7 @@ __device__ __forceinline__ void cgemm_item3(const CgItem& it, int64_t tseg, doub
   const int S = it.ns;
   const int nch = (S + KC - 1) / KC;
   const bool active = wave < it.nrt;
-  gdbl* Aw = SYM ? (gdbl*)it.A : (gdbl*)(it.A + (int64_t)(active ? wave : 0) * it.a_rt + (int64_t)it.s0 * 64 + lane);
-  const int rtw = it.rt0 + (active ? wave : 0);
-  auto a_idx = [&](int s) -> int64_t {
-    if constexpr (SYM) {
-      const int sa = it.s0 + s;
-      const int m = (int)((unsigned)sa / (unsigned)it.nks);
-      return khat_sym_off(it, rtw, m, sa - m * it.nks, lane);
-    } else {
-      return (int64_t)s * 64;
-    }
-  };
+  gdbl* Aw = (gdbl*)(it.A + (int64_t)(active ? wave : 0) * it.a_rt + (int64_t)it.s0 * 64 + lane);
   const int64_t apl = it.a_pl;
   const int xpl = tid / (4 * KC * TPR);                 // plane this thread stages (0: Xr, 1: Xi)
   const int xr = (tid % (4 * KC * TPR)) / TPR, xc = (tid % TPR) * XPT;
@@ -260,7 +223,7 @@ __device__ __forceinline__ void cgemm_item3(const CgItem& it, int64_t tseg, doub
     for (int n = 0; n < RN; ++n) acc[g][n] = d4{0.0, 0.0, 0.0, 0.0};
 #ifdef GLE_BOUNDS
 #define CG3_BCHK_X(u) GLE_BCHK(Xp + (int64_t)(4 * ks_ + (xr & 3)) * it.ldx + (int64_t)slot_ * it.cs + it.col0 + xc + (u))
-#define CG3_BCHK_A(s, o) GLE_BCHK((const double*)Aw + a_idx(s) + (o))
+#define CG3_BCHK_A(s, o) GLE_BCHK(it.A + (int64_t)(active ? wave : 0) * it.a_rt + (int64_t)it.s0 * 64 + lane + (int64_t)(s) * 64 + (o))
 #else
 #define CG3_BCHK_X(u) ((void)0)
 #define CG3_BCHK_A(s, o) ((void)0)
@@ -287,7 +250,7 @@ __device__ __forceinline__ void cgemm_item3(const CgItem& it, int64_t tseg, doub
   do {                                                                                                \
     _Pragma("unroll") for (int u = 0; u < KC; ++u) {                                               \
       const int s0_ = (c) * KC + u;                                                                \
-      const int64_t o_ = a_idx(s0_ < S ? s0_ : S - 1);                                                 \
+      const int64_t o_ = (int64_t)(s0_ < S ? s0_ : S - 1) * 64;                                       \
       CG3_BCHK_A(s0_ < S ? s0_ : S - 1, 0);                                                           \
       CG3_BCHK_A(s0_ < S ? s0_ : S - 1, apl);                                                         \
       ar[R][u] = CG_ALOAD(&Aw[o_]);                                                                   \
@@ -371,14 +334,11 @@ template <int RN, int KC, int AD, int XD, int DBG = 0>
 __device__ __forceinline__ void cgemm_any(const CgItem& it, int64_t tseg, double* lds) {
   if constexpr (RN <= 2) {
     if (it.g3) {
-      if (it.sym) cgemm_item3<RN, cg3_kc<RN, KC>(), (AD < 4 ? AD : 4), true>(it, tseg, lds);
-      else cgemm_item3<RN, cg3_kc<RN, KC>(), (AD < 4 ? AD : 4), false>(it, tseg, lds);
+      cgemm_item3<RN, cg3_kc<RN, KC>(), (AD < 4 ? AD : 4)>(it, tseg, lds);
       return;
     }
   }
-  auto& xs = *reinterpret_cast<double(*)[2][4 * KC * CG_LD]>(lds);
-  if (it.sym) cgemm_item<RN, KC, AD, XD, DBG, true>(it, tseg, xs);
-  else cgemm_item<RN, KC, AD, XD, DBG, false>(it, tseg, xs);
+  cgemm_item<RN, KC, AD, XD, DBG>(it, tseg, *reinterpret_cast<double(*)[2][4 * KC * CG_LD]>(lds));
 }
 
 }  // namespace gle

@@ -1158,13 +1158,10 @@ __device__ __forceinline__ void far_tile(const StepArgs& ta, double* lds) {
     // one-plane items only (the planner keeps two-plane levels out of the fused schedule): the
     // two-plane path's three accumulator sets would set the whole chain kernel's register budget
     auto& xs = *reinterpret_cast<double(*)[2][4 * 4 * CG_LD]>(lds);
-    switch ((it.ncols > 32 ? 4 : (it.ncols > 16 ? 2 : 1)) + (it.sym ? 8 : 0)) {
+    switch (it.ncols > 32 ? 4 : (it.ncols > 16 ? 2 : 1)) {
       case 4: cgemm_item<4, 4, 3, 1>(it, tseg, xs); break;
       case 2: cgemm_item<2, 4, 3, 1>(it, tseg, xs); break;
-      case 1: cgemm_item<1, 4, 3, 1>(it, tseg, xs); break;
-      case 12: cgemm_item<4, 4, 3, 1, 0, true>(it, tseg, xs); break;
-      case 10: cgemm_item<2, 4, 3, 1, 0, true>(it, tseg, xs); break;
-      default: cgemm_item<1, 4, 3, 1, 0, true>(it, tseg, xs); break;
+      default: cgemm_item<1, 4, 3, 1>(it, tseg, xs); break;
     }
   }
 }

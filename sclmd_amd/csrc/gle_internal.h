@@ -130,10 +130,6 @@ struct CgItem {
   int64_t a_pl;      // doubles from the Kr plane to the Ki plane
   int64_t x_pl;      // doubles from the Xr plane to the Xi plane
   int64_t o_pl;      // doubles between the T_g planes
-  // symmetric K-hat layout (every K_i of the bath symmetric: K-hat(f) complex symmetric): A is the
-  // plane base, only the 16 x 16 blocks on and above the diagonal are stored (row tile I: k-steps
-  // [4I, nksS) of every partition), the item's row tiles are rt0 + wave (gle_cgemm.h khat_sym_off)
-  int32_t sym, rt0, nksS, pad3;
 };
 
 // Deterministic fixed-order sum of split partial tiles (+ optional far-field addend).
@@ -411,16 +407,7 @@ void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStre
                   unsigned long long* ts = nullptr);
 // nplanes: 2 (Re, Im: two-plane Gauss items) or 3 (the three Gauss planes, one item per part)
 void launch_khat_pack(const double* Kf, int ml, int nks_k, double* khat, int P, int m0, int M,
-                      int nc, int nrt2, int nks2, const double* cstab, int cstride, hipStream_t s, int nplanes,
-                      int sym = 0);
-// doubles of one K-hat plane of one frequency: dense nrt M nks 64, symmetric 64 M sum_I (4 nrt - 4 I)
-__host__ __device__ inline int64_t khat_plane_doubles(int nrt, int nks, int M, int sym) {
-  if (!sym) return (int64_t)nrt * M * nks * 64;
-  const int64_t nS = 4 * (int64_t)nrt;
-  return 64ll * M * (nrt * nS - 2ll * nrt * (nrt - 1));
-}
-// per slice i of a fragment-native kernel: mx[2 i] = max |K_i|, mx[2 i + 1] = max |K_i - K_i^T|
-void launch_sym_check(const double* Kf, int ml, int nc, int nks, double* mx, hipStream_t s);
+                      int nc, int nrt2, int nks2, const double* cstab, int cstride, hipStream_t s, int nplanes);
 // One bath's operands of a ladder level's transform launch: the baths of a piece go out as ONE
 // launch (blocks [blk0, next bath's blk0) are this bath's), not one launch per bath
 struct FftBath {

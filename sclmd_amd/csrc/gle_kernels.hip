@@ -723,25 +723,21 @@ namespace gle {
 //   planes Re, Im (nplanes = 2: the two-plane Gauss items form Re + Im, Im - Re in registers) or as
 //   the three Gauss planes Re, Re + Im, Im - Re (nplanes = 3: one item per Gauss part), read
 //   straight out of the fragment-native K already on the device (one-time setup).
-// sym: the symmetric layout (CgItem::sym, gle_cgemm.h khat_sym_off): k-steps run to 4 nrt2 (zero past
-// nc) and only those with ks2 >= 4 rt2 are stored
 __global__ void khat_pack_kernel(const double* __restrict__ Kf, int ml, int nks_k,
                                  double* __restrict__ khat, int P, int m0, int M, int nc, int nrt2,
-                                 int nks2, const double2* __restrict__ cstab, int cstride, int nplanes, int sym) {
-  const int nkl = sym ? 4 * nrt2 : nks2;  // k-steps of the loop
-  const int64_t total = (int64_t)(P + 1) * nrt2 * M * nkl * 64;
-  const int64_t plane = khat_plane_doubles(nrt2, nks2, M, sym);
+                                 int nks2, const double2* __restrict__ cstab, int cstride, int nplanes) {
+  const int64_t total = (int64_t)(P + 1) * nrt2 * M * nks2 * 64;
+  const int64_t plane = (int64_t)nrt2 * M * nks2 * 64;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int lane = (int)(e & 63);
     int64_t r_ = e >> 6;
-    const int ks2 = (int)(r_ % nkl);
-    r_ /= nkl;
+    const int ks2 = (int)(r_ % nks2);
+    r_ /= nks2;
     const int mm = (int)(r_ % M);
     r_ /= M;
     const int rt2 = (int)(r_ % nrt2);
     const int f = (int)(r_ / nrt2);
-    if (sym && ks2 < 4 * rt2) continue;  // below the diagonal: read from the mirror block
     const int r = 16 * rt2 + (lane & 15);
     const int k = 4 * ks2 + (lane >> 4);
     double re = 0.0, im = 0.0;
@@ -757,10 +753,7 @@ __global__ void khat_pack_kernel(const double* __restrict__ Kf, int ml, int nks_
         im -= kv * cs.y;
       }
     }
-    const int64_t o = (int64_t)f * nplanes * plane +
-                      (sym ? 64ll * M * ((int64_t)rt2 * nkl - 2ll * rt2 * (rt2 - 1)) +
-                                 ((int64_t)mm * (nkl - 4 * rt2) + (ks2 - 4 * rt2)) * 64
-                           : (((int64_t)rt2 * M + mm) * nks2 + ks2) * 64) + lane;
+    const int64_t o = (int64_t)f * nplanes * plane + (((int64_t)rt2 * M + mm) * nks2 + ks2) * 64 + lane;
     khat[o] = re;
     if (nplanes == 2) {
       khat[o + plane] = im;
@@ -772,48 +765,9 @@ __global__ void khat_pack_kernel(const double* __restrict__ Kf, int ml, int nks_
 }
 
 void launch_khat_pack(const double* Kf, int ml, int nks_k, double* khat, int P, int m0, int M,
-                      int nc, int nrt2, int nks2, const double* cstab, int cstride, hipStream_t s, int nplanes,
-                      int sym) {
+                      int nc, int nrt2, int nks2, const double* cstab, int cstride, hipStream_t s, int nplanes) {
   khat_pack_kernel<<<8192, 256, 0, s>>>(Kf, ml, nks_k, khat, P, m0, M, nc, nrt2, nks2,
-                                        (const double2*)cstab, cstride, nplanes, sym);
-}
-
-// symmetry of every slice of a fragment-native kernel ([rt][ks][i][64], lane l of fragment (rt, ks, i)
-// = K_i[16 rt + (l & 15)][4 ks + (l >> 4)]): block i writes mx[2 i] = max |K_i|, mx[2 i + 1] =
-// max_{r<c} |K_i[r][c] - K_i[c][r]|
-__global__ __launch_bounds__(256) void sym_check_kernel(const double* __restrict__ Kf, int ml, int nc, int nks,
-                                                        double* __restrict__ mx) {
-  const int i = blockIdx.x;
-  auto at = [&](int rr, int cc) {
-    return Kf[(((int64_t)(rr >> 4) * nks + (cc >> 2)) * ml + i) * 64 + (rr & 15) + 16 * (cc & 3)];
-  };
-  double amax = 0.0, dmax = 0.0;
-  const int64_t n = (int64_t)nc * nc;
-  for (int64_t e = threadIdx.x; e < n; e += blockDim.x) {
-    const int r = (int)(e / nc), c = (int)(e % nc);
-    const double a = at(r, c);
-    amax = fmax(amax, fabs(a));
-    if (c > r) dmax = fmax(dmax, fabs(a - at(c, r)));
-  }
-  __shared__ double red[2][256];
-  red[0][threadIdx.x] = amax;
-  red[1][threadIdx.x] = dmax;
-  __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) {
-      red[0][threadIdx.x] = fmax(red[0][threadIdx.x], red[0][threadIdx.x + w]);
-      red[1][threadIdx.x] = fmax(red[1][threadIdx.x], red[1][threadIdx.x + w]);
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    mx[2 * i] = red[0][0];
-    mx[2 * i + 1] = red[1][0];
-  }
-}
-
-void launch_sym_check(const double* Kf, int ml, int nc, int nks, double* mx, hipStream_t s) {
-  sym_check_kernel<<<(unsigned)ml, 256, 0, s>>>(Kf, ml, nc, nks, mx);
+                                        (const double2*)cstab, cstride, nplanes);
 }
 
 // In-place radix-2 FFT of NS complex series of length N = 2^logn held bit-reversed in LDS

@@ -72,7 +72,7 @@ def test_composed_plan_is_the_c3_bench_plan():
     st.set_state(np.zeros((64, meta["nph"])), np.zeros((64, meta["nph"])), 0)
     d = st.plan_detail()
     st.close()
-    assert d["composed_step"] and d["plan_class"] == "small" and d["khat_sym"]
+    assert d["composed_step"] and d["plan_class"] == "small"
 
 
 @pytest.mark.parametrize("B", [8, 3])
@@ -142,38 +142,4 @@ def test_cache_audit_counts_reuse_at_rest():
     st.run(10)
     st.sync()
     assert st.cache_audit()[0] > 0
-    st.close()
-
-
-def test_asymmetric_kernel_takes_the_dense_khat_layout():
-    """A kernel with one entry off its transpose plans the dense K-hat layout (no khat_sym flag) and
-    still matches the oracle; the symmetric layout is exercised by every other spectral test."""
-    from oracle import sclmd_oracle as O
-    from sclmd_amd import _native as N
-    from sclmd_amd import synthetic
-
-    dyn, _, baths, meta = synthetic.junction("C3", natom=40, ml=96, nmd=256, nw=60, seed=3)
-    B, nph, nmd, dt = 8, meta["nph"], meta["nmd"], meta["dt"]
-    kern = [np.array(b.kernel) for b in baths]
-    for k in kern:  # K_40 (a spectral level's lag) of both baths off its transpose
-        k[40, 3, 7] += 1e-6 * np.abs(k[40]).max()
-    st = N.Stepper(nph, B, nmd, dt, 0)
-    for b, k in zip(baths, kern):
-        st.add_bath(N.GLE_BATH_PHONON, b.cids, k)
-    st.set_dyn(dyn)
-    rng = np.random.default_rng(11)
-    p, q = rng.normal(size=(B, nph)) * 1e-2, rng.normal(size=(B, nph)) * 1e-2
-    noise = [rng.normal(size=(B, nmd, b.nc)) * 1e-3 for b in baths]
-    st.set_state(p, q, 0)
-    for i in range(len(baths)):
-        st.set_history(i, None)
-        st.set_noise(i, noise[i])
-    assert not st.plan_detail()["khat_sym"]
-    ob = [O.Bath("ph", b.cids, k, noise[i], dt, nmd) for i, (b, k) in enumerate(zip(baths, kern))]
-    sim = O.GLEBatch(nph, dt, nmd, ob, dyn, ntr=B)
-    sim.p, sim.q = p.T.copy(), q.T.copy()
-    st.run(150)
-    for _ in range(150):
-        sim.step()
-    _check(st, sim, 150)
     st.close()
