@@ -324,6 +324,10 @@ int gle_plan_detail(gle_handle* h, int32_t* plan_class, int32_t* fused_waves, do
  * reference's md.potforce reuses the force at q0 when 0 < max|q~ - q0| < 1e-9 (md.py:767-779); such
  * steps are counted, see gle_cache_audit. */
 #define GLE_PLAN_COMPOSED_STEP 8
+/* GLE_PLAN_SPLIT_TILES: composed-step plans with few DOF tiles (small B, e.g. one trajectory) split
+ * each tile's products over up to 8 workgroups by k-steps; the last to finish adds the partial sums
+ * in a fixed order and runs the tile's md.vv epilogue (same result to fp64 rounding). */
+#define GLE_PLAN_SPLIT_TILES 16
 int gle_plan_flags(gle_handle* h, int32_t* flags);
 /* Composed steps (GLE_PLAN_COMPOSED_STEP) at which md.potforce's cache rule (sameq, md.py:767-779)
  * would have reused a force at a point within 1e-9 but not equal to the evaluation point: counts[0]

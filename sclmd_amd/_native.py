@@ -619,7 +619,7 @@ class Stepper:
         return {"plan_class": names.get(int(c.value), int(c.value)), "fused_waves": int(w.value),
                 "cg_per_cu": float(cu.value), "nlevel": int(n.value), "dyn_dropped": int(dd.value),
                 "far_fused": bool(ff.value), "fpot_launch": bool(fl.value & 2),
-                "composed_step": bool(fl.value & 8)}
+                "composed_step": bool(fl.value & 8), "split_tiles": bool(fl.value & 16)}
 
     def cache_audit(self):
         """(at q~, at q_{t+1} after a constraint): composed steps at which md.potforce's cache rule

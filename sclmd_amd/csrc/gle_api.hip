@@ -259,6 +259,10 @@ struct gle_handle {
   double *d_P2 = nullptr, *d_Q2 = nullptr;
   double* d_xfrag = nullptr;           // composed-operator DOF-tile fragments
   unsigned long long* d_guard = nullptr;
+  double* d_xslab = nullptr;           // split stage-4 DOF tiles: slabs and arrival counters
+  unsigned long long* d_xcnt = nullptr;
+  int64_t xslab_n = 0;
+  bool x_split = false;                // the composed plan splits DOF tiles
   double x_alg_flops = 0, x_alg_bytes = 0;  // algorithmic chain work per composed step
   // fused stage with the potential force at q~ evaluated before it (bc_fpot): a small launch between
   // A and BC computes md.potforce at q~ for every DOF (cache rule included) and adds it to the bath
@@ -2073,6 +2077,15 @@ int plan_xstep(gle_handle* h) {
   const int drn = h->ch_drn;
   const int ncol1 = (int)((B + 16 * drn - 1) / (16 * drn));
   const bool xsplit = gle_env("GLE_XSPLIT") != nullptr;
+  // DOF tiles split over workgroups by k-steps (xsub_combine, gle_chain.hip) when the plan has few
+  // of them (small B): a tile's products are then streamed by up to CH_XSUB_MAX workgroups instead
+  // of one CU's four waves
+  int xks = ntile * ncol1 < 128 ? 128 : 0;  // C2 (B = 1): 23.3 us/step vs 26.2 unsplit, 24.0 at 32 k-steps; C3 slower split
+  if (const char* e = gle_env("GLE_XSUB_KS")) xks = std::max(0, atoi(e));
+  const int64_t xne = (int64_t)256 * drn;
+  std::vector<int> xns((size_t)ntile * ncol1, 1);
+  std::vector<int64_t> xoff((size_t)ntile * ncol1, 0);
+  int64_t xslab_n = 0;
   auto err_off = [&](int code) {  // a plan the chain cannot hold: keep the two-launch plan
     h->err.clear();
     (void)code;
@@ -2190,6 +2203,25 @@ int plan_xstep(gle_handle* h) {
         }
         int64_t W = 0;
         for (auto& sg : segs) W += sg.nks;
+        const size_t ti = (size_t)rt * ncol1 + ct;
+        if (v == 0 && xks > 0) {
+          xns[ti] = (int)std::min<int64_t>(CH_XSUB_MAX, std::max<int64_t>(1, (W + xks - 1) / xks));
+          xoff[ti] = xslab_n;
+          if (xns[ti] > 1) xslab_n += (int64_t)xns[ti] * CH_XO * xne;
+        }
+        if (xns[ti] > 1) {
+          for (int sub = 0; sub < xns[ti]; ++sub) {
+            ChTile Ts = T;
+            Ts.xsub = sub;
+            Ts.xnsub = xns[ti];
+            Ts.first = sub == 0 ? T.first : 0;
+            Ts.xslab = (double*)(uintptr_t)(xoff[ti] + 1);  // slab offset + 1, resolved below
+            Ts.xcnt = (unsigned long long*)(uintptr_t)(ti + 1);
+            if (fill_tasks(h, Ts, segs, CH_NOUT, W * sub / xns[ti], W * (sub + 1) / xns[ti], c)) return err_off(0);
+            c.tiles.push_back(Ts);
+          }
+          continue;
+        }
         if (fill_tasks(h, T, segs, CH_NOUT, 0, W, c)) return err_off(0);
         c.tiles.push_back(T);
       }
@@ -2265,6 +2297,23 @@ int plan_xstep(gle_handle* h) {
           }
         }
     }
+  }
+  h->x_split = xslab_n > 0;
+  if (xslab_n > 0) {  // split DOF tiles: slabs and arrival counters (zeroed: the counters count from 0)
+    if (!h->d_xslab || h->xslab_n < xslab_n) {
+      rc = dalloc_n(h, &h->d_xslab, (size_t)xslab_n);
+      if (!rc) rc = dalloc_n(h, &h->d_xcnt, (size_t)ntile * ncol1);
+      if (rc) return rc;
+      h->xslab_n = xslab_n;
+    } else {
+      HIPCHK(h, hipMemsetAsync(h->d_xcnt, 0, (size_t)ntile * ncol1 * 8, h->stream));
+    }
+    for (int v = 0; v < 2; ++v)
+      for (ChTile& T : h->chX[v].tiles)
+        if (T.kind == CH_DOF && T.xnsub > 1) {
+          T.xslab = h->d_xslab + ((int64_t)(uintptr_t)T.xslab - 1);
+          T.xcnt = h->d_xcnt + ((int64_t)(uintptr_t)T.xcnt - 1);
+        }
   }
   for (Chain* c : {&h->chX[0], &h->chX[1], &h->chNear3}) {
     if (c->tiles.empty()) continue;
@@ -4756,7 +4805,8 @@ int gle_plan_flags(gle_handle* h, int32_t* flags) {
   if (!h || !flags) return GLE_ERR_ARG;
   if (!h->frozen) return fail(h, GLE_ERR_STATE, "no plan yet (gle_set_state builds it)");
   *flags = (h->fuse_bc ? GLE_PLAN_FUSED_BC : 0) | (h->bc_fpot ? GLE_PLAN_FPOT_LAUNCH : 0) |
-           (h->far_fused ? GLE_PLAN_FAR_FUSED : 0) | (h->xstep ? GLE_PLAN_COMPOSED_STEP : 0);
+           (h->far_fused ? GLE_PLAN_FAR_FUSED : 0) | (h->xstep ? GLE_PLAN_COMPOSED_STEP : 0) |
+           (h->xstep && h->x_split ? GLE_PLAN_SPLIT_TILES : 0);
   return GLE_OK;
 }
 

@@ -830,6 +830,62 @@ __device__ __forceinline__ void dof_BC(const ChTile* __restrict__ T, const StepD
   }
 }
 
+// A stage-4 DOF tile split over T->xnsub workgroups (k-ranges of its products): this workgroup's
+// output sums go to its slab with write-through (sc1) stores, drained by every wave before the
+// workgroup's barrier; lane 0 then adds to the tile's arrival counter (relaxed, agent scope).  The
+// last arriver reads every slab with sc1 loads (no stale L1 / L2 line of another XCD can serve
+// them) and sums them in slab order, so the result does not depend on the arrival order.  The
+// counter is never reset: every launch adds exactly xnsub per tile (zeroed with the plan).
+template <int NW, int NE, int EPT>
+__device__ __forceinline__ bool xsub_combine(const ChTile* __restrict__ T, double (&ov)[EPT][CH_XO], double* lds) {
+  typedef __attribute__((address_space(1))) unsigned long long gull;
+  gull* slab = (gull*)T->xslab;
+  const int ns = T->xnsub;
+#pragma unroll
+  for (int x = 0; x < EPT; ++x) {
+    const int e = threadIdx.x + x * NW * 64;
+    if (e < NE) {
+#pragma unroll
+      for (int o = 0; o < CH_XO; ++o)
+        __hip_atomic_store(slab + ((int64_t)T->xsub * CH_XO + o) * NE + e,
+                           (unsigned long long)__double_as_longlong(ov[x][o]), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave's slab stores have completed; the LDS partial slots are read
+  if (threadIdx.x == 0) {
+    const unsigned long long old = __hip_atomic_fetch_add((gull*)T->xcnt, 1ull, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+    lds[0] = (old + 1) % (unsigned long long)ns == 0 ? 1.0 : 0.0;
+  }
+  __syncthreads();
+  if (lds[0] == 0.0) return false;
+#pragma unroll
+  for (int x = 0; x < EPT; ++x) {
+    const int e = min((int)threadIdx.x + x * NW * 64, NE - 1);
+#pragma unroll
+    for (int o = 0; o < CH_XO; ++o) ov[x][o] = 0.0;
+    // slabs four at a time, all loads of a group in flight together; masked slabs add 0.0
+    for (int s0 = 0; s0 < ns; s0 += 4) {
+      double v[4][CH_XO];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int sl = min(s0 + k, ns - 1);
+#pragma unroll
+        for (int o = 0; o < CH_XO; ++o)
+          v[k][o] = __longlong_as_double((long long)__hip_atomic_load(slab + ((int64_t)sl * CH_XO + o) * NE + e,
+                                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int o = 0; o < CH_XO; ++o) ov[x][o] += s0 + k < ns ? v[k][o] : 0.0;
+    }
+  }
+  return true;
+}
+
 // stage 4 (composed one-launch step, gle_internal.h), DOF tile: p_{t+1} is the composed product
 // (output CH_OYB); K0.p_t (u), Kq.q_t (CH_TB + u) and dyn.q_t (2 CH_TB) give md.vv's id0 phase for the
 // tile's elements: F0, heat current, kinetic energy, recordings, q_{t+1} = q~ (md.py:383-398);
@@ -882,15 +938,26 @@ __device__ __forceinline__ void dof_X(const ChTile* __restrict__ T, const StepDe
   run_products_rn<NW, DRN>(T, t, lds);
   __syncthreads();
   stamp(sd, 4, 2, ta);
+  // the tile's output sums: K0.p_t of tile bath u (u), dyn.q_t (CH_TB), p_{t+1} (CH_TB + 1)
+  double ov[EPT][CH_XO];
+#pragma unroll
+  for (int x = 0; x < EPT; ++x) {
+    const int e = min((int)threadIdx.x + x * NW * 64, Geo::NE - 1);
+#pragma unroll
+    for (int u = 0; u < CH_TB; ++u) ov[x][u] = out_sum<NW>(T, lds, u, e, Geo::NE);
+    ov[x][CH_TB] = out_sum<NW>(T, lds, 2 * CH_TB, e, Geo::NE);
+    ov[x][CH_TB + 1] = out_sum<NW>(T, lds, CH_OYB, e, Geo::NE);
+  }
+  if (T->xnsub > 1 && !xsub_combine<NW, Geo::NE, EPT>(T, ov, lds)) return;
   double cur[EPT][CH_TB], ee[EPT], d1[EPT], d0[EPT];
 #pragma unroll
   for (int x = 0; x < EPT; ++x) {
     const int e = min((int)threadIdx.x + x * NW * 64, Geo::NE - 1);
-    const double yd = out_sum<NW>(T, lds, 2 * CH_TB, e, Geo::NE);
-    const double xp = out_sum<NW>(T, lds, CH_OYB, e, Geo::NE);
+    const double yd = ov[x][CH_TB];
+    const double xp = ov[x][CH_TB + 1];
     double y[CH_TB];
 #pragma unroll
-    for (int u = 0; u < CH_TB; ++u) y[u] = out_sum<NW>(T, lds, u, e, Geo::NE);
+    for (int u = 0; u < CH_TB; ++u) y[u] = ov[x][u];
     double f = -1.0 * yd;  // potforce(q_t) = -1.0*mdot(dyn, q) (md.py:467)
 #pragma unroll
     for (int u = 0; u < CH_TB; ++u) {

@@ -235,6 +235,8 @@ constexpr int CH_OYF = CH_OYE + CH_TB;
 constexpr int CH_NOUT = CH_OYF + CH_TB;
 constexpr int CH_LDS_PER_WAVE = 1024;  // doubles of LDS partial slots per wave
 constexpr int CH_NPMAX = 16;    // near-field partial slots read by one SFIN element
+constexpr int CH_XO = CH_TB + 2;  // split stage-4 DOF tile slab outputs: K0.p_t of tile bath u, dyn.q_t, p_{t+1}
+constexpr int CH_XSUB_MAX = 8;    // workgroups one stage-4 DOF tile may be split over
 enum { CH_DOF = 0, CH_SFIN = 1, CH_RAW = 2 };
 
 struct ChTask {
@@ -307,7 +309,13 @@ struct ChTile {
   double* xp_out;
   double* xq_out;
   int32_t xpart;     // stage 4 CH_DOF: 0 the whole tile, 1 p_{t+1} only, 2 the id0 phase and q_{t+1} only
-  int32_t xpad;
+  // stage 4 CH_DOF split over xnsub workgroups (k-ranges of the tile's products, xsub = this one's):
+  // each stores its output sums to slab xsub of xslab ([xnsub][CH_XO][16 x 16 rn], write-through),
+  // adds to the tile's arrival counter xcnt, and the last arriver sums the slabs in slab order and
+  // runs the epilogue
+  int32_t xsub, xnsub;
+  double* xslab;
+  unsigned long long* xcnt;
   int32_t ntw[CH_NW]; // tasks of wave w (32-bit: read with scalar loads)
   int32_t ob[CH_NOUT + 1];  // output o adds LDS slots [ob[o], ob[o+1]); outputs: Y of tile bath u
                             // (u < CH_TB), YQ of tile bath u (CH_TB + u), YD (2 CH_TB);

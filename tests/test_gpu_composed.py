@@ -72,7 +72,7 @@ def test_composed_plan_is_the_c3_bench_plan():
     st.set_state(np.zeros((64, meta["nph"])), np.zeros((64, meta["nph"])), 0)
     d = st.plan_detail()
     st.close()
-    assert d["composed_step"] and d["plan_class"] == "small"
+    assert d["composed_step"] and d["plan_class"] == "small" and not d["split_tiles"]
 
 
 @pytest.mark.parametrize("B", [8, 3])
@@ -109,6 +109,33 @@ def test_composed_vs_oracle_with_path_switches(B):
     nst += 41
     _check(st, sim, nst)
     assert st.cache_audit() == (0, 0)
+    st.close()
+
+
+@pytest.mark.parametrize("B", [1, 2])
+def test_split_tiles_vs_oracle(B):
+    """Few DOF tiles (small B): each tile's products split over workgroups, the last arriver adding
+    the slabs in fixed order (GLE_PLAN_SPLIT_TILES, xsub_combine in gle_chain.hip); 130 steps across
+    level boundaries, a host-force segment and a new noise realisation, against the oracle."""
+    st, sim, baths, ob, meta, dyn, rng = _setup(B, natom=120)
+    d = st.plan_detail()
+    assert d["composed_step"] and d["split_tiles"]
+    st.run(61)
+    for _ in range(61):
+        sim.step()
+    _check(st, sim, 61)
+    for _ in range(3):
+        qt = st.step_begin(-(st.get_state()[1] @ dyn.T))
+        st.step_end(-(qt @ dyn.T))
+        sim.step()
+    for i, b in enumerate(baths):
+        n = rng.normal(size=(B, meta["nmd"], b.nc)) * 1e-3
+        st.set_noise(i, n)
+        ob[i].noise = n
+    st.run(66)
+    for _ in range(66):
+        sim.step()
+    _check(st, sim, 130)
     st.close()
 
 
