@@ -158,7 +158,7 @@ pmc|pmc_c5)
       python3 bench.py $A > $O/pmc_$n/$c.json 2> $O/pmc_$n/$c.err || fail "pmc $c" $O/pmc_$n/$c.err
   done
   python3 scripts/pmc_summary.py $O/pmc_$n $O/pmc_$n/traffic_cgemm.json --kernel cgemm_kernel $cfg
-  python3 scripts/pmc_summary.py $O/pmc_$n $O/pmc_$n/traffic_chain.json --kernel chain_kernel $cfg --last 1024 --skip-chain-window 0 ;;
+  python3 scripts/pmc_summary.py $O/pmc_$n $O/pmc_$n/traffic_chain.json --kernel chain_kernel $cfg --last ${CHAIN_LAST:-512} --skip-chain-window 0 ;;
 *)
   echo "unknown task $task"; exit 2 ;;
 esac
