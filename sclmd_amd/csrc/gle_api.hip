@@ -2527,9 +2527,10 @@ int freeze(gle_handle* h) {
     // chain of small dependent launches, so the ladder is bound by its streams' serial latency, and
     // the first level, due every P0 steps, gets a stream of its own; round 5 with the composed step:
     // 42.4-42.9 vs 46.0 us/step, `profiles/r05/composed/sched_ab_c3.jsonl`; round 4's 4,32 was best
-    // beside the two-launch chain), large baths and direct plans {.. 8 P0}, {.. 64 P0}, rest (C2,
-    // direct: 30.8 vs 31.6 us/step at 512 steps with 4,32; `profiles/r04/sched_c2.jsonl`)
-    const bool g_small = h->small_baths && spec_ok;
+    // beside the two-launch chain; small-bath direct plans too since the composed step: C2 21.1 vs
+    // 23.4 us/step, the largest level's 0.56 ms contraction no longer holds up the first level's
+    // blocks, `profiles/r05/split/bg_group_ab_c2.jsonl`), large baths {.. 8 P0}, {.. 64 P0}, rest
+    const bool g_small = h->small_baths;
     int g1 = g_small ? 1 : 8, g2 = g_small ? 8 : 64;
     if (const char* e = gle_env("GLE_BG_GROUP")) sscanf(e, "%d,%d", &g1, &g2);
     lv.sidx = lv.P <= g1 * P0 ? 0 : (lv.P <= g2 * P0 ? 1 : 2);
