@@ -11,7 +11,8 @@
 #              first via --early-collective), interleaved twice; 8-rank same-device gloo rehearsal
 #   trace      rocprofv3 kernel trace + stats of the C3 bench, summarised
 #   pmc        FETCH_SIZE / WRITE_SIZE passes over the C3 bench (cgemm and chain traffic)
-#   trace_c5 / pmc_c5   the same for the C5 line
+#   trace_c5 / pmc_c5   the same for the C5 line; trace_c2 the C2 line's trace
+#   blocklen   bench lines at several first block lengths (BLS, CONFIGS, ROUNDS)
 #   c5run      md.Run wall time per run at C5 (scripts/c5_run_timing.py: noise, stepping, MD{j}.nc)
 #   negf       GLE ensemble current vs the NEGF Landauer current (tests/test_gpu_negf.py)
 #   ab         experiment libraries x GLE_* variants, interleaved (LIBS, VARIANTS, ROUNDS, EXPARGS,
@@ -142,14 +143,29 @@ for k, v in agg.items():
     print("%-12s 512-step %s   20-step median %s" % (k, " ".join("%.2f" % x[0] for x in v), " ".join("%.2f" % x[1] for x in v)))
 PY
   ;;
-trace|trace_c5)
-  if [ $task = trace ]; then A="--no-cpu-baseline"; n=c3; else A="--config C5 --ntraj 32 --steps 256 --warmup 32 --no-cpu-baseline"; n=c5; fi
+trace|trace_c5|trace_c2)
+  K=cgemm
+  case $task in
+    trace) A="--no-cpu-baseline"; n=c3 ;;
+    trace_c5) A="--config C5 --ntraj 32 --steps 256 --warmup 32 --no-cpu-baseline"; n=c5 ;;
+    trace_c2) A="--config C2 --ntraj 1 --steps 256 --warmup 32 --no-cpu-baseline"; n=c2; K=contract ;;
+  esac
   mkdir -p $O/prof_$n
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$n -o run -- \
     python3 bench.py $A > $O/prof_$n/bench.json 2> $O/prof_$n/bench.err || fail trace $O/prof_$n/bench.err
   N=$(python3 -c "import json;print(json.load(open('$O/prof_$n/bench.json'))['roofline']['launches'])")
-  python3 scripts/trace_summary.py $O/prof_$n/run_kernel_trace.csv --steps --gaps --last cgemm $N --skip $N > $O/prof_$n/summary.txt
+  python3 scripts/trace_summary.py $O/prof_$n/run_kernel_trace.csv --steps --gaps --last $K $N --skip $N > $O/prof_$n/summary.txt
   tail -8 $O/prof_$n/summary.txt ;;
+blocklen)
+  # bench lines at first block lengths BLS (0: the planner's choice), CONFIGS among c3 c2 c5, ROUNDS interleaved
+  for r in $(seq 1 ${ROUNDS:-2}); do for c in ${CONFIGS:-c3 c2}; do for bl in ${BLS:-0 4}; do
+    case $c in
+      c3) A="" ;; c2) A="--config C2 --ntraj 1 --steps 256 --warmup 32" ;; c5) A="--config C5 --ntraj 32 --steps 256 --warmup 32" ;;
+    esac
+    timeout -k 10 400 python bench.py --no-cpu-baseline --block-len $bl $A > $O/${c}_bl${bl}_$r.json 2> $O/${c}_bl${bl}_$r.err \
+      || fail "blocklen $c $bl" $O/${c}_bl${bl}_$r.err
+  done; done; done
+  summ $O/*_bl*_*.json ;;
 pmc|pmc_c5)
   if [ $task = pmc ]; then A="--no-cpu-baseline"; n=c3; cfg="--config C3 --ntraj 64"; else A="--config C5 --ntraj 32 --steps 256 --warmup 32 --no-cpu-baseline"; n=c5; cfg="--config C5 --ntraj 32"; fi
   mkdir -p $O/pmc_$n
