@@ -91,6 +91,10 @@ __device__ __forceinline__ int64_t cmod(int64_t a, int64_t m) {
 #ifndef CH_PRIO_RAW
 #define CH_PRIO_RAW CH_PRIO
 #endif
+// FPOT_PRIO: the potential-force launch at the chain's issue priority
+#ifndef FPOT_PRIO
+#define FPOT_PRIO 0
+#endif
 // CH_DB: double-buffered operand batches (the next batch of a task in flight during this one's MFMAs)
 #ifndef CH_DB
 #define CH_DB 0
@@ -1381,6 +1385,9 @@ namespace {
 // V row; CSR (EW = 0) keeps the row-pointer round trip.
 template <int EW>
 __global__ __launch_bounds__(256) void fpot_kernel(FpotArgs a) {
+#if FPOT_PRIO
+  __builtin_amdgcn_s_setprio(CH_PRIO);  // on the main stream's critical path, like the chain stages
+#endif
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= (int64_t)a.nph * a.B) return;
   const int d = (int)(i / a.B), b = (int)(i - (int64_t)d * a.B);

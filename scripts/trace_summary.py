@@ -92,6 +92,12 @@ if "--gaps" in sys.argv:
     rows.sort(key=lambda r: r["s"])
     ch = [r for r in rows if r["n"].startswith("chain_kernel")][-301:]
     gaps = [(b["s"] - a["e"]) / 1e3 for a, b in zip(ch, ch[1:])]
+    # the large-bath plan's fpot launch runs on the main stream between stage A and the fused stage:
+    # main-stream idle time counts it as work
+    fp = [r for r in rows if r["n"].startswith("fpot_kernel") and ch and r["s"] >= ch[0]["s"]]
+    if fp:
+        ms = sorted(ch + fp, key=lambda r: r["s"])
+        idle = sum(max(0.0, (b["s"] - a["e"]) / 1e3) for a, b in zip(ms, ms[1:]))
     # steps in the window = its step-closing launches (1 chain launch per step in composed plans, 2 in
     # fused plans, 3 otherwise), not a fixed 3
     nsteps = sum(1 for r in ch[1:] if r["n"].startswith(step_end_stage(ch)))
@@ -99,3 +105,6 @@ if "--gaps" in sys.argv:
         print("\nchain gaps over %d launches (%d steps): total %.1f us = %.2f us/step; largest %s"
               % (len(gaps), nsteps, sum(gaps), sum(gaps) / nsteps,
                  [round(x, 1) for x in sorted(gaps)[-8:]]))
+        if fp:
+            print("main-stream idle (chain and fpot launches as work): %.1f us = %.2f us/step; fpot %.2f us/step"
+                  % (idle, idle / nsteps, sum((r["e"] - r["s"]) / 1e3 for r in fp) / nsteps))
