@@ -2401,7 +2401,10 @@ int freeze(gle_handle* h) {
     const bool last = P >= Pmax || 4 * P >= mlmax || (int)h->levels.size() == MAXLVL - 1;
     lv.lag1 = last ? mlmax : (int)(4 * P);
     const bool pow2 = (P & (P - 1)) == 0;
-    int pmin = mode == GLE_FAR_SPECTRAL ? 2 : 8;
+    // auto: spectral from P = 8, and from P = 4 for large baths (C5: 252.7 vs 256.6 us/step at 512
+    // steps, 3 interleaved rounds, `profiles/r05/c5_ab/spec_min_ab_c5.jsonl`; its direct form was a
+    // 0.39 ms contraction every 4 steps)
+    int pmin = mode == GLE_FAR_SPECTRAL ? 2 : (h->small_baths ? 8 : 4);
     if (const char* e = gle_env("GLE_SPEC_MIN")) pmin = std::max(2, atoi(e));
     lv.spectral = spec_ok && pow2 && P >= pmin && 2 * P <= 8192;
     h->levels.push_back(lv);
