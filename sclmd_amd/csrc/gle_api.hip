@@ -3198,6 +3198,10 @@ int step_end_impl(gle_handle* h, const double* fpot_host_T) {
 // Composed one-launch step (STAGE 4): V0[t & 1], W1[t & 1] and the near partials of lags >= 3 for
 // target t+2 from the two-launch path's state at step t (S(t), near partials of target t+1, the
 // level blocks of target t+1); the caller's ladder_step has made the main stream wait for them.
+// the composed stage's kernel: 5 (one-column VALU products) for one-trajectory plans, else 4 (C2:
+// 20.6 vs 21.4 us/step, `profiles/r05/split/gemv_ab_c2.jsonl`)
+int xstage(const gle_handle* h) { return h->B == 1 ? 5 : 4; }
+
 int x_prime_buffers(gle_handle* h) {
   const StepArgs ta = step_args(h);
   for (auto& b : h->baths) {
@@ -3224,8 +3228,8 @@ int x_prime_buffers(gle_handle* h) {
     launch_xprime(a, h->stream);
   }
   if (!h->chNear3.tiles.empty())
-    launch_chain(4, h->chNear3.nw, h->ch_drn, h->chNear3.lds, h->chNear3.d, (int)h->chNear3.tiles.size(), h->d_sd,
-                 step_args(h, h->t - 1), 0, h->stream);
+    launch_chain(xstage(h), h->chNear3.nw, h->ch_drn, h->chNear3.lds, h->chNear3.d, (int)h->chNear3.tiles.size(),
+                 h->d_sd, step_args(h, h->t - 1), 0, h->stream);
   HIPCHK(h, hipMemsetAsync(h->d_pmax, 0, (size_t)4 * h->B * sizeof(unsigned long long), h->stream));
   h->x_live = true;
   return GLE_OK;
@@ -3260,7 +3264,7 @@ int run_xstep(gle_handle* h, int64_t nsteps) {
     StepArgs ta = step_args(h);
     const StepArgs t2 = step_args(h, h->t + 1);  // the S tiles read the levels at target t+2
     for (int l = 0; l < MAXLVL; ++l) ta.lvl_off[l] = t2.lvl_off[l];
-    run_chain(h, 4, h->chX[h->t & 1], ta, 0, h->levels.empty(), 0);
+    run_chain(h, xstage(h), h->chX[h->t & 1], ta, 0, h->levels.empty(), 0);
     h->std_stale = true;
     if (!h->levels.empty() && (h->t + 1) % h->P0 == 0) HIPCHK(h, hipEventRecord(h->ev_step, h->stream));
     h->t += 1;

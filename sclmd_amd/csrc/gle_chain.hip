@@ -126,9 +126,12 @@ __device__ __forceinline__ void stamp(const StepDev* __restrict__ sd, int stage,
 #ifndef CH_NA
 #define CH_NA 1
 #endif
-template <int RN, int NW>
+template <int RN, int NW, bool GEMV = false>
 __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave, int lane, int64_t t,
                                          double* lds, int skip) {
+  // GEMV (one-trajectory plans, chain stage 5 = stage 4 at B = 1): a 16x16x4 MFMA would use 1 of its
+  // 16 columns; each lane instead multiplies its own A element by the X value of its k row on the VALU
+  static_assert(!GEMV || RN == 1, "GEMV tiles have one column tile");
   constexpr int U = Batch<RN, NW>::U;
   constexpr int NT = 16 * RN;
   constexpr int NA = (CH_NA / RN) > 1 ? (CH_NA / RN) : 1;  // independent accumulators: NA * RN
@@ -146,7 +149,17 @@ __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave,
 #pragma unroll
   for (int n = 0; n < RN; ++n) xc[n] = min(bcol + 16 * n, max(T->ncols - 1, 0));
   int cur = -1;
+  double gacc = 0.0;  // GEMV: lane l's partial of row l % 16 over the k rows 4 s + l / 16
   auto flush = [&]() {
+    if constexpr (GEMV) {
+      // the four k-groups of a row are lanes l, l + 16, l + 32, l + 48: row sums in fixed order
+      double v = gacc;
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if (lane < 16) lds[cur * 16 * NT + lane * NT] = v;
+      gacc = 0.0;
+      return;
+    }
 #pragma unroll
     for (int n = 0; n < RN; ++n)
 #pragma unroll
@@ -205,6 +218,11 @@ __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave,
       }
     };
     auto compute = [&](int s0, double (&a)[U], double (&b)[U][RN]) {
+      if constexpr (GEMV) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) gacc = fma(s0 + u < nks ? a[u] : 0.0, b[u][0], gacc);
+        return;
+      }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const double av = s0 + u < nks ? a[u] : 0.0;
@@ -237,19 +255,19 @@ __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave,
 // DOF and S(t+1) tiles have the kernel's DRN columns (T->rn == DRN): products of that width only,
 // so the 64-column near-field variant is not instantiated beside the DOF prologue's live values
 // (it made the register allocator spill the DOF stages)
-template <int NW, int RN>
+template <int NW, int RN, bool GV = false>
 __device__ __forceinline__ void run_products_rn(const ChTile* __restrict__ T, int64_t t, double* lds, int skip = 0) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  products<RN, NW>(T, wave, lane, t, lds, skip);
+  products<RN, NW, GV && RN == 1>(T, wave, lane, t, lds, skip);
 }
 
-template <int NW>
+template <int NW, bool GV = false>
 __device__ __forceinline__ void run_products(const ChTile* __restrict__ T, int64_t t, double* lds, int skip = 0) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   switch (T->rn) {
-    case 1: products<1, NW>(T, wave, lane, t, lds, skip); break;
+    case 1: products<1, NW, GV>(T, wave, lane, t, lds, skip); break;
     case 2: products<2, NW>(T, wave, lane, t, lds, skip); break;
     default: products<4, NW>(T, wave, lane, t, lds, skip); break;
   }
@@ -894,7 +912,7 @@ __device__ __forceinline__ bool xsub_combine(const ChTile* __restrict__ T, doubl
 // (output CH_OYB); K0.p_t (u), Kq.q_t (CH_TB + u) and dyn.q_t (2 CH_TB) give md.vv's id0 phase for the
 // tile's elements: F0, heat current, kinetic energy, recordings, q_{t+1} = q~ (md.py:383-398);
 // constraints zero p_{t+1} and q_{t+1} (md.py:407-408); history push of p_{t+1}.
-template <int NW, int DRN>
+template <int NW, int DRN, bool GV = false>
 __device__ __forceinline__ void dof_X(const ChTile* __restrict__ T, const StepDev* __restrict__ sd,
                                       const StepArgs& ta, double* lds) {
   using Geo = DofGeo<NW, DRN>;
@@ -939,7 +957,7 @@ __device__ __forceinline__ void dof_X(const ChTile* __restrict__ T, const StepDe
       *G(w) = 0ull;
     }
   }
-  run_products_rn<NW, DRN>(T, t, lds);
+  run_products_rn<NW, DRN, GV>(T, t, lds);
   __syncthreads();
   stamp(sd, 4, 2, ta);
   // the tile's output sums: K0.p_t of tile bath u (u), dyn.q_t (CH_TB), p_{t+1} (CH_TB + 1)
@@ -1063,7 +1081,7 @@ __device__ __forceinline__ void dof_X(const ChTile* __restrict__ T, const StepDe
 
 // stage 4 S tile, bath rows [row0, row0+16): V0(t+1) = W1(t) - c K1.p_t and W1(t+1) = n_{t+2} -
 // c (K2.p_t + near partials (lags >= 3, written by launch t-1) + levels at target t+2)
-template <int NW, int DRN>
+template <int NW, int DRN, bool GV = false>
 __device__ __forceinline__ void sfin_X(const ChTile* __restrict__ T, const StepDev* __restrict__ sd,
                                        const StepArgs& ta, double* lds) {
   const int B = sd->B;
@@ -1099,7 +1117,7 @@ __device__ __forceinline__ void sfin_X(const ChTile* __restrict__ T, const StepD
     for (int l = 0; l < MAXLVL; ++l) lvs += lv[l];
     pre[x] = lvs + sn;
   }
-  run_products_rn<NW, DRN>(T, t, lds);
+  run_products_rn<NW, DRN, GV>(T, t, lds);
   __syncthreads();
   stamp(sd, 4, 2, ta);
 #pragma unroll
@@ -1169,11 +1187,11 @@ __device__ __forceinline__ void sfin(const ChTile* __restrict__ T, const StepDev
 }
 
 // near-field partial tile: rows [0, nrows) x columns [0, ncols) of the parity buffer of t + par_shift
-template <int NW>
+template <int NW, bool GV = false>
 __device__ __forceinline__ void raw(const ChTile* __restrict__ T, const StepDev* __restrict__ sd, const StepArgs& ta,
                                     double* lds, int stage) {
   const int64_t t = ta.t;
-  run_products<NW>(T, t, lds);
+  run_products<NW, GV>(T, t, lds);
   __syncthreads();
   stamp(sd, stage, 2, ta);
   const int NT = 16 * T->rn;
@@ -1297,17 +1315,18 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(DRN == 
   if (kind == CH_RAW) __builtin_amdgcn_s_setprio(CH_PRIO_RAW);
 #endif
   stamp(sd, STAGE, 1, ta);
+  constexpr bool GV = STAGE == 5;  // stage 5: the composed stage with one-column (VALU) products
   if (kind == CH_DOF) {
     if (STAGE == 0) dof_A<NW, DRN>(T, sd, ta, mode, lds);
     else if (STAGE == 1) dof_B<NW, DRN>(T, sd, ta, mode, lds);
     else if (STAGE == 2) dof_C<NW, DRN>(T, sd, ta, mode, lds);
     else if (STAGE == 3) dof_BC<NW, DRN>(T, sd, ta, mode, lds);
-    else dof_X<NW, DRN>(T, sd, ta, lds);
+    else dof_X<NW, DRN, GV>(T, sd, ta, lds);
   } else if (kind == CH_SFIN) {
-    if (STAGE == 4) sfin_X<NW, DRN>(T, sd, ta, lds);
+    if (STAGE >= 4) sfin_X<NW, DRN, GV>(T, sd, ta, lds);
     else sfin<NW, DRN>(T, sd, ta, lds, STAGE);
   } else {
-    raw<NW>(T, sd, ta, lds, STAGE);
+    raw<NW, GV>(T, sd, ta, lds, STAGE);
   }
   stamp(sd, STAGE, 3, ta);
   if (ta.ts) {  // launch-uniform
@@ -1375,7 +1394,8 @@ void launch_chain(int stage, int nw, int drn, size_t lds_bytes, const ChTile* ti
   else if (stage == 1) launch_st<1>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
   else if (stage == 2) launch_st<2>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
   else if (stage == 3) launch_st<3>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
-  else launch_st<4>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
+  else if (stage == 4) launch_st<4>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
+  else launch_st<5>(nw, drn, lds_bytes, tiles, ntiles, sd, ta, mode, s);
 }
 
 namespace {

@@ -351,7 +351,8 @@ struct StepArgs {
 void launch_contract(int rn, int cu, const CItem* items, int nitems, StepArgs ta, hipStream_t s);
 void launch_reduce(const RItem* items, int nitems, int max_elems, StepArgs ta,
                    hipStream_t s);
-// stage 0/1/2 = A/B/C.  mode: A: 1 = harmonic id0 potential with md.potforce's cache rule (YD = dyn.q_t
+// stage 0/1/2 = A/B/C, 3 = fused B + C, 4 = the composed step, 5 = the composed step with one-column
+// (VALU) products, for one-trajectory plans.  mode: A: 1 = harmonic id0 potential with md.potforce's cache rule (YD = dyn.q_t
 // present), 0 = potential force at q_t already in Fc; bit 1: write the id1 cache distance.
 // B / C: 1 = harmonic force at q~ (B computes YD = dyn.q~), 0 = host force in Fc.
 void launch_chain(int stage, int nw, int drn, size_t lds_bytes, const ChTile* tiles, int ntiles, const StepDev* sd,
