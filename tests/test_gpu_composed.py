@@ -139,6 +139,19 @@ def test_split_tiles_vs_oracle(B):
     st.close()
 
 
+def test_one_trajectory_split_valu_with_constraints_vs_oracle():
+    """B = 1: split DOF tiles on the one-column VALU stage (chain stage 5) with constrained DOFs in and
+    out of the baths (ApplyConstraint in the last arriver's epilogue), 150 steps against the oracle."""
+    st, sim, *_ = _setup(1, natom=120, constr=[0, 1, 2, 150, 151, 300])
+    d = st.plan_detail()
+    assert d["composed_step"] and d["split_tiles"]
+    st.run(150)
+    for _ in range(150):
+        sim.step()
+    _check(st, sim, 150)
+    st.close()
+
+
 def test_composed_with_constraints_vs_oracle():
     """ApplyConstraint (md.py:407-408, 782-794) inside the composed step."""
     st, sim, *_ = _setup(8, constr=[0, 1, 2, 60, 61])
