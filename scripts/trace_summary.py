@@ -16,10 +16,10 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 
 
 def step_end_stage(rs):
-    """The chain launch that closes a step: the composed step (chain_kernel<4, ...>, plans with
-    GLE_PLAN_COMPOSED_STEP: one chain launch per step), the fused velocity stage (chain_kernel<3, ...>,
+    """The chain launch that closes a step: the composed step (chain_kernel<4, ...>, or <5, ...> with
+    one-column VALU products, plans with GLE_PLAN_COMPOSED_STEP: one chain launch per step), the fused velocity stage (chain_kernel<3, ...>,
     plans with GLE_PLAN_FUSED_BC: 2 per step) or stage C (chain_kernel<2, ...>: 3 per step)."""
-    for k in ("chain_kernel<4", "chain_kernel<3"):
+    for k in ("chain_kernel<5", "chain_kernel<4", "chain_kernel<3"):
         if any(r["n"].startswith(k) for r in rs):
             return k
     return "chain_kernel<2"
