@@ -115,6 +115,30 @@ def cpu_baseline(baths_host, dyn, nph, dt, nmd, budget_s=20.0, nsample=5):
             "samples": [float(r) for r in rates]}
 
 
+def cpu_single_pass(baths_host, dyn, nph, dt, nmd, ntraj, budget_s=8.0):
+    """Best-effort CPU context number (CPU-baseline plan step 3): the oracle's batched
+    step (oracle.GLEBatch: the memory sum once per step as ONE GEMM of the flattened kernel
+    [K_1 | ... | K_{ml-1}] with the history window of all ntraj trajectories, BLAS-threaded), timed on
+    the same junction and ensemble size as the GPU line.  Context beside the baseline, not the baseline:
+    the reference steps one trajectory with three history passes."""
+    from oracle import sclmd_oracle as O
+
+    bs = [O.Bath(kind, c, k, n, dt, nmd, **extra) for (kind, c, k, n, extra) in baths_host]
+    sim = O.GLEBatch(nph, dt, nmd, bs, dyn, ntr=ntraj)
+    rng = np.random.default_rng(0)
+    sim.p = rng.normal(size=(nph, ntraj)) * 1e-3
+    sim.q = rng.normal(size=(nph, ntraj)) * 1e-3
+    sim.step()  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        sim.step()
+        n += 1
+    el = time.perf_counter() - t0
+    return {"value": n * ntraj / el, "unit": "traj-steps/s", "cores": blas_threads(), "kind": "port",
+            "sample": "%d steps of a %d-trajectory batch in %.1f s (oracle.GLEBatch: one flattened-kernel GEMM per "
+                      "bath per step), numpy %s + %s" % (n, ntraj, el, np.__version__, blas_info())}
+
+
 METRIC = "GLE steps/sec/GPU, 300-atom junction, 1024-step kernel, 64-traj ensemble"
 
 
@@ -214,6 +238,8 @@ def main():
                          "that communicates before it builds the stepper)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--single-pass-budget", type=float, default=8.0,
+                    help="seconds of the best-effort batched CPU context number (0: skip)")
     ap.add_argument("--traffic-json", default="",
                     help="PMC-derived HBM bytes per dominant-kernel launch (from rocprofv3 --pmc passes); "
                          "default: profiles/traffic_<config>_<ntraj>.json if present, else "
@@ -489,14 +515,26 @@ def main():
         # its own device timestamps: algorithmic flops of its products / its kernel durations;
         # us_per_step = chain kernel time per step (beside the far field, so > its time alone)
         cms = prof["chain_ms"]
+        _, cby = st.chain_work()  # algorithmic bytes of one step's chain launches (every entry once)
+        tf = prof["chain_flops"] / (cms * 1e-3) / 1e12
+        gbs = cby * args.steps / (cms * 1e-3) / 1e9
+        # one-trajectory composed plans run the chain's products on the VALU (one column: chain stage
+        # 5, a GEMV): their rate is priced on bytes, the MFMA-tiled plans' on the fp64 matrix peak
+        gemv = bool(detail.get("composed_step")) and args.ntraj == 1
         res["chain_roofline"] = {
             "kernel": "chain_kernel (per-step md.vv: %s)" % (
-                "one composed launch" if detail.get("composed_step") else "stage A and the fused velocity stage"),
-            "bound": "mfma", "achieved": prof["chain_flops"] / (cms * 1e-3) / 1e12,
-            "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": prof["chain_flops"] / (cms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS,
+                ("one composed launch, one-column VALU products (GEMV)" if gemv else "one composed launch")
+                if detail.get("composed_step") else "stage A and the fused velocity stage"),
+            "bound": "hbm" if gemv else "mfma",
+            "achieved": gbs if gemv else tf,
+            "peak": HBM_PEAK_GBS if gemv else FP64_MFMA_PEAK_TFLOPS,
+            "unit": "GB/s" if gemv else "TFLOP/s",
+            "frac": gbs / HBM_PEAK_GBS if gemv else tf / FP64_MFMA_PEAK_TFLOPS,
+            "achieved_tflops": tf, "frac_mfma": tf / FP64_MFMA_PEAK_TFLOPS,
+            "achieved_gbs": gbs, "frac_hbm": gbs / HBM_PEAK_GBS,
             "launches": prof["chain_launches"], "us_per_step": cms / args.steps * 1e3,
             "algorithmic_flops_per_step": prof["chain_flops"] / args.steps,
+            "algorithmic_bytes_per_step": cby,
             "timing": "device timestamps (per-workgroup stores)",
             "window": "third window of the same %d steps" % args.steps}
     # The reduce runs (it is the ensemble's one collective), but its result is not reported: over a
@@ -516,6 +554,9 @@ def main():
                 bh.append(("ph", b.cids, st.get_kernel(i), noise[i], {}))
         res["cpu_baseline"] = cpu_baseline(bh, m.dyn, meta["nph"], meta["dt"], meta["nmd"], args.cpu_budget)
         res["speedup_vs_cpu_baseline"] = value / res["cpu_baseline"]["value"]
+        if args.single_pass_budget > 0:
+            res["cpu_baseline"]["single_pass"] = cpu_single_pass(bh, m.dyn, meta["nph"], meta["dt"], meta["nmd"],
+                                                                 args.ntraj, args.single_pass_budget)
     if rank == 0:
         print(json.dumps(res), flush=True)
     m.close()

@@ -189,8 +189,13 @@ int gle_noise_stream_abort(gle_handle* h, int32_t bath);
  * from begin to end) in device memory, so that each later run (md.Run draws new noise per run from
  * the same spectrum, md.py:569-570) replays them with new draws instead of handing them over PCIe
  * again (C5: ~11 GB of dense factors per run).  retain = 0 frees them.  A plan that does not fit
- * beside the resident state is streamed as without retention and nothing is kept. */
+ * beside the resident state is streamed as without retention and nothing is kept: retention stops
+ * before it would leave less device memory free than every bath's stream scratch plus the history
+ * getters' chunk buffer and slack, or exceed the cap of gle_noise_stream_retain_cap. */
 int gle_noise_stream_retain(gle_handle* h, int32_t bath, int32_t retain);
+/* Cap on the bytes of retained plans over all baths of the handle (max_bytes < 0: no cap, the
+ * default; 0: nothing is retained). */
+int gle_noise_stream_retain_cap(gle_handle* h, int64_t max_bytes);
 /* *bytes = device bytes of the retained complete plan of `bath`, 0 when none is retained. */
 int gle_noise_stream_retained(gle_handle* h, int32_t bath, int64_t* bytes);
 /* New noise of `bath` from its retained plan: the same result as streaming that plan again with
@@ -320,19 +325,23 @@ int gle_plan_detail(gle_handle* h, int32_t* plan_class, int32_t* fused_waves, do
  * without a biased electron bath): md.vv is linear in (p_t, q_t) and the bath vectors, so p_{t+1}
  * is one product of composed operators (precomputed at plan time) and q_{t+1} = q~ follows from the
  * step's own K0.p_t and dyn.q_t (same result to fp64 rounding; steps with a host force, gle_step_begin
- * / gle_step_end, keep the two-launch path).  The potential force at q~ is evaluated fresh: the
- * reference's md.potforce reuses the force at q0 when 0 < max|q~ - q0| < 1e-9 (md.py:767-779); such
- * steps are counted, see gle_cache_audit. */
+ * / gle_step_end, keep the two-launch path).  The potential force is evaluated fresh, which is
+ * md.potforce's result unless its cache rule (sameq, md.py:449-450, 767-779) reuses the force of q0 at
+ * a point within 1e-9 of q0 but not equal to it.  Each launch audits the previous step for that
+ * case; a run that meets it stops storing at once and the library replays it from the step it
+ * tripped at on the two-launch path, which applies the rule, before any call reads the state (the
+ * replay runs in gle_sync or the next call on the handle).  See gle_cache_audit. */
 #define GLE_PLAN_COMPOSED_STEP 8
 /* GLE_PLAN_SPLIT_TILES: composed-step plans with few DOF tiles (small B, e.g. one trajectory) split
  * each tile's products over up to 8 workgroups by k-steps; the last to finish adds the partial sums
  * in a fixed order and runs the tile's md.vv epilogue (same result to fp64 rounding). */
 #define GLE_PLAN_SPLIT_TILES 16
 int gle_plan_flags(gle_handle* h, int32_t* flags);
-/* Composed steps (GLE_PLAN_COMPOSED_STEP) at which md.potforce's cache rule (sameq, md.py:767-779)
- * would have reused a force at a point within 1e-9 but not equal to the evaluation point: counts[0]
- * at q~ (0 < max|q~ - q_t| < 1e-9 for some trajectory), counts[1] at q_{t+1} after a constraint; the
- * composed step evaluated the force fresh there (a difference below dyn x 1e-9).  Cumulative. */
+/* Trajectories found by the composed step's audit (GLE_PLAN_COMPOSED_STEP) at which md.potforce's
+ * cache rule (sameq, md.py:767-779) reuses a force at a point within 1e-9 of, but not equal to, the
+ * point it was evaluated at: counts[0] at q~ (0 < max|q~ - q_t| < 1e-9), counts[1] at q_{t+1} after
+ * a constraint (0 < max|q_{t+1} - q~_t| < 1e-9).  Each such finding stopped a composed run, which
+ * was replayed on the two-launch path from that step.  Cumulative. */
 int gle_cache_audit(gle_handle* h, int64_t* counts);
 /* Memory-sum ladder levels: *nlevel = number of levels; for the first nmax levels the block length
  * P[l] and the blocks of that level issued since profiling was enabled (a block issued in pieces
@@ -342,6 +351,9 @@ int gle_profile_levels(gle_handle* h, int32_t nmax, int32_t* nlevel, int32_t* P,
  * flops and bytes (every matrix entry read once, every product counted once, no padding; ladder
  * blocks averaged over their period).  Requires a plan (after gle_set_state). */
 int gle_step_work(gle_handle* h, double* flops, double* bytes);
+/* The per-step chain's part of gle_step_work (the md.vv launches on the main stream: for the
+ * composed step its operators' nonzeros, K0 / K1 / K2, the near lags and dyn, every entry once). */
+int gle_chain_work(gle_handle* h, double* flops, double* bytes);
 
 #ifdef __cplusplus
 }

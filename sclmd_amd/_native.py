@@ -35,7 +35,7 @@ EXPORTS = [
     "gle_noise_stream_chunk", "gle_noise_stream_end", "gle_set_plan_class", "gle_plan_detail", "gle_plan_flags",
     "gle_comm_allreduce", "gle_noise_stream_abort", "gle_device_mem_info", "gle_noise_stream_shared",
     "gle_noise_stream_retain", "gle_noise_stream_retained", "gle_noise_stream_replay", "gle_get_full_history",
-    "gle_host_alloc", "gle_host_free", "gle_cache_audit",
+    "gle_host_alloc", "gle_host_free", "gle_cache_audit", "gle_noise_stream_retain_cap", "gle_chain_work",
 ]
 
 REC_P, REC_Q, REC_F, REC_HIST = 1, 2, 4, 8
@@ -99,6 +99,7 @@ _SIGS = {
     "gle_profile_levels": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32),
                                           ctypes.POINTER(ctypes.c_int32), _D]),
     "gle_step_work": (ctypes.c_int, [_P, _D, _D]),
+    "gle_chain_work": (ctypes.c_int, [_P, _D, _D]),
     "gle_set_plan_class": (ctypes.c_int, [_P, ctypes.c_int32]),
     "gle_plan_detail": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32), _D,
                                        ctypes.POINTER(ctypes.c_int32), _I64, ctypes.POINTER(ctypes.c_int32)]),
@@ -129,6 +130,7 @@ _SIGS = {
     "gle_cache_audit": (ctypes.c_int, [_P, _I64]),
     "gle_noise_stream_retain": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32]),
     "gle_noise_stream_retained": (ctypes.c_int, [_P, ctypes.c_int32, _I64]),
+    "gle_noise_stream_retain_cap": (ctypes.c_int, [_P, ctypes.c_int64]),
     "gle_noise_stream_replay": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint64]),
 }
 
@@ -449,6 +451,11 @@ class Stepper:
         """Keep the next complete streamed plan's factors on the device (False frees them)."""
         self._chk(self.lib.gle_noise_stream_retain(self.h, int(bath), 1 if retain else 0), "gle_noise_stream_retain")
 
+    def noise_stream_retain_cap(self, max_bytes):
+        """Cap on the retained plans' device bytes over all baths (None: no cap)."""
+        self._chk(self.lib.gle_noise_stream_retain_cap(self.h, -1 if max_bytes is None else int(max_bytes)),
+                  "gle_noise_stream_retain_cap")
+
     def noise_stream_retained(self, bath):
         """Device bytes of the retained complete plan of `bath` (0: none)."""
         n = ctypes.c_int64(0)
@@ -642,4 +649,10 @@ class Stepper:
         """Algorithmic (flops, bytes) of one steady-state step of the plan (gle_step_work)."""
         fl, by = ctypes.c_double(0), ctypes.c_double(0)
         self._chk(self.lib.gle_step_work(self.h, ctypes.byref(fl), ctypes.byref(by)), "gle_step_work")
+        return fl.value, by.value
+
+    def chain_work(self):
+        """Algorithmic (flops, bytes) of one step's chain launches (gle_chain_work)."""
+        fl, by = ctypes.c_double(0), ctypes.c_double(0)
+        self._chk(self.lib.gle_chain_work(self.h, ctypes.byref(fl), ctypes.byref(by)), "gle_chain_work")
         return fl.value, by.value

@@ -259,6 +259,15 @@ struct gle_handle {
   double *d_P2 = nullptr, *d_Q2 = nullptr;
   double* d_xfrag = nullptr;           // composed-operator DOF-tile fragments
   unsigned long long* d_guard = nullptr;
+  // md.potforce's cache rule on the composed path (StepArgs::xw): audit words [3][2][B], the device
+  // stop word and its host-mapped copy; a gle_run of composed steps leaves x_pend set until xresolve
+  // has read the stop word (and replayed from the stop step on the two-launch path)
+  unsigned long long *d_xw = nullptr, *d_xstop = nullptr, *h_xstop = nullptr, *d_xstop_h = nullptr;
+  bool x_pend = false;
+  int64_t x_call_t0 = 0;               // first step of the last gle_run of composed steps
+  int64_t x_replays = 0;               // composed runs stopped and replayed (gle_cache_audit)
+  bool std_words_live = false;         // d_pmax holds the two-launch path's id0 distance of step t
+  int64_t ret_cap = -1;                // retained streamed-noise factors: byte cap over all baths (< 0: none)
   double* d_xslab = nullptr;           // split stage-4 DOF tiles: slabs and arrival counters
   unsigned long long* d_xcnt = nullptr;
   int64_t xslab_n = 0;
@@ -2064,6 +2073,19 @@ int plan_xstep(gle_handle* h) {
   rc = dalloc_n(h, &h->d_xfrag, frag.size());
   if (!rc) rc = upload(h, h->d_xfrag, frag.data(), frag.size() * 8);
   if (!rc) rc = dalloc_n(h, &h->d_guard, 2);
+  if (!rc) rc = dalloc_n(h, &h->d_xw, (size_t)6 * B);
+  if (!rc) rc = dalloc_n(h, &h->d_xstop, 1);
+  if (!rc && !h->h_xstop) {
+    void* hp = nullptr;
+    if (hipHostMalloc(&hp, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+      return fail(h, GLE_ERR_NOMEM, "hipHostMalloc (composed-step stop word)");
+    h->h_xstop = (unsigned long long*)hp;
+    *(volatile unsigned long long*)h->h_xstop = 0ull;
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, hp, 0) != hipSuccess)
+      return fail(h, GLE_ERR_HIP, "hipHostGetDevicePointer (composed-step stop word)");
+    h->d_xstop_h = (unsigned long long*)dp;
+  }
   if (rc) return rc;
   // algorithmic work per step: the composed operators, K0 / K1 / K2 and the near lags [3, nn) on the
   // bath rows, dyn (F0), every matrix entry read once
@@ -3191,6 +3213,7 @@ int step_end_impl(gle_handle* h, const double* fpot_host_T) {
   if (!h->levels.empty() && (h->t + 1) % h->P0 == 0) HIPCHK(h, hipEventRecord(h->ev_step, h->stream));
   h->t += 1;
   h->pot_cache_exact = (fpot_host_T == nullptr) && h->constr.empty();
+  h->std_words_live = fpot_host_T == nullptr;  // the velocity stage wrote step t + 1's id0 distances
   HIPCHK(h, hipGetLastError());
   return GLE_OK;
 }
@@ -3230,7 +3253,14 @@ int x_prime_buffers(gle_handle* h) {
   if (!h->chNear3.tiles.empty())
     launch_chain(xstage(h), h->chNear3.nw, h->ch_drn, h->chNear3.lds, h->chNear3.d, (int)h->chNear3.tiles.size(),
                  h->d_sd, step_args(h, h->t - 1), 0, h->stream);
-  HIPCHK(h, hipMemsetAsync(h->d_pmax, 0, (size_t)4 * h->B * sizeof(unsigned long long), h->stream));
+  // audit words: zero, except that after a two-launch step the first composed launch audits that
+  // step's id0 distance for step t (md.potforce's cache as the two-launch path left it: a distance in
+  // (0, 1e-9) stops the composed run before it stores anything, and the two-launch path goes on)
+  const size_t nw = (size_t)2 * h->B;
+  HIPCHK(h, hipMemsetAsync(h->d_xw, 0, 3 * nw * sizeof(unsigned long long), h->stream));
+  if (h->std_words_live)
+    HIPCHK(h, hipMemcpyAsync(h->d_xw + ((h->t + 2) % 3) * nw + h->B, h->d_pmax + (h->t & 1) * h->B,
+                             (size_t)h->B * sizeof(unsigned long long), hipMemcpyDeviceToDevice, h->stream));
   h->x_live = true;
   return GLE_OK;
 }
@@ -3254,6 +3284,7 @@ int run_xstep(gle_handle* h, int64_t nsteps) {
     HIPCHK(h, hipMemcpyAsync(h->d_P2, h->d_P, nst, hipMemcpyDeviceToDevice, h->stream));
     HIPCHK(h, hipMemcpyAsync(h->d_Q2, h->d_Q, nst, hipMemcpyDeviceToDevice, h->stream));
   }
+  h->x_call_t0 = h->t;
   for (int64_t s = 0; s < nsteps; ++s) {
     rc = ladder_step(h, 1);
     if (rc) return rc;
@@ -3264,17 +3295,76 @@ int run_xstep(gle_handle* h, int64_t nsteps) {
     StepArgs ta = step_args(h);
     const StepArgs t2 = step_args(h, h->t + 1);  // the S tiles read the levels at target t+2
     for (int l = 0; l < MAXLVL; ++l) ta.lvl_off[l] = t2.lvl_off[l];
+    ta.xw = h->d_xw;
+    ta.xstop = h->d_xstop;
+    ta.xstop_host = h->d_xstop_h;
+    ta.xB = (int32_t)h->B;
     run_chain(h, xstage(h), h->chX[h->t & 1], ta, 0, h->levels.empty(), 0);
     h->std_stale = true;
+    h->std_words_live = false;
     if (!h->levels.empty() && (h->t + 1) % h->P0 == 0) HIPCHK(h, hipEventRecord(h->ev_step, h->stream));
     h->t += 1;
   }
-  if (h->t & 1) {  // the state lives in d_P / d_Q between calls
+  // the audit of the last step (as launch t would), and the state into d_P / d_Q between calls unless
+  // the run stopped (xresolve replays it)
+  {
+    XFinishArgs fa{};
+    fa.P = h->d_P;
+    fa.Q = h->d_Q;
+    fa.P2 = h->d_P2;
+    fa.Q2 = h->d_Q2;
+    fa.n = (h->t & 1) ? (int64_t)h->nphp * h->B : 0;
+    fa.xw = h->d_xw;
+    fa.xstop = h->d_xstop;
+    fa.xstop_host = h->d_xstop_h;
+    fa.guard = h->d_guard;
+    fa.t = h->t;
+    fa.B = (int32_t)h->B;
+    launch_xfinish(fa, h->stream);
+  }
+  h->x_pend = true;
+  h->pot_cache_exact = false;
+  HIPCHK(h, hipGetLastError());
+  return GLE_OK;
+}
+
+// After a gle_run of composed steps (x_pend): wait for it and read the stop word.  A stopped run
+// (a launch found that md.potforce would have reused its cached force at a point other than q0,
+// md.py:449-450, 767-779) left the state of the step r before the stopping launch in its parity
+// buffer and stored nothing after step r's launch; r's launch itself ran, but the step whose words
+// tripped is r, so the run resumes at r on the two-launch path (which applies the cache rule) up to
+// the step the caller asked for.  If the stop came from the first launch of the run auditing the
+// two-launch path's own distance (x_prime_buffers), nothing composed ran: the run resumes at its
+// first step with that path's potential cache as it was.
+int xresolve(gle_handle* h) {
+  if (!h->x_pend) return GLE_OK;
+  h->x_pend = false;
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  const unsigned long long v = *(volatile unsigned long long*)h->h_xstop;
+  if (v == 0ull) return GLE_OK;
+  const int64_t t_end = h->t;
+  int64_t r = (int64_t)v - 2;
+  const bool entry = r < h->x_call_t0;
+  if (entry) r = h->x_call_t0;
+  if (r < h->x_call_t0 || r >= t_end) return fail(h, GLE_ERR_STATE, "composed-step stop outside the run");
+  const size_t nst = (size_t)h->nphp * h->B * 8;
+  if (r & 1) {
     HIPCHK(h, hipMemcpyAsync(h->d_P, h->d_P2, nst, hipMemcpyDeviceToDevice, h->stream));
     HIPCHK(h, hipMemcpyAsync(h->d_Q, h->d_Q2, nst, hipMemcpyDeviceToDevice, h->stream));
   }
-  h->pot_cache_exact = false;
-  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipMemsetAsync(h->d_xstop, 0, sizeof(unsigned long long), h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  *(volatile unsigned long long*)h->h_xstop = 0ull;
+  h->x_replays += 1;
+  h->t = r;
+  h->x_live = false;
+  h->need_prime = true;   // the ladder's schedule and blocks ran ahead to t_end
+  h->std_stale = !entry;  // composed steps ran: the two-launch path's cache starts empty at r
+  for (int64_t s = r; s < t_end; ++s) {
+    int rc = step_begin_impl(h, nullptr);
+    if (!rc) rc = step_end_impl(h, nullptr);
+    if (rc) return rc;
+  }
   return GLE_OK;
 }
 
@@ -3301,6 +3391,14 @@ int download(gle_handle* h, void* dst, const void* src, size_t bytes) {
 #ifdef GLE_BOUNDS
 void gle::bounds_sync() { bounds_table_sync(); }
 #endif
+
+// every entry that reads or changes the state, the noise or the recordings first finishes a pending
+// composed run (xresolve: a stopped run is replayed before anything sees the state)
+#define XRESOLVE(h)                  \
+  do {                               \
+    const int xr_ = xresolve(h);     \
+    if (xr_) return xr_;             \
+  } while (0)
 
 // =========================================================================================
 extern "C" {
@@ -3535,6 +3633,7 @@ int gle_destroy(gle_handle* h) {
     bounds_del(p);
     hipFree(p);
   }
+  if (h->h_xstop) hipHostFree(h->h_xstop);
   for (auto e : h->ev) hipEventDestroy(e);
   for (auto& lv : h->levels)
     for (auto e : lv.ev)
@@ -3807,6 +3906,7 @@ int gle_set_state(gle_handle* h, const double* p, const double* q, int64_t t) {
   if (!h || !p || !q) return GLE_ERR_ARG;
   if (t < 0) return fail(h, GLE_ERR_ARG, "t must be >= 0");
   hipSetDevice(h->cfg.device);
+  XRESOLVE(h);
   int rc = freeze(h);
   if (rc) return rc;
   rc = sync_bg(h);  // background blocks read the ring rewritten here
@@ -3847,6 +3947,7 @@ int gle_set_state(gle_handle* h, const double* p, const double* q, int64_t t) {
 int gle_get_state(gle_handle* h, double* p, double* q, int64_t* t) {
   if (!h) return GLE_ERR_ARG;
   hipSetDevice(h->cfg.device);
+  XRESOLVE(h);
   const int64_t B = h->B, n = h->nph;
   std::vector<double> buf((size_t)n * B);
   if (p) {
@@ -3868,6 +3969,7 @@ int gle_set_history(gle_handle* h, int32_t bath, const double* phis) {
   if (rc) return rc;
   if (!h->state_set) return fail(h, GLE_ERR_STATE, "call gle_set_state first (history slots are relative to t)");
   hipSetDevice(h->cfg.device);
+  XRESOLVE(h);
   rc = sync_bg(h);  // background blocks read the ring rewritten here
   if (rc) return rc;
   Bath& b = h->baths[bath];
@@ -3922,6 +4024,7 @@ int gle_get_history(gle_handle* h, int32_t bath, double* phis) {
   if (!phis) return fail(h, GLE_ERR_ARG, "null output");
   if (!h->frozen) return fail(h, GLE_ERR_STATE, "no state yet");
   hipSetDevice(h->cfg.device);
+  XRESOLVE(h);
   Bath& b = h->baths[bath];
   // row i (newest first) = time t-1-i of the ring (both mirror copies hold it)
   return hist_to_host(h, b.d_H, b.ldh, h->B, b.R, h->t - 1, b.ml, b.nc, phis);
@@ -3930,6 +4033,7 @@ int gle_get_history(gle_handle* h, int32_t bath, double* phis) {
 int gle_get_force(gle_handle* h, double* f) {
   if (!h || !f) return GLE_ERR_ARG;
   hipSetDevice(h->cfg.device);
+  XRESOLVE(h);
   std::vector<double> buf((size_t)h->nph * h->B);
   int rc = download(h, buf.data(), h->d_Flast, buf.size() * 8);
   if (rc) return rc;
@@ -3942,6 +4046,7 @@ int gle_set_noise(gle_handle* h, int32_t bath, const double* noise) {
   if (rc) return rc;
   if (!noise) return fail(h, GLE_ERR_ARG, "null noise");
   hipSetDevice(h->cfg.device);
+  XRESOLVE(h);
   Bath& b = h->baths[bath];
   const int64_t B = h->B, nmd = h->nmd, nc = b.nc;
   std::vector<double> buf((size_t)nmd * nc * B);
@@ -3960,6 +4065,7 @@ int gle_get_noise(gle_handle* h, int32_t bath, double* noise) {
   if (rc) return rc;
   if (!noise) return fail(h, GLE_ERR_ARG, "null output");
   hipSetDevice(h->cfg.device);
+  XRESOLVE(h);
   Bath& b = h->baths[bath];
   const int64_t B = h->B, nmd = h->nmd, nc = b.nc;
   std::vector<double> buf((size_t)nmd * nc * B);
@@ -3999,6 +4105,7 @@ int gle_noise_generate(gle_handle* h, int32_t bath, const double* x_host, uint64
   Bath& b = h->baths[bath];
   if (!b.d_fac) return fail(h, GLE_ERR_STATE, "gle_noise_factors not set for this bath");
   hipSetDevice(h->cfg.device);
+  XRESOLVE(h);
   const int64_t B = h->B, nf = b.nfreq, ncp = b.ncp, nc = b.nc;
   // x [nfreq][ncp][B]
   double* d_x = nullptr;
@@ -4108,10 +4215,31 @@ void free_retained(Bath& b, hipStream_t s) {
 
 // device memory for one retained segment of `nd` doubles, or nullptr (then nothing of the plan in
 // progress is retained: the stream goes on through the chunk buffer)
+// device memory a retention must leave free: every bath's stream scratch at its widest (a later
+// bath's stream allocates its own while this bath's factors are kept), the ~256 MB chunk buffer the
+// history getters and md.dump's snapshot use, and 256 MB of slack
+size_t retain_margin(const gle_handle* h) {
+  size_t m = (size_t)512 << 20;
+  const int64_t nf = h->nmd / 2 + 1, B = h->B;
+  for (const Bath& o : h->baths) {
+    const int64_t cap = std::min<int64_t>(std::max<int64_t>(o.s_ret_cap, 64), nf);
+    m += (size_t)(nf * 2 * o.nc * B + cap * o.ncp * B + cap * o.nc * o.nc * 2) * 8;
+  }
+  return m;
+}
+
+// device memory for one retained segment of `nd` doubles, or nullptr (then nothing of the plan in
+// progress is retained: the stream goes on through the chunk buffer, and md keeps the factors on the
+// host).  Retention stops before it leaves less than retain_margin free or exceeds the handle's cap.
 double* retain_alloc(gle_handle* h, Bath& b, size_t nd) {
   if (!b.s_retain || !b.s_ret_ok) return nullptr;
+  size_t held = 0;
+  for (const Bath& o : h->baths) held += o.s_ret_bytes;
+  size_t fr = 0, tot = 0;
+  bool ok = h->ret_cap < 0 || held + nd * 8 <= (size_t)h->ret_cap;
+  if (ok) ok = hipMemGetInfo(&fr, &tot) == hipSuccess && fr >= nd * 8 + retain_margin(h);
   double* p = nullptr;
-  if (tmalloc(&p, nd * 8) != hipSuccess) {
+  if (!ok || tmalloc(&p, nd * 8) != hipSuccess) {
     (void)hipGetLastError();
     b.s_ret_ok = false;
     free_retained(b, h->stream);
@@ -4200,6 +4328,7 @@ int gle_noise_stream_begin(gle_handle* h, int32_t bath, int32_t is_complex, int6
   if (rc) return rc;
   if (max_chunk < 1) return fail(h, GLE_ERR_ARG, "max_chunk must be >= 1");
   hipSetDevice(h->cfg.device);
+  XRESOLVE(h);
   Bath& b = h->baths[bath];
   free_retained(b, h->stream);  // a new plan replaces the retained one
   b.s_ret_ok = b.s_retain;
@@ -4264,6 +4393,7 @@ int gle_noise_stream_end(gle_handle* h, int32_t bath) {
   Bath& b = h->baths[bath];
   if (!b.d_sa) return fail(h, GLE_ERR_STATE, "gle_noise_stream_begin first");
   hipSetDevice(h->cfg.device);
+  XRESOLVE(h);
   if (b.s_retain && b.s_ret_ok) {
     b.s_ret_complete = true;
     b.s_ret_complex = b.s_complex;
@@ -4283,6 +4413,12 @@ int gle_noise_stream_retain(gle_handle* h, int32_t bath, int32_t retain) {
   return GLE_OK;
 }
 
+int gle_noise_stream_retain_cap(gle_handle* h, int64_t max_bytes) {
+  if (!h) return GLE_ERR_ARG;
+  h->ret_cap = max_bytes;
+  return GLE_OK;
+}
+
 int gle_noise_stream_retained(gle_handle* h, int32_t bath, int64_t* bytes) {
   int rc = check_bath(h, bath);
   if (rc) return rc;
@@ -4298,6 +4434,7 @@ int gle_noise_stream_replay(gle_handle* h, int32_t bath, uint64_t seed, uint64_t
   Bath& b = h->baths[bath];
   if (!b.s_ret_complete) return fail(h, GLE_ERR_STATE, "no retained noise plan (gle_noise_stream_retain)");
   hipSetDevice(h->cfg.device);
+  XRESOLVE(h);
   rc = stream_scratch(h, b, b.s_ret_complex, b.s_ret_cap, false);
   if (rc) return rc;
   for (const auto& r : b.s_ret) {
@@ -4310,6 +4447,7 @@ int gle_noise_stream_replay(gle_handle* h, int32_t bath, uint64_t seed, uint64_t
 int gle_step_begin(gle_handle* h, const double* fpot, double* q_tilde_out) {
   if (!h) return GLE_ERR_ARG;
   hipSetDevice(h->cfg.device);
+  XRESOLVE(h);
   int rc = 0;
   if (fpot) {
     std::vector<double> tf;
@@ -4345,6 +4483,7 @@ int gle_step_end(gle_handle* h, const double* fpot_qt) {
 int gle_run(gle_handle* h, int64_t nsteps) {
   if (!h || nsteps < 0) return GLE_ERR_ARG;
   hipSetDevice(h->cfg.device);
+  XRESOLVE(h);
   if (h->xstep && h->frozen) return run_xstep(h, nsteps);
   for (int64_t s = 0; s < nsteps; ++s) {
     int rc = step_begin_impl(h, nullptr);
@@ -4369,6 +4508,14 @@ int gle_sync(gle_handle* h) {
     join_bg(h);
   }
   HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (h->x_pend) {  // the composed run just waited for: replay it if it stopped (xresolve)
+    const int64_t replays = h->x_replays;
+    XRESOLVE(h);
+    if (h->x_replays != replays) {
+      join_bg(h);
+      HIPCHK(h, hipStreamSynchronize(h->stream));
+    }
+  }
   HIPCHK(h, hipGetLastError());
   return bounds_report(h);
 }
@@ -4376,6 +4523,7 @@ int gle_sync(gle_handle* h) {
 int gle_get_current(gle_handle* h, double* cur) {
   if (!h || !cur) return GLE_ERR_ARG;
   hipSetDevice(h->cfg.device);
+  XRESOLVE(h);
   if (h->frozen) launch_finalize(h->d_sd, (int)h->B, (int)h->nmd, (int)h->baths.size(), h->stream);
   const int64_t B = h->B, nmd = h->nmd;
   std::vector<double> buf((size_t)nmd * B);
@@ -4391,6 +4539,7 @@ int gle_get_current(gle_handle* h, double* cur) {
 int gle_get_energy(gle_handle* h, double* etot) {
   if (!h || !etot) return GLE_ERR_ARG;
   hipSetDevice(h->cfg.device);
+  XRESOLVE(h);
   if (h->frozen) launch_finalize(h->d_sd, (int)h->B, (int)h->nmd, (int)h->baths.size(), h->stream);
   const int64_t B = h->B, nmd = h->nmd;
   std::vector<double> buf((size_t)nmd * B);
@@ -4426,6 +4575,7 @@ int gle_current_sums(gle_handle* h, double* out) {
 int gle_profile(gle_handle* h, int32_t enable) {
   if (!h) return GLE_ERR_ARG;
   hipSetDevice(h->cfg.device);
+  XRESOLVE(h);
   if ((enable & GLE_PROFILE_EVENTS) && h->ev.empty()) {
     h->ev.resize(4096);
     for (auto& e : h->ev) HIPCHK(h, hipEventCreate(&e));
@@ -4471,6 +4621,7 @@ int gle_profile(gle_handle* h, int32_t enable) {
 int gle_profile_read(gle_handle* h, int64_t* nlaunch, double* total_ms, double* flops, double* bytes) {
   if (!h) return GLE_ERR_ARG;
   hipSetDevice(h->cfg.device);
+  XRESOLVE(h);
   drain_profile(h);
   HIPCHK(h, hipGetLastError());
   if (nlaunch) *nlaunch = h->prof_n;
@@ -4483,6 +4634,7 @@ int gle_profile_read(gle_handle* h, int64_t* nlaunch, double* total_ms, double* 
 int gle_profile_read_chain(gle_handle* h, int64_t* nlaunch, double* total_ms, double* flops) {
   if (!h) return GLE_ERR_ARG;
   hipSetDevice(h->cfg.device);
+  XRESOLVE(h);
   drain_profile(h);
   HIPCHK(h, hipGetLastError());
   if (nlaunch) *nlaunch = h->prof_ch_n;
@@ -4494,6 +4646,7 @@ int gle_profile_read_chain(gle_handle* h, int64_t* nlaunch, double* total_ms, do
 int gle_profile_read_device(gle_handle* h, int64_t* nlaunch, double* total_ms) {
   if (!h) return GLE_ERR_ARG;
   hipSetDevice(h->cfg.device);
+  XRESOLVE(h);
   drain_profile(h);
   HIPCHK(h, hipGetLastError());
   if (nlaunch) *nlaunch = h->prof_n_dev;
@@ -4519,11 +4672,11 @@ int gle_profile_levels(gle_handle* h, int32_t nmax, int32_t* nlevel, int32_t* P,
 //          dyn.q~) and the bias products;
 //   ladder per level (block work) / P: spectral = Gauss GEMMs + segment / inverse transforms
 //          (5 N log2 N per complex length-N transform, two real series each), direct = contraction.
-int gle_step_work(gle_handle* h, double* flops, double* bytes) {
-  if (!h) return GLE_ERR_ARG;
-  if (!h->frozen) return fail(h, GLE_ERR_STATE, "no plan yet (call gle_set_state first)");
+// the per-step chain's part of gle_step_work (every launch on the main stream)
+static void chain_work(const gle_handle* h, double& fl, double& by) {
   const double B = (double)h->B;
-  double fl = 0.0, by = 0.0;
+  fl = 0.0;
+  by = 0.0;
   double dyn_nnz = 0.0;
   for (double v : h->dyn_h) dyn_nnz += v != 0.0 ? 1.0 : 0.0;
   for (const Bath& b : h->baths) {
@@ -4554,6 +4707,24 @@ int gle_step_work(gle_handle* h, double* flops, double* bytes) {
     fl = h->x_alg_flops;
     by = h->x_alg_bytes;
   }
+}
+
+int gle_chain_work(gle_handle* h, double* flops, double* bytes) {
+  if (!h) return GLE_ERR_ARG;
+  if (!h->frozen) return fail(h, GLE_ERR_STATE, "no plan yet (call gle_set_state first)");
+  double fl = 0.0, by = 0.0;
+  chain_work(h, fl, by);
+  if (flops) *flops = fl;
+  if (bytes) *bytes = by;
+  return GLE_OK;
+}
+
+int gle_step_work(gle_handle* h, double* flops, double* bytes) {
+  if (!h) return GLE_ERR_ARG;
+  if (!h->frozen) return fail(h, GLE_ERR_STATE, "no plan yet (call gle_set_state first)");
+  const double B = (double)h->B;
+  double fl = 0.0, by = 0.0;
+  chain_work(h, fl, by);
   for (const Level& lv : h->levels) {
     const double P = (double)lv.P;
     if (lv.spectral) {
@@ -4584,6 +4755,7 @@ int gle_record(gle_handle* h, int32_t flags) {
   if (!h) return GLE_ERR_ARG;
   if (flags & ~(GLE_REC_P | GLE_REC_Q | GLE_REC_F | GLE_REC_HIST)) return fail(h, GLE_ERR_ARG, "bad record flags");
   hipSetDevice(h->cfg.device);
+  XRESOLVE(h);
   h->rec_flags = flags;
   if (!h->frozen) return GLE_OK;  // applied when the plan is built
   return apply_record(h);
@@ -4592,6 +4764,7 @@ int gle_record(gle_handle* h, int32_t flags) {
 int gle_record_zero(gle_handle* h, int32_t flags) {
   if (!h) return GLE_ERR_ARG;
   hipSetDevice(h->cfg.device);
+  XRESOLVE(h);
   const size_t n = (size_t)h->nmd * h->nph * h->B * 8;
   if ((flags & GLE_REC_P) && h->d_rec_p) HIPCHK(h, hipMemsetAsync(h->d_rec_p, 0, n, h->stream));
   if ((flags & GLE_REC_Q) && h->d_rec_q) HIPCHK(h, hipMemsetAsync(h->d_rec_q, 0, n, h->stream));
@@ -4609,6 +4782,7 @@ int gle_record_zero(gle_handle* h, int32_t flags) {
 int gle_get_record(gle_handle* h, int32_t what, int32_t bath, double* out) {
   if (!h || !out) return GLE_ERR_ARG;
   hipSetDevice(h->cfg.device);
+  XRESOLVE(h);
   const int64_t B = h->B, nmd = h->nmd;
   const double* src = nullptr;
   int64_t rows = 0, cols = 0;
@@ -4641,6 +4815,7 @@ int gle_get_record_history(gle_handle* h, double* phis, double* qhis, int64_t* m
   if (!phis && !qhis) return GLE_OK;
   if (!h->d_rec_hp) return fail(h, GLE_ERR_STATE, "histories were never recorded (gle_record GLE_REC_HIST)");
   hipSetDevice(h->cfg.device);
+  XRESOLVE(h);
   const int64_t B = h->B, n = h->nph, R = h->rec_ml;
   // row i (newest first) = time t-1-i = ring slot (t-1-i) mod R
   for (int k = 0; k < 2; ++k) {
@@ -4657,6 +4832,7 @@ int gle_get_full_history(gle_handle* h, int64_t ml, double* phis, double* qhis) 
   if (!phis && !qhis) return GLE_OK;
   if (!h->frozen) return fail(h, GLE_ERR_STATE, "no state yet");
   hipSetDevice(h->cfg.device);
+  XRESOLVE(h);
   const int64_t B = h->B, n = h->nph, per = ml * n;
   if (per == 0) return GLE_OK;
   // trajectory chunks through a <= 256 MB device buffer; the copies and the next chunk's kernels
@@ -4706,6 +4882,7 @@ int gle_host_free(void* p) {
 int gle_set_record(gle_handle* h, int32_t what, int32_t bath, const double* in) {
   if (!h || !in) return GLE_ERR_ARG;
   hipSetDevice(h->cfg.device);
+  XRESOLVE(h);
   const int64_t B = h->B, nmd = h->nmd;
   double* dst = nullptr;
   int64_t cols = 0;
@@ -4732,6 +4909,7 @@ int gle_set_record_history(gle_handle* h, const double* phis, const double* qhis
   if (!h) return GLE_ERR_ARG;
   if (!h->d_rec_hp) return fail(h, GLE_ERR_STATE, "enable GLE_REC_HIST first (gle_record)");
   hipSetDevice(h->cfg.device);
+  XRESOLVE(h);
   const int64_t B = h->B, n = h->nph, R = h->rec_ml;
   std::vector<double> buf((size_t)R * n * B);
   for (int k = 0; k < 2; ++k) {
@@ -4752,6 +4930,7 @@ int gle_power_spectrum(gle_handle* h, int32_t ngroup, const int64_t* group_len, 
   if (!h || ngroup < 1 || !group_len || !dofs || !out) return GLE_ERR_ARG;
   if (!h->d_rec_p) return fail(h, GLE_ERR_STATE, "gle_power_spectrum needs the recorded velocities (gle_record GLE_REC_P)");
   hipSetDevice(h->cfg.device);
+  XRESOLVE(h);
   std::vector<int64_t> off(ngroup + 1, 0);
   for (int g = 0; g < ngroup; ++g) {
     if (group_len[g] < 0) return fail(h, GLE_ERR_ARG, "negative group length");
@@ -4823,6 +5002,7 @@ int gle_cache_audit(gle_handle* h, int64_t* counts) {
   counts[0] = counts[1] = 0;
   if (!h->d_guard) return GLE_OK;
   hipSetDevice(h->cfg.device);
+  XRESOLVE(h);
   unsigned long long v[2] = {0, 0};
   const int rc = download(h, v, h->d_guard, sizeof(v));
   if (rc) return rc;

@@ -854,10 +854,17 @@ __device__ __forceinline__ void dof_BC(const ChTile* __restrict__ T, const StepD
 
 // A stage-4 DOF tile split over T->xnsub workgroups (k-ranges of its products): this workgroup's
 // output sums go to its slab with write-through (sc1) stores, drained by every wave before the
-// workgroup's barrier; lane 0 then adds to the tile's arrival counter (relaxed, agent scope).  The
-// last arriver reads every slab with sc1 loads (no stale L1 / L2 line of another XCD can serve
-// them) and sums them in slab order, so the result does not depend on the arrival order.  The
-// counter is never reset: every launch adds exactly xnsub per tile (zeroed with the plan).
+// workgroup's barrier; lane 0 then adds to the tile's arrival counter (agent scope).  The last
+// arriver reads every slab with sc1 loads (no stale L1 / L2 line of another XCD can serve them) and
+// sums them in slab order, so the result does not depend on the arrival order.  The counter is
+// never reset: every launch adds exactly xnsub per tile (zeroed with the plan).
+// CH_XSUB_ORDER 1: the counter add is a release and the last arriver issues an acquire fence
+// before its slab loads (the happens-before edge of the HIP / C++ model; on gfx950 an L2 write-back
+// and invalidate per tile and launch); 0: relaxed, ordered by the slab stores' completion wait and
+// the loads' issue after the counter's return (ISA-level ordering only)
+#ifndef CH_XSUB_ORDER
+#define CH_XSUB_ORDER 1
+#endif
 template <int NW, int NE, int EPT>
 __device__ __forceinline__ bool xsub_combine(const ChTile* __restrict__ T, double (&ov)[EPT][CH_XO], double* lds) {
   typedef __attribute__((address_space(1))) unsigned long long gull;
@@ -877,12 +884,16 @@ __device__ __forceinline__ bool xsub_combine(const ChTile* __restrict__ T, doubl
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // every wave's slab stores have completed; the LDS partial slots are read
   if (threadIdx.x == 0) {
-    const unsigned long long old = __hip_atomic_fetch_add((gull*)T->xcnt, 1ull, __ATOMIC_RELAXED,
+    const unsigned long long old = __hip_atomic_fetch_add((gull*)T->xcnt, 1ull,
+                                                          CH_XSUB_ORDER ? __ATOMIC_RELEASE : __ATOMIC_RELAXED,
                                                           __HIP_MEMORY_SCOPE_AGENT);
     lds[0] = (old + 1) % (unsigned long long)ns == 0 ? 1.0 : 0.0;
   }
   __syncthreads();
   if (lds[0] == 0.0) return false;
+#if CH_XSUB_ORDER
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every other slab's stores happen-before the loads
+#endif
 #pragma unroll
   for (int x = 0; x < EPT; ++x) {
     const int e = min((int)threadIdx.x + x * NW * 64, NE - 1);
@@ -942,21 +953,8 @@ __device__ __forceinline__ void dof_X(const ChTile* __restrict__ T, const StepDe
       v0[x][u] = G(bd.V)[(int64_t)par * bd.vs + bath_idx(E[x], kk[x][u], B)];
     }
   }
-  // md.potforce cache audit of the previous step (its words at parity par1): the first row tile of
-  // each column tile counts the trajectories whose cache rule would have reused a force at a point
-  // within 1e-9 but not equal, and zeroes the words for step t + 1
+  // (md.potforce's cache audit of the previous step ran in chain_kernel before this tile started)
   const int part = T->xpart;  // 1: p_{t+1} only, 2: id0 phase and q_{t+1} only, 0: both
-  if (T->first && part != 1 && threadIdx.x < 2 * Geo::NT) {
-    const int id = threadIdx.x / Geo::NT, b = T->c0 + (int)threadIdx.x % Geo::NT;
-    if (b < B) {
-      unsigned long long* w = pmax_word(sd, id, par1, b);
-      const unsigned long long v = *G(w);
-      if (v != 0ull && word_hit(v))
-        __hip_atomic_fetch_add((__attribute__((address_space(1))) unsigned long long*)(sd->guard + id), 1ull,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *G(w) = 0ull;
-    }
-  }
   run_products_rn<NW, DRN, GV>(T, t, lds);
   __syncthreads();
   stamp(sd, 4, 2, ta);
@@ -1036,7 +1034,7 @@ __device__ __forceinline__ void dof_X(const ChTile* __restrict__ T, const StepDe
   }
   if (part == 1) return;  // the p_{t+1} half of a split tile: no reductions
   // per-trajectory sums over the tile's DOFs (fixed row order): currents and energy into the step's
-  // partial table, the two cache distances as maxima into the parity-par words
+  // partial table, the two cache distances as maxima into the audit words of slot t mod 3
   __syncthreads();
   double* red = lds;
 #pragma unroll
@@ -1064,9 +1062,9 @@ __device__ __forceinline__ void dof_X(const ChTile* __restrict__ T, const StepDe
         if (j >= 0) prow[(int64_t)j * B + b] = v;
       } else if (qn == CH_TB) {
         prow[(int64_t)nb * B + b] = v;
-      } else {
+      } else if (ta.xw) {
         const unsigned long long bits = nan ? 0x7FF8000000000000ull : (unsigned long long)__double_as_longlong(v);
-        gmax(pmax_word(sd, qn - CH_TB - 1, par, b), bits);
+        gmax(ta.xw + ((t % 3) * 2 + (qn - CH_TB - 1)) * (int64_t)B + b, bits);
       }
     }
   }
@@ -1306,7 +1304,43 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(DRN == 
       else if (i < NCP) sdw[i - NTW] = v[k];
     }
   }
-  __syncthreads();
+  if constexpr (STAGE >= 4) {
+    // md.potforce cache audit of the previous step (StepArgs::xw): every workgroup reads the 2 B
+    // distance words and the stop word with its descriptor; a distance in (0, 1e-9) -- the reference
+    // reuses a force computed at another point -- or a set stop word leaves this launch without
+    // stores, and the launches after it (the host replays from step t - 1 on the two-launch path)
+    int nh0 = 0, nh1 = 0, st = 0;
+    if (ta.xw) {
+      const int n2 = 2 * ta.xB;
+      const int64_t wprev = ((ta.t + 2) % 3) * (int64_t)n2;
+      for (int i = threadIdx.x; i <= n2; i += NW * 64) {
+        const unsigned long long w = i < n2 ? *G(ta.xw + wprev + i) : *G(ta.xstop);
+        if (i == n2) st = w != 0ull;
+        else if (w != 0ull && word_hit(w)) (i < ta.xB ? nh0 : nh1) += 1;
+      }
+    }
+    if (__syncthreads_or((nh0 | nh1 | st) != 0)) {
+      const bool was = __syncthreads_or(st) != 0;
+      if (!was && blockIdx.x == 0) {  // the first stopping launch: count and publish the stop
+        const StepDev* sdl = (const StepDev*)sdw;
+        typedef __attribute__((address_space(1))) unsigned long long gull;
+        if (nh0) __hip_atomic_fetch_add((gull*)(sdl->guard + 0), (unsigned long long)nh0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (nh1) __hip_atomic_fetch_add((gull*)(sdl->guard + 1), (unsigned long long)nh1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x == 0) {
+          const unsigned long long v = (unsigned long long)ta.t + 1ull;
+          __hip_atomic_store((gull*)ta.xstop, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(ta.xstop_host, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
+      return;
+    }
+    if (ta.xw && blockIdx.x == 0) {  // slot (t + 1) mod 3 for launch t + 1 (read by launch t - 1)
+      const int n2 = 2 * ta.xB;
+      for (int i = threadIdx.x; i < n2; i += NW * 64) *G(ta.xw + ((ta.t + 1) % 3) * (int64_t)n2 + i) = 0ull;
+    }
+  } else {
+    __syncthreads();
+  }
   const ChTile* T = (const ChTile*)tdw;
   sd = (const StepDev*)sdw;  // header only: bath[] is not copied (tiles carry their baths)
   const int kind = T->kind;

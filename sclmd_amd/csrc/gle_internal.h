@@ -188,9 +188,10 @@ struct StepDev {
   double* rec_hq;         //   rec_ml holds p_t / q_t, md.py:386-387)
   double* rec_f[MAXBATH]; // md.fhis[i] bath-local [nmd][nc][B] (md.py:398)
   int32_t rec_ml, rec_pad;
-  // composed one-launch step (stage 4): [0] steps whose md.potforce cache would have hit at q~ with
-  // q~ != q0 (0 < max|q~ - q_t| < 1e-9, the reference then reuses the force at q_t), [1] the same at
-  // q_{t+1} after a constraint (0 < max|q_{t+1} - q~_t| < 1e-9); per-trajectory maxima in pmax
+  // composed one-launch step (stage 4): trajectories found by a stopping launch (StepArgs::xw) whose
+  // md.potforce cache would have hit at a point other than q0: [0] at q~ (0 < max|q~ - q_t| < 1e-9,
+  // the reference then reuses the force at q_t), [1] at q_{t+1} after a constraint (0 < max|q_{t+1}
+  // - q~_t| < 1e-9)
   unsigned long long* guard;
   BathDev bath[MAXBATH];
 };
@@ -207,8 +208,9 @@ struct StepDev {
 // The DOF tiles also form K0 p_t, Kq q_t, dyn q_t for F0 (current, energy, recordings), the
 // S tiles V0(t+1) = W1(t) - c K1 p_t and W1(t+1) = n_{t+2} - c (K2 p_t + near(t+2) + levels), the
 // near tiles the partials of lags >= 3 for target t+3.  One dependent launch per step instead of
-// two (A, BC); the potential force is evaluated fresh at q~ (md.potforce's 1e-9 cache reuse is
-// counted by StepDev::guard when it would have applied with q~ != q0).
+// two (A, BC); the potential force is evaluated fresh, which equals md.potforce unless its 1e-9 cache
+// reuse applies at a point q != q0: such a step is detected by the next launch (StepArgs::xw), which
+// stops the composed launches, and the host replays from that step on the two-launch path.
 // One md.vv is three launches A, B, C.  Every workgroup is one ChTile: a 16-row x 16*rn-column
 // output tile whose products are split over the 4 waves by k-steps (each wave's run of tasks
 // accumulates into an LDS partial slot; the epilogue adds the slots of an output in fixed order),
@@ -347,6 +349,17 @@ struct StepArgs {
   // far-field items of far[0..nfar) in order (fused schedule; nfar = 0 otherwise)
   int32_t nstatic, nfar;
   FarRange far[MAXLVL];
+  // composed step (stage 4/5) launches of gle_run, else nullptr: md.potforce's cache audit words
+  // xw [3][2][xB] (launch t reads slot (t - 1) mod 3, zeroes (t + 1) mod 3, writes t mod 3; index 0 =
+  // max |q~ - q_t| of the id1 call, 1 = max |q_{t+1} - q~_t| of the next id0 call) and the stop words:
+  // a launch that finds a distance in (0, 1e-9) -- where md.potforce would reuse a force at another
+  // point (md.py:449-450, 767-779) -- or a set xstop stores nothing; the first such launch sets
+  // *xstop = *xstop_host = t + 1 (device word / host-mapped word), and the host replays from step
+  // t - 1 on the two-launch path, which applies the cache rule (gle_api.hip xresolve)
+  unsigned long long* xw;
+  unsigned long long* xstop;
+  unsigned long long* xstop_host;
+  int32_t xB, xpad;
 };
 void launch_contract(int rn, int cu, const CItem* items, int nitems, StepArgs ta, hipStream_t s);
 void launch_reduce(const RItem* items, int nitems, int max_elems, StepArgs ta,
@@ -393,6 +406,18 @@ struct XPrimeArgs {
   int32_t nc, B, nmd, nqn;
 };
 void launch_xprime(const XPrimeArgs& a, hipStream_t s);
+// end of a gle_run of composed steps at step t: the audit of step t - 1's words as launch t would do
+// it (StepArgs::xw), then, at odd t, the state moves from the odd-parity buffers (P2, Q2) to P / Q
+// unless the run stopped (the state of the step to replay from stays in the buffer its parity names)
+struct XFinishArgs {
+  double *P, *Q;
+  const double *P2, *Q2;
+  int64_t n;  // doubles per state array to move (0: even t, audit only)
+  unsigned long long *xw, *xstop, *xstop_host, *guard;
+  int64_t t;
+  int32_t B, pad;
+};
+void launch_xfinish(const XFinishArgs& a, hipStream_t s);
 void launch_philox_normal(double* x, int64_t nfreq, int64_t ncp, int64_t nc, int64_t B,
                           uint64_t seed, uint64_t traj_offset, hipStream_t s, int64_t w_off = 0);
 // streamed noise: a[w0 + w][row_off + r][b] = wscale[w] sum_k M[w][r][k] x[w][k][b] for w < nw (M of

@@ -638,6 +638,42 @@ void launch_xprime(const XPrimeArgs& a, hipStream_t s) {
   xprime_kernel<<<(unsigned)std::min<int64_t>((n + 255) / 256, 4096), 256, 0, s>>>(a);
 }
 
+// md.potforce cache audit of the run's last step (the chain kernel's stage-4 prologue, gle_chain.hip)
+// in every workgroup, then the state copy unless the run stopped
+__global__ __launch_bounds__(256) void xfinish_kernel(XFinishArgs a) {
+  typedef __attribute__((address_space(1))) unsigned long long gull;
+  const int n2 = 2 * a.B;
+  const unsigned long long* wp = a.xw + ((a.t + 2) % 3) * (int64_t)n2;
+  int nh0 = 0, nh1 = 0, st = 0;
+  for (int i = threadIdx.x; i <= n2; i += 256) {
+    const unsigned long long w = i < n2 ? wp[i] : *a.xstop;
+    const double m = __longlong_as_double((long long)w);
+    if (i == n2) st = w != 0ull;
+    else if (w != 0ull && m == m && m < 10e-10) (i < a.B ? nh0 : nh1) += 1;  // sameq, md.py:767-779
+  }
+  if (__syncthreads_or((nh0 | nh1 | st) != 0)) {
+    if (!__syncthreads_or(st) && blockIdx.x == 0) {
+      if (nh0) __hip_atomic_fetch_add((gull*)(a.guard + 0), (unsigned long long)nh0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (nh1) __hip_atomic_fetch_add((gull*)(a.guard + 1), (unsigned long long)nh1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (threadIdx.x == 0) {
+        const unsigned long long v = (unsigned long long)a.t + 1ull;
+        __hip_atomic_store((gull*)a.xstop, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.xstop_host, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    return;  // a stopped run: the host replays from the buffer of the stop step
+  }
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < a.n; e += (int64_t)gridDim.x * blockDim.x) {
+    a.P[e] = a.P2[e];
+    a.Q[e] = a.Q2[e];
+  }
+}
+
+void launch_xfinish(const XFinishArgs& a, hipStream_t s) {
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((a.n + 255) / 256, 1024));
+  xfinish_kernel<<<g, 256, 0, s>>>(a);
+}
+
 // md.phis / md.qhis rows (newest first) of trajectories [b0, b0 + nb) into out [nb][nt][nph]: row i
 // = slot (tau0 - i) mod R of the full-DOF recording ring rec [R][nph][B] for i < R, zero past the
 // ring (or everywhere when rec is null)

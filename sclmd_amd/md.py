@@ -787,22 +787,36 @@ class md:
         self._tick("dump_join", t1 - t0)
         self._tick("dump_snapshot", time.perf_counter() - t1)
         if not self.async_dump:
-            self._write_snapshot(snap)
+            self._apply_written(self._write_snapshot(snap))
             return
         import threading
 
-        box = {"snap": snap}
+        box = {"snap": snap, "lock": threading.Lock(), "committed": False, "remove": []}
         th = threading.Thread(target=self._write_snapshot_bg, args=(box,), name="sclmd-dump", daemon=True)
         self._dump_pending = (snap["fn"], int(self.t), ipie, th, box)
         th.start()
 
-    def _write_snapshot_bg(self, box):
+    @staticmethod
+    def _write_snapshot_bg(box):
+        # the writer thread touches only its box: what it wrote and its time are applied to the md by
+        # _join_dump on the caller's thread
         try:
-            self._write_snapshot(box["snap"])
+            box["written"] = md._write_snapshot(box["snap"])
+            with box["lock"]:
+                box["committed"] = True
+                rm = list(box["remove"])
+            for fn in rm:  # files to drop once this one is on disk (remove_after_dump)
+                if os.path.exists(fn):
+                    os.remove(fn)
         except BaseException as e:  # re-raised by _join_dump on the caller's thread
             box["error"] = e
         finally:
             box.pop("snap", None)   # the host copy is freed as soon as the file is written
+
+    def _apply_written(self, written):
+        last, dt = written
+        self._last_dump = last
+        self._tick("dump_write", dt)
 
     def _join_dump(self):
         """Wait for the background MD{j}.nc write, if any, and raise its error."""
@@ -813,6 +827,21 @@ class md:
         pend[3].join()
         if "error" in pend[4]:
             raise RuntimeError("md.dump: writing %s failed" % pend[0]) from pend[4]["error"]
+        self._apply_written(pend[4]["written"])
+
+    def remove_after_dump(self, fn):
+        """Remove fn once the newest MD{j}.nc is committed (md.py:676-679 removes MD{j-1}.nc after
+        MD{j}.nc is on disk): at once when no dump is pending or it has committed, else by the writer
+        thread right after its commit -- a checkpoint is on disk at every moment."""
+        pend = getattr(self, "_dump_pending", None)
+        if pend is not None:
+            box = pend[4]
+            with box["lock"]:
+                if not box["committed"]:
+                    box["remove"].append(fn)
+                    return
+        if os.path.exists(fn):
+            os.remove(fn)
 
     def _dump_snapshot(self, ipie, id):
         """Host copy of everything MD{id}.nc holds: dimensions and (name, array, dims) variables."""
@@ -880,7 +909,9 @@ class md:
         return {"fn": self._ncname(id), "dims": dims, "vars": var, "t": int(self.t), "ipie": ipie,
                 "savep": bool(self.savep)}
 
-    def _write_snapshot(self, snap):
+    @staticmethod
+    def _write_snapshot(snap):
+        """Write the snapshot's file; returns ((fn, mtime, size, t, ipie, savep), seconds)."""
         from . import checkpoint as C
 
         t0 = time.perf_counter()
@@ -898,8 +929,7 @@ class md:
         st_ = os.stat(fn)
         # what this process wrote: the next run's start can skip reading its own file back, and an
         # unchanged second dump of the same piece need not be rewritten
-        self._last_dump = (fn, st_.st_mtime_ns, st_.st_size, snap["t"], snap["ipie"], snap["savep"])
-        self._tick("dump_write", time.perf_counter() - t0)
+        return (fn, st_.st_mtime_ns, st_.st_size, snap["t"], snap["ipie"], snap["savep"]), time.perf_counter() - t0
 
     def _tick(self, name, dt):
         """Wall time of the named host phase, accumulated (md.phase_times: where a Run's time goes)."""
@@ -1026,10 +1056,7 @@ class md:
                         tt = self.t - 1
                         if traj is not None and (tt == 0 or tt % self.nstep == 0):
                             self._write_frame(traj, tt)
-                # with savep the last piece's file is written once, after the power spectra below
-                # (the reference writes it before and again after them, md.py:596, 654: same file)
-                if piece < self.npie - 1 or not self.savep:
-                    self.dump(piece, j)
+                self.dump(piece, j)  # md.py:596 (with savep written again after the power spectra)
             if traj is not None:
                 traj.close()
             if self.cf:
@@ -1057,7 +1084,7 @@ class md:
                     self._join_dump()
                 if os.path.exists(self._ncname(j - 1)):
                     self._log("Remove " + self._ncname(j - 1))
-                    os.remove(self._ncname(j - 1))
+                    self.remove_after_dump(self._ncname(j - 1))  # once MD{j}.nc is committed
         # the last file is on disk (or its write error raised) when Run returns
         self._join_dump()
         self._in_run = False

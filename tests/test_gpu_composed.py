@@ -163,23 +163,91 @@ def test_composed_with_constraints_vs_oracle():
     st.close()
 
 
-def test_cache_audit_counts_reuse_at_rest():
-    """A system at rest with noise of 1e-16: |q~ - q| stays below md.potforce's 1e-9, where the
-    reference reuses the force at q_t; the composed step counts those steps."""
-    from sclmd_amd import _native as N
-    from sclmd_amd import synthetic
-
-    dyn, _, baths, meta = synthetic.junction("C3", natom=40, ml=96, nmd=256, nw=60, seed=3)
-    B = 8
-    st = N.Stepper(meta["nph"], B, meta["nmd"], meta["dt"], 0)
-    for b in baths:
-        st.add_bath(N.GLE_BATH_PHONON, b.cids, b.kernel)
-    st.set_dyn(dyn)
-    st.set_state(np.zeros((B, meta["nph"])), np.zeros((B, meta["nph"])), 0)
+def _at_rest_setup(B, constr=None, kick=None, rest=()):
+    """Trajectories `rest` start at rest (p = q = 0, empty history) with zero noise, and from step
+    `kick` on (None: from the start) their noise is 1e-16: |q~ - q| then stays below md.potforce's
+    1e-9 and the reference reuses the force computed at another point (md.py:449-450, 767-779).
+    The other trajectories move as in _setup."""
+    st, sim, baths, ob, meta, dyn, rng = _setup(B, constr=constr)
+    p, q, _ = st.get_state()
+    p, q = p.copy(), q.copy()
+    hist = [rng.normal(size=(B, b.kernel.shape[0], b.nc)) * 1e-2 for b in baths]
+    for r in rest:
+        p[r] = 0.0
+        q[r] = 0.0
+        for h in hist:
+            h[r] = 0.0
+    if constr is not None:
+        p[:, constr] = 0.0
+        q[:, constr] = 0.0
+    st.set_state(p, q, 0)
+    sim.p, sim.q = p.T.copy(), q.T.copy()
     for i, b in enumerate(baths):
-        st.set_history(i, None)
-        st.set_noise(i, np.full((B, meta["nmd"], b.nc), 1e-16))
-    st.run(10)
-    st.sync()
+        n = rng.normal(size=(B, meta["nmd"], b.nc)) * 1e-3
+        for r in rest:
+            n[r] = 0.0
+            n[r, (kick or 0):] = 1e-16
+        st.set_history(i, hist[i])
+        st.set_noise(i, n)
+        sim.set_history(i, hist[i])
+        ob[i].noise = n
+    return st, sim
+
+
+@pytest.mark.parametrize("constr", [None, [0, 1, 2, 60, 61]])
+def test_potforce_cache_reuse_at_rest_vs_oracle(constr):
+    """Every trajectory at rest under noise of 1e-16 (with and without constrained DOFs): each step
+    hits md.potforce's cache at a point that is not q0, at q~ and (with constraints) at q_{t+1}.  Each
+    composed run stops at its first step and is replayed on the two-launch path, which applies the
+    rule per trajectory: p, q and the currents equal the oracle's (oracle.GLEBatch.potforce, sameq)."""
+    B = 8
+    st, sim = _at_rest_setup(B, constr=constr, rest=range(B))
+    assert st.plan_detail()["composed_step"]
+    nst = 0
+    for k in (5, 1, 7):
+        st.run(k)
+        for _ in range(k):
+            sim.step()
+        nst += k
+        _check(st, sim, nst)
+    a = st.cache_audit()
+    assert a[0] > 0 and (constr is None or a[1] > 0), a
+    st.close()
+
+
+@pytest.mark.parametrize("kick", [30, 31])
+@pytest.mark.parametrize("constr", [None, [0, 1, 2, 60, 61]])
+def test_potforce_cache_reuse_mid_run_vs_oracle(kick, constr):
+    """Seven trajectories move; the eighth rests (exact zeros: its cache hits are at q0 itself, which
+    the composed step reproduces) until its noise turns to 1e-16 at step `kick`.  The composed run
+    stops there (an even and an odd step: the state it resumes from sits in either parity buffer),
+    the rest of it is replayed on the two-launch path, and a later run goes back to composed steps:
+    all against the oracle."""
+    B = 8
+    st, sim = _at_rest_setup(B, constr=constr, kick=kick, rest=[7])
+    st.run(60)
+    for _ in range(60):
+        sim.step()
+    _check(st, sim, 60)
     assert st.cache_audit()[0] > 0
+    st.run(23)
+    for _ in range(23):
+        sim.step()
+    _check(st, sim, 83)
+    st.close()
+
+
+def test_exact_rest_runs_composed_steps():
+    """A trajectory at exact rest (zero noise, zero state): md.potforce hits its cache at q0 itself
+    every step, which is the fresh evaluation -- no stop, no replay.  B = 3 plans the direct ladder,
+    whose products keep an all-zero trajectory exactly zero (the spectral levels' transforms leave
+    roundoff of the other trajectories' size in it, ~1e-18 here, which is then a near hit and is
+    replayed like one)."""
+    B = 3
+    st, sim = _at_rest_setup(B, kick=10 ** 9, rest=[1])
+    st.run(40)
+    for _ in range(40):
+        sim.step()
+    _check(st, sim, 40)
+    assert st.cache_audit() == (0, 0)
     st.close()

@@ -233,3 +233,52 @@ def test_retained_plan_replay_equals_stream(kind, monkeypatch):
     fresh.noise_stream_plan(0, Nz.stream_factor_plan(bi), cplx, seed=seed1, traj_offset=0)
     assert np.array_equal(got, fresh.get_noise(0))
     fresh.close()
+
+
+def test_retention_cap_streams_without_keeping():
+    """Retention that would exceed the handle's cap (gle_noise_stream_retain_cap; the same path as
+    running short of free device memory beside the plan) keeps nothing and streams as without it:
+    the noise is bit-identical, the bath's run and the history getters (md.dump's snapshot buffer)
+    still work, and md.gen_noise falls back to the host factor cache."""
+    from sclmd_amd import _native as N
+    from sclmd_amd import md as MD
+    from sclmd_amd import noise as Nz
+    from sclmd_amd import synthetic
+
+    rng = np.random.default_rng(4)
+    nmd, B = 512, 4
+    b = synthetic.make_phbath(300.0, list(range(24)), 8, nmd, rng, nw=40)
+    st = N.Stepper(b.nc, B, nmd, synthetic.DT, 0)
+    st.add_bath(N.GLE_BATH_PHONON, np.arange(b.nc), np.zeros((2, b.nc, b.nc)))
+    st.set_dyn(np.eye(b.nc) * 0.01)
+    st.noise_stream_plan(0, Nz.stream_factor_plan(b, chunk=16), False, seed=5, traj_offset=0, max_chunk=16)
+    want = st.get_noise(0)
+    st.noise_stream_retain(0, True)
+    st.noise_stream_retain_cap(4096)  # far below one chunk of factors
+    st.noise_stream_plan(0, Nz.stream_factor_plan(b, chunk=16), False, seed=5, traj_offset=0, max_chunk=16)
+    assert st.noise_stream_retained(0) == 0
+    assert np.array_equal(st.get_noise(0), want)
+    with pytest.raises(N.GLEError):
+        st.noise_stream_replay(0, 5, 0)
+    st.set_state(np.zeros((B, b.nc)), np.zeros((B, b.nc)), 0)
+    st.set_history(0, None)
+    st.run(20)
+    st.sync()
+    assert st.get_history(0).shape == (B, 2, b.nc)
+    st.noise_stream_retain_cap(None)
+    st.noise_stream_plan(0, Nz.stream_factor_plan(b, chunk=16), False, seed=5, traj_offset=0, max_chunk=16)
+    assert st.noise_stream_retained(0) > 0 and np.array_equal(st.get_noise(0), want)
+    st.close()
+
+    dyn, axyz, baths, meta = synthetic.junction("C5", natom=12, ml=8, nmd=nmd, nw=60, seed=8)
+    m = MD.md(meta["dt"], meta["nmd"], meta["T"], axyz=axyz, dyn=dyn, ntraj=B, seed=3, noise_mode="device",
+              verbose=False)
+    m.noise_stream_bytes = 0  # force the streamed path
+    for bb in baths:
+        m.AddBath(bb)
+    m.initialise()
+    m._ensure_device().noise_stream_retain_cap(0)
+    m.gen_noise(0, 0)
+    assert m._st.noise_stream_retained(0) == 0 and getattr(baths[0], "_stream_cache", None)
+    m.gen_noise(0, 1)  # from the host factor cache
+    m.close()

@@ -167,3 +167,39 @@ def test_no_bath_nve_vs_oracle():
             sim.step()
         assert relerr(q[b], sim.q) < RTOL_TRAJ and relerr(p[b], sim.p) < RTOL_TRAJ
     st.close()
+
+
+@pytest.mark.parametrize("case", vv_cases())
+@pytest.mark.parametrize("far_mode,block_len", [("auto", 0), ("spectral", 4)])
+def test_vv_golden_through_run(case, far_mode, block_len):
+    """The golden trajectories through gle_run (st.run), the path bench and md.Run take: the composed
+    one-launch step where the plan allows it (GLE_PLAN_COMPOSED_STEP; the biased ebath and the
+    overlapping phonon baths keep the two-launch path), one step per call with the state read after
+    each, then the whole run in one call -- against the reference's own fixtures."""
+    g = load_golden(case)
+    st = stepper_from_golden(g, 1, block_len, far_mode)
+    composed = st.plan_detail()["composed_step"]
+    if case == "vv_mixed":  # unbiased ebath + memory-kernel phonon bath + constraints
+        assert composed
+    if case in ("vv_biased", "vv_twoph"):
+        assert not composed
+    n = int(g["nsteps"])
+    qs, ps = [], []
+    for _ in range(n):
+        st.run(1)
+        p, q, _ = st.get_state()
+        ps.append(p[0])
+        qs.append(q[0])
+    assert relerr(qs, g["q"]) < RTOL_TRAJ, case
+    assert relerr(ps, g["p"]) < RTOL_TRAJ, case
+    st.close()
+    st = stepper_from_golden(g, 1, block_len, far_mode)
+    st.run(n)
+    p, q, t = st.get_state()
+    assert t == n
+    assert relerr(q[0], g["q"][-1]) < RTOL_TRAJ and relerr(p[0], g["p"][-1]) < RTOL_TRAJ, case
+    nmd = int(g["nmd"])
+    tn = [t % nmd for t in range(max(0, n - nmd), n)]
+    assert relerr(st.get_current()[:, 0, tn], g["cur"][max(0, n - nmd):n].T) < RTOL_CUR, case
+    assert st.cache_audit() == (0, 0)
+    st.close()

@@ -247,6 +247,40 @@ def test_background_dump_writes_and_raises_on_the_callers_thread(tmp_path, monke
     m._join_dump()  # the error is raised once
 
 
+def test_rmnc_removes_previous_file_only_after_the_new_one_is_committed(tmp_path, monkeypatch):
+    """md.Run with RemoveNC: MD{j-1}.nc goes only once MD{j}.nc is on disk (md.py:596, 676-679), also
+    while MD{j}.nc is still being written by the background dump: at every moment one of the two
+    files is a complete checkpoint."""
+    import threading
+
+    m = _cpu_md()
+    monkeypatch.chdir(tmp_path)
+    from sclmd_amd import checkpoint as C
+
+    snap = {"fn": "MD0.nc", "dims": [("nnmd", None), ("nph", 3)], "t": 5, "ipie": 0, "savep": False,
+            "vars": [("ps", np.arange(12.0).reshape(4, 3), ("nnmd", "nph"))]}
+    monkeypatch.setattr(m, "_dump_snapshot", lambda ipie, id: dict(snap, fn="MD%d.nc" % id))
+    m.dump(0, 0)
+    m._join_dump()
+    gate, seen = threading.Event(), []
+    real_commit = C.commit
+
+    def slow_commit(f, tmp, fn):  # MD1.nc's commit waits until the removal has been requested
+        gate.wait(10)
+        seen.append(os.path.exists("MD0.nc"))
+        real_commit(f, tmp, fn)
+
+    monkeypatch.setattr(C, "commit", slow_commit)
+    m.dump(0, 1)
+    m.remove_after_dump("MD0.nc")
+    assert os.path.exists("MD0.nc")  # MD1.nc is not committed yet
+    gate.set()
+    m._join_dump()
+    assert seen == [True] and os.path.exists("MD1.nc") and not os.path.exists("MD0.nc")
+    m.remove_after_dump("MD1.nc")  # nothing pending: at once
+    assert not os.path.exists("MD1.nc")
+
+
 def test_noise_key_follows_content():
     """The noise-factor cache key changes when a spectrum array is edited in place (an id() key
     would not) and is equal for equal content in a different array."""
