@@ -236,6 +236,9 @@ def main():
                     help="one collective right after the process group is joined, before the stepper exists "
                          "(RCCL's streams then take their hardware queues first; rehearsal of a host program "
                          "that communicates before it builds the stepper)")
+    ap.add_argument("--stream-noise", action="store_true",
+                    help="generate the coloured noise through the streamed-factor path whatever the bath size "
+                         "(the C5 path; rehearses the node-shared factorisation at small configs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--single-pass-budget", type=float, default=8.0,
@@ -292,19 +295,24 @@ def main():
     log("[bench] rank %d system built (%.1fs)" % (rank, time.perf_counter() - t_setup))
     for b in baths:
         m.AddBath(b)
+    if args.stream_noise:
+        m.noise_stream_bytes = 0
     m.initialise()
     m.ResetHis()
     log("[bench] rank %d state initialised (%.1fs)" % (rank, time.perf_counter() - t_setup))
+    noise_s = 0.0
     if args.noise == "white":
         rng = np.random.default_rng(4321 + rank)
         for b in baths:
             b.noise = rng.standard_normal((args.ntraj, meta["nmd"], b.nc)) * 1e-3
     else:
+        t_noise = time.perf_counter()
         for i in range(len(baths)):
             tn = time.perf_counter()
             m.gen_noise(i, 0)
             log("[bench] rank %d noise of bath %d (%s, nc %d): %.1fs" % (rank, i, baths[i].kind, baths[i].nc,
                                                                       time.perf_counter() - tn))
+        noise_s = time.perf_counter() - t_noise
     st = m._ensure_device()
     tp = time.perf_counter()
     m.steps(0)  # uploads assigned noise
@@ -314,6 +322,12 @@ def main():
     plan = st.plan_info()
     detail = st.plan_detail()
     log("[bench] rank %d setup %.1fs plan %s %s" % (rank, setup_s, plan, detail))
+    # per-rank setup: wall time, noise phase and the noise factorisations this rank computed (the
+    # ranks of a node split them, noise.NodeShare: their sum is one rank's count alone)
+    share = getattr(m, "_share", None)
+    row = np.zeros((world, 3))
+    row[rank] = [setup_s, noise_s, share.total if share is not None else -1.0]
+    setup_ranks = m._allreduce(row) if world > 1 else row
 
     def barrier():
         if dist is not None:
@@ -434,6 +448,9 @@ def main():
         "value_per_gpu": value / world,
         "runtime_libs": loaded_runtime(),
         "setup_s": setup_s,
+        "setup_ranks": [{"rank": r, "setup_s": round(float(v[0]), 3), "noise_s": round(float(v[1]), 3),
+                         "factorisations": (int(v[2]) if v[2] >= 0 else None)}
+                        for r, v in enumerate(np.asarray(setup_ranks).reshape(world, 3))],
         "fill_steps": fill,
         "window_t0": int(t_now + fill + args.warmup),
         "window_phase": phase,

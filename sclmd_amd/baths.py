@@ -61,6 +61,40 @@ def gmem_coefficients(tl, wl, gwl, eta_ad=0):
     return c @ interp
 
 
+def _eigh_parts(spec):
+    """(evals, evecs) of a stack of matrices, split over threads with one BLAS thread each (numpy
+    releases the GIL): every matrix goes through the same single-threaded LAPACK call however the
+    stack is split (across threads, or across the ranks of a node: noise.NodeShare.gather)."""
+    n = spec.shape[0]
+    if n == 0:
+        return np.zeros((0, spec.shape[1])), np.zeros(spec.shape, dtype=spec.dtype)
+    nthr = max(1, min(16, os.cpu_count() or 1, n))
+    parts = np.array_split(np.arange(n), min(n, 4 * nthr))
+    try:
+        from threadpoolctl import threadpool_limits
+        lim = threadpool_limits(1)
+    except Exception:  # pragma: no cover
+        lim = None
+    try:
+        with ThreadPoolExecutor(nthr) as ex:
+            res = list(ex.map(lambda ix: np.linalg.eigh(spec[ix]), parts))
+    finally:
+        if lim is not None:
+            lim.restore_original_limits()
+    return np.concatenate([r[0] for r in res]), np.concatenate([r[1] for r in res])
+
+
+def _factor_from(ev, vec):
+    f = _noise.NoiseFactor.__new__(_noise.NoiseFactor)
+    f.nfreq, f.nc = vec.shape[0], vec.shape[1]
+    f.evals = ev
+    f.evecs = vec
+    f.pos = f.evals > 0
+    f.sigma = np.sqrt(np.where(f.pos, f.evals, 0.0))
+    f.complex = np.iscomplexobj(f.evecs)
+    return f
+
+
 def _eigh_stack(spec):
     """eigh of a stack of matrices; large stacks are split over threads (numpy releases the GIL)."""
     n = spec.shape[0]
@@ -112,11 +146,21 @@ class _BathBase:
     def _noise_key(self):
         raise NotImplementedError
 
-    def noise_factor(self):
-        """Eigendecomposition of the noise spectrum, cached until a parameter changes."""
+    def noise_factor(self, share=None):
+        """Eigendecomposition of the noise spectrum, cached until a parameter changes.  share: a
+        noise.NodeShare -- the node's ranks each decompose a block of the frequencies and exchange
+        the blocks, the same factor bit for bit as one rank's _eigh_parts."""
         key = self._noise_key()
         if getattr(self, "_fac_key", None) != key:
-            self._fac = _eigh_stack(self._spectrum())
+            spec = self._spectrum()
+            if share is not None and share.world > 1 and spec.shape[-1] >= 64 and spec.shape[0] >= 64:
+                import hashlib
+
+                tag = "f%s" % hashlib.sha1(repr(key).encode()).hexdigest()[:16]
+                ev, vec = share.gather(tag, spec.shape[0], lambda lo, hi: _eigh_parts(spec[lo:hi]))
+                self._fac = _factor_from(ev, vec)
+            else:
+                self._fac = _eigh_stack(spec)
             self._fac_key = key
         return self._fac
 

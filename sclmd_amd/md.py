@@ -482,6 +482,26 @@ class md:
     # largest fixed-size variable of an MD{j}.nc file (NetCDF classic format, scipy.io)
     nc_var_limit = 2**31 - 4096
 
+    # the ranks of one node split each streamed bath's factorisations and exchange the factors through
+    # node-local shared memory (noise.NodeShare) instead of each factorising the whole spectrum
+    share_factors = True
+
+    def _node_share(self):
+        """noise.NodeShare over this md's ranks, or None when it runs alone."""
+        from . import ensemble
+        from . import noise as _noise
+
+        w = ensemble.world_size(self.comm)
+        if w <= 1 or not self.share_factors:
+            return None
+        sh = getattr(self, "_share", None)
+        if sh is None:
+            r = ensemble.rank(self.comm)
+            tok = float(int.from_bytes(os.urandom(6), "little")) if r == 0 else 0.0  # < 2^48: exact
+            tok = int(np.asarray(self._allreduce(np.array([tok]))).reshape(-1)[0])
+            sh = self._share = _noise.NodeShare(r, w, lambda: self._allreduce(np.zeros(1)), "%012x" % tok)
+        return sh
+
     def _noise_seed(self, i, run):
         base = 0 if self.seed is None else int(self.seed)
         return (base * 0x9E3779B97F4A7C15 + (run + 1) * 0xBF58476D1CE4E5B9 + (i + 1) * 0x94D049BB133111EB) % 2**64
@@ -500,8 +520,10 @@ class md:
             # md.py:569-570): on the device when they fit there (the stepper replays them with new
             # draws), else in host memory
             seed = self._noise_seed(i, run)
+            share = self._node_share()
             if not self.noise_factor_cache:
-                st.noise_stream_plan(i, _noise.stream_factor_plan(b), b.kind == "ebath", seed, self.traj_offset)
+                st.noise_stream_plan(i, _noise.stream_factor_plan(b, share=share), b.kind == "ebath", seed,
+                                     self.traj_offset)
             else:
                 key = b._noise_key()
                 dev = st.__dict__.setdefault("noise_plan_keys", {})  # bath -> key of its retained plan
@@ -512,8 +534,8 @@ class md:
                     if getattr(b, "_stream_cache_key", None) != key:
                         b._stream_cache, b._stream_cache_key = {}, key
                     st.noise_stream_retain(i, True)
-                    st.noise_stream_plan(i, _noise.stream_factor_plan(b, cache=b._stream_cache), b.kind == "ebath",
-                                         seed, self.traj_offset)
+                    st.noise_stream_plan(i, _noise.stream_factor_plan(b, cache=b._stream_cache, share=share),
+                                         b.kind == "ebath", seed, self.traj_offset)
                     if st.noise_stream_retained(i):
                         dev[i] = key
                         b._stream_cache, b._stream_cache_key = None, None  # the device copy serves
@@ -521,7 +543,7 @@ class md:
             b._noise_version = getattr(b, "_noise_version", 0) + 1
             self._noise_versions[i] = b._noise_version
             return
-        fac = b.noise_factor()
+        fac = b.noise_factor(share=self._node_share())
         key = (self.noise_mode, b._fac_key)
         if getattr(self, "_fac_loaded", {}).get(i) != key:
             st.noise_factors(i, fac.evecs if self.noise_mode == "numpy" else fac.scaled())

@@ -166,7 +166,170 @@ def stream_factor_chunks(bath, chunk=64, workers=None):
             yield w, np.stack([f.result() for f in fl])
 
 
-def stream_factor_plan(bath, chunk=64, workers=None, cache=None):
+class NodeShare:
+    """The ranks of one node factorising a bath's noise spectrum together (the factors
+    are the same on every rank, only the draws differ): rank r computes the dense factors of its
+    contiguous block of the dense frequencies and publishes them as two node-local shared-memory
+    files (the factors, [planes][n][nc][nc] float64, then their frequency indices); after a barrier
+    every rank maps every block and hands the factors to its device in frequency order.  Each
+    factor is computed once on the node, by the same single-threaded LAPACK call one rank would
+    make, so every rank's factors -- and noise -- are bitwise those of one rank factorising alone.
+    A block whose files are missing after the barrier (a rank on another node) is computed locally.
+
+    barrier(): a collective over the ranks (md: a one-double all-reduce of its process group or
+    C-ABI communicator); token: the same string on every rank and unique to the job (md: rank 0's
+    random number, summed over the ranks)."""
+
+    def __init__(self, rank, world, barrier, token, root=None):
+        import os
+
+        self.rank, self.world, self.barrier, self.token = int(rank), int(world), barrier, str(token)
+        self.root = root or os.environ.get("SCLMD_SHM_DIR", "/dev/shm")
+        self.computed = 0   # factorisations this rank computed in the last plan / gather
+        self.total = 0      # ... and over every plan / gather so far
+
+    def gather(self, key, n, compute):
+        """Arrays over the range [0, n) computed in blocks across the ranks: compute(lo, hi) returns a
+        tuple of arrays with hi - lo rows each; every rank gets the tuple concatenated over [0, n)."""
+        import os
+
+        lo, hi = self.block(n)
+        mine = tuple(compute(lo, hi))
+        self.computed = hi - lo
+        self.total += hi - lo
+        base = os.path.join(self.root, "sclmd_%s_%s_r%%d" % (self.token, key))
+        files = ["%s.%d.npy" % (base % self.rank, k) for k in range(len(mine))] + [base % self.rank + ".done"]
+        try:
+            for f, a in zip(files, mine):
+                np.save(f + ".tmp.npy", a)
+                os.replace(f + ".tmp.npy", f)
+            open(files[-1], "w").close()  # written last: the block is complete
+        except OSError:  # no room in shared memory: the other ranks compute this block themselves
+            for f in files:
+                for g in (f, f + ".tmp.npy"):
+                    if os.path.exists(g):
+                        os.remove(g)
+        self.barrier()
+        parts = []
+        for r in range(self.world):
+            if r == self.rank:
+                parts.append(mine)
+            elif os.path.exists(base % r + ".done"):
+                parts.append(tuple(np.load("%s.%d.npy" % (base % r, k)) for k in range(len(mine))))
+            else:
+                parts.append(tuple(compute(*self.block(n, r))))
+        out = tuple(np.concatenate([p[k] for p in parts]) for k in range(len(mine)))
+        self.barrier()  # every rank has read every block
+        for f in files:
+            if os.path.exists(f):
+                os.remove(f)
+        return out
+
+    def block(self, n, r=None):
+        r = self.rank if r is None else r
+        return n * r // self.world, n * (r + 1) // self.world
+
+    def paths(self, key, r):
+        import os
+
+        base = os.path.join(self.root, "sclmd_%s_%s_r%d" % (self.token, key, r))
+        return base + ".fac.npy", base + ".idx.npy"
+
+
+def _dense_factors(bath, idx, dtype, workers):
+    """Dense factors of frequencies idx on a thread pool (BLAS one thread per worker)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from threadpoolctl import threadpool_limits
+
+    with threadpool_limits(1, user_api="blas"), ThreadPoolExecutor(max_workers=workers) as pool:
+        return list(pool.map(lambda i: dense_factor(bath._spectrum_term(i)[3]).astype(dtype, copy=False), idx))
+
+
+def _shared_plan(bath, chunk, workers, cache, share, terms, runs, dtype):
+    """stream_factor_plan's segments with the dense factors split over the node's ranks (NodeShare)."""
+    import os
+
+    nc = bath.nc
+    cplx = dtype is complex
+    dense = [i for kind, _, ws in runs if kind == "dense" for i in ws]
+    import hashlib
+
+    key = "b%s" % hashlib.sha1(repr((bath._noise_key(), chunk)).encode()).hexdigest()[:16]
+    a, b = share.block(len(dense))
+    mine = dense[a:b]
+    fpath, ipath = share.paths(key, share.rank)
+    facs = _dense_factors(bath, mine, dtype, workers)
+    share.computed = len(mine)
+    share.total += len(mine)
+    arr = np.empty((2 if cplx else 1, len(mine), nc, nc))
+    for k, m in enumerate(facs):
+        arr[0, k] = m.real
+        if cplx:
+            arr[1, k] = m.imag
+    del facs
+    try:
+        np.save(fpath + ".tmp.npy", arr)
+        os.replace(fpath + ".tmp.npy", fpath)
+        np.save(ipath + ".tmp.npy", np.asarray(mine, dtype=np.int64))
+        os.replace(ipath + ".tmp.npy", ipath)  # the index file last: its presence marks the block complete
+    except OSError:  # no room in shared memory: the other ranks compute this block themselves
+        for f in (fpath, ipath, fpath + ".tmp.npy", ipath + ".tmp.npy"):
+            if os.path.exists(f):
+                os.remove(f)
+    del arr
+    share.barrier()
+    where = {}  # frequency -> (block array, row)
+    blocks = []
+    for r in range(share.world):
+        fr, ir = share.paths(key, r)
+        if os.path.exists(ir):
+            idx = np.load(ir)
+            fac = np.load(fr, mmap_mode="r")
+        else:  # not on this node's shared memory: compute the block here
+            lo, hi = share.block(len(dense), r)
+            idx = np.asarray(dense[lo:hi], dtype=np.int64)
+            fl = _dense_factors(bath, list(idx), dtype, workers)
+            fac = np.empty((2 if cplx else 1, len(fl), nc, nc))
+            for k, m in enumerate(fl):
+                fac[0, k] = m.real
+                if cplx:
+                    fac[1, k] = m.imag
+        blocks.append(fac)
+        for k, i in enumerate(idx):
+            where[int(i)] = (len(blocks) - 1, k)
+    shared = {}
+    need = {k for kind, k, _ in runs if kind == "shared"}
+    for k, h in bath._shared_matrices():
+        if k in need:
+            shared[k] = positive_factor(h).astype(dtype, copy=False)
+    keep = [] if cache is not None else None
+    for kind, k, ws in runs:
+        if kind == "shared":
+            seg = ("shared", ws[0], len(ws), np.sqrt(np.array([terms[i][2] for i in ws])), shared[k])
+        else:
+            loc = [where[i] for i in ws]
+            bi, r0 = loc[0]
+            if all(l == (bi, r0 + j) for j, l in enumerate(loc)):  # one block's contiguous rows: views
+                planes = [blocks[bi][p, r0:r0 + len(ws)] for p in range(blocks[bi].shape[0])]
+            else:
+                planes = [np.stack([blocks[l[0]][p, l[1]] for l in loc]) for p in range(2 if cplx else 1)]
+            if keep is not None:  # the host cache outlives the shared files: own copies
+                planes = [np.array(x) for x in planes]
+            seg = ("dense", ws[0], (planes[0], planes[1]) if cplx else planes[0])
+        if keep is not None:
+            keep.append(seg)
+        yield seg
+    share.barrier()  # every rank has handed every block to its device
+    for path in share.paths(key, share.rank):
+        if os.path.exists(path):
+            os.remove(path)
+    if cache is not None:
+        cache["segments"] = keep
+        cache["complete"] = True
+
+
+def stream_factor_plan(bath, chunk=64, workers=None, cache=None, share=None):
     """The streamed factors of a bath as device work segments, in frequency order:
       ("shared", w0, nw, scale, F)  frequencies [w0, w0 + nw) whose spectrum is s_w H for one shared
                                     H: factor F = H_+^(1/2) handed over once, scale = sqrt(s_w)
@@ -176,7 +339,8 @@ def stream_factor_plan(bath, chunk=64, workers=None, cache=None):
     factors are computed on a thread pool (LAPACK releases the GIL; BLAS pinned to one thread per
     worker), two chunks ahead of the consumer.  cache: a dict that keeps the dense chunks (and the
     shared factors) of this bath across runs -- the factors do not change between runs, only the
-    draws (md.py:569-570) -- so later runs hand over the cached factors without factorising."""
+    draws (md.py:569-570) -- so later runs hand over the cached factors without factorising.
+    share: a NodeShare -- the node's ranks split the dense factorisations and exchange them."""
     import os
     from concurrent.futures import ThreadPoolExecutor
 
@@ -206,6 +370,9 @@ def stream_factor_plan(bath, chunk=64, workers=None, cache=None):
         except AttributeError:  # pragma: no cover
             workers = os.cpu_count() or 1
         workers = max(1, min(16, workers))
+    if share is not None and share.world > 1:
+        yield from _shared_plan(bath, chunk, workers, cache, share, terms, runs, dtype)
+        return
     keep = [] if cache is not None else None
     shared = {}
     with threadpool_limits(1, user_api="blas"), ThreadPoolExecutor(max_workers=workers) as pool:

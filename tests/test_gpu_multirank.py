@@ -43,19 +43,23 @@ def _env(**kw):
     return env
 
 
-def test_md_run_two_ranks_gloo_matches_one_rank(tmp_path):
+@pytest.mark.parametrize("stream", [False, True])
+def test_md_run_two_ranks_gloo_matches_one_rank(tmp_path, stream):
+    """stream: the noise through the streamed-factor path, whose factorisations the two ranks split
+    (noise.NodeShare: each computes its block once, the node exchanges them in shared memory) --
+    the same noise bit for bit, so the same kappa as one rank factorising everything."""
     sys.path.insert(0, HERE)
     from multirank_child import run_md
 
-    kap1, p1, q1 = run_md(str(tmp_path / "one"), 8, 0)
+    kap1, p1, q1 = run_md(str(tmp_path / "one"), 8, 0, stream=stream)
     port = _free_port()
     out = str(tmp_path / "res")
     procs = []
     for r in range(2):
         env = _env(RANK=r, LOCAL_RANK=r, WORLD_SIZE=2, MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "multirank_child.py"), str(tmp_path), out,
-                                       "4", "gloo"], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                                      text=True))
+                                       "4", "gloo"] + (["stream"] if stream else []), env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
     res = []
     for pr in procs:
         o, e = pr.communicate(timeout=240)
@@ -69,6 +73,9 @@ def test_md_run_two_ranks_gloo_matches_one_rank(tmp_path):
     assert rel(r0["kap"], kap1) < 1e-12, (r0["kap"], kap1)
     assert rel(np.concatenate([r0["p"], r1["p"]]), p1) < 1e-9
     assert rel(np.concatenate([r0["q"], r1["q"]]), q1) < 1e-9
+    if stream:  # each dense factor computed once over both ranks
+        n = [int(np.load(str(tmp_path / ("rank%d" % r) / "factorisations.npy"))[0]) for r in range(2)]
+        assert min(n) > 0 and abs(n[0] - n[1]) <= 64, n
 
 
 def test_bench_gpus2_spawns_two_ranks(tmp_path):
