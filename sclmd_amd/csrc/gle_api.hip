@@ -2543,8 +2543,9 @@ int freeze(gle_handle* h) {
       if (!rc) rc = dalloc_n(h, &L.d_seg, (size_t)(lv.P + 1) * L.seg_fstride, 4096);
       if (!rc) rc = dalloc_n(h, &L.d_Yspec, (size_t)lv.cg_split * (lv.P + 1) * L.yfstride, 4096);
       if (rc) return rc;
-      launch_khat_pack(b.d_K, b.ml, b.nks, L.d_khat, lv.P, 2, L.M, b.nc, b.nrt, b.nks, h->d_cstab,
-                       lv.cstride, h->stream, lv.nplanes);
+      if (launch_khat_pack(b.d_K, b.ml, b.nks, L.d_khat, lv.P, 2, L.M, b.nc, b.nrt, b.nks, h->d_cstab,
+                           lv.cstride, h->stream, lv.nplanes))
+        return fail(h, GLE_ERR_UNSUP, "K-hat transform launch failed (P = " + std::to_string(lv.P) + ")");
       HIPCHK(h, hipStreamSynchronize(h->stream));
     }
     // background stream per level group, bounds in units of P0 (GLE_BG_GROUP=g1,g2 in the experiment

@@ -318,6 +318,43 @@ __device__ __forceinline__ bool word_hit(unsigned long long w) {
   return m == m && m < 10e-10;
 }
 
+// md.potforce cache audit of the previous step in a composed-step launch (StepArgs::xw): thread i <=
+// 2B holds word i of the previous step's distances (i < 2B) or the stop word (i = 2B), loaded with
+// the tile descriptor and first looked at after the tile's products, at the barrier that ends them
+// (the load's latency hides behind the products).  A distance in (0, 1e-9) -- the reference reuses a
+// force computed at another point (md.py:449-450, 767-779) -- or a set stop word makes the tile
+// return before any store; the first stopping launch counts the trajectories and publishes the stop
+// (the host replays from step t - 1 on the two-launch path, gle_api.hip xresolve).
+struct XCheck {
+  unsigned long long w = 0ull;
+  int i = -1;       // this thread's word (-1: none)
+  int n2 = 0;       // 2 B
+  bool on = false;  // a composed-step launch of gle_run
+  // the barrier after the products; true: the tile stores nothing
+  __device__ bool stop(const StepDev* __restrict__ sd, const StepArgs& ta) const {
+    if (!on) {
+      __syncthreads();
+      return false;
+    }
+    int pred = 0, st = 0;
+    if (i == n2) st = w != 0ull;
+    else if (i >= 0 && w != 0ull && word_hit(w)) pred = 1;
+    if (!__syncthreads_or(pred | st)) return false;
+    if (!__syncthreads_or(st) && blockIdx.x == 0) {  // the first stopping launch: count and publish
+      typedef __attribute__((address_space(1))) unsigned long long gull;
+      if (pred)
+        __hip_atomic_fetch_add((gull*)(sd->guard + (i < n2 / 2 ? 0 : 1)), 1ull, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      if (threadIdx.x == 0) {
+        const unsigned long long v = (unsigned long long)ta.t + 1ull;
+        __hip_atomic_store((gull*)ta.xstop, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ta.xstop_host, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    return true;
+  }
+};
+
 // ------------------------------------------------------------------------------------------
 // DOF tiles: 16 DOFs x NT = 16 DRN trajectories; thread element i is e = threadIdx.x + i NW 64
 // (row e / NT, column e % NT).
@@ -863,7 +900,7 @@ __device__ __forceinline__ void dof_BC(const ChTile* __restrict__ T, const StepD
 // and invalidate per tile and launch); 0: relaxed, ordered by the slab stores' completion wait and
 // the loads' issue after the counter's return (ISA-level ordering only)
 #ifndef CH_XSUB_ORDER
-#define CH_XSUB_ORDER 1
+#define CH_XSUB_ORDER 0
 #endif
 template <int NW, int NE, int EPT>
 __device__ __forceinline__ bool xsub_combine(const ChTile* __restrict__ T, double (&ov)[EPT][CH_XO], double* lds) {
@@ -925,7 +962,7 @@ __device__ __forceinline__ bool xsub_combine(const ChTile* __restrict__ T, doubl
 // constraints zero p_{t+1} and q_{t+1} (md.py:407-408); history push of p_{t+1}.
 template <int NW, int DRN, bool GV = false>
 __device__ __forceinline__ void dof_X(const ChTile* __restrict__ T, const StepDev* __restrict__ sd,
-                                      const StepArgs& ta, double* lds) {
+                                      const StepArgs& ta, double* lds, const XCheck& xc) {
   using Geo = DofGeo<NW, DRN>;
   constexpr int EPT = Geo::EPT;
   const int B = sd->B, nb = sd->nbath;
@@ -953,10 +990,9 @@ __device__ __forceinline__ void dof_X(const ChTile* __restrict__ T, const StepDe
       v0[x][u] = G(bd.V)[(int64_t)par * bd.vs + bath_idx(E[x], kk[x][u], B)];
     }
   }
-  // (md.potforce's cache audit of the previous step ran in chain_kernel before this tile started)
   const int part = T->xpart;  // 1: p_{t+1} only, 2: id0 phase and q_{t+1} only, 0: both
   run_products_rn<NW, DRN, GV>(T, t, lds);
-  __syncthreads();
+  if (xc.stop(sd, ta)) return;
   stamp(sd, 4, 2, ta);
   // the tile's output sums: K0.p_t of tile bath u (u), dyn.q_t (CH_TB), p_{t+1} (CH_TB + 1)
   double ov[EPT][CH_XO];
@@ -1081,7 +1117,7 @@ __device__ __forceinline__ void dof_X(const ChTile* __restrict__ T, const StepDe
 // c (K2.p_t + near partials (lags >= 3, written by launch t-1) + levels at target t+2)
 template <int NW, int DRN, bool GV = false>
 __device__ __forceinline__ void sfin_X(const ChTile* __restrict__ T, const StepDev* __restrict__ sd,
-                                       const StepArgs& ta, double* lds) {
+                                       const StepArgs& ta, double* lds, const XCheck& xc) {
   const int B = sd->B;
   const int64_t t = ta.t;
   const int par = (int)(t & 1), par1 = par ^ 1;  // target t+2 has parity par
@@ -1116,7 +1152,7 @@ __device__ __forceinline__ void sfin_X(const ChTile* __restrict__ T, const StepD
     pre[x] = lvs + sn;
   }
   run_products_rn<NW, DRN, GV>(T, t, lds);
-  __syncthreads();
+  if (xc.stop(sd, ta)) return;
   stamp(sd, 4, 2, ta);
 #pragma unroll
   for (int x = 0; x < EPT; ++x) {
@@ -1187,10 +1223,10 @@ __device__ __forceinline__ void sfin(const ChTile* __restrict__ T, const StepDev
 // near-field partial tile: rows [0, nrows) x columns [0, ncols) of the parity buffer of t + par_shift
 template <int NW, bool GV = false>
 __device__ __forceinline__ void raw(const ChTile* __restrict__ T, const StepDev* __restrict__ sd, const StepArgs& ta,
-                                    double* lds, int stage) {
+                                    double* lds, int stage, const XCheck& xc) {
   const int64_t t = ta.t;
   run_products<NW, GV>(T, t, lds);
-  __syncthreads();
+  if (xc.stop(sd, ta)) return;
   stamp(sd, stage, 2, ta);
   const int NT = 16 * T->rn;
   double* dst = T->dst + ((t + T->par_shift) & 1) * T->par_stride;
@@ -1304,43 +1340,42 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(DRN == 
       else if (i < NCP) sdw[i - NTW] = v[k];
     }
   }
+  XCheck xc;
   if constexpr (STAGE >= 4) {
-    // md.potforce cache audit of the previous step (StepArgs::xw): every workgroup reads the 2 B
-    // distance words and the stop word with its descriptor; a distance in (0, 1e-9) -- the reference
-    // reuses a force computed at another point -- or a set stop word leaves this launch without
-    // stores, and the launches after it (the host replays from step t - 1 on the two-launch path)
-    int nh0 = 0, nh1 = 0, st = 0;
+    // md.potforce cache audit of the previous step (XCheck): one word per thread, loaded now and
+    // looked at after the products
     if (ta.xw) {
-      const int n2 = 2 * ta.xB;
-      const int64_t wprev = ((ta.t + 2) % 3) * (int64_t)n2;
-      for (int i = threadIdx.x; i <= n2; i += NW * 64) {
-        const unsigned long long w = i < n2 ? *G(ta.xw + wprev + i) : *G(ta.xstop);
-        if (i == n2) st = w != 0ull;
-        else if (w != 0ull && word_hit(w)) (i < ta.xB ? nh0 : nh1) += 1;
-      }
-    }
-    if (__syncthreads_or((nh0 | nh1 | st) != 0)) {
-      const bool was = __syncthreads_or(st) != 0;
-      if (!was && blockIdx.x == 0) {  // the first stopping launch: count and publish the stop
-        const StepDev* sdl = (const StepDev*)sdw;
-        typedef __attribute__((address_space(1))) unsigned long long gull;
-        if (nh0) __hip_atomic_fetch_add((gull*)(sdl->guard + 0), (unsigned long long)nh0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (nh1) __hip_atomic_fetch_add((gull*)(sdl->guard + 1), (unsigned long long)nh1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (threadIdx.x == 0) {
-          const unsigned long long v = (unsigned long long)ta.t + 1ull;
-          __hip_atomic_store((gull*)ta.xstop, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(ta.xstop_host, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      xc.on = true;
+      xc.n2 = 2 * ta.xB;
+      if (xc.n2 + 1 <= NW * 64) {
+        if ((int)threadIdx.x <= xc.n2) {
+          xc.i = threadIdx.x;
+          xc.w = xc.i < xc.n2 ? *G(ta.xw + ((ta.t + 2) % 3) * (int64_t)xc.n2 + xc.i) : *G(ta.xstop);
         }
+      } else {  // more words than threads: decided here, before the products
+        int pred = 0;
+        for (int i = threadIdx.x; i <= xc.n2; i += NW * 64) {
+          const unsigned long long w = i < xc.n2 ? *G(ta.xw + ((ta.t + 2) % 3) * (int64_t)xc.n2 + i) : *G(ta.xstop);
+          if (i == xc.n2 ? w != 0ull : (w != 0ull && word_hit(w))) {
+            pred = 1;
+            if (i < xc.n2 || xc.i < 0) {
+              xc.i = i;
+              xc.w = w;
+            }
+          }
+        }
+        if (__syncthreads_or(pred)) {
+          __syncthreads();  // the descriptor copy (the stop path reads sd->guard)
+          if (xc.stop((const StepDev*)sdw, ta)) return;
+        }
+        xc.i = -1;  // nothing to stop: the later barrier is a plain one
       }
-      return;
+      if (blockIdx.x == 0) {  // slot (t + 1) mod 3 for launch t + 1 (read by launch t - 1)
+        for (int i = threadIdx.x; i < xc.n2; i += NW * 64) *G(ta.xw + ((ta.t + 1) % 3) * (int64_t)xc.n2 + i) = 0ull;
+      }
     }
-    if (ta.xw && blockIdx.x == 0) {  // slot (t + 1) mod 3 for launch t + 1 (read by launch t - 1)
-      const int n2 = 2 * ta.xB;
-      for (int i = threadIdx.x; i < n2; i += NW * 64) *G(ta.xw + ((ta.t + 1) % 3) * (int64_t)n2 + i) = 0ull;
-    }
-  } else {
-    __syncthreads();
   }
+  __syncthreads();
   const ChTile* T = (const ChTile*)tdw;
   sd = (const StepDev*)sdw;  // header only: bath[] is not copied (tiles carry their baths)
   const int kind = T->kind;
@@ -1355,12 +1390,12 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(DRN == 
     else if (STAGE == 1) dof_B<NW, DRN>(T, sd, ta, mode, lds);
     else if (STAGE == 2) dof_C<NW, DRN>(T, sd, ta, mode, lds);
     else if (STAGE == 3) dof_BC<NW, DRN>(T, sd, ta, mode, lds);
-    else dof_X<NW, DRN, GV>(T, sd, ta, lds);
+    else dof_X<NW, DRN, GV>(T, sd, ta, lds, xc);
   } else if (kind == CH_SFIN) {
-    if (STAGE >= 4) sfin_X<NW, DRN, GV>(T, sd, ta, lds);
+    if (STAGE >= 4) sfin_X<NW, DRN, GV>(T, sd, ta, lds, xc);
     else sfin<NW, DRN>(T, sd, ta, lds, STAGE);
   } else {
-    raw<NW, GV>(T, sd, ta, lds, STAGE);
+    raw<NW, GV>(T, sd, ta, lds, STAGE, xc);
   }
   stamp(sd, STAGE, 3, ta);
   if (ta.ts) {  // launch-uniform

@@ -440,8 +440,8 @@ void launch_hist_out(const double* src, int64_t ks, int64_t ss, int R, int64_t t
 void launch_cgemm(int rn, const CgItem* items, int nitems, int64_t tseg, hipStream_t s, int max_grid = 0,
                   unsigned long long* ts = nullptr);
 // nplanes: 2 (Re, Im: two-plane Gauss items) or 3 (the three Gauss planes, one item per part)
-void launch_khat_pack(const double* Kf, int ml, int nks_k, double* khat, int P, int m0, int M,
-                      int nc, int nrt2, int nks2, const double* cstab, int cstride, hipStream_t s, int nplanes);
+int launch_khat_pack(const double* Kf, int ml, int nks_k, double* khat, int P, int m0, int M,
+                     int nc, int nrt2, int nks2, const double* cstab, int cstride, hipStream_t s, int nplanes);
 // One bath's operands of a ladder level's transform launch: the baths of a piece go out as ONE
 // launch (blocks [blk0, next bath's blk0) are this bath's), not one launch per bath
 struct FftBath {

@@ -759,53 +759,6 @@ namespace gle {
 //   planes Re, Im (nplanes = 2: the two-plane Gauss items form Re + Im, Im - Re in registers) or as
 //   the three Gauss planes Re, Re + Im, Im - Re (nplanes = 3: one item per Gauss part), read
 //   straight out of the fragment-native K already on the device (one-time setup).
-__global__ void khat_pack_kernel(const double* __restrict__ Kf, int ml, int nks_k,
-                                 double* __restrict__ khat, int P, int m0, int M, int nc, int nrt2,
-                                 int nks2, const double2* __restrict__ cstab, int cstride, int nplanes) {
-  const int64_t total = (int64_t)(P + 1) * nrt2 * M * nks2 * 64;
-  const int64_t plane = (int64_t)nrt2 * M * nks2 * 64;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int lane = (int)(e & 63);
-    int64_t r_ = e >> 6;
-    const int ks2 = (int)(r_ % nks2);
-    r_ /= nks2;
-    const int mm = (int)(r_ % M);
-    r_ /= M;
-    const int rt2 = (int)(r_ % nrt2);
-    const int f = (int)(r_ / nrt2);
-    const int r = 16 * rt2 + (lane & 15);
-    const int k = 4 * ks2 + (lane >> 4);
-    double re = 0.0, im = 0.0;
-    if (r < nc && k < nc) {
-      const int64_t base = (((int64_t)(r >> 4) * nks_k + (k >> 2)) * ml) * 64 + (r & 15) + 16 * (k & 3);
-      const int m = mm + m0;
-      for (int ip = 0; ip < P; ++ip) {
-        const int i = m * P + ip;
-        if (i >= ml) break;
-        const double kv = Kf[base + (int64_t)i * 64];
-        const double2 cs = cstab[((f * ip) % (2 * P)) * cstride];
-        re += kv * cs.x;
-        im -= kv * cs.y;
-      }
-    }
-    const int64_t o = (int64_t)f * nplanes * plane + (((int64_t)rt2 * M + mm) * nks2 + ks2) * 64 + lane;
-    khat[o] = re;
-    if (nplanes == 2) {
-      khat[o + plane] = im;
-    } else {  // three Gauss planes Re, Re + Im, Im - Re
-      khat[o + plane] = re + im;
-      khat[o + 2 * plane] = im - re;
-    }
-  }
-}
-
-void launch_khat_pack(const double* Kf, int ml, int nks_k, double* khat, int P, int m0, int M,
-                      int nc, int nrt2, int nks2, const double* cstab, int cstride, hipStream_t s, int nplanes) {
-  khat_pack_kernel<<<8192, 256, 0, s>>>(Kf, ml, nks_k, khat, P, m0, M, nc, nrt2, nks2,
-                                        (const double2*)cstab, cstride, nplanes);
-}
-
 // In-place radix-2 FFT of NS complex series of length N = 2^logn held bit-reversed in LDS
 // (buf[s * N + i]); sign -1 = forward, +1 = inverse (unscaled).
 template <int NS>
@@ -1059,6 +1012,111 @@ static int fft_bc(int B, int P) {
   int bc = 64;
   while (bc > 8 && (bc > ((B + 7) / 8) * 8 || ((size_t)(bc / 2) * 2 * P + P) * 16 > 64 * 1024)) bc /= 2;
   return bc;
+}
+
+// K-hat of a spectral level (gle_api.hip freeze): for partition m = m0 + mm and frequency f <= P,
+//   Khat(f)[r][k] = sum_{ip < P} K_{m P + ip}[r][k] e^{-i pi f ip / P}
+// i.e. the 2P-point transform of the zero-padded P slices of every kernel element, written as the
+// planes Re, Im (nplanes 2) or the three Gauss planes Re, Re + Im, Im - Re (nplanes 3) in the
+// fragment-native layout [f][plane][rt][mm][ks][64].  A fragment's lane is the element's position in
+// the kernel's own fragment layout [rt][ks][i][64], so block (fragment, mm, lane chunk) streams the P
+// slices of BC lanes (BC doubles contiguous per slice) into LDS as BC/2 complex series (two real
+// series per complex FFT, bit-reversed), transforms them (lds_fft, radix 2) and separates the pairs:
+// O(P log P) per element instead of the O(P^2) direct sum (C5's P = 1024 level: 8.8 s of setup).
+template <int BC>
+__global__ __launch_bounds__(256) void khat_fft_kernel(const double* __restrict__ Kf, int ml, int nks_k,
+                                                       double* __restrict__ khat, int P, int logn, int m0, int M,
+                                                       int nc, int nrt2, int nks2, const double2* __restrict__ cstab,
+                                                       int cstride, int nplanes) {
+  extern __shared__ double2 fbuf[];  // BC/2 series of N = 2P points, then N/2 twiddles
+  const int N = 2 * P;
+  stage_twiddles(fbuf + (BC / 2) * N, N, cstab, cstride);
+  constexpr int NLC = 64 / BC;
+  int64_t blk = blockIdx.x;
+  const int lc = (int)(blk % NLC);
+  blk /= NLC;
+  const int mm = (int)(blk % M);
+  blk /= M;
+  const int ks2 = (int)(blk % nks2);
+  const int rt2 = (int)(blk / nks2);
+  const int l0 = lc * BC;
+  const int m = m0 + mm;
+  const double* __restrict__ src = Kf + ((int64_t)rt2 * nks_k + ks2) * ml * 64 + l0;
+  for (int e = threadIdx.x; e < N * (BC / 2); e += blockDim.x) {
+    const int q = e % (BC / 2);
+    const int n = e / (BC / 2);
+    const int i = m * P + n;
+    double xr = 0.0, xi = 0.0;
+    if (n < P && i < ml) {
+      const int la = 2 * q, lb = la + 1;
+      const int ra = 16 * rt2 + ((l0 + la) & 15), ka = 4 * ks2 + ((l0 + la) >> 4);
+      const int rb = 16 * rt2 + ((l0 + lb) & 15), kb = 4 * ks2 + ((l0 + lb) >> 4);
+      if (ra < nc && ka < nc) xr = src[(int64_t)i * 64 + la];
+      if (rb < nc && kb < nc) xi = src[(int64_t)i * 64 + lb];
+    }
+    const unsigned rev = __brev((unsigned)n) >> (32 - logn);
+    fbuf[q * N + rev] = make_double2(xr, xi);
+  }
+  __syncthreads();
+  lds_fft<BC / 2>(fbuf, logn, fbuf + (BC / 2) * N, -1.0);
+  const int64_t plane = (int64_t)nrt2 * M * nks2 * 64;
+  double* __restrict__ out = khat + (((int64_t)rt2 * M + mm) * nks2 + ks2) * 64 + l0;
+  for (int e = threadIdx.x; e < (P + 1) * BC; e += blockDim.x) {
+    const int l = e % BC;
+    const int f = e / BC;
+    const int q = l >> 1;
+    const double2 z = fbuf[q * N + f];
+    const double2 zc = fbuf[q * N + ((N - f) & (N - 1))];
+    // X_even = (Z[f] + conj Z[N-f]) / 2, X_odd = (Z[f] - conj Z[N-f]) / (2i)
+    double re, im;
+    if ((l & 1) == 0) {
+      re = 0.5 * (z.x + zc.x);
+      im = 0.5 * (z.y - zc.y);
+    } else {
+      re = 0.5 * (z.y + zc.y);
+      im = -0.5 * (z.x - zc.x);
+    }
+    double* o = out + (int64_t)f * nplanes * plane + l;
+    o[0] = re;
+    if (nplanes == 2) {
+      o[plane] = im;
+    } else {  // three Gauss planes Re, Re + Im, Im - Re
+      o[plane] = re + im;
+      o[2 * plane] = im - re;
+    }
+  }
+}
+
+template <int BC>
+static int khat_fft_launch(const double* Kf, int ml, int nks_k, double* khat, int P, int logn, int m0, int M,
+                           int nc, int nrt2, int nks2, const double* cstab, int cstride, hipStream_t s,
+                           int nplanes) {
+  const size_t shmem = ((size_t)(BC / 2) * 2 * P + P) * sizeof(double2);
+  if (shmem > 160 * 1024) return -2;
+  if (!lds_attr_once((const void*)khat_fft_kernel<BC>)) return -3;
+  const int64_t blocks = (int64_t)nrt2 * nks2 * M * (64 / BC);
+  if (blocks <= 0) return 0;
+  khat_fft_kernel<BC><<<(unsigned)blocks, 256, shmem, s>>>(Kf, ml, nks_k, khat, P, logn, m0, M, nc, nrt2, nks2,
+                                                           (const double2*)cstab, cstride, nplanes);
+  return 0;
+}
+
+int launch_khat_pack(const double* Kf, int ml, int nks_k, double* khat, int P, int m0, int M, int nc, int nrt2,
+                     int nks2, const double* cstab, int cstride, hipStream_t s, int nplanes) {
+  int logn = 0;
+  while ((1 << logn) < 2 * P) ++logn;
+  if ((1 << logn) != 2 * P) return -1;
+  // lanes per block: the most whose BC/2 series of 2P points (+ twiddles) fit 160 KiB of LDS
+  int bc = 64;
+  while (bc > 2 && ((size_t)(bc / 2) * 2 * P + P) * sizeof(double2) > 160 * 1024) bc /= 2;
+  switch (bc) {
+    case 64: return khat_fft_launch<64>(Kf, ml, nks_k, khat, P, logn, m0, M, nc, nrt2, nks2, cstab, cstride, s, nplanes);
+    case 32: return khat_fft_launch<32>(Kf, ml, nks_k, khat, P, logn, m0, M, nc, nrt2, nks2, cstab, cstride, s, nplanes);
+    case 16: return khat_fft_launch<16>(Kf, ml, nks_k, khat, P, logn, m0, M, nc, nrt2, nks2, cstab, cstride, s, nplanes);
+    case 8: return khat_fft_launch<8>(Kf, ml, nks_k, khat, P, logn, m0, M, nc, nrt2, nks2, cstab, cstride, s, nplanes);
+    case 4: return khat_fft_launch<4>(Kf, ml, nks_k, khat, P, logn, m0, M, nc, nrt2, nks2, cstab, cstride, s, nplanes);
+    default: return khat_fft_launch<2>(Kf, ml, nks_k, khat, P, logn, m0, M, nc, nrt2, nks2, cstab, cstride, s, nplanes);
+  }
 }
 
 template <int BC>
