@@ -153,14 +153,24 @@ class _BathBase:
         key = self._noise_key()
         if getattr(self, "_fac_key", None) != key:
             spec = self._spectrum()
-            if share is not None and share.world > 1 and spec.shape[-1] >= 64 and spec.shape[0] >= 64:
+            n, nc = spec.shape[0], spec.shape[1]
+            # frequencies whose matrix is exactly zero (above the cutoff: most of them) are not
+            # decomposed: eigenvalues 0 with unit eigenvectors, no vargau draw (noise.py:297-303) and a
+            # zero factor, what LAPACK returns for them (C3: 99 of 2049 frequencies are nonzero)
+            nz = np.flatnonzero(spec.reshape(n, -1).any(axis=1))
+            if share is not None and share.world > 1 and len(nz) >= 2 * share.world:
                 import hashlib
 
                 tag = "f%s" % hashlib.sha1(repr(key).encode()).hexdigest()[:16]
-                ev, vec = share.gather(tag, spec.shape[0], lambda lo, hi: _eigh_parts(spec[lo:hi]))
-                self._fac = _factor_from(ev, vec)
+                ev_nz, vec_nz = share.gather(tag, len(nz), lambda lo, hi: _eigh_parts(spec[nz[lo:hi]]))
             else:
-                self._fac = _eigh_stack(spec)
+                ev_nz, vec_nz = _eigh_parts(spec[nz])
+            ev = np.zeros((n, nc))
+            vec = np.zeros(spec.shape, dtype=np.result_type(spec.dtype, vec_nz.dtype))
+            vec[:] = np.eye(nc)
+            ev[nz] = ev_nz
+            vec[nz] = vec_nz
+            self._fac = _factor_from(ev, vec)
             self._fac_key = key
         return self._fac
 

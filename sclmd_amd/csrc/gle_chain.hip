@@ -330,7 +330,10 @@ struct XCheck {
   int i = -1;       // this thread's word (-1: none)
   int n2 = 0;       // 2 B
   bool on = false;  // a composed-step launch of gle_run
-  // the barrier after the products; true: the tile stores nothing
+  int* flags = nullptr;  // one LDS word per wave
+  // the barrier after the products; true: the tile stores nothing.  The vote is one wave ballot and
+  // one LDS word per wave around the barrier the products end with anyway (a workgroup reduction
+  // such as __syncthreads_or costs two more barriers in every workgroup of every step)
   __device__ bool stop(const StepDev* __restrict__ sd, const StepArgs& ta) const {
     if (!on) {
       __syncthreads();
@@ -339,7 +342,12 @@ struct XCheck {
     int pred = 0, st = 0;
     if (i == n2) st = w != 0ull;
     else if (i >= 0 && w != 0ull && word_hit(w)) pred = 1;
-    if (!__syncthreads_or(pred | st)) return false;
+    const int any = __any(pred | st);
+    if ((threadIdx.x & 63) == 0) flags[threadIdx.x >> 6] = any;
+    __syncthreads();
+    int vote = 0;
+    for (int v = 0; v < (int)(blockDim.x >> 6); ++v) vote |= flags[v];
+    if (!vote) return false;
     if (!__syncthreads_or(st) && blockIdx.x == 0) {  // the first stopping launch: count and publish
       typedef __attribute__((address_space(1))) unsigned long long gull;
       if (pred)
@@ -1341,6 +1349,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(DRN == 
     }
   }
   XCheck xc;
+  __shared__ int xflags[NW];
+  xc.flags = xflags;
   if constexpr (STAGE >= 4) {
     // md.potforce cache audit of the previous step (XCheck): one word per thread, loaded now and
     // looked at after the products

@@ -482,6 +482,22 @@ class md:
     # largest fixed-size variable of an MD{j}.nc file (NetCDF classic format, scipy.io)
     nc_var_limit = 2**31 - 4096
 
+    # device-mode baths whose spectrum is zero or one shared matrix at most of its frequencies (above
+    # the cutoff: C3's phonon baths have 99 dense frequencies of 2049) take the streamed path too, which
+    # factorises only the dense ones (the resident path decomposes, stores and uploads every frequency)
+    stream_sparse_spectra = True
+
+    def _sparse_spectrum(self, b):
+        if not self.stream_sparse_spectra:
+            return False
+        key = b._noise_key()
+        memo = getattr(b, "_sparse_memo", None)
+        if memo is None or memo[0] != key:
+            nfreq = int(self.nmd / 2) + 1
+            ndense = sum(1 for i in range(nfreq) if b._spectrum_term(i, matrix=False)[0] == "dense")
+            memo = b._sparse_memo = (key, 2 * ndense <= nfreq)
+        return memo[1]
+
     # the ranks of one node split each streamed bath's factorisations and exchange the factors through
     # node-local shared memory (noise.NodeShare) instead of each factorising the whole spectrum
     share_factors = True
@@ -514,7 +530,7 @@ class md:
         b = self.baths[i]
         nfreq = int(self.nmd / 2) + 1
         fac_bytes = nfreq * b.nc * b.nc * 8 * (2 if b.kind == "ebath" else 1)
-        if self.noise_mode == "device" and fac_bytes > self.noise_stream_bytes:
+        if self.noise_mode == "device" and (fac_bytes > self.noise_stream_bytes or self._sparse_spectrum(b)):
             # zero frequencies skipped, shared-matrix frequencies as one factor and scales, dense
             # factors computed once and kept for the following runs (only the draws change per run,
             # md.py:569-570): on the device when they fit there (the stepper replays them with new
