@@ -259,7 +259,7 @@ struct gle_handle {
   double *d_P2 = nullptr, *d_Q2 = nullptr;
   double* d_xfrag = nullptr;           // composed-operator DOF-tile fragments
   unsigned long long* d_guard = nullptr;
-  // md.potforce's cache rule on the composed path (StepArgs::xw): audit words [3][2][B], the device
+  // md.potforce's cache rule on the composed path (StepArgs::xw): audit words [3][ceil(B / 16)], the device
   // stop word and its host-mapped copy; a gle_run of composed steps leaves x_pend set until xresolve
   // has read the stop word (and replayed from the stop step on the two-launch path)
   unsigned long long *d_xw = nullptr, *d_xstop = nullptr, *h_xstop = nullptr, *d_xstop_h = nullptr;
@@ -268,6 +268,7 @@ struct gle_handle {
   int64_t x_replays = 0;               // composed runs stopped and replayed (gle_cache_audit)
   bool std_words_live = false;         // d_pmax holds the two-launch path's id0 distance of step t
   int64_t ret_cap = -1;                // retained streamed-noise factors: byte cap over all baths (< 0: none)
+  int x_rep = 1;                       // composed-step audit word replicas (StepArgs::xR)
   double* d_xslab = nullptr;           // split stage-4 DOF tiles: slabs and arrival counters
   unsigned long long* d_xcnt = nullptr;
   int64_t xslab_n = 0;
@@ -1965,8 +1966,9 @@ int plan_xstep(gle_handle* h) {
   const int64_t nph = h->nph, B = h->B;
   if (const char* e = gle_env("GLE_XSTEP"))
     if (atoi(e) == 0) return GLE_OK;
+  // B <= 1008: the audit words (ceil(B / 16)) and the stop word fit the lanes of one wave (XCheck)
   bool ok = h->fuse_bc && !h->bc_fpot && h->small_baths && !h->far_fused && h->P0 >= 2 && nb > 0 && nph <= 4096 &&
-            h->exp_one == 0;
+            h->exp_one == 0 && B <= 1008;
   for (const Bath& b : h->baths) ok = ok && !b.has_q && b.nc <= 512;
   if (!ok) return GLE_OK;
   const double dt = h->dt, hh = dt / 2.0, h2 = hh * hh, h3 = h2 * hh, dt22 = dt * dt / 2.0;
@@ -2073,7 +2075,8 @@ int plan_xstep(gle_handle* h) {
   rc = dalloc_n(h, &h->d_xfrag, frag.size());
   if (!rc) rc = upload(h, h->d_xfrag, frag.data(), frag.size() * 8);
   if (!rc) rc = dalloc_n(h, &h->d_guard, 2);
-  if (!rc) rc = dalloc_n(h, &h->d_xw, (size_t)6 * B);
+  h->x_rep = B <= 112 ? 8 : 1;  // audit replicas: 8 nw + 1 lanes of one wave (XCheck)
+  if (!rc) rc = dalloc_n(h, &h->d_xw, (size_t)3 * h->x_rep * ((B + 15) / 16) * 16);
   if (!rc) rc = dalloc_n(h, &h->d_xstop, 1);
   if (!rc && !h->h_xstop) {
     void* hp = nullptr;
@@ -3257,11 +3260,10 @@ int x_prime_buffers(gle_handle* h) {
   // audit words: zero, except that after a two-launch step the first composed launch audits that
   // step's id0 distance for step t (md.potforce's cache as the two-launch path left it: a distance in
   // (0, 1e-9) stops the composed run before it stores anything, and the two-launch path goes on)
-  const size_t nw = (size_t)2 * h->B;
-  HIPCHK(h, hipMemsetAsync(h->d_xw, 0, 3 * nw * sizeof(unsigned long long), h->stream));
+  const size_t nl = (size_t)((h->B + 15) / 16) * h->x_rep;  // words of a slot (16 doubles apart)
+  HIPCHK(h, hipMemsetAsync(h->d_xw, 0, 3 * nl * 16 * sizeof(unsigned long long), h->stream));
   if (h->std_words_live)
-    HIPCHK(h, hipMemcpyAsync(h->d_xw + ((h->t + 2) % 3) * nw + h->B, h->d_pmax + (h->t & 1) * h->B,
-                             (size_t)h->B * sizeof(unsigned long long), hipMemcpyDeviceToDevice, h->stream));
+    launch_xinject(h->d_pmax + (h->t & 1) * h->B, (int)h->B, h->d_xw + ((h->t + 2) % 3) * nl * 16, h->stream);
   h->x_live = true;
   return GLE_OK;
 }
@@ -3300,6 +3302,7 @@ int run_xstep(gle_handle* h, int64_t nsteps) {
     ta.xstop = h->d_xstop;
     ta.xstop_host = h->d_xstop_h;
     ta.xB = (int32_t)h->B;
+    ta.xR = h->x_rep;
     run_chain(h, xstage(h), h->chX[h->t & 1], ta, 0, h->levels.empty(), 0);
     h->std_stale = true;
     h->std_words_live = false;
@@ -3321,6 +3324,7 @@ int run_xstep(gle_handle* h, int64_t nsteps) {
     fa.guard = h->d_guard;
     fa.t = h->t;
     fa.B = (int32_t)h->B;
+    fa.R = h->x_rep;
     launch_xfinish(fa, h->stream);
   }
   h->x_pend = true;

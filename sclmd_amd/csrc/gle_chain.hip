@@ -318,41 +318,65 @@ __device__ __forceinline__ bool word_hit(unsigned long long w) {
   return m == m && m < 10e-10;
 }
 
-// md.potforce cache audit of the previous step in a composed-step launch (StepArgs::xw): thread i <=
-// 2B holds word i of the previous step's distances (i < 2B) or the stop word (i = 2B), loaded with
-// the tile descriptor and first looked at after the tile's products, at the barrier that ends them
-// (the load's latency hides behind the products).  A distance in (0, 1e-9) -- the reference reuses a
-// force computed at another point (md.py:449-450, 767-779) -- or a set stop word makes the tile
-// return before any store; the first stopping launch counts the trajectories and publishes the stop
-// (the host replays from step t - 1 on the two-launch path, gle_api.hip xresolve).
+// md.potforce cache audit of a composed-step launch (StepArgs::xw).  Per trajectory b, nibble b % 16
+// of word b / 16 of the step's audit slot collects, over the DOF tiles, bit 0: some tile's
+// max|q~ - q_t| > 0, bit 1: some tile's is >= 1e-9 (or NaN), bits 2 / 3: the same for max|q_{t+1} -
+// q~_t| -- so the step's maximum over all DOFs lies in (0, 1e-9), where md.potforce would reuse a force
+// computed at another point (md.py:449-450, 767-779), iff bit 0 and not bit 1 (or 2 and not 3).
+// Lanes 0 .. nw - 1 of wave 0 load the previous step's words and lane nw the stop word, with the tile
+// descriptor; they are looked at after the tile's products, at the barrier those end with (the
+// load's latency hides behind the products).  A hit or a set stop word makes a DOF tile return
+// before any store (its state, ring and recordings; the S and near tiles write only the composed
+// step's own buffers, which the replay rebuilds); the first stopping launch counts the trajectories
+// and publishes the stop (the host replays from step t - 1 on the two-launch path, gle_api.hip
+// xresolve).
+constexpr int XW_PAD = 16;  // audit words one 128-byte line apart
+__device__ __forceinline__ unsigned long long xw_hits(unsigned long long w) {
+  return w & ~(w >> 1) & 0x5555555555555555ull;  // bit 4j: d1 hit of trajectory j, bit 4j + 2: d0 hit
+}
+
 struct XCheck {
   unsigned long long w = 0ull;
-  int i = -1;       // this thread's word (-1: none)
-  int n2 = 0;       // 2 B
-  bool on = false;  // a composed-step launch of gle_run
-  int* flags = nullptr;  // one LDS word per wave
-  // the barrier after the products; true: the tile stores nothing.  The vote is one wave ballot and
-  // one LDS word per wave around the barrier the products end with anyway (a workgroup reduction
-  // such as __syncthreads_or costs two more barriers in every workgroup of every step)
+  int lane = -1;    // wave-0 lane holding a word: < nw nr word lane % nw of replica lane / nw, == nw nr
+                    // the stop word
+  int nw = 0;       // audit words (ceil(B / 16)) per replica
+  int nr = 1;       // replicas (StepArgs::xR)
+  bool on = false;  // a DOF tile of a composed-step launch of gle_run
+  int* flags = nullptr;  // LDS: wave 0's vote
+  // the barrier after the products; true: the tile stores nothing
   __device__ bool stop(const StepDev* __restrict__ sd, const StepArgs& ta) const {
     if (!on) {
       __syncthreads();
       return false;
     }
-    int pred = 0, st = 0;
-    if (i == n2) st = w != 0ull;
-    else if (i >= 0 && w != 0ull && word_hit(w)) pred = 1;
-    const int any = __any(pred | st);
-    if ((threadIdx.x & 63) == 0) flags[threadIdx.x >> 6] = any;
+    const int nl = nw * nr;
+    unsigned long long h = 0ull;
+    int st = 0;
+    if (threadIdx.x < 64) {
+      // lane j < nw: word j ORed over the replicas (lanes r nw + j), then its hits
+      unsigned long long x = 0ull;
+      for (int r = 0; r < nr; ++r) x |= __shfl(w, r * nw + ((int)threadIdx.x % max(nw, 1)));
+      h = (int)threadIdx.x < nw ? xw_hits(x) : 0ull;
+      st = (lane == nl && w != 0ull) ? 1 : 0;
+    }
+    if (threadIdx.x < 64) {
+      const int any = __any(h != 0ull || st);
+      const int was = __any(st);
+      if (threadIdx.x == 0) {
+        flags[0] = any;
+        flags[1] = was;
+      }
+    }
     __syncthreads();
-    int vote = 0;
-    for (int v = 0; v < (int)(blockDim.x >> 6); ++v) vote |= flags[v];
-    if (!vote) return false;
-    if (!__syncthreads_or(st) && blockIdx.x == 0) {  // the first stopping launch: count and publish
+    if (!flags[0]) return false;
+    if (!flags[1] && blockIdx.x == 0 && threadIdx.x < 64) {  // the first stopping launch: count, publish
       typedef __attribute__((address_space(1))) unsigned long long gull;
-      if (pred)
-        __hip_atomic_fetch_add((gull*)(sd->guard + (i < n2 / 2 ? 0 : 1)), 1ull, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+      if (h) {
+        __hip_atomic_fetch_add((gull*)(sd->guard + 0), (unsigned long long)__popcll(h & 0x1111111111111111ull),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add((gull*)(sd->guard + 1), (unsigned long long)__popcll(h & 0x4444444444444444ull),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       if (threadIdx.x == 0) {
         const unsigned long long v = (unsigned long long)ta.t + 1ull;
         __hip_atomic_store((gull*)ta.xstop, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1098,17 +1122,43 @@ __device__ __forceinline__ void dof_X(const ChTile* __restrict__ T, const StepDe
     static_assert((CH_TB + 3) * Geo::NT <= NW * 64, "one thread per column reduction");
     const int qn = threadIdx.x / Geo::NT, c = threadIdx.x % Geo::NT;
     const int b = T->c0 + c;
-    if (qn < CH_TB + 3 && b < B) {
+    if (qn <= CH_TB && b < B) {
       bool nan;
-      const double v = col_red<NW, DRN>(red, qn, c, qn > CH_TB, nan);
+      const double v = col_red<NW, DRN>(red, qn, c, false, nan);
       if (qn < CH_TB) {
         const int j = T->tb[qn].bath;
         if (j >= 0) prow[(int64_t)j * B + b] = v;
-      } else if (qn == CH_TB) {
+      } else {
         prow[(int64_t)nb * B + b] = v;
-      } else if (ta.xw) {
-        const unsigned long long bits = nan ? 0x7FF8000000000000ull : (unsigned long long)__double_as_longlong(v);
-        gmax(ta.xw + ((t % 3) * 2 + (qn - CH_TB - 1)) * (int64_t)B + b, bits);
+      }
+    }
+    if (ta.xw) {
+      // the two cache distances as audit nibbles (XCheck): the (quantity, column) threads of the two
+      // distances are lanes of one wave; OR over them, one atomic per audit word of the tile's columns
+      const int q0 = (CH_TB + 1) * Geo::NT;  // first thread of the distances (wave q0 / 64)
+      static_assert(((CH_TB + 1) * Geo::NT) / 64 == ((CH_TB + 3) * Geo::NT - 1) / 64, "one wave");
+      if ((int)threadIdx.x / 64 == q0 / 64) {
+        unsigned long long nib = 0ull;
+        if (qn > CH_TB && qn < CH_TB + 3 && b < B) {
+          bool nan;
+          const double v = col_red<NW, DRN>(red, qn, c, true, nan);
+          const unsigned long long m = (v > 0.0 ? 1ull : 0ull) | ((nan || !(v < 10e-10)) ? 2ull : 0ull);
+          nib = m << (4 * (b % 16) + 2 * (qn - CH_TB - 1));
+        }
+        typedef __attribute__((address_space(1))) unsigned long long gull;
+        const int lane = threadIdx.x & 63;
+        // replica tile % xR of the step's words, one 128-byte line per word: a word takes the atomics
+        // of ~ntile / xR tiles, not of all of them (one line for every tile's atomic measured +2 us/step)
+        const int nw = (B + 15) / 16;
+        gull* wrep = (gull*)(ta.xw + ((t % 3) * (int64_t)ta.xR + T->tile % ta.xR) * nw * XW_PAD);
+#pragma unroll
+        for (int j = 0; j < Geo::NT / 16; ++j) {  // the tile's columns c0 .. c0 + NT - 1: NT / 16 words
+          unsigned long long x = (c / 16 == j) ? nib : 0ull;
+#pragma unroll
+          for (int o = 1; o < 64; o <<= 1) x |= __shfl_xor(x, o);
+          if (lane == 0 && x != 0ull)
+            __hip_atomic_fetch_or(wrep + (T->c0 / 16 + j) * XW_PAD, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
     }
   }
@@ -1125,7 +1175,7 @@ __device__ __forceinline__ void dof_X(const ChTile* __restrict__ T, const StepDe
 // c (K2.p_t + near partials (lags >= 3, written by launch t-1) + levels at target t+2)
 template <int NW, int DRN, bool GV = false>
 __device__ __forceinline__ void sfin_X(const ChTile* __restrict__ T, const StepDev* __restrict__ sd,
-                                       const StepArgs& ta, double* lds, const XCheck& xc) {
+                                       const StepArgs& ta, double* lds) {
   const int B = sd->B;
   const int64_t t = ta.t;
   const int par = (int)(t & 1), par1 = par ^ 1;  // target t+2 has parity par
@@ -1160,7 +1210,7 @@ __device__ __forceinline__ void sfin_X(const ChTile* __restrict__ T, const StepD
     pre[x] = lvs + sn;
   }
   run_products_rn<NW, DRN, GV>(T, t, lds);
-  if (xc.stop(sd, ta)) return;
+  __syncthreads();  // (only DOF tiles audit: this tile writes the composed step's own buffers)
   stamp(sd, 4, 2, ta);
 #pragma unroll
   for (int x = 0; x < EPT; ++x) {
@@ -1231,10 +1281,10 @@ __device__ __forceinline__ void sfin(const ChTile* __restrict__ T, const StepDev
 // near-field partial tile: rows [0, nrows) x columns [0, ncols) of the parity buffer of t + par_shift
 template <int NW, bool GV = false>
 __device__ __forceinline__ void raw(const ChTile* __restrict__ T, const StepDev* __restrict__ sd, const StepArgs& ta,
-                                    double* lds, int stage, const XCheck& xc) {
+                                    double* lds, int stage) {
   const int64_t t = ta.t;
   run_products<NW, GV>(T, t, lds);
-  if (xc.stop(sd, ta)) return;
+  __syncthreads();
   stamp(sd, stage, 2, ta);
   const int NT = 16 * T->rn;
   double* dst = T->dst + ((t + T->par_shift) & 1) * T->par_stride;
@@ -1349,40 +1399,22 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(DRN == 
     }
   }
   XCheck xc;
-  __shared__ int xflags[NW];
+  __shared__ int xflags[2];
   xc.flags = xflags;
   if constexpr (STAGE >= 4) {
-    // md.potforce cache audit of the previous step (XCheck): one word per thread, loaded now and
-    // looked at after the products
+    // md.potforce cache audit of the previous step (XCheck), DOF tiles only: wave 0 loads the words
+    // now (the tile kind is in the descriptor being copied: every workgroup's wave 0 issues the loads,
+    // the non-DOF tiles ignore them)
     if (ta.xw) {
-      xc.on = true;
-      xc.n2 = 2 * ta.xB;
-      if (xc.n2 + 1 <= NW * 64) {
-        if ((int)threadIdx.x <= xc.n2) {
-          xc.i = threadIdx.x;
-          xc.w = xc.i < xc.n2 ? *G(ta.xw + ((ta.t + 2) % 3) * (int64_t)xc.n2 + xc.i) : *G(ta.xstop);
-        }
-      } else {  // more words than threads: decided here, before the products
-        int pred = 0;
-        for (int i = threadIdx.x; i <= xc.n2; i += NW * 64) {
-          const unsigned long long w = i < xc.n2 ? *G(ta.xw + ((ta.t + 2) % 3) * (int64_t)xc.n2 + i) : *G(ta.xstop);
-          if (i == xc.n2 ? w != 0ull : (w != 0ull && word_hit(w))) {
-            pred = 1;
-            if (i < xc.n2 || xc.i < 0) {
-              xc.i = i;
-              xc.w = w;
-            }
-          }
-        }
-        if (__syncthreads_or(pred)) {
-          __syncthreads();  // the descriptor copy (the stop path reads sd->guard)
-          if (xc.stop((const StepDev*)sdw, ta)) return;
-        }
-        xc.i = -1;  // nothing to stop: the later barrier is a plain one
+      xc.nw = (ta.xB + 15) / 16;
+      xc.nr = ta.xR;
+      const int nl = xc.nw * xc.nr;  // lane r nw + j: word j of replica r; lane nl: the stop word
+      if ((int)threadIdx.x <= nl) {
+        xc.lane = threadIdx.x;
+        xc.w = xc.lane < nl ? *G(ta.xw + (((ta.t + 2) % 3) * (int64_t)nl + xc.lane) * XW_PAD) : *G(ta.xstop);
       }
-      if (blockIdx.x == 0) {  // slot (t + 1) mod 3 for launch t + 1 (read by launch t - 1)
-        for (int i = threadIdx.x; i < xc.n2; i += NW * 64) *G(ta.xw + ((ta.t + 1) % 3) * (int64_t)xc.n2 + i) = 0ull;
-      }
+      if (blockIdx.x == 0 && (int)threadIdx.x < nl)  // slot (t + 1) mod 3 for launch t + 1 (read by t - 1)
+        *G(ta.xw + (((ta.t + 1) % 3) * (int64_t)nl + threadIdx.x) * XW_PAD) = 0ull;
     }
   }
   __syncthreads();
@@ -1400,12 +1432,15 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(DRN == 
     else if (STAGE == 1) dof_B<NW, DRN>(T, sd, ta, mode, lds);
     else if (STAGE == 2) dof_C<NW, DRN>(T, sd, ta, mode, lds);
     else if (STAGE == 3) dof_BC<NW, DRN>(T, sd, ta, mode, lds);
-    else dof_X<NW, DRN, GV>(T, sd, ta, lds, xc);
+    else {
+      xc.on = ta.xw != nullptr;
+      dof_X<NW, DRN, GV>(T, sd, ta, lds, xc);
+    }
   } else if (kind == CH_SFIN) {
-    if (STAGE >= 4) sfin_X<NW, DRN, GV>(T, sd, ta, lds, xc);
+    if (STAGE >= 4) sfin_X<NW, DRN, GV>(T, sd, ta, lds);
     else sfin<NW, DRN>(T, sd, ta, lds, STAGE);
   } else {
-    raw<NW, GV>(T, sd, ta, lds, STAGE, xc);
+    raw<NW, GV>(T, sd, ta, lds, STAGE);
   }
   stamp(sd, STAGE, 3, ta);
   if (ta.ts) {  // launch-uniform

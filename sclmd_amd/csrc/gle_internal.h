@@ -350,16 +350,18 @@ struct StepArgs {
   int32_t nstatic, nfar;
   FarRange far[MAXLVL];
   // composed step (stage 4/5) launches of gle_run, else nullptr: md.potforce's cache audit words
-  // xw [3][2][xB] (launch t reads slot (t - 1) mod 3, zeroes (t + 1) mod 3, writes t mod 3; index 0 =
-  // max |q~ - q_t| of the id1 call, 1 = max |q_{t+1} - q~_t| of the next id0 call) and the stop words:
-  // a launch that finds a distance in (0, 1e-9) -- where md.potforce would reuse a force at another
-  // point (md.py:449-450, 767-779) -- or a set xstop stores nothing; the first such launch sets
-  // *xstop = *xstop_host = t + 1 (device word / host-mapped word), and the host replays from step
-  // t - 1 on the two-launch path, which applies the cache rule (gle_api.hip xresolve)
+  // xw [3][xR][ceil(xB / 16)], each word padded to 128 bytes (launch t reads slot (t - 1) mod 3, zeroes
+  // (t + 1) mod 3, writes t mod 3;
+  // per trajectory a nibble of bits "some DOF tile's distance > 0 / >= 1e-9" for max |q~ - q_t| (id1
+  // call) and max |q_{t+1} - q~_t| (next id0 call), XCheck in gle_chain.hip) and the stop words: a
+  // launch that finds a distance in (0, 1e-9) -- where md.potforce would reuse a force at another
+  // point (md.py:449-450, 767-779) -- or a set xstop stores nothing from its DOF tiles; the first such
+  // launch sets *xstop = *xstop_host = t + 1 (device word / host-mapped word), and the host replays
+  // from step t - 1 on the two-launch path, which applies the cache rule (gle_api.hip xresolve)
   unsigned long long* xw;
   unsigned long long* xstop;
   unsigned long long* xstop_host;
-  int32_t xB, xpad;
+  int32_t xB, xR;  // trajectories; replicas of a slot's words (DOF tile % xR writes replica tile % xR)
 };
 void launch_contract(int rn, int cu, const CItem* items, int nitems, StepArgs ta, hipStream_t s);
 void launch_reduce(const RItem* items, int nitems, int max_elems, StepArgs ta,
@@ -415,9 +417,12 @@ struct XFinishArgs {
   int64_t n;  // doubles per state array to move (0: even t, audit only)
   unsigned long long *xw, *xstop, *xstop_host, *guard;
   int64_t t;
-  int32_t B, pad;
+  int32_t B, R;  // trajectories, audit replicas (StepArgs::xR)
 };
 void launch_xfinish(const XFinishArgs& a, hipStream_t s);
+// the two-launch path's id0 distances of step t (pmax words of B trajectories) into replica 0 of the
+// audit slot of step t - 1 (composed-step entry, x_prime_buffers); words XW_PAD doubles apart
+void launch_xinject(const unsigned long long* pw, int B, unsigned long long* slot, hipStream_t s);
 void launch_philox_normal(double* x, int64_t nfreq, int64_t ncp, int64_t nc, int64_t B,
                           uint64_t seed, uint64_t traj_offset, hipStream_t s, int64_t w_off = 0);
 // streamed noise: a[w0 + w][row_off + r][b] = wscale[w] sum_k M[w][r][k] x[w][k][b] for w < nw (M of

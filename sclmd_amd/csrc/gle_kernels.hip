@@ -638,23 +638,32 @@ void launch_xprime(const XPrimeArgs& a, hipStream_t s) {
   xprime_kernel<<<(unsigned)std::min<int64_t>((n + 255) / 256, 4096), 256, 0, s>>>(a);
 }
 
-// md.potforce cache audit of the run's last step (the chain kernel's stage-4 prologue, gle_chain.hip)
-// in every workgroup, then the state copy unless the run stopped
+// md.potforce cache audit of the run's last step (XCheck in gle_chain.hip: word b / 16, nibble b % 16,
+// bit 0 / 1 and 2 / 3: some DOF tile's distance > 0 / >= 1e-9) in every workgroup, then the state
+// copy unless the run stopped
 __global__ __launch_bounds__(256) void xfinish_kernel(XFinishArgs a) {
   typedef __attribute__((address_space(1))) unsigned long long gull;
-  const int n2 = 2 * a.B;
-  const unsigned long long* wp = a.xw + ((a.t + 2) % 3) * (int64_t)n2;
-  int nh0 = 0, nh1 = 0, st = 0;
-  for (int i = threadIdx.x; i <= n2; i += 256) {
-    const unsigned long long w = i < n2 ? wp[i] : *a.xstop;
-    const double m = __longlong_as_double((long long)w);
-    if (i == n2) st = w != 0ull;
-    else if (w != 0ull && m == m && m < 10e-10) (i < a.B ? nh0 : nh1) += 1;  // sameq, md.py:767-779
+  const int nw = (a.B + 15) / 16;
+  const unsigned long long* wp = a.xw + ((a.t + 2) % 3) * (int64_t)nw * a.R * 16;  // words 16 doubles apart
+  unsigned long long h = 0ull;
+  int st = 0;
+  for (int j = threadIdx.x; j <= nw; j += 256) {
+    if (j == nw) {
+      st = *a.xstop != 0ull;
+    } else {
+      unsigned long long w = 0ull;
+      for (int r = 0; r < a.R; ++r) w |= wp[((int64_t)r * nw + j) * 16];
+      h |= w & ~(w >> 1) & 0x5555555555555555ull;  // sameq hits (md.py:767-779)
+    }
   }
-  if (__syncthreads_or((nh0 | nh1 | st) != 0)) {
+  if (__syncthreads_or(h != 0ull || st)) {
     if (!__syncthreads_or(st) && blockIdx.x == 0) {
-      if (nh0) __hip_atomic_fetch_add((gull*)(a.guard + 0), (unsigned long long)nh0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (nh1) __hip_atomic_fetch_add((gull*)(a.guard + 1), (unsigned long long)nh1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (h) {
+        __hip_atomic_fetch_add((gull*)(a.guard + 0), (unsigned long long)__popcll(h & 0x1111111111111111ull),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add((gull*)(a.guard + 1), (unsigned long long)__popcll(h & 0x4444444444444444ull),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       if (threadIdx.x == 0) {
         const unsigned long long v = (unsigned long long)a.t + 1ull;
         __hip_atomic_store((gull*)a.xstop, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -667,6 +676,25 @@ __global__ __launch_bounds__(256) void xfinish_kernel(XFinishArgs a) {
     a.P[e] = a.P2[e];
     a.Q[e] = a.Q2[e];
   }
+}
+
+// the two-launch path's id0 distance of step t (pmax word per trajectory, a maximum) as the d0 bits
+// of the audit nibbles (bits 2 / 3: > 0 / >= 1e-9 or NaN) of slot (t - 1) mod 3
+__global__ void xinject_kernel(const unsigned long long* __restrict__ pw, int B, unsigned long long* __restrict__ slot) {
+  const int nw = (B + 15) / 16;
+  for (int j = threadIdx.x; j < nw; j += blockDim.x) {
+    unsigned long long x = 0ull;
+    for (int b = 16 * j; b < min(B, 16 * j + 16); ++b) {
+      const double m = __longlong_as_double((long long)pw[b]);
+      const unsigned long long bits = (m > 0.0 ? 1ull : 0ull) | (!(m < 10e-10) ? 2ull : 0ull);
+      x |= bits << (4 * (b % 16) + 2);
+    }
+    slot[(int64_t)j * 16] = x;
+  }
+}
+
+void launch_xinject(const unsigned long long* pw, int B, unsigned long long* slot, hipStream_t s) {
+  xinject_kernel<<<1, 64, 0, s>>>(pw, B, slot);
 }
 
 void launch_xfinish(const XFinishArgs& a, hipStream_t s) {
