@@ -52,6 +52,7 @@ struct Chain {
   double flops = 0;  // algorithmic flops of the launch's products
   int nw = 4;        // waves per workgroup
   size_t lds = 0;    // dynamic LDS bytes per workgroup
+  int ndof = 0;      // leading DOF tiles (upload_chain)
 };
 
 struct Bath {
@@ -1124,6 +1125,12 @@ int upload_chain(gle_handle* h, Chain& c) {
   if (c.tiles.empty()) return GLE_OK;
   lpt_order(h, c);
   xcd_order(h, c);
+  // DOF tiles first (plan order): the composed step's audit words are read by them alone; any other
+  // order (experiment tile orders) makes every workgroup read them
+  int nd = 0, ndof = 0;
+  while (nd < (int)c.tiles.size() && c.tiles[nd].kind == CH_DOF) ++nd;
+  for (const ChTile& T : c.tiles) ndof += T.kind == CH_DOF ? 1 : 0;
+  c.ndof = nd == ndof ? nd : (int)c.tiles.size();
   int rc = dalloc_n(h, &c.d, c.tiles.size());
   if (!rc) rc = upload(h, c.d, c.tiles.data(), c.tiles.size() * sizeof(ChTile));
   return rc;
@@ -2076,7 +2083,7 @@ int plan_xstep(gle_handle* h) {
   if (!rc) rc = upload(h, h->d_xfrag, frag.data(), frag.size() * 8);
   if (!rc) rc = dalloc_n(h, &h->d_guard, 2);
   h->x_rep = B <= 112 ? 8 : 1;  // audit replicas: 8 nw + 1 lanes of one wave (XCheck)
-  if (!rc) rc = dalloc_n(h, &h->d_xw, (size_t)3 * h->x_rep * ((B + 15) / 16) * 16);
+  if (!rc) rc = dalloc_n(h, &h->d_xw, (size_t)3 * h->x_rep * ((B + 15) / 16));
   if (!rc) rc = dalloc_n(h, &h->d_xstop, 1);
   if (!rc && !h->h_xstop) {
     void* hp = nullptr;
@@ -3260,10 +3267,10 @@ int x_prime_buffers(gle_handle* h) {
   // audit words: zero, except that after a two-launch step the first composed launch audits that
   // step's id0 distance for step t (md.potforce's cache as the two-launch path left it: a distance in
   // (0, 1e-9) stops the composed run before it stores anything, and the two-launch path goes on)
-  const size_t nl = (size_t)((h->B + 15) / 16) * h->x_rep;  // words of a slot (16 doubles apart)
-  HIPCHK(h, hipMemsetAsync(h->d_xw, 0, 3 * nl * 16 * sizeof(unsigned long long), h->stream));
+  const size_t nl = (size_t)((h->B + 15) / 16) * h->x_rep;  // words of a slot
+  HIPCHK(h, hipMemsetAsync(h->d_xw, 0, 3 * nl * sizeof(unsigned long long), h->stream));
   if (h->std_words_live)
-    launch_xinject(h->d_pmax + (h->t & 1) * h->B, (int)h->B, h->d_xw + ((h->t + 2) % 3) * nl * 16, h->stream);
+    launch_xinject(h->d_pmax + (h->t & 1) * h->B, (int)h->B, h->d_xw + ((h->t + 2) % 3) * nl, h->stream);
   h->x_live = true;
   return GLE_OK;
 }
@@ -3303,6 +3310,7 @@ int run_xstep(gle_handle* h, int64_t nsteps) {
     ta.xstop_host = h->d_xstop_h;
     ta.xB = (int32_t)h->B;
     ta.xR = h->x_rep;
+    ta.xndof = h->chX[h->t & 1].ndof;
     run_chain(h, xstage(h), h->chX[h->t & 1], ta, 0, h->levels.empty(), 0);
     h->std_stale = true;
     h->std_words_live = false;

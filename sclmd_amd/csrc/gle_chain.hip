@@ -330,7 +330,6 @@ __device__ __forceinline__ bool word_hit(unsigned long long w) {
 // step's own buffers, which the replay rebuilds); the first stopping launch counts the trajectories
 // and publishes the stop (the host replays from step t - 1 on the two-launch path, gle_api.hip
 // xresolve).
-constexpr int XW_PAD = 16;  // audit words one 128-byte line apart
 __device__ __forceinline__ unsigned long long xw_hits(unsigned long long w) {
   return w & ~(w >> 1) & 0x5555555555555555ull;  // bit 4j: d1 hit of trajectory j, bit 4j + 2: d0 hit
 }
@@ -345,6 +344,10 @@ struct XCheck {
   int* flags = nullptr;  // LDS: wave 0's vote
   // the barrier after the products; true: the tile stores nothing
   __device__ bool stop(const StepDev* __restrict__ sd, const StepArgs& ta) const {
+#if defined(XC_DBG) && (XC_DBG & 1)  // timing diagnostics only: no vote
+    __syncthreads();
+    return false;
+#endif
     if (!on) {
       __syncthreads();
       return false;
@@ -1132,7 +1135,11 @@ __device__ __forceinline__ void dof_X(const ChTile* __restrict__ T, const StepDe
         prow[(int64_t)nb * B + b] = v;
       }
     }
+#if defined(XC_DBG) && (XC_DBG & 2)  // timing diagnostics only: no audit words written
+    if (false) {
+#else
     if (ta.xw) {
+#endif
       // the two cache distances as audit nibbles (XCheck): the (quantity, column) threads of the two
       // distances are lanes of one wave; OR over them, one atomic per audit word of the tile's columns
       const int q0 = (CH_TB + 1) * Geo::NT;  // first thread of the distances (wave q0 / 64)
@@ -1147,17 +1154,17 @@ __device__ __forceinline__ void dof_X(const ChTile* __restrict__ T, const StepDe
         }
         typedef __attribute__((address_space(1))) unsigned long long gull;
         const int lane = threadIdx.x & 63;
-        // replica tile % xR of the step's words, one 128-byte line per word: a word takes the atomics
-        // of ~ntile / xR tiles, not of all of them (one line for every tile's atomic measured +2 us/step)
+        // replica tile % xR of the step's words: a word takes the atomics of ~ntile / xR tiles (one word
+        // line for every tile's atomic measured +2 us/step at C3)
         const int nw = (B + 15) / 16;
-        gull* wrep = (gull*)(ta.xw + ((t % 3) * (int64_t)ta.xR + T->tile % ta.xR) * nw * XW_PAD);
+        gull* wrep = (gull*)(ta.xw + ((t % 3) * (int64_t)ta.xR + T->tile % ta.xR) * nw);
 #pragma unroll
         for (int j = 0; j < Geo::NT / 16; ++j) {  // the tile's columns c0 .. c0 + NT - 1: NT / 16 words
           unsigned long long x = (c / 16 == j) ? nib : 0ull;
 #pragma unroll
           for (int o = 1; o < 64; o <<= 1) x |= __shfl_xor(x, o);
           if (lane == 0 && x != 0ull)
-            __hip_atomic_fetch_or(wrep + (T->c0 / 16 + j) * XW_PAD, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_or(wrep + (T->c0 / 16 + j), x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
     }
@@ -1409,12 +1416,16 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(DRN == 
       xc.nw = (ta.xB + 15) / 16;
       xc.nr = ta.xR;
       const int nl = xc.nw * xc.nr;  // lane r nw + j: word j of replica r; lane nl: the stop word
-      if ((int)threadIdx.x <= nl) {
+#if defined(XC_DBG) && (XC_DBG & 4)  // timing diagnostics only: no audit loads
+      if (false) {
+#else
+      if ((int)blockIdx.x < ta.xndof && (int)threadIdx.x <= nl) {  // DOF tiles only (the first xndof)
+#endif
         xc.lane = threadIdx.x;
-        xc.w = xc.lane < nl ? *G(ta.xw + (((ta.t + 2) % 3) * (int64_t)nl + xc.lane) * XW_PAD) : *G(ta.xstop);
+        xc.w = xc.lane < nl ? *G(ta.xw + ((ta.t + 2) % 3) * (int64_t)nl + xc.lane) : *G(ta.xstop);
       }
       if (blockIdx.x == 0 && (int)threadIdx.x < nl)  // slot (t + 1) mod 3 for launch t + 1 (read by t - 1)
-        *G(ta.xw + (((ta.t + 1) % 3) * (int64_t)nl + threadIdx.x) * XW_PAD) = 0ull;
+        *G(ta.xw + ((ta.t + 1) % 3) * (int64_t)nl + threadIdx.x) = 0ull;
     }
   }
   __syncthreads();

@@ -350,7 +350,7 @@ struct StepArgs {
   int32_t nstatic, nfar;
   FarRange far[MAXLVL];
   // composed step (stage 4/5) launches of gle_run, else nullptr: md.potforce's cache audit words
-  // xw [3][xR][ceil(xB / 16)], each word padded to 128 bytes (launch t reads slot (t - 1) mod 3, zeroes
+  // xw [3][xR][ceil(xB / 16)] (launch t reads slot (t - 1) mod 3, zeroes
   // (t + 1) mod 3, writes t mod 3;
   // per trajectory a nibble of bits "some DOF tile's distance > 0 / >= 1e-9" for max |q~ - q_t| (id1
   // call) and max |q_{t+1} - q~_t| (next id0 call), XCheck in gle_chain.hip) and the stop words: a
@@ -362,6 +362,8 @@ struct StepArgs {
   unsigned long long* xstop;
   unsigned long long* xstop_host;
   int32_t xB, xR;  // trajectories; replicas of a slot's words (DOF tile % xR writes replica tile % xR)
+  int32_t xndof;   // the launch's DOF tiles are its first xndof workgroups (they alone read the words)
+  int32_t xpad;
 };
 void launch_contract(int rn, int cu, const CItem* items, int nitems, StepArgs ta, hipStream_t s);
 void launch_reduce(const RItem* items, int nitems, int max_elems, StepArgs ta,
@@ -421,7 +423,7 @@ struct XFinishArgs {
 };
 void launch_xfinish(const XFinishArgs& a, hipStream_t s);
 // the two-launch path's id0 distances of step t (pmax words of B trajectories) into replica 0 of the
-// audit slot of step t - 1 (composed-step entry, x_prime_buffers); words XW_PAD doubles apart
+// audit slot of step t - 1 (composed-step entry, x_prime_buffers)
 void launch_xinject(const unsigned long long* pw, int B, unsigned long long* slot, hipStream_t s);
 void launch_philox_normal(double* x, int64_t nfreq, int64_t ncp, int64_t nc, int64_t B,
                           uint64_t seed, uint64_t traj_offset, hipStream_t s, int64_t w_off = 0);

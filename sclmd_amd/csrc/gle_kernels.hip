@@ -644,7 +644,7 @@ void launch_xprime(const XPrimeArgs& a, hipStream_t s) {
 __global__ __launch_bounds__(256) void xfinish_kernel(XFinishArgs a) {
   typedef __attribute__((address_space(1))) unsigned long long gull;
   const int nw = (a.B + 15) / 16;
-  const unsigned long long* wp = a.xw + ((a.t + 2) % 3) * (int64_t)nw * a.R * 16;  // words 16 doubles apart
+  const unsigned long long* wp = a.xw + ((a.t + 2) % 3) * (int64_t)nw * a.R;
   unsigned long long h = 0ull;
   int st = 0;
   for (int j = threadIdx.x; j <= nw; j += 256) {
@@ -652,7 +652,7 @@ __global__ __launch_bounds__(256) void xfinish_kernel(XFinishArgs a) {
       st = *a.xstop != 0ull;
     } else {
       unsigned long long w = 0ull;
-      for (int r = 0; r < a.R; ++r) w |= wp[((int64_t)r * nw + j) * 16];
+      for (int r = 0; r < a.R; ++r) w |= wp[(int64_t)r * nw + j];
       h |= w & ~(w >> 1) & 0x5555555555555555ull;  // sameq hits (md.py:767-779)
     }
   }
@@ -689,7 +689,7 @@ __global__ void xinject_kernel(const unsigned long long* __restrict__ pw, int B,
       const unsigned long long bits = (m > 0.0 ? 1ull : 0ull) | (!(m < 10e-10) ? 2ull : 0ull);
       x |= bits << (4 * (b % 16) + 2);
     }
-    slot[(int64_t)j * 16] = x;
+    slot[j] = x;
   }
 }
 
