@@ -126,9 +126,97 @@ __device__ __forceinline__ void stamp(const StepDev* __restrict__ sd, int stage,
 #ifndef CH_NA
 #define CH_NA 1
 #endif
+// md.potforce cache audit of a composed-step launch (StepArgs::xw).  Per trajectory b, nibble b % 16
+// of word b / 16 of the step's audit slot collects, over the DOF tiles, bit 0: some tile's
+// max|q~ - q_t| > 0, bit 1: some tile's is >= 1e-9 (or NaN), bits 2 / 3: the same for max|q_{t+1} -
+// q~_t| -- so the step's maximum over all DOFs lies in (0, 1e-9), where md.potforce would reuse a force
+// computed at another point (md.py:449-450, 767-779), iff bit 0 and not bit 1 (or 2 and not 3).
+// Lanes 0 .. nw - 1 of wave 0 load the previous step's words and lane nw the stop word, with the tile
+// descriptor; they are looked at after the tile's products, at the barrier those end with (the
+// load's latency hides behind the products).  A hit or a set stop word makes a DOF tile return
+// before any store (its state, ring and recordings; the S and near tiles write only the composed
+// step's own buffers, which the replay rebuilds); the first stopping launch counts the trajectories
+// and publishes the stop (the host replays from step t - 1 on the two-launch path, gle_api.hip
+// xresolve).
+__device__ __forceinline__ unsigned long long xw_hits(unsigned long long w) {
+  return w & ~(w >> 1) & 0x5555555555555555ull;  // bit 4j: d1 hit of trajectory j, bit 4j + 2: d0 hit
+}
+
+// XC_LATE (default): wave 0 issues the loads after its first operand batch's loads (in products), so
+// the products' first wait does not include them (issued with the descriptor they cost ~0.7 us/step
+// at C3, profiles/r06/ab7)
+#ifndef XC_LATE
+#define XC_LATE 1
+#endif
+struct XCheck {
+  unsigned long long w = 0ull;
+  const unsigned long long* src = nullptr;   // the slot's words (late load), the stop word after them
+  const unsigned long long* stopw = nullptr;
+  bool pending = false;  // the late load is still to be issued
+  int lane = -1;    // wave-0 lane holding a word: < nw nr word lane % nw of replica lane / nw, == nw nr
+                    // the stop word
+  int nw = 0;       // audit words (ceil(B / 16)) per replica
+  int nr = 1;       // replicas (StepArgs::xR)
+  bool on = false;  // a DOF tile of a composed-step launch of gle_run
+  int* flags = nullptr;  // LDS: wave 0's vote
+  // the barrier after the products; true: the tile stores nothing
+  __device__ void load() {  // wave 0
+    if (!pending) return;
+    pending = false;
+    const int nl = nw * nr;
+    if (lane >= 0) w = lane < nl ? *G(src + lane) : *G(stopw);
+  }
+  __device__ bool stop(const StepDev* __restrict__ sd, const StepArgs& ta) {
+#if defined(XC_DBG) && (XC_DBG & 1)  // timing diagnostics only: no vote
+    __syncthreads();
+    return false;
+#endif
+    if (!on) {
+      __syncthreads();
+      return false;
+    }
+    if (threadIdx.x < 64) load();  // (a wave 0 without products)
+    const int nl = nw * nr;
+    unsigned long long h = 0ull;
+    int st = 0;
+    if (threadIdx.x < 64) {
+      // lane j < nw: word j ORed over the replicas (lanes r nw + j), then its hits
+      unsigned long long x = 0ull;
+      for (int r = 0; r < nr; ++r) x |= __shfl(w, r * nw + ((int)threadIdx.x % max(nw, 1)));
+      h = (int)threadIdx.x < nw ? xw_hits(x) : 0ull;
+      st = (lane == nl && w != 0ull) ? 1 : 0;
+    }
+    if (threadIdx.x < 64) {
+      const int any = __any(h != 0ull || st);
+      const int was = __any(st);
+      if (threadIdx.x == 0) {
+        flags[0] = any;
+        flags[1] = was;
+      }
+    }
+    __syncthreads();
+    if (!flags[0]) return false;
+    if (!flags[1] && blockIdx.x == 0 && threadIdx.x < 64) {  // the first stopping launch: count, publish
+      typedef __attribute__((address_space(1))) unsigned long long gull;
+      if (h) {
+        __hip_atomic_fetch_add((gull*)(sd->guard + 0), (unsigned long long)__popcll(h & 0x1111111111111111ull),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add((gull*)(sd->guard + 1), (unsigned long long)__popcll(h & 0x4444444444444444ull),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (threadIdx.x == 0) {
+        const unsigned long long v = (unsigned long long)ta.t + 1ull;
+        __hip_atomic_store((gull*)ta.xstop, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ta.xstop_host, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    return true;
+  }
+};
+
 template <int RN, int NW, bool GEMV = false>
 __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave, int lane, int64_t t,
-                                         double* lds, int skip) {
+                                         double* lds, int skip, XCheck* xl = nullptr) {
   // GEMV (one-trajectory plans, chain stage 5 = stage 4 at B = 1): a 16x16x4 MFMA would use 1 of its
   // 16 columns; each lane instead multiplies its own A element by the X value of its k row on the VALU
   static_assert(!GEMV || RN == 1, "GEMV tiles have one column tile");
@@ -245,6 +333,7 @@ __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave,
       (void)b1;
       for (int s0 = 0; s0 < nks; s0 += U) {
         fetch(s0, a0, b0);
+        if (xl != nullptr && wave == 0) xl->load();  // the audit words behind the first batch (XC_LATE)
         compute(s0, a0, b0);
       }
     }
@@ -256,10 +345,11 @@ __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave,
 // so the 64-column near-field variant is not instantiated beside the DOF prologue's live values
 // (it made the register allocator spill the DOF stages)
 template <int NW, int RN, bool GV = false>
-__device__ __forceinline__ void run_products_rn(const ChTile* __restrict__ T, int64_t t, double* lds, int skip = 0) {
+__device__ __forceinline__ void run_products_rn(const ChTile* __restrict__ T, int64_t t, double* lds, int skip = 0,
+                                                XCheck* xl = nullptr) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  products<RN, NW, GV && RN == 1>(T, wave, lane, t, lds, skip);
+  products<RN, NW, GV && RN == 1>(T, wave, lane, t, lds, skip, xl);
 }
 
 template <int NW, bool GV = false>
@@ -317,78 +407,6 @@ __device__ __forceinline__ bool word_hit(unsigned long long w) {
   const double m = __longlong_as_double((long long)w);
   return m == m && m < 10e-10;
 }
-
-// md.potforce cache audit of a composed-step launch (StepArgs::xw).  Per trajectory b, nibble b % 16
-// of word b / 16 of the step's audit slot collects, over the DOF tiles, bit 0: some tile's
-// max|q~ - q_t| > 0, bit 1: some tile's is >= 1e-9 (or NaN), bits 2 / 3: the same for max|q_{t+1} -
-// q~_t| -- so the step's maximum over all DOFs lies in (0, 1e-9), where md.potforce would reuse a force
-// computed at another point (md.py:449-450, 767-779), iff bit 0 and not bit 1 (or 2 and not 3).
-// Lanes 0 .. nw - 1 of wave 0 load the previous step's words and lane nw the stop word, with the tile
-// descriptor; they are looked at after the tile's products, at the barrier those end with (the
-// load's latency hides behind the products).  A hit or a set stop word makes a DOF tile return
-// before any store (its state, ring and recordings; the S and near tiles write only the composed
-// step's own buffers, which the replay rebuilds); the first stopping launch counts the trajectories
-// and publishes the stop (the host replays from step t - 1 on the two-launch path, gle_api.hip
-// xresolve).
-__device__ __forceinline__ unsigned long long xw_hits(unsigned long long w) {
-  return w & ~(w >> 1) & 0x5555555555555555ull;  // bit 4j: d1 hit of trajectory j, bit 4j + 2: d0 hit
-}
-
-struct XCheck {
-  unsigned long long w = 0ull;
-  int lane = -1;    // wave-0 lane holding a word: < nw nr word lane % nw of replica lane / nw, == nw nr
-                    // the stop word
-  int nw = 0;       // audit words (ceil(B / 16)) per replica
-  int nr = 1;       // replicas (StepArgs::xR)
-  bool on = false;  // a DOF tile of a composed-step launch of gle_run
-  int* flags = nullptr;  // LDS: wave 0's vote
-  // the barrier after the products; true: the tile stores nothing
-  __device__ bool stop(const StepDev* __restrict__ sd, const StepArgs& ta) const {
-#if defined(XC_DBG) && (XC_DBG & 1)  // timing diagnostics only: no vote
-    __syncthreads();
-    return false;
-#endif
-    if (!on) {
-      __syncthreads();
-      return false;
-    }
-    const int nl = nw * nr;
-    unsigned long long h = 0ull;
-    int st = 0;
-    if (threadIdx.x < 64) {
-      // lane j < nw: word j ORed over the replicas (lanes r nw + j), then its hits
-      unsigned long long x = 0ull;
-      for (int r = 0; r < nr; ++r) x |= __shfl(w, r * nw + ((int)threadIdx.x % max(nw, 1)));
-      h = (int)threadIdx.x < nw ? xw_hits(x) : 0ull;
-      st = (lane == nl && w != 0ull) ? 1 : 0;
-    }
-    if (threadIdx.x < 64) {
-      const int any = __any(h != 0ull || st);
-      const int was = __any(st);
-      if (threadIdx.x == 0) {
-        flags[0] = any;
-        flags[1] = was;
-      }
-    }
-    __syncthreads();
-    if (!flags[0]) return false;
-    if (!flags[1] && blockIdx.x == 0 && threadIdx.x < 64) {  // the first stopping launch: count, publish
-      typedef __attribute__((address_space(1))) unsigned long long gull;
-      if (h) {
-        __hip_atomic_fetch_add((gull*)(sd->guard + 0), (unsigned long long)__popcll(h & 0x1111111111111111ull),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add((gull*)(sd->guard + 1), (unsigned long long)__popcll(h & 0x4444444444444444ull),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      if (threadIdx.x == 0) {
-        const unsigned long long v = (unsigned long long)ta.t + 1ull;
-        __hip_atomic_store((gull*)ta.xstop, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(ta.xstop_host, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-    }
-    return true;
-  }
-};
 
 // ------------------------------------------------------------------------------------------
 // DOF tiles: 16 DOFs x NT = 16 DRN trajectories; thread element i is e = threadIdx.x + i NW 64
@@ -997,7 +1015,7 @@ __device__ __forceinline__ bool xsub_combine(const ChTile* __restrict__ T, doubl
 // constraints zero p_{t+1} and q_{t+1} (md.py:407-408); history push of p_{t+1}.
 template <int NW, int DRN, bool GV = false>
 __device__ __forceinline__ void dof_X(const ChTile* __restrict__ T, const StepDev* __restrict__ sd,
-                                      const StepArgs& ta, double* lds, const XCheck& xc) {
+                                      const StepArgs& ta, double* lds, XCheck& xc) {
   using Geo = DofGeo<NW, DRN>;
   constexpr int EPT = Geo::EPT;
   const int B = sd->B, nb = sd->nbath;
@@ -1026,7 +1044,7 @@ __device__ __forceinline__ void dof_X(const ChTile* __restrict__ T, const StepDe
     }
   }
   const int part = T->xpart;  // 1: p_{t+1} only, 2: id0 phase and q_{t+1} only, 0: both
-  run_products_rn<NW, DRN, GV>(T, t, lds);
+  run_products_rn<NW, DRN, GV>(T, t, lds, 0, XC_LATE ? &xc : nullptr);
   if (xc.stop(sd, ta)) return;
   stamp(sd, 4, 2, ta);
   // the tile's output sums: K0.p_t of tile bath u (u), dyn.q_t (CH_TB), p_{t+1} (CH_TB + 1)
@@ -1422,7 +1440,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(DRN == 
       if ((int)blockIdx.x < ta.xndof && (int)threadIdx.x <= nl) {  // DOF tiles only (the first xndof)
 #endif
         xc.lane = threadIdx.x;
-        xc.w = xc.lane < nl ? *G(ta.xw + ((ta.t + 2) % 3) * (int64_t)nl + xc.lane) : *G(ta.xstop);
+        xc.src = ta.xw + ((ta.t + 2) % 3) * (int64_t)nl;
+        xc.stopw = ta.xstop;
+        xc.pending = true;
+        if (!XC_LATE) xc.load();
       }
       if (blockIdx.x == 0 && (int)threadIdx.x < nl)  // slot (t + 1) mod 3 for launch t + 1 (read by t - 1)
         *G(ta.xw + ((ta.t + 1) % 3) * (int64_t)nl + threadIdx.x) = 0ull;
