@@ -324,9 +324,8 @@ def main():
     log("[bench] rank %d setup %.1fs plan %s %s" % (rank, setup_s, plan, detail))
     # per-rank setup: wall time, noise phase and the noise factorisations this rank computed (the
     # ranks of a node split them, noise.NodeShare: their sum is one rank's count alone)
-    share = getattr(m, "_share", None)
     row = np.zeros((world, 3))
-    row[rank] = [setup_s, noise_s, share.total if share is not None else -1.0]
+    row[rank] = [setup_s, noise_s, float(getattr(m, "noise_factorisations", -1))]
     setup_ranks = m._allreduce(row) if world > 1 else row
 
     def barrier():

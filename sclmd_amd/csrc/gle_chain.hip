@@ -142,17 +142,8 @@ __device__ __forceinline__ unsigned long long xw_hits(unsigned long long w) {
   return w & ~(w >> 1) & 0x5555555555555555ull;  // bit 4j: d1 hit of trajectory j, bit 4j + 2: d0 hit
 }
 
-// XC_LATE (default): wave 0 issues the loads after its first operand batch's loads (in products), so
-// the products' first wait does not include them (issued with the descriptor they cost ~0.7 us/step
-// at C3, profiles/r06/ab7)
-#ifndef XC_LATE
-#define XC_LATE 1
-#endif
 struct XCheck {
   unsigned long long w = 0ull;
-  const unsigned long long* src = nullptr;   // the slot's words (late load), the stop word after them
-  const unsigned long long* stopw = nullptr;
-  bool pending = false;  // the late load is still to be issued
   int lane = -1;    // wave-0 lane holding a word: < nw nr word lane % nw of replica lane / nw, == nw nr
                     // the stop word
   int nw = 0;       // audit words (ceil(B / 16)) per replica
@@ -160,12 +151,6 @@ struct XCheck {
   bool on = false;  // a DOF tile of a composed-step launch of gle_run
   int* flags = nullptr;  // LDS: wave 0's vote
   // the barrier after the products; true: the tile stores nothing
-  __device__ void load() {  // wave 0
-    if (!pending) return;
-    pending = false;
-    const int nl = nw * nr;
-    if (lane >= 0) w = lane < nl ? *G(src + lane) : *G(stopw);
-  }
   __device__ bool stop(const StepDev* __restrict__ sd, const StepArgs& ta) {
 #if defined(XC_DBG) && (XC_DBG & 1)  // timing diagnostics only: no vote
     __syncthreads();
@@ -175,7 +160,6 @@ struct XCheck {
       __syncthreads();
       return false;
     }
-    if (threadIdx.x < 64) load();  // (a wave 0 without products)
     const int nl = nw * nr;
     unsigned long long h = 0ull;
     int st = 0;
@@ -216,7 +200,7 @@ struct XCheck {
 
 template <int RN, int NW, bool GEMV = false>
 __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave, int lane, int64_t t,
-                                         double* lds, int skip, XCheck* xl = nullptr) {
+                                         double* lds, int skip) {
   // GEMV (one-trajectory plans, chain stage 5 = stage 4 at B = 1): a 16x16x4 MFMA would use 1 of its
   // 16 columns; each lane instead multiplies its own A element by the X value of its k row on the VALU
   static_assert(!GEMV || RN == 1, "GEMV tiles have one column tile");
@@ -333,7 +317,6 @@ __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave,
       (void)b1;
       for (int s0 = 0; s0 < nks; s0 += U) {
         fetch(s0, a0, b0);
-        if (xl != nullptr && wave == 0) xl->load();  // the audit words behind the first batch (XC_LATE)
         compute(s0, a0, b0);
       }
     }
@@ -345,11 +328,10 @@ __device__ __forceinline__ void products(const ChTile* __restrict__ T, int wave,
 // so the 64-column near-field variant is not instantiated beside the DOF prologue's live values
 // (it made the register allocator spill the DOF stages)
 template <int NW, int RN, bool GV = false>
-__device__ __forceinline__ void run_products_rn(const ChTile* __restrict__ T, int64_t t, double* lds, int skip = 0,
-                                                XCheck* xl = nullptr) {
+__device__ __forceinline__ void run_products_rn(const ChTile* __restrict__ T, int64_t t, double* lds, int skip = 0) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  products<RN, NW, GV && RN == 1>(T, wave, lane, t, lds, skip, xl);
+  products<RN, NW, GV && RN == 1>(T, wave, lane, t, lds, skip);
 }
 
 template <int NW, bool GV = false>
@@ -1044,7 +1026,7 @@ __device__ __forceinline__ void dof_X(const ChTile* __restrict__ T, const StepDe
     }
   }
   const int part = T->xpart;  // 1: p_{t+1} only, 2: id0 phase and q_{t+1} only, 0: both
-  run_products_rn<NW, DRN, GV>(T, t, lds, 0, XC_LATE ? &xc : nullptr);
+  run_products_rn<NW, DRN, GV>(T, t, lds);
   if (xc.stop(sd, ta)) return;
   stamp(sd, 4, 2, ta);
   // the tile's output sums: K0.p_t of tile bath u (u), dyn.q_t (CH_TB), p_{t+1} (CH_TB + 1)
@@ -1176,7 +1158,7 @@ __device__ __forceinline__ void dof_X(const ChTile* __restrict__ T, const StepDe
         // line for every tile's atomic measured +2 us/step at C3)
         const int nw = (B + 15) / 16;
         gull* wrep = (gull*)(ta.xw + ((t % 3) * (int64_t)ta.xR + T->tile % ta.xR) * nw);
-#pragma unroll
+#pragma unroll 1
         for (int j = 0; j < Geo::NT / 16; ++j) {  // the tile's columns c0 .. c0 + NT - 1: NT / 16 words
           unsigned long long x = (c / 16 == j) ? nib : 0ull;
 #pragma unroll
@@ -1373,7 +1355,7 @@ __device__ __forceinline__ void far_tile(const StepArgs& ta, double* lds) {
 }
 
 template <int STAGE, int NW, int DRN>
-__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(DRN == 1 && NW <= 8 ? CH_WPE : 1, 8))) void chain_kernel(const ChTile* __restrict__ tiles, const StepDev* sd,
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(DRN == 1 && NW <= 8 ? CH_WPE : (NW == 8 ? 4 : 1), 8))) void chain_kernel(const ChTile* __restrict__ tiles, const StepDev* sd,
                                                         StepArgs ta, int mode) {
   extern __shared__ double lds[];
   if ((int)blockIdx.x >= ta.nstatic) {  // far-field item (fused schedule), launch-uniform ranges
@@ -1406,6 +1388,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(DRN == 
   constexpr int NCP = NTW + NSW, NIT = (NCP + NW * 64 - 1) / (NW * 64);
   __shared__ unsigned long long tdw[sizeof(ChTile) / 8], sdw[NSW];
   stamp(sd, STAGE, 0, ta);
+  XCheck xc;
+  __shared__ int xflags[2];
+  xc.flags = xflags;
   {
     typedef const __attribute__((address_space(1))) unsigned long long gull;
     gull* tsrc = (gull*)(tiles + blockIdx.x);
@@ -1416,37 +1401,31 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(DRN == 
       const int j = min((int)threadIdx.x + k * NW * 64, NCP - 1);
       v[k] = *(j < NTW ? tsrc + j : ssrc + (j - NTW));
     }
+    if constexpr (STAGE >= 4) {
+      // md.potforce cache audit of the previous step (XCheck), DOF tiles only (the launch's first
+      // xndof workgroups): wave 0 loads the words in the descriptor's round trip (loaded after it,
+      // the products' first wait included them: +0.5-0.9 us/step at C3, profiles/r06/audit_ab)
+      if (ta.xw) {
+        xc.nw = (ta.xB + 15) / 16;
+        xc.nr = ta.xR;
+        const int nl = xc.nw * xc.nr;  // lane r nw + j: word j of replica r; lane nl: the stop word
+#if defined(XC_DBG) && (XC_DBG & 4)  // timing diagnostics only: no audit loads
+        if (false) {
+#else
+        if ((int)blockIdx.x < ta.xndof && (int)threadIdx.x <= nl) {
+#endif
+          xc.lane = threadIdx.x;
+          xc.w = xc.lane < nl ? *G(ta.xw + ((ta.t + 2) % 3) * (int64_t)nl + xc.lane) : *G(ta.xstop);
+        }
+        if (blockIdx.x == 0 && (int)threadIdx.x < nl)  // slot (t + 1) mod 3 for launch t + 1 (read by t - 1)
+          *G(ta.xw + ((ta.t + 1) % 3) * (int64_t)nl + threadIdx.x) = 0ull;
+      }
+    }
 #pragma unroll
     for (int k = 0; k < NIT; ++k) {
       const int i = threadIdx.x + k * NW * 64;
       if (i < NTW) tdw[i] = v[k];
       else if (i < NCP) sdw[i - NTW] = v[k];
-    }
-  }
-  XCheck xc;
-  __shared__ int xflags[2];
-  xc.flags = xflags;
-  if constexpr (STAGE >= 4) {
-    // md.potforce cache audit of the previous step (XCheck), DOF tiles only: wave 0 loads the words
-    // now (the tile kind is in the descriptor being copied: every workgroup's wave 0 issues the loads,
-    // the non-DOF tiles ignore them)
-    if (ta.xw) {
-      xc.nw = (ta.xB + 15) / 16;
-      xc.nr = ta.xR;
-      const int nl = xc.nw * xc.nr;  // lane r nw + j: word j of replica r; lane nl: the stop word
-#if defined(XC_DBG) && (XC_DBG & 4)  // timing diagnostics only: no audit loads
-      if (false) {
-#else
-      if ((int)blockIdx.x < ta.xndof && (int)threadIdx.x <= nl) {  // DOF tiles only (the first xndof)
-#endif
-        xc.lane = threadIdx.x;
-        xc.src = ta.xw + ((ta.t + 2) % 3) * (int64_t)nl;
-        xc.stopw = ta.xstop;
-        xc.pending = true;
-        if (!XC_LATE) xc.load();
-      }
-      if (blockIdx.x == 0 && (int)threadIdx.x < nl)  // slot (t + 1) mod 3 for launch t + 1 (read by t - 1)
-        *G(ta.xw + ((ta.t + 1) % 3) * (int64_t)nl + threadIdx.x) = 0ull;
     }
   }
   __syncthreads();

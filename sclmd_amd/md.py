@@ -518,6 +518,19 @@ class md:
             sh = self._share = _noise.NodeShare(r, w, lambda: self._allreduce(np.zeros(1)), "%012x" % tok)
         return sh
 
+    def _counted(self, plan, share):
+        """The plan's segments, counting the dense factorisations this rank computes into
+        md.noise_factorisations (with a NodeShare: its own block only)."""
+        t0 = share.total if share is not None else 0
+        n = 0
+        for seg in plan:
+            if seg[0] == "dense":
+                m = seg[2][0] if isinstance(seg[2], tuple) else seg[2]
+                n += m.shape[0]
+            yield seg
+        self.noise_factorisations = getattr(self, "noise_factorisations", 0) + (
+            share.total - t0 if share is not None else n)
+
     def _noise_seed(self, i, run):
         base = 0 if self.seed is None else int(self.seed)
         return (base * 0x9E3779B97F4A7C15 + (run + 1) * 0xBF58476D1CE4E5B9 + (i + 1) * 0x94D049BB133111EB) % 2**64
@@ -538,8 +551,8 @@ class md:
             seed = self._noise_seed(i, run)
             share = self._node_share()
             if not self.noise_factor_cache:
-                st.noise_stream_plan(i, _noise.stream_factor_plan(b, share=share), b.kind == "ebath", seed,
-                                     self.traj_offset)
+                st.noise_stream_plan(i, self._counted(_noise.stream_factor_plan(b, share=share), share), b.kind == "ebath",
+                                     seed, self.traj_offset)
             else:
                 key = b._noise_key()
                 dev = st.__dict__.setdefault("noise_plan_keys", {})  # bath -> key of its retained plan
@@ -550,8 +563,10 @@ class md:
                     if getattr(b, "_stream_cache_key", None) != key:
                         b._stream_cache, b._stream_cache_key = {}, key
                     st.noise_stream_retain(i, True)
-                    st.noise_stream_plan(i, _noise.stream_factor_plan(b, cache=b._stream_cache, share=share),
-                                         b.kind == "ebath", seed, self.traj_offset)
+                    fresh = not b._stream_cache.get("complete")
+                    plan = _noise.stream_factor_plan(b, cache=b._stream_cache, share=share)
+                    st.noise_stream_plan(i, self._counted(plan, share) if fresh else plan, b.kind == "ebath", seed,
+                                         self.traj_offset)
                     if st.noise_stream_retained(i):
                         dev[i] = key
                         b._stream_cache, b._stream_cache_key = None, None  # the device copy serves

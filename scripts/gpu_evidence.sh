@@ -14,6 +14,9 @@
 #   trace_c5 / pmc_c5   the same for the C5 line; trace_c2 the C2 line's trace
 #   blocklen   bench lines at several first block lengths (BLS, CONFIGS, ROUNDS)
 #   c5run      md.Run wall time per run at C5 (scripts/c5_run_timing.py: noise, stepping, MD{j}.nc)
+#   c1         the C1 host-driver step (scripts/c1_driver_timing.py)
+#   noiseshare per-rank host factorisation of the C5 noise split over a node's 8 ranks (no GPU)
+#   rehearse_share  8 same-device gloo ranks with streamed C3 noise: per-rank setup / factorisations
 #   negf       GLE ensemble current vs the NEGF Landauer current (tests/test_gpu_negf.py)
 #   ab         experiment libraries x GLE_* variants, interleaved (LIBS, VARIANTS, ROUNDS, EXPARGS,
 #              TIMELINES=1 for per-workgroup chain timelines); build them with make experiments
@@ -52,6 +55,23 @@ lines)
   timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_c3.json 2> $O/bench_c3.err || fail b512 $O/bench_c3.err
   timeout -k 10 300 python bench.py --config C2 --ntraj 1 --steps 256 --warmup 32 > $O/bench_c2.json 2> $O/bench_c2.err || fail c2 $O/bench_c2.err
   summ $O/bench_c3_20x5.json $O/bench_c3.json $O/bench_c2.json ;;
+c1)
+  timeout -k 10 300 python scripts/c1_driver_timing.py --nmd 1024 > $O/c1_driver_timing.json 2> $O/c1_driver_timing.err || fail c1 $O/c1_driver_timing.err
+  cat $O/c1_driver_timing.json ;;
+noiseshare)
+  # host only: per-rank factorisation time of the C5 noise spectra when 8 ranks of a node split them
+  timeout -k 10 600 python scripts/noise_share_timing.py --world 8 --workers 16 > $O/noise_share_c5.json 2> $O/noise_share_c5.err || fail noiseshare $O/noise_share_c5.err
+  cat $O/noise_share_c5.json ;;
+rehearse_share)
+  # 8 ranks on one GPU over gloo with the C3 noise streamed: every rank's setup, noise phase and
+  # factorisation count (noise.NodeShare: the counts add up to one rank's)
+  timeout -k 10 600 python bench.py --gpus 8 --same-device --dist-backend gloo --ntraj 8 --stream-noise --steps 8 --warmup 2 \
+    --fill 16 --no-cpu-baseline > $O/rehearsal_share8.json 2> $O/rehearsal_share8.err || fail share8 $O/rehearsal_share8.err
+  timeout -k 10 600 python bench.py --ntraj 8 --stream-noise --steps 8 --warmup 2 --fill 16 --no-cpu-baseline \
+    > $O/rehearsal_share1.json 2> $O/rehearsal_share1.err || fail share1 $O/rehearsal_share1.err
+  python3 -c "import json,sys
+for f in sys.argv[1:]:
+    d=json.loads([l for l in open(f) if l.startswith('{')][-1]); print(f.split('/')[-1], d['n_gpus'], d['setup_ranks'])" $O/rehearsal_share8.json $O/rehearsal_share1.json ;;
 c5run)
   timeout -k 10 900 python scripts/c5_run_timing.py --runs ${RUNS:-3} > $O/c5_run_timing.json 2> $O/c5_run_timing.log || fail c5run $O/c5_run_timing.log
   cat $O/c5_run_timing.json ;;
