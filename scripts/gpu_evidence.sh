@@ -15,6 +15,7 @@
 #   blocklen   bench lines at several first block lengths (BLS, CONFIGS, ROUNDS)
 #   c5run      md.Run wall time per run at C5 (scripts/c5_run_timing.py: noise, stepping, MD{j}.nc)
 #   c1         the C1 host-driver step (scripts/c1_driver_timing.py)
+#   c4shape    BASELINE config 4's shape (8 ranks x 64 trajectories) as 8 gloo ranks on one GPU
 #   noiseshare per-rank host factorisation of the C5 noise split over a node's 8 ranks (no GPU)
 #   rehearse_share  8 same-device gloo ranks with streamed C3 noise: per-rank setup / factorisations
 #   negf       GLE ensemble current vs the NEGF Landauer current (tests/test_gpu_negf.py)
@@ -72,6 +73,13 @@ rehearse_share)
   python3 -c "import json,sys
 for f in sys.argv[1:]:
     d=json.loads([l for l in open(f) if l.startswith('{')][-1]); print(f.split('/')[-1], d['n_gpus'], d['setup_ranks'])" $O/rehearsal_share8.json $O/rehearsal_share1.json ;;
+c4shape)
+  # BASELINE config 4's shape (512 trajectories over 8 ranks, 64 each) rehearsed on one GPU: 8 gloo
+  # ranks on device 0 (the control flow, the node-shared noise factorisation and the reduce; the
+  # rate is 8 ranks time-sharing one GPU, not the 8-GPU node's)
+  timeout -k 10 900 python bench.py --gpus 8 --same-device --dist-backend gloo --ntraj 64 --steps 20 --warmup 5 \
+    --no-cpu-baseline > $O/c4shape_8x64.json 2> $O/c4shape_8x64.err || fail c4shape $O/c4shape_8x64.err
+  summ $O/c4shape_8x64.json ;;
 c5run)
   timeout -k 10 900 python scripts/c5_run_timing.py --runs ${RUNS:-3} > $O/c5_run_timing.json 2> $O/c5_run_timing.log || fail c5run $O/c5_run_timing.log
   cat $O/c5_run_timing.json ;;
