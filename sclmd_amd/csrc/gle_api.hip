@@ -1421,7 +1421,8 @@ int plan_chain(gle_handle* h) {
     if (rc) return rc;
   }
   // near-field partial items (lags [2, nn), target t+2) per bath: sizes and slot counts
-  int rn_raw = (int)std::min<int64_t>(4, (B + 15) / 16);
+  // 16, 32 or 64 columns: the product routines have no 48-column form (B in (32, 48] rounds up)
+  int rn_raw = std::min(4, rn_for(B));
   if (const char* e = gle_env("GLE_RAW_RN")) rn_raw = std::max(1, std::min(rn_raw, atoi(e) >= 4 ? 4 : (atoi(e) >= 2 ? 2 : 1)));
   const int nt_raw = 16 * rn_raw;
   const int ncolr = (int)((B + nt_raw - 1) / nt_raw);
@@ -2038,7 +2039,7 @@ int plan_xstep(gle_handle* h) {
   }
   if (rc) return rc;
   // near-field partials of lags [3, nn) for target t+3 (the S tiles of the next launch sum them)
-  int rn_raw = (int)std::min<int64_t>(4, (B + 15) / 16);
+  int rn_raw = std::min(4, rn_for(B));  // 16, 32 or 64 columns (no 48-column product form)
   const int nt_raw = 16 * rn_raw;
   const int ncolr = (int)((B + nt_raw - 1) / nt_raw);
   int raw_ks = 24;
@@ -2500,7 +2501,7 @@ int freeze(gle_handle* h) {
   }
   for (auto& lv : h->levels) {
     lv.cstride = lv.spectral ? Pspec / lv.P : 1;
-    lv.cg_rn = (int)std::min<int64_t>(4, (B + 15) / 16);
+    lv.cg_rn = std::min(4, rn_for(B));  // 16, 32 or 64 columns (cgemm_kernel has no 48-column form)
     lv.nplanes = lv.cg_rn <= 2 ? 2 : 3;  // (64-column items have no two-plane kernel path)
     lv.cg_split = 1;
     if (lv.spectral) {

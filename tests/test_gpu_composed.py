@@ -75,11 +75,13 @@ def test_composed_plan_is_the_c3_bench_plan():
     assert d["composed_step"] and d["plan_class"] == "small" and not d["split_tiles"]
 
 
-@pytest.mark.parametrize("B", [8, 3])
+@pytest.mark.parametrize("B", [8, 3, 40, 50])
 def test_composed_vs_oracle_with_path_switches(B):
     """Composed steps, then steps with a host force (the two-launch path), then composed steps again,
     a new noise realisation, more composed steps: every segment against the oracle.  B = 8 plans a
-    spectral ladder, B = 3 a direct one."""
+    spectral ladder, B = 3 a direct one; B = 40 and 50 a partial last column tile of the 64-column
+    near-field and far-field products (B in (32, 48] once planned a 48-column width those products do
+    not have)."""
     st, sim, baths, ob, meta, dyn, rng = _setup(B)
     assert st.plan_detail()["composed_step"]
     nst = 0
@@ -234,6 +236,25 @@ def test_potforce_cache_reuse_mid_run_vs_oracle(kick, constr):
     for _ in range(23):
         sim.step()
     _check(st, sim, 83)
+    st.close()
+
+
+@pytest.mark.parametrize("B,rest", [(40, [21, 38]), (64, [63]), (130, [5, 129])])
+def test_potforce_cache_reuse_audit_words_vs_oracle(B, rest):
+    """The audit packs a nibble per trajectory into ceil(B / 16) words, replicated 8 times up to B = 112
+    and once above (XCheck in gle_chain.hip): near-rest trajectories in later words and nibbles (B = 64
+    is the benched ensemble) stop the composed run at the kick and are replayed, against the oracle."""
+    st, sim = _at_rest_setup(B, kick=31, rest=rest)
+    assert st.plan_detail()["composed_step"]
+    st.run(50)
+    for _ in range(50):
+        sim.step()
+    _check(st, sim, 50)
+    assert st.cache_audit()[0] >= len(rest)
+    st.run(9)
+    for _ in range(9):
+        sim.step()
+    _check(st, sim, 59)
     st.close()
 
 
