@@ -1,0 +1,112 @@
+"""Plan classes x ensemble widths against the oracle.  The plans pick tile widths from B (16-, 32- and
+64-column products, partial last column tiles, split DOF tiles below 128 tiles, audit words of 16
+trajectories) and from the bath size (small- or large-bath plan); the benched shapes are B = 64 (C3)
+and B = 32 (C5).  A 40-trajectory ensemble once planned a 48-column product width that the kernels
+do not have (profiles/r06/bwidth), so every plan class runs here at widths across those boundaries:
+composed or two-launch steps, a segment with a host force (md.potforce on the host), constraints,
+levels firing at ml = 96, against oracle.GLEBatch at 1e-10."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-10
+
+
+def rel(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
+
+
+def _run(B, plan_class, far_mode="auto", constr=None, natom=40, ml=96, nmd=256, seed=11, config="C3"):
+    from oracle import sclmd_oracle as O
+    from sclmd_amd import _native as N
+    from sclmd_amd import synthetic
+
+    dyn, _, baths, meta = synthetic.junction(config, natom=natom, ml=ml, nmd=nmd, nw=60, seed=seed)
+    nph, dt = meta["nph"], meta["dt"]
+    st = N.Stepper(nph, B, nmd, dt, 0, 0, far_mode, 0)
+    try:
+        for b in baths:
+            if b.kind == "ebath":
+                st.add_bath(N.GLE_BATH_ELECTRON, b.cids, b.kernel, b.bias, b.exim, b.zeta1, b.zeta2)
+            else:
+                st.add_bath(N.GLE_BATH_PHONON, b.cids, b.kernel)
+        st.set_dyn(dyn)
+        if constr is not None:
+            st.set_constraint(constr)
+        st.set_plan_class(plan_class)
+        rng = np.random.default_rng(seed)
+        p = rng.normal(size=(B, nph)) * 1e-2
+        q = rng.normal(size=(B, nph)) * 1e-2
+        if constr is not None:
+            p[:, constr] = 0.0
+            q[:, constr] = 0.0
+        noise = [rng.normal(size=(B, nmd, b.nc)) * 1e-3 for b in baths]
+        hist = [rng.normal(size=(B, b.kernel.shape[0], b.nc)) * 1e-2 for b in baths]
+        st.set_state(p, q, 5)
+        for i in range(len(baths)):
+            st.set_history(i, hist[i])
+            st.set_noise(i, noise[i])
+        ob = [O.Bath("e", b.cids, b.kernel, noise[i], dt, nmd, bias=b.bias, exim=b.exim, zeta1=b.zeta1, zeta2=b.zeta2)
+              if b.kind == "ebath" else O.Bath("ph", b.cids, b.kernel, noise[i], dt, nmd) for i, b in enumerate(baths)]
+        sim = O.GLEBatch(nph, dt, nmd, ob, dyn, ntr=B,
+                         constr=None if constr is None else [range(int(c), int(c) + 1) for c in constr])
+        sim.p, sim.q, sim.t = p.T.copy(), q.T.copy(), 5
+        for i in range(len(baths)):
+            sim.set_history(i, hist[i])
+        detail = st.plan_detail()
+        st.run(37)
+        for _ in range(37):
+            sim.step()
+        for _ in range(3):  # host force: the two-launch path
+            qt = st.step_begin(-(st.get_state()[1] @ dyn.T))
+            st.step_end(-(qt @ dyn.T))
+            sim.step()
+        st.run(61)
+        for _ in range(61):
+            sim.step()
+        pg, qg, t = st.get_state()
+        cur = st.get_current()
+        audit = st.cache_audit()
+    finally:
+        st.close()
+    assert t == 5 + 101
+    assert rel(qg, sim.q.T) < TOL and rel(pg, sim.p.T) < TOL, (rel(qg, sim.q.T), rel(pg, sim.p.T))
+    steps = (5 + np.arange(101)) % nmd
+    want = np.stack([c[:, steps] for c in sim.cur])
+    assert rel(cur[:, :, steps], want) < 1e-9
+    assert audit == (0, 0)
+    return detail
+
+
+@pytest.mark.parametrize("B", [1, 3, 8, 17, 40, 64, 100])
+def test_large_bath_plan_widths_vs_oracle(B):
+    """The large-bath plan (C5's: first block length 4, the potential-force launch between A and the
+    fused velocity stage, split far-field GEMMs) forced on a small junction at several widths."""
+    d = _run(B, "large")
+    assert d["plan_class"] == "large" and d["fpot_launch"] and not d["composed_step"], d
+
+
+@pytest.mark.parametrize("B", [24, 40, 96])
+def test_small_bath_plan_widths_with_constraints_vs_oracle(B):
+    """The small-bath plan (composed step) with constrained DOFs inside and outside the baths."""
+    d = _run(B, "small", constr=[0, 1, 2, 60, 61, 119])
+    assert d["plan_class"] == "small" and d["composed_step"], d
+
+
+@pytest.mark.parametrize("B", [8, 40])
+def test_direct_ladder_widths_vs_oracle(B):
+    """far_mode direct: every ladder level a contraction (the spectral levels' transforms and GEMMs
+    out of the plan)."""
+    d = _run(B, "auto", far_mode="direct")
+    assert d["composed_step"], d
+
+
+@pytest.mark.parametrize("plan_class", ["small", "large"])
+@pytest.mark.parametrize("B", [8, 40])
+def test_biased_electron_bath_widths_vs_oracle(plan_class, B):
+    """C5's bath mix at a small size: two phonon baths and a biased electron bath (exim, zeta1, zeta2
+    != 0: the baths.py:233 bias terms), both plan classes (the biased bath keeps the two-launch path)."""
+    d = _run(B, plan_class, config="C5")
+    assert d["plan_class"] == plan_class and not d["composed_step"], d
