@@ -18,13 +18,17 @@ def rel(a, b):
     return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
 
 
-def _run(B, plan_class, far_mode="auto", constr=None, natom=40, ml=96, nmd=256, seed=11, config="C3"):
+def _run(B, plan_class, far_mode="auto", constr=None, natom=40, ml=96, nmd=256, seed=11, config="C3",
+         trim=None):
     from oracle import sclmd_oracle as O
     from sclmd_amd import _native as N
     from sclmd_amd import synthetic
 
     dyn, _, baths, meta = synthetic.junction(config, natom=natom, ml=ml, nmd=nmd, nw=60, seed=seed)
     nph, dt = meta["nph"], meta["dt"]
+    if trim is not None:  # bath i's memory kernel cut to its first m lags
+        i, m = trim
+        baths[i].kernel = np.ascontiguousarray(baths[i].kernel[:m])
     st = N.Stepper(nph, B, nmd, dt, 0, 0, far_mode, 0)
     try:
         for b in baths:
@@ -110,3 +114,21 @@ def test_biased_electron_bath_widths_vs_oracle(plan_class, B):
     != 0: the baths.py:233 bias terms), both plan classes (the biased bath keeps the two-launch path)."""
     d = _run(B, plan_class, config="C5")
     assert d["plan_class"] == plan_class and not d["composed_step"], d
+
+
+@pytest.mark.parametrize("plan_class", ["small", "large"])
+@pytest.mark.parametrize("ml", [1, 2, 3, 7, 17, 40])
+def test_memory_lengths_vs_oracle(plan_class, ml):
+    """Short memory kernels: ml = 1 (no memory: c = 1, baths.py:454-457), lengths inside the near field
+    (ml < 2 P0: no ladder level) and just past the first levels, both plan classes, B = 8 and 40."""
+    for B in (8, 40):
+        _run(B, plan_class, ml=ml)
+
+
+@pytest.mark.parametrize("plan_class", ["small", "large"])
+@pytest.mark.parametrize("trim", [(0, 1), (1, 5), (0, 33)])
+def test_mixed_memory_lengths_vs_oracle(plan_class, trim):
+    """Baths of different memory lengths in one plan (one without memory, one inside the near field,
+    one with ladder levels the other lacks)."""
+    for B in (8, 40):
+        _run(B, plan_class, trim=trim)
