@@ -18,17 +18,19 @@ def rel(a, b):
     return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
 
 
+@pytest.mark.parametrize("B,nc", [(5, 20), (40, 70), (33, 130)])
 @pytest.mark.parametrize("kind", ["ph", "e"])
-def test_stream_equals_resident_generator(kind):
+def test_stream_equals_resident_generator(kind, B, nc):
+    """(partial 64-row factor tiles and 32-trajectory tiles of noise_gemm at B = 33 / 40, nc = 70 / 130)"""
     from sclmd_amd import _native as N
     from sclmd_amd import synthetic
 
     rng = np.random.default_rng(2)
-    nmd, B = 256, 5
+    nmd = 256
     if kind == "ph":
-        b = synthetic.make_phbath(300.0, list(range(20)), 8, nmd, rng, nw=40)
+        b = synthetic.make_phbath(300.0, list(range(nc)), 8, nmd, rng, nw=40)
     else:
-        b = synthetic.make_biased_ebath(300.0, list(range(18)), nmd, rng)
+        b = synthetic.make_biased_ebath(300.0, list(range(nc - 2)), nmd, rng)
     fac = b.noise_factor().scaled()
     cplx = np.iscomplexobj(fac)
     out = []
