@@ -371,34 +371,47 @@ def test_host_driver_ensemble_per_trajectory_drivers(case):
     assert rel(out[0][1], out[1][1]) < 1e-10 and rel(out[0][0], out[1][0]) < 1e-10
 
 
-def test_ensemble_sharding_invariance(tmp_path, monkeypatch):
+@pytest.mark.parametrize("ntraj,cut", [(16, 8), (40, 33)])
+def test_ensemble_sharding_invariance(tmp_path, monkeypatch, ntraj, cut):
     """The multi-GPU ensemble by construction: trajectory g's initial state and device noise are keyed
-    by its global index (seed + traj_offset + b), so one 16-trajectory md equals two 8-trajectory
-    shards with traj_offset 0 and 8 -- what ranks 0 and 1 hold -- up to the summation order of the
-    batched kernels (1e-9 relative on p, q and the heat currents)."""
+    by its global index (seed + traj_offset + b), so one md of ntraj trajectories equals two shards with
+    traj_offset 0 and cut -- what ranks 0 and 1 hold -- up to the summation order of the batched
+    kernels (1e-9 relative on p, q and the heat currents).  Also per trajectory: the recorded p / q / bath
+    force series (savep, saveq, saveall), the bath history rings, the full-DOF histories MD{j}.nc
+    stores, and the per-trajectory power spectra.  (40 = 33 + 7: partial column tiles everywhere.)"""
+    from sclmd_amd import _native as NV
     from sclmd_amd import md as MD
     from sclmd_amd import synthetic
 
     monkeypatch.chdir(tmp_path)
 
-    def run(ntraj, offset):
+    def run(n, offset):
         dyn, axyz, baths, meta = synthetic.junction("C3", seed=5, natom=12, ml=64, nmd=256, nw=80)
-        m = MD.md(meta["dt"], meta["nmd"], meta["T"], axyz=axyz, dyn=dyn, ntraj=ntraj, seed=77,
+        m = MD.md(meta["dt"], meta["nmd"], meta["T"], axyz=axyz, dyn=dyn, ntraj=n, seed=77,
                   traj_offset=offset, noise_mode="device", verbose=False)
         for b in baths:
             m.AddBath(b)
+        m.Savep()
+        m.Saveq()
+        m.SaveAll()
         m.initialise()
         m.ResetHis()
         for i in range(len(baths)):
             m.gen_noise(i, 0)
+        m._in_run = True  # record the full-DOF p / q rings as md.Run does (REC_HIST)
         m.steps(300)
-        p, q, _ = m._st.get_state()
-        cur = m._st.get_current()
+        st = m._st
+        p, q, _ = st.get_state()
+        out = {"p": p, "q": q, "cur": st.get_current().transpose(1, 0, 2),
+               "ps": st.get_record(NV.REC_P), "qs": st.get_record(NV.REC_Q),
+               "f0": st.get_record(NV.REC_F, 0), "f1": st.get_record(NV.REC_F, 1),
+               "h0": st.get_history(0), "h1": st.get_history(1),
+               "fullp": st.get_full_history(64)[0],
+               "pow": st.power_spectrum([list(range(0, 6)), list(range(20, 36))]).transpose(1, 0, 2)}
+        m._in_run = False
         m.close()
-        return p, q, cur
+        return out
 
-    p, q, cur = run(16, 0)
-    p0, q0, c0 = run(8, 0)
-    p1, q1, c1 = run(8, 8)
-    assert rel(np.concatenate([p0, p1]), p) < 1e-9 and rel(np.concatenate([q0, q1]), q) < 1e-9
-    assert rel(np.concatenate([c0, c1], axis=1), cur) < 1e-9
+    whole, a, b = run(ntraj, 0), run(cut, 0), run(ntraj - cut, cut)
+    for k in whole:
+        assert rel(np.concatenate([a[k], b[k]]), whole[k]) < 1e-9, k
