@@ -19,13 +19,22 @@ def rel(a, b):
 
 
 def _run(B, plan_class, far_mode="auto", constr=None, natom=40, ml=96, nmd=256, seed=11, config="C3",
-         trim=None):
+         trim=None, scatter=None):
     from oracle import sclmd_oracle as O
     from sclmd_amd import _native as N
     from sclmd_amd import synthetic
 
     dyn, _, baths, meta = synthetic.junction(config, natom=natom, ml=ml, nmd=nmd, nw=60, seed=seed)
     nph, dt = meta["nph"], meta["dt"]
+    if scatter is not None:  # phonon baths on scattered DOF sets (non-affine DOF maps in the tiles)
+        r = np.random.default_rng(seed + 7)
+        perm = r.permutation(nph)
+        d0, d1 = np.sort(perm[:37]), np.sort(perm[37:66])
+        if scatter == "overlap":
+            d1 = np.sort(np.concatenate([d1[:20], d0[:9]]))
+        elif scatter == "unsorted":
+            d0, d1 = perm[:37], perm[37:66]
+        baths = [synthetic.make_phbath(300.0, list(map(int, d)), ml, nmd, r, nw=60) for d in (d0, d1)]
     if trim is not None:  # bath i's memory kernel cut to its first m lags
         i, m = trim
         baths[i].kernel = np.ascontiguousarray(baths[i].kernel[:m])
@@ -132,3 +141,36 @@ def test_mixed_memory_lengths_vs_oracle(plan_class, trim):
     one with ladder levels the other lacks)."""
     for B in (8, 40):
         _run(B, plan_class, trim=trim)
+
+
+@pytest.mark.parametrize("plan_class", ["small", "large"])
+@pytest.mark.parametrize("scatter", ["disjoint", "overlap", "unsorted"])
+def test_scattered_bath_dofs_vs_oracle(plan_class, scatter):
+    """Baths on scattered DOF sets: sorted and disjoint (composed step with non-affine DOF maps), two
+    baths sharing 9 DOFs (the two-launch path; exlist / mf of noise.py), and cids in no order."""
+    for B in (8, 40):
+        d = _run(B, plan_class, scatter=scatter)
+        assert d["composed_step"] == (plan_class == "small" and scatter != "overlap"), d
+
+
+@pytest.mark.parametrize("B", [1008, 1009])
+def test_widest_composed_ensembles_vs_oracle(B):
+    """The composed step's audit holds ceil(B / 16) words and the stop word in one wave's 64 lanes, so
+    B = 1008 is the widest composed plan and B = 1009 takes the two-launch plan."""
+    d = _run(B, "small")
+    assert d["composed_step"] == (B <= 1008), d
+
+
+def test_widest_composed_audit_replays_vs_oracle():
+    """B = 1008 with near-rest trajectories in the first and the last audit word (lanes 0 and 62; the
+    stop word in lane 63): the run stops at the kick and is replayed on the two-launch path."""
+    import test_gpu_composed as C
+
+    st, sim = C._at_rest_setup(1008, kick=31, rest=[3, 1007])
+    assert st.plan_detail()["composed_step"]
+    st.run(45)
+    for _ in range(45):
+        sim.step()
+    C._check(st, sim, 45)
+    assert st.cache_audit()[0] >= 2
+    st.close()
