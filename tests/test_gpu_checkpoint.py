@@ -225,3 +225,51 @@ def test_full_history_getter_matches_host_composition(tmp_path, monkeypatch):
         assert np.array_equal(ph, m.phis) and np.array_equal(qh, m.qhis)
     assert np.abs(qh).max() > 0.0
     m.close()
+
+
+def test_wide_ensemble_continue_and_resume(tmp_path, monkeypatch):
+    """40 trajectories (partial column tiles of every product width): continuing from the previous run's
+    MD0.nc and resuming an unfinished run 1 both reproduce the uninterrupted run."""
+    from sclmd_amd import md as MD
+
+    full = tmp_path / "full"
+    full.mkdir()
+    monkeypatch.chdir(full)
+    m = _md(0, 2, ntraj=40)
+    m.Run()
+    p, q, t, kap = _final(m)
+    m.close()
+    cont = tmp_path / "cont"
+    cont.mkdir()
+    shutil.copy(full / "MD0.nc", cont / "MD0.nc")
+    monkeypatch.chdir(cont)
+    m = _md(1, 2, ntraj=40)
+    m.Run()
+    p2, q2, t2, kap2 = _final(m)
+    m.close()
+    assert t2 == t and rel(q2, q) < 1e-10 and rel(p2, p) < 1e-10 and rel(kap2[-1], kap[-1]) < 1e-9
+
+    res = tmp_path / "resume"
+    res.mkdir()
+    monkeypatch.chdir(res)
+    real_dump = MD.md.dump
+
+    class Stop(Exception):
+        pass
+
+    def dump_then_stop(self, ipie, id):
+        real_dump(self, ipie, id)
+        if id == 1 and ipie == 0:
+            raise Stop()
+
+    monkeypatch.setattr(MD.md, "dump", dump_then_stop)
+    m = _md(0, 2, ntraj=40)
+    with pytest.raises(Stop):
+        m.Run()
+    m.close()
+    monkeypatch.setattr(MD.md, "dump", real_dump)
+    m = _md(0, 2, ntraj=40)
+    m.Run()
+    p3, q3, t3, _ = _final(m)
+    m.close()
+    assert t3 == t and rel(q3, q) < 1e-10 and rel(p3, p) < 1e-10
