@@ -3225,7 +3225,7 @@ int step_end_impl(gle_handle* h, const double* fpot_host_T) {
   if (!h->levels.empty() && (h->t + 1) % h->P0 == 0) HIPCHK(h, hipEventRecord(h->ev_step, h->stream));
   h->t += 1;
   h->pot_cache_exact = (fpot_host_T == nullptr) && h->constr.empty();
-  h->std_words_live = fpot_host_T == nullptr;  // the velocity stage wrote step t + 1's id0 distances
+  h->std_words_live = true;  // the velocity stage wrote step t + 1's id0 distances (host force: against q~)
   HIPCHK(h, hipGetLastError());
   return GLE_OK;
 }

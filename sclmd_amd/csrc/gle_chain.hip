@@ -723,7 +723,7 @@ __device__ __forceinline__ void dof_C(const ChTile* __restrict__ T, const StepDe
   }
   if (T->first && threadIdx.x < Geo::NT && T->c0 + (int)threadIdx.x < B) {
     *G(pmax_word(sd, 1, par1, T->c0 + threadIdx.x)) = 0ull;
-    if (harm) G(sd->qvalid)[T->c0 + threadIdx.x] = 1;
+    G(sd->qvalid)[T->c0 + threadIdx.x] = 1;
   }
   run_products_rn<NW, DRN>(T, t, lds);
   __syncthreads();
@@ -750,6 +750,8 @@ __device__ __forceinline__ void dof_C(const ChTile* __restrict__ T, const StepDe
       G(sd->P)[E[x].i] = p2;
       G(sd->Q)[E[x].i] = qn;
       G(sd->Flast)[E[x].i] = f;
+      // a host force at q~ (gle_step_end with fpot): md.potforce's cache now holds (q~, Fc)
+      if (!harm) G(sd->Q0)[E[x].i] = qt[x];
     }
 #pragma unroll
     for (int u = 0; u < CH_TB; ++u) {
@@ -766,9 +768,10 @@ __device__ __forceinline__ void dof_C(const ChTile* __restrict__ T, const StepDe
         if (bd.has_q) G(bd.Xq)[kb] = qn;
       }
     }
-    dq[x] = E[x].ok ? fabs(qn - q0[x]) : 0.0;
+    dq[x] = E[x].ok ? fabs(qn - (harm ? q0[x] : qt[x])) : 0.0;
   }
-  if (harm) {  // cache distance of q_{t+1} for the next step's id0 call
+  {  // cache distance of q_{t+1} for the next step's id0 call (after a host force too: the next step
+     // may evaluate the force on the device, with md.potforce's rule against q~)
     __syncthreads();
 #pragma unroll
     for (int x = 0; x < EPT; ++x) {

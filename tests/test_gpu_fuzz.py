@@ -1,0 +1,155 @@
+"""Seeded random configurations against the oracle: the plan space has many switches (bath size class,
+ensemble width, memory lengths, DOF maps, bath kinds and bias, constraints, far mode, first block
+length, composed or two-launch steps, host-force segments), and a fixed list of cases samples their
+combinations.  Each case draws a junction (chain or chain + long-range couplings), 1-3 baths on
+random DOF sets (contiguous, scattered, overlapping), B in [1, 70], ml in [1, 130], then runs a random
+sequence of device runs and host-force steps over more than nmd steps (noise wrap-around) from a
+nonzero t0 and history, against oracle.GLEBatch at 1e-9 on p, q and the heat currents.  A failing
+case prints its parameters (case index = seed)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-9
+NCASE = 40
+
+
+def rel(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
+
+
+def _case(seed):
+    from sclmd_amd import synthetic
+
+    r = np.random.default_rng(1000 + seed)
+    natom = int(r.integers(5, 60))
+    nph = 3 * natom
+    dyn = synthetic.chain_dyn(natom)
+    if r.random() < 0.5:  # long-range couplings: the block-sparse dyn with scattered blocks
+        n = int(r.integers(1, 3 * natom))
+        i, j = r.integers(0, nph, n), r.integers(0, nph, n)
+        v = r.normal(size=n) * 1e-3
+        add = np.zeros((nph, nph))
+        add[i, j] += v
+        add = add + add.T
+        dyn = dyn + add + np.eye(nph) * 2 * np.abs(add).sum(axis=1).max()
+    nmd = int(r.choice([64, 128, 256]))
+    B = int(r.choice([1, 2, 3, 5, 8, 13, 16, 17, 24, 31, 32, 33, 40, 48, 49, 63, 64, 70]))
+    nb = int(r.integers(1, 4))
+    baths, used = [], np.zeros(nph, bool)
+    for k in range(nb):
+        kind = "e" if (k == nb - 1 and r.random() < 0.4) else "ph"
+        nc = int(r.integers(2, max(3, min(nph, 90))))
+        mode = r.choice(["range", "scatter", "overlap"])
+        if mode == "range":
+            a = int(r.integers(0, nph - nc + 1))
+            d = list(range(a, a + nc))
+        elif mode == "scatter":
+            d = sorted(int(x) for x in r.choice(nph, nc, replace=False))
+        else:  # prefer DOFs already in a bath
+            pool = np.nonzero(used)[0]
+            take = min(len(pool), nc // 2)
+            d = set(int(x) for x in r.choice(pool, take, replace=False)) if take else set()
+            rest = [x for x in r.permutation(nph) if x not in d][: nc - len(d)]
+            d = sorted(d | set(int(x) for x in rest))
+        used[d] = True
+        if kind == "e":
+            b = synthetic.make_biased_ebath(300.0, d, nmd, r, bias=float(r.choice([0.0, 1.0])))
+        else:
+            ml = min(nmd, int(r.choice([1, 2, 3, 6, 17, 40, 96, 130])))
+            b = synthetic.make_phbath(300.0 * (1 + 0.1 * k), d, ml, nmd, r, nw=60)
+        baths.append(b)
+    constr = None
+    if r.random() < 0.4:
+        constr = sorted(set(int(x) for x in r.choice(nph, int(r.integers(1, 8)), replace=False)))
+    plan = str(r.choice(["auto", "small", "large"]))
+    far = str(r.choice(["auto", "auto", "direct", "spectral"]))
+    block_len = int(r.choice([0, 0, 1, 2, 4, 8]))
+    segs = []
+    total = 0
+    while total < nmd + 40:
+        if r.random() < 0.2:
+            k = int(r.integers(1, 4))
+            segs.append(("host", k))
+        else:
+            k = int(r.integers(1, 90))
+            segs.append(("run", k))
+        total += k
+    t0 = int(r.integers(0, nmd))
+    return dict(natom=natom, nph=nph, dyn=dyn, nmd=nmd, B=B, baths=baths, constr=constr, plan=plan, far=far,
+                block_len=block_len, segs=segs, t0=t0, seed=seed)
+
+
+def _describe(c):
+    return ("seed %d natom %d B %d nmd %d plan %s far %s block_len %d t0 %d constr %s baths %s" % (
+        c["seed"], c["natom"], c["B"], c["nmd"], c["plan"], c["far"], c["block_len"], c["t0"], c["constr"],
+        [(b.kind, b.nc, b.kernel.shape[0], getattr(b, "bias", None)) for b in c["baths"]]))
+
+
+@pytest.mark.parametrize("seed", range(NCASE))
+def test_random_configuration_vs_oracle(seed):
+    from oracle import sclmd_oracle as O
+    from sclmd_amd import _native as N
+
+    c = _case(seed)
+    desc = _describe(c)
+    B, nph, nmd, dyn, baths = c["B"], c["nph"], c["nmd"], c["dyn"], c["baths"]
+    dt = baths[0].dt
+    r = np.random.default_rng(seed)
+    try:
+        st = N.Stepper(nph, B, nmd, dt, 0, c["block_len"], c["far"], 0)
+    except Exception as e:  # noqa: BLE001
+        pytest.fail("%s: %s" % (desc, e))
+    try:
+        for b in baths:
+            if b.kind == "ebath":
+                st.add_bath(N.GLE_BATH_ELECTRON, b.cids, b.kernel, b.bias, b.exim, b.zeta1, b.zeta2)
+            else:
+                st.add_bath(N.GLE_BATH_PHONON, b.cids, b.kernel)
+        st.set_dyn(dyn)
+        if c["constr"] is not None:
+            st.set_constraint(c["constr"])
+        st.set_plan_class(c["plan"])
+        p = r.normal(size=(B, nph)) * 1e-2
+        q = r.normal(size=(B, nph)) * 1e-2
+        if c["constr"] is not None:
+            p[:, c["constr"]] = 0.0
+            q[:, c["constr"]] = 0.0
+        noise = [r.normal(size=(B, nmd, b.nc)) * 1e-3 for b in baths]
+        hist = [r.normal(size=(B, b.kernel.shape[0], b.nc)) * 1e-2 for b in baths]
+        st.set_state(p, q, c["t0"])
+        for i in range(len(baths)):
+            st.set_history(i, hist[i])
+            st.set_noise(i, noise[i])
+        ob = [O.Bath("e", b.cids, b.kernel, noise[i], dt, nmd, bias=b.bias, exim=b.exim, zeta1=b.zeta1,
+                     zeta2=b.zeta2) if b.kind == "ebath" else O.Bath("ph", b.cids, b.kernel, noise[i], dt, nmd)
+              for i, b in enumerate(baths)]
+        sim = O.GLEBatch(nph, dt, nmd, ob, dyn, ntr=B,
+                         constr=None if c["constr"] is None else [range(x, x + 1) for x in c["constr"]])
+        sim.p, sim.q, sim.t = p.T.copy(), q.T.copy(), c["t0"]
+        for i in range(len(baths)):
+            sim.set_history(i, hist[i])
+        nst = 0
+        for kind, k in c["segs"]:
+            if kind == "run":
+                st.run(k)
+                for _ in range(k):
+                    sim.step()
+            else:
+                for _ in range(k):
+                    qt = st.step_begin(-(st.get_state()[1] @ dyn.T))
+                    st.step_end(-(qt @ dyn.T))
+                    sim.step()
+            nst += k
+        pg, qg, t = st.get_state()
+        cur = st.get_current()
+    finally:
+        st.close()
+    assert t == c["t0"] + nst, desc
+    assert rel(qg, sim.q.T) < TOL and rel(pg, sim.p.T) < TOL, (desc, rel(qg, sim.q.T), rel(pg, sim.p.T))
+    # currents of the last nmd steps (older ones are overwritten by the ring of nmd entries)
+    steps = (c["t0"] + np.arange(max(0, nst - nmd), nst)) % nmd
+    want = np.stack([cc[:, steps] for cc in sim.cur])
+    assert rel(cur[:, :, steps], want) < TOL, desc

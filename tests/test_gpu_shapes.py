@@ -174,3 +174,15 @@ def test_widest_composed_audit_replays_vs_oracle():
     C._check(st, sim, 45)
     assert st.cache_audit()[0] >= 2
     st.close()
+
+
+@pytest.mark.parametrize("plan_class,scatter", [("small", "overlap"), ("large", "overlap"), ("small", None),
+                                                ("large", None)])
+def test_device_steps_after_host_force_with_constraints(plan_class, scatter):
+    """Device steps after steps with a host force, with constrained DOFs: md.potforce's cache then holds
+    the host's force at q~, and the next device step's id0 call at q_{t+1} (q~ with the constrained
+    DOFs zeroed) must miss it.  The velocity stage used to leave that step's cache distance unwritten
+    after a host force, so the device reused the force at q~ (1e-5 error; found by
+    tests/test_gpu_fuzz.py).  Three-launch (overlapping baths), fused and composed plans."""
+    for B in (3, 40):
+        _run(B, plan_class, constr=[0, 1, 2, 60, 61, 119], scatter=scatter)
