@@ -2,17 +2,21 @@
 ensemble width, memory lengths, DOF maps, bath kinds and bias, constraints, far mode, first block
 length, composed or two-launch steps, host-force segments), and a fixed list of cases samples their
 combinations.  Each case draws a junction (chain or chain + long-range couplings), 1-3 baths on
-random DOF sets (contiguous, scattered, overlapping), B in [1, 70], ml in [1, 130], then runs a random
-sequence of device runs and host-force steps over more than nmd steps (noise wrap-around) from a
-nonzero t0 and history, against oracle.GLEBatch at 1e-9 on p, q and the heat currents.  A failing
+random DOF sets (contiguous, scattered, overlapping), B in [1, 70], ml in [1, 130], sometimes
+near-rest trajectories (md.potforce's 1e-9 cache reuse), then runs a random sequence of device runs,
+host-force steps and new noise realisations over more than nmd steps (noise wrap-around) from a
+nonzero t0 and history, against oracle.GLEBatch at 1e-9 on p, q, the heat currents and the kinetic
+energy.  A failing
 case prints its parameters (case index = seed)."""
+import os
+
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
 TOL = 1e-9
-NCASE = 40
+NCASE = int(os.environ.get("SCLMD_FUZZ_CASES", "60"))  # a wider sweep: SCLMD_FUZZ_CASES=300
 
 
 def rel(a, b):
@@ -70,21 +74,35 @@ def _case(seed):
     segs = []
     total = 0
     while total < nmd + 40:
-        if r.random() < 0.2:
+        u = r.random()
+        if u < 0.2:
             k = int(r.integers(1, 4))
             segs.append(("host", k))
+        elif u < 0.27:  # a new noise realisation (md.py:569-570)
+            k = 0
+            segs.append(("noise", 0))
         else:
             k = int(r.integers(1, 90))
             segs.append(("run", k))
         total += k
+    # near-rest trajectories: zero state and history, noise 1e-16 from step `kick` on (md.potforce's
+    # 1e-9 cache reuse at points that are not q0; the composed step's audit and replay)
+    rest = []
+    if r.random() < 0.25:
+        rest = sorted(set(int(x) for x in r.choice(B, int(r.integers(1, min(B, 3) + 1)), replace=False)))
+    kick = int(r.integers(0, nmd))
+    if rest:  # host-force steps take the force as given; md.potforce's cache in front of a host driver is
+        # the md layer's (md.py's per-trajectory sameq), so near-rest cases step on the device only
+        segs = [("run", k) if kind == "host" else (kind, k) for kind, k in segs]
     t0 = int(r.integers(0, nmd))
     return dict(natom=natom, nph=nph, dyn=dyn, nmd=nmd, B=B, baths=baths, constr=constr, plan=plan, far=far,
-                block_len=block_len, segs=segs, t0=t0, seed=seed)
+                block_len=block_len, segs=segs, t0=t0, seed=seed, rest=rest, kick=kick)
 
 
 def _describe(c):
-    return ("seed %d natom %d B %d nmd %d plan %s far %s block_len %d t0 %d constr %s baths %s" % (
-        c["seed"], c["natom"], c["B"], c["nmd"], c["plan"], c["far"], c["block_len"], c["t0"], c["constr"],
+    return ("seed %d natom %d B %d nmd %d plan %s far %s block_len %d t0 %d constr %s rest %s kick %d baths %s" % (
+        c["seed"], c["natom"], c["B"], c["nmd"], c["plan"], c["far"], c["block_len"], c["t0"], c["constr"], c["rest"],
+        c["kick"],
         [(b.kind, b.nc, b.kernel.shape[0], getattr(b, "bias", None)) for b in c["baths"]]))
 
 
@@ -117,8 +135,20 @@ def test_random_configuration_vs_oracle(seed):
         if c["constr"] is not None:
             p[:, c["constr"]] = 0.0
             q[:, c["constr"]] = 0.0
-        noise = [r.normal(size=(B, nmd, b.nc)) * 1e-3 for b in baths]
+        def draw_noise():
+            out = [r.normal(size=(B, nmd, b.nc)) * 1e-3 for b in baths]
+            for n in out:
+                n[c["rest"]] = 0.0
+                for j in c["rest"]:
+                    n[j, (c["t0"] + c["kick"]) % nmd:] = 1e-16
+            return out
+
+        noise = draw_noise()
         hist = [r.normal(size=(B, b.kernel.shape[0], b.nc)) * 1e-2 for b in baths]
+        p[c["rest"]] = 0.0
+        q[c["rest"]] = 0.0
+        for h in hist:
+            h[c["rest"]] = 0.0
         st.set_state(p, q, c["t0"])
         for i in range(len(baths)):
             st.set_history(i, hist[i])
@@ -137,6 +167,11 @@ def test_random_configuration_vs_oracle(seed):
                 st.run(k)
                 for _ in range(k):
                     sim.step()
+            elif kind == "noise":
+                noise = draw_noise()
+                for i in range(len(baths)):
+                    st.set_noise(i, noise[i])
+                    ob[i].noise = noise[i]
             else:
                 for _ in range(k):
                     qt = st.step_begin(-(st.get_state()[1] @ dyn.T))
@@ -145,6 +180,7 @@ def test_random_configuration_vs_oracle(seed):
             nst += k
         pg, qg, t = st.get_state()
         cur = st.get_current()
+        en = st.get_energy()
     finally:
         st.close()
     assert t == c["t0"] + nst, desc
@@ -153,3 +189,4 @@ def test_random_configuration_vs_oracle(seed):
     steps = (c["t0"] + np.arange(max(0, nst - nmd), nst)) % nmd
     want = np.stack([cc[:, steps] for cc in sim.cur])
     assert rel(cur[:, :, steps], want) < TOL, desc
+    assert rel(en[:, steps], sim.etot[:, steps]) < TOL, desc
