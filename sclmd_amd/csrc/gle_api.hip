@@ -4196,7 +4196,7 @@ int gle_noise_generate(gle_handle* h, int32_t bath, const double* x_host, uint64
     tfree(d_items);
     if (frc) {
       cleanup();
-      return fail(h, GLE_ERR_UNSUP, "device noise FFT needs nmd a power of two <= 8192 (got " + std::to_string(h->nmd) + ")");
+      return fail(h, GLE_ERR_HIP, "device noise FFT: transform launch or work buffers failed (nmd " + std::to_string(h->nmd) + ")");
     }
     if (e != hipSuccess) {
       cleanup();
@@ -4318,7 +4318,7 @@ int stream_finish(gle_handle* h, Bath& b) {
                                    b.s_complex ? 1 : 0, scale, h->stream);
   const hipError_t e = hipStreamSynchronize(h->stream);
   free_stream(b);
-  if (frc) return fail(h, GLE_ERR_UNSUP, "device noise FFT needs nmd a power of two <= 8192");
+  if (frc) return fail(h, GLE_ERR_HIP, "device noise FFT: transform launch or work buffers failed");
   if (e != hipSuccess) return fail(h, GLE_ERR_HIP, std::string("noise stream: ") + hipGetErrorString(e));
   b.noise_set = true;
   h->x_live = false;  // V0 / W1 carry the noise
@@ -4962,8 +4962,8 @@ int gle_power_spectrum(gle_handle* h, int32_t ngroup, const int64_t* group_len, 
     HIPCHK(h, hipMemcpyAsync(d_dofs.p, dofs, off[ngroup] * 8, hipMemcpyHostToDevice, h->stream));
   sync_bg(h);
   if (launch_power(h->d_rec_p, h->nph, (int)h->B, h->nmd, ngroup, (const int64_t*)d_off.p, (const int64_t*)d_dofs.p,
-                   h->d_tw, (double*)d_out.p, h->stream))
-    return fail(h, GLE_ERR_UNSUP, "device power spectrum needs nmd a power of two <= 8192");
+                   h->d_tw, (double*)d_out.p, h->stream, off[ngroup]))
+    return fail(h, GLE_ERR_HIP, "device power spectrum: transform launch or work buffers failed");
   HIPCHK(h, hipMemcpyAsync(out, d_out.p, no * 8, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return GLE_OK;

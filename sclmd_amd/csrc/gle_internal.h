@@ -481,7 +481,7 @@ int launch_far_ifft(const double* Y, int64_t yfstride, int64_t ysplit, int nc, i
                     int64_t ldout, const double* cstab, int cstride, hipStream_t s, int k0 = 0, int k1 = -1);
 // velocity power spectra of recorded series (functions.powerspecp): out [ngroup][B][nmd]
 int launch_power(const double* ps, int64_t nph, int B, int64_t nmd, int ngroup, const int64_t* goff,
-                 const int64_t* dofs, const double* tw, double* out, hipStream_t s);
+                 const int64_t* dofs, const double* tw, double* out, hipStream_t s, int64_t nentry);
 int launch_fft_noise(const double* a, double* noise, const double* tw, int64_t nmd, int64_t nc,
                      int64_t arows, int64_t B, int is_complex, double scale, hipStream_t s);
 // memory-kernel construction (gle_gmem.hip): out[b o_blk + i o_row + l] = sum_g W[i][g] G[b g_blk + g g_row + l]

@@ -461,11 +461,262 @@ __global__ __launch_bounds__(256) void fft_noise_kernel(const double* __restrict
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Transforms of any length (nmd not a power of two <= 8192: numpy's FFT takes any length, and the
+// reference's noise needs only an even nmd, functions.py:47-50; examples/current-induced/rundp.py
+// runs nmd = 2 10^5).  Batched complex forward DFT X[k] = sum_n x[n] e^{-2 pi i n k / N} of S
+// series (series c at c ld): Stockham autosort passes of radix 8, 4, 2, 3, 5, 7 in global memory --
+// the pass of radix R after sub-transforms of length p: thread i < N / R reads x[i + q N / R],
+// multiplies by e^{-2 pi i q (i mod p) / (p R)} and writes its R-point DFT to
+// (i - i mod p) R + i mod p + m p -- and any other prime factor through Bluestein's chirp-z with a
+// power-of-two transform of length M >= 2N - 1 (n k = (n^2 + k^2 - (k - n)^2) / 2).  Setup work,
+// once per noise realisation or power spectrum.
+namespace {
+__device__ __forceinline__ double2 zmul(double2 a, double2 b) {
+  return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+
+template <int R>
+__global__ __launch_bounds__(256) void gfft_pass_kernel(const double2* __restrict__ in, double2* __restrict__ out,
+                                                        int64_t N, int64_t ld, int64_t p, int64_t total) {
+  const int64_t T = N / R, pr = p * R;
+  double2 wr[R];
+#pragma unroll
+  for (int e = 0; e < R; ++e) {
+    double sn, cs;
+    sincospi(-2.0 * (double)e / (double)R, &sn, &cs);
+    wr[e] = make_double2(cs, sn);
+  }
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total; g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = g / T, i = g - c * T;
+    const double2* x = in + c * ld;
+    double2* y = out + c * ld;
+    const int64_t k = i % p;
+    double2 v[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) v[q] = x[i + q * T];
+#pragma unroll
+    for (int q = 1; q < R; ++q) {
+      double sn, cs;
+      sincospi(-2.0 * (double)((q * k) % pr) / (double)pr, &sn, &cs);
+      v[q] = zmul(v[q], make_double2(cs, sn));
+    }
+    const int64_t j = (i - k) * R + k;
+#pragma unroll
+    for (int m = 0; m < R; ++m) {
+      double2 acc = v[0];
+#pragma unroll
+      for (int q = 1; q < R; ++q) {
+        const double2 t = zmul(v[q], wr[(q * m) % R]);
+        acc.x += t.x;
+        acc.y += t.y;
+      }
+      y[j + m * p] = acc;
+    }
+  }
+}
+
+// chirp w_n = e^{-i pi (n^2 mod 2N) / N}
+__device__ __forceinline__ double2 chirp(int64_t n, int64_t N) {
+  double sn, cs;
+  sincospi(-(double)((n * n) % (2 * N)) / (double)N, &sn, &cs);
+  return make_double2(cs, sn);
+}
+
+// x[c][n] *= w_n (n < N), 0 for N <= n < M
+__global__ void gblue_pre_kernel(double2* x, int64_t N, int64_t M, int64_t S) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < S * M; g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t n = g % M;
+    x[g] = n < N ? zmul(x[g], chirp(n, N)) : make_double2(0.0, 0.0);
+  }
+}
+
+// b[m] = conj(w_m) for m < N, conj(w_{M - m}) for m > M - N, else 0 (the circular kernel)
+__global__ void gblue_chirp_kernel(double2* b, int64_t N, int64_t M) {
+  for (int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; m < M; m += (int64_t)gridDim.x * blockDim.x) {
+    double2 v = make_double2(0.0, 0.0);
+    if (m < N) v = chirp(m, N);
+    else if (m > M - N) v = chirp(M - m, N);
+    b[m] = make_double2(v.x, -v.y);
+  }
+}
+
+// a = conj(a bh): the inverse transform of a bh as a forward one of its conjugate
+__global__ void gblue_mid_kernel(double2* a, const double2* __restrict__ bh, int64_t M, int64_t S) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < S * M; g += (int64_t)gridDim.x * blockDim.x) {
+    const double2 v = zmul(a[g], bh[g % M]);
+    a[g] = make_double2(v.x, -v.y);
+  }
+}
+
+// X[c][k] = conj(c[k]) w_k / M, k < N
+__global__ void gblue_post_kernel(double2* x, int64_t N, int64_t M, int64_t S) {
+  const double inv = 1.0 / (double)M;
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < S * N; g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = g / N, k = g - c * N;
+    const double2 v = x[c * M + k];
+    const double2 r = zmul(make_double2(v.x, -v.y), chirp(k, N));
+    x[c * M + k] = make_double2(r.x * inv, r.y * inv);
+  }
+}
+
+unsigned grid_of(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 1 << 16)); }
+
+struct Gfft {
+  int64_t N = 0, M = 0;  // M > 0: Bluestein with transforms of length M
+  std::vector<int> rad, radM;
+  double2* bh = nullptr;  // transform of the circular chirp kernel (Bluestein)
+  int64_t ld() const { return M ? M : N; }
+};
+
+std::vector<int> gfft_radices(int64_t N, int64_t* rest) {
+  std::vector<int> r;
+  for (int q : {8, 4, 2, 3, 5, 7})
+    while (N % q == 0) {
+      r.push_back(q);
+      N /= q;
+    }
+  *rest = N;
+  return r;
+}
+
+// S series of length N at stride ld, x -> (x or y): the buffer holding the result
+double2* gfft_mixed(double2* x, double2* y, int64_t S, int64_t N, int64_t ld, const std::vector<int>& rad,
+                    hipStream_t s) {
+  int64_t p = 1;
+  const unsigned grid = grid_of(S * N);
+  for (int r : rad) {
+    const int64_t total = S * (N / r);
+    switch (r) {
+      case 8: gfft_pass_kernel<8><<<grid, 256, 0, s>>>(x, y, N, ld, p, total); break;
+      case 4: gfft_pass_kernel<4><<<grid, 256, 0, s>>>(x, y, N, ld, p, total); break;
+      case 2: gfft_pass_kernel<2><<<grid, 256, 0, s>>>(x, y, N, ld, p, total); break;
+      case 3: gfft_pass_kernel<3><<<grid, 256, 0, s>>>(x, y, N, ld, p, total); break;
+      case 5: gfft_pass_kernel<5><<<grid, 256, 0, s>>>(x, y, N, ld, p, total); break;
+      default: gfft_pass_kernel<7><<<grid, 256, 0, s>>>(x, y, N, ld, p, total); break;
+    }
+    std::swap(x, y);
+    p *= r;
+  }
+  return x;
+}
+
+int gfft_plan(Gfft& g, int64_t N, hipStream_t s) {
+  g.N = N;
+  int64_t rest = 1;
+  g.rad = gfft_radices(N, &rest);
+  if (rest == 1) return 0;
+  g.M = 1;
+  while (g.M < 2 * N - 1) g.M *= 2;
+  g.radM = gfft_radices(g.M, &rest);
+  double2* tmp = nullptr;
+  if (hipMalloc((void**)&g.bh, (size_t)g.M * 2 * sizeof(double2)) != hipSuccess) return -4;
+  tmp = g.bh + g.M;
+  gblue_chirp_kernel<<<grid_of(g.M), 256, 0, s>>>(g.bh, N, g.M);
+  double2* r = gfft_mixed(g.bh, tmp, 1, g.M, g.M, g.radM, s);
+  if (r != g.bh) hipMemcpyAsync(g.bh, r, (size_t)g.M * sizeof(double2), hipMemcpyDeviceToDevice, s);
+  return 0;
+}
+
+// work buffers are plain allocations released after the stream drains (setup paths; stream-ordered
+// pool allocations interleaved with the library's other allocations gave wrong noise on some runs)
+void gfft_release(Gfft& g, hipStream_t s) {
+  if (g.bh) {
+    hipStreamSynchronize(s);
+    hipFree(g.bh);
+  }
+  g.bh = nullptr;
+}
+
+// forward DFT of the S series in x (stride g.ld(), first N entries); y: scratch of the same size
+double2* gfft_exec(const Gfft& g, double2* x, double2* y, int64_t S, hipStream_t s) {
+  if (!g.M) return gfft_mixed(x, y, S, g.N, g.N, g.rad, s);
+  gblue_pre_kernel<<<grid_of(S * g.M), 256, 0, s>>>(x, g.N, g.M, S);
+  double2* a = gfft_mixed(x, y, S, g.M, g.M, g.radM, s);
+  gblue_mid_kernel<<<grid_of(S * g.M), 256, 0, s>>>(a, g.bh, g.M, S);
+  double2* c = gfft_mixed(a, a == x ? y : x, S, g.M, g.M, g.radM, s);
+  gblue_post_kernel<<<grid_of(S * g.N), 256, 0, s>>>(c, g.N, g.M, S);
+  return c;
+}
+
+// series per pass of a generic transform within a work-buffer budget (two buffers of S ld complex)
+int64_t gfft_chunk(const Gfft& g, int64_t nseries) {
+  const int64_t budget = (int64_t)1 << 30;
+  return std::max<int64_t>(1, std::min<int64_t>(nseries, budget / (2 * g.ld() * (int64_t)sizeof(double2))));
+}
+
+// the Hermitian spectra of series pairs (as fft_noise_kernel builds them) for pairs [c0, c0 + S)
+__global__ void gnoise_pack_kernel(const double* __restrict__ a, double2* __restrict__ z, int64_t N, int64_t ld,
+                                   int nc, int arows, int B, int is_complex, int64_t c0, int64_t S, int64_t nseries) {
+  const int64_t h = N / 2;
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < S * N; g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = g / N, w = g - c * N;
+    const int64_t s1 = 2 * (c0 + c), s2 = s1 + 1;
+    const bool has2 = s2 < nseries;
+    const int64_t k1 = s1 / B, b1 = s1 % B, k2 = has2 ? s2 / B : 0, b2 = has2 ? s2 % B : 0;
+    const bool cj = w > h;
+    const int64_t src = cj ? N - w : w;
+    const bool realonly = (w == 0) || (w == h);
+    double r1 = a[(src * arows + k1) * B + b1];
+    double i1 = (is_complex && !realonly) ? a[(src * arows + nc + k1) * B + b1] : 0.0;
+    double r2 = 0.0, i2 = 0.0;
+    if (has2) {
+      r2 = a[(src * arows + k2) * B + b2];
+      i2 = (is_complex && !realonly) ? a[(src * arows + nc + k2) * B + b2] : 0.0;
+    }
+    if (cj) {
+      i1 = -i1;
+      i2 = -i2;
+    }
+    z[c * ld + w] = make_double2(r1 - i2, i1 + r2);
+  }
+}
+
+__global__ void gnoise_unpack_kernel(const double2* __restrict__ z, double* __restrict__ noise, int64_t N, int64_t ld,
+                                     int nc, int B, double scale, int64_t c0, int64_t S, int64_t nseries) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < S * N; g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = g / N, t = g - c * N;
+    const int64_t s1 = 2 * (c0 + c), s2 = s1 + 1;
+    const double2 v = z[c * ld + t];
+    noise[(t * nc + s1 / B) * B + s1 % B] = v.x * scale;
+    if (s2 < nseries) noise[(t * nc + s2 / B) * B + s2 % B] = v.y * scale;
+  }
+}
+
+int launch_fft_noise_generic(const double* a, double* noise, int64_t nmd, int64_t nc, int64_t arows, int64_t B,
+                             int is_complex, double scale, hipStream_t s) {
+  Gfft g;
+  if (gfft_plan(g, nmd, s)) return -4;
+  const int64_t nseries = nc * B, npair = (nseries + 1) / 2;
+  const int64_t S = gfft_chunk(g, npair);
+  double2* buf = nullptr;
+  if (hipMalloc((void**)&buf, (size_t)2 * S * g.ld() * sizeof(double2)) != hipSuccess) {
+    gfft_release(g, s);
+    return -4;
+  }
+  for (int64_t c0 = 0; c0 < npair; c0 += S) {
+    const int64_t n = std::min(S, npair - c0);
+    gnoise_pack_kernel<<<grid_of(n * nmd), 256, 0, s>>>(a, buf, nmd, g.ld(), (int)nc, (int)arows, (int)B, is_complex,
+                                                         c0, n, nseries);
+    const double2* r = gfft_exec(g, buf, buf + S * g.ld(), n, s);
+    gnoise_unpack_kernel<<<grid_of(n * nmd), 256, 0, s>>>(r, noise, nmd, g.ld(), (int)nc, (int)B, scale, c0, n,
+                                                           nseries);
+  }
+  const hipError_t e = hipStreamSynchronize(s);
+  hipFree(buf);
+  gfft_release(g, s);
+  if (e != hipSuccess) return -5;
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+}  // namespace
+
 int launch_fft_noise(const double* a, double* noise, const double* tw, int64_t nmd, int64_t nc,
                      int64_t arows, int64_t B, int is_complex, double scale, hipStream_t s) {
   int logn = 0;
   while ((1ll << logn) < nmd) ++logn;
-  if ((1ll << logn) != nmd || logn < 1) return -1;
+  if ((1ll << logn) != nmd || nmd > 8192)  // any other even length: the global-memory transforms
+    return nmd >= 2 && nmd % 2 == 0 ? launch_fft_noise_generic(a, noise, nmd, nc, arows, B, is_complex, scale, s) : -1;
+  if (logn < 1) return -1;
   const size_t shmem = (size_t)nmd * sizeof(double2);
   if (shmem > 160 * 1024) return -2;
   if (hipFuncSetAttribute((const void*)fft_noise_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -537,11 +788,68 @@ __global__ __launch_bounds__(256) void power_kernel(const double* __restrict__ p
   }
 }
 
+// Power spectra of any length nmd (not a power of two <= 8192): each (DOF entry, trajectory) series
+// through the generic transform (gfft_exec) as a complex series with zero imaginary part, then
+// out[g][b][f] += |X(f)|^2 over the chunk's entries in entry order (one thread per (b, f):
+// deterministic).
+__global__ void gpower_pack_kernel(const double* __restrict__ ps, double2* __restrict__ z, int64_t N, int64_t ld,
+                                   int64_t nph, int B, const int64_t* __restrict__ dofs, int64_t c0, int64_t S) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < S * N; g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = g / N, t = g - c * N;
+    const int64_t e = (c0 + c) / B, b = (c0 + c) % B;
+    z[c * ld + t] = make_double2(ps[(t * nph + dofs[e]) * B + b], 0.0);
+  }
+}
+
+__global__ void gpower_acc_kernel(const double2* __restrict__ z, double* __restrict__ out, int64_t N, int64_t ld, int B,
+                                  const int64_t* __restrict__ goff, int ngroup, int64_t c0, int64_t S) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < (int64_t)B * N; g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = g / N, f = g - b * N;
+    int grp = 0;
+    for (int64_t c = 0; c < S; ++c) {
+      if ((c0 + c) % B != b) continue;
+      const int64_t e = (c0 + c) / B;
+      while (grp + 1 < ngroup && goff[grp + 1] <= e) ++grp;
+      const double2 v = z[c * ld + f];
+      out[((int64_t)grp * B + b) * N + f] += v.x * v.x + v.y * v.y;
+    }
+  }
+}
+
+int launch_power_generic(const double* ps, int64_t nph, int B, int64_t nmd, int ngroup, const int64_t* goff,
+                         const int64_t* dofs, int64_t nentry, double* out, hipStream_t s) {
+  if (hipMemsetAsync(out, 0, (size_t)ngroup * B * nmd * sizeof(double), s) != hipSuccess) return -4;
+  const int64_t nseries = nentry * B;
+  if (nseries == 0) return 0;
+  Gfft g;
+  if (gfft_plan(g, nmd, s)) return -4;
+  // whole trajectories' worth of series per chunk, so that a chunk's entries stay in order per (b, f)
+  const int64_t S = gfft_chunk(g, nseries);
+  double2* buf = nullptr;
+  if (hipMalloc((void**)&buf, (size_t)2 * S * g.ld() * sizeof(double2)) != hipSuccess) {
+    gfft_release(g, s);
+    return -4;
+  }
+  for (int64_t c0 = 0; c0 < nseries; c0 += S) {
+    const int64_t n = std::min(S, nseries - c0);
+    gpower_pack_kernel<<<grid_of(n * nmd), 256, 0, s>>>(ps, buf, nmd, g.ld(), nph, B, dofs, c0, n);
+    const double2* r = gfft_exec(g, buf, buf + S * g.ld(), n, s);
+    gpower_acc_kernel<<<grid_of((int64_t)B * nmd), 256, 0, s>>>(r, out, nmd, g.ld(), B, goff, ngroup, c0, n);
+  }
+  const hipError_t e = hipStreamSynchronize(s);
+  hipFree(buf);
+  gfft_release(g, s);
+  if (e != hipSuccess) return -5;
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 int launch_power(const double* ps, int64_t nph, int B, int64_t nmd, int ngroup, const int64_t* goff,
-                 const int64_t* dofs, const double* tw, double* out, hipStream_t s) {
+                 const int64_t* dofs, const double* tw, double* out, hipStream_t s, int64_t nentry) {
   int logn = 0;
   while ((1ll << logn) < nmd) ++logn;
-  if ((1ll << logn) != nmd || nmd > 8192 || nmd < 2) return -1;
+  if (nmd < 2) return -1;
+  if ((1ll << logn) != nmd || nmd > 8192)
+    return launch_power_generic(ps, nph, B, nmd, ngroup, goff, dofs, nentry, out, s);
   const int tw_lds = nmd <= 4096 ? 1 : 0;
   const size_t shm = (size_t)nmd * sizeof(double2) + (tw_lds ? (size_t)nmd / 2 * sizeof(double2) : 0);
   const dim3 grid((unsigned)(ngroup * B));
