@@ -81,6 +81,9 @@ def _case(seed):
         elif u < 0.27:  # a new noise realisation (md.py:569-570)
             k = 0
             segs.append(("noise", 0))
+        elif u < 0.31:  # a new state, history and step counter (a resumed run, md.py:506-567)
+            k = 0
+            segs.append(("restate", int(r.integers(0, 3 * nmd))))
         else:
             k = int(r.integers(1, 90))
             segs.append(("run", k))
@@ -161,7 +164,7 @@ def test_random_configuration_vs_oracle(seed):
         sim.p, sim.q, sim.t = p.T.copy(), q.T.copy(), c["t0"]
         for i in range(len(baths)):
             sim.set_history(i, hist[i])
-        nst = 0
+        nst, t_start = 0, c["t0"]
         for kind, k in c["segs"]:
             if kind == "run":
                 st.run(k)
@@ -172,6 +175,27 @@ def test_random_configuration_vs_oracle(seed):
                 for i in range(len(baths)):
                     st.set_noise(i, noise[i])
                     ob[i].noise = noise[i]
+            elif kind == "restate":
+                p = r.normal(size=(B, nph)) * 1e-2
+                q = r.normal(size=(B, nph)) * 1e-2
+                p[c["rest"]] = 0.0
+                q[c["rest"]] = 0.0
+                if c["constr"] is not None:
+                    p[:, c["constr"]] = 0.0
+                    q[:, c["constr"]] = 0.0
+                hist = [r.normal(size=(B, b.kernel.shape[0], b.nc)) * 1e-2 for b in baths]
+                for h in hist:
+                    h[c["rest"]] = 0.0
+                st.set_state(p, q, k)
+                for i in range(len(baths)):
+                    st.set_history(i, hist[i])
+                sim = O.GLEBatch(nph, dt, nmd, ob, dyn, ntr=B,
+                                 constr=None if c["constr"] is None else [range(x, x + 1) for x in c["constr"]])
+                sim.p, sim.q, sim.t = p.T.copy(), q.T.copy(), k
+                for i in range(len(baths)):
+                    sim.set_history(i, hist[i])
+                t_start, nst = k, 0
+                continue
             else:
                 for _ in range(k):
                     qt = st.step_begin(-(st.get_state()[1] @ dyn.T))
@@ -183,10 +207,13 @@ def test_random_configuration_vs_oracle(seed):
         en = st.get_energy()
     finally:
         st.close()
-    assert t == c["t0"] + nst, desc
+    assert t == t_start + nst, desc
     assert rel(qg, sim.q.T) < TOL and rel(pg, sim.p.T) < TOL, (desc, rel(qg, sim.q.T), rel(pg, sim.p.T))
-    # currents of the last nmd steps (older ones are overwritten by the ring of nmd entries)
-    steps = (c["t0"] + np.arange(max(0, nst - nmd), nst)) % nmd
+    # currents of the last nmd steps since the last restate (older ones are overwritten by the ring of
+    # nmd entries; a restate starts a fresh oracle)
+    steps = (t_start + np.arange(max(0, nst - nmd), nst)) % nmd
+    if nst == 0:
+        return
     want = np.stack([cc[:, steps] for cc in sim.cur])
     assert rel(cur[:, :, steps], want) < TOL, desc
     assert rel(en[:, steps], sim.etot[:, steps]) < TOL, desc
