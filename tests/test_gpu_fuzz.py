@@ -5,8 +5,8 @@ combinations.  Each case draws a junction (chain or chain + long-range couplings
 random DOF sets (contiguous, scattered, overlapping), B in [1, 70], ml in [1, 130], sometimes
 near-rest trajectories (md.potforce's 1e-9 cache reuse), then runs a random sequence of device runs,
 host-force steps and new noise realisations over more than nmd steps (noise wrap-around) from a
-nonzero t0 and history, against oracle.GLEBatch at 1e-9 on p, q, the heat currents and the kinetic
-energy.  A failing
+nonzero t0 and history, against oracle.GLEBatch at 1e-9 on p, q, the heat currents, the kinetic
+energy and the recordings (ps, qs, each bath's id0 force).  A failing
 case prints its parameters (case index = seed)."""
 import os
 
@@ -102,6 +102,33 @@ def _case(seed):
                 block_len=block_len, segs=segs, t0=t0, seed=seed, rest=rest, kick=kick)
 
 
+def _rec_batch():
+    """oracle.GLEBatch that also keeps md's recordings: ps / qs (md.py:374-377) and each bath's id0
+    force fhis[i] (md.py:398), at slot t mod nmd."""
+    from oracle import sclmd_oracle as O
+
+    class RecBatch(O.GLEBatch):
+        def step(self):
+            t = int(self.t) % self.nmd
+            if not hasattr(self, "rps"):
+                self.rps = np.zeros((self.ntr, self.nmd, self.nph))
+                self.rqs = np.zeros((self.ntr, self.nmd, self.nph))
+                self.rf = [np.zeros((self.ntr, self.nmd, b.nc)) for b in self.baths]
+            self.rps[:, t] = self.p.T
+            self.rqs[:, t] = self.q.T
+            self._seen = set()
+            super().step()
+
+        def _bath_force(self, i, t_noise, S, x, qarg):
+            f = super()._bath_force(i, t_noise, S, x, qarg)
+            if i not in self._seen:  # the step's first call per bath is md.force id0
+                self._seen.add(i)
+                self.rf[i][:, int(self.t) % self.nmd] = f.T
+            return f
+
+    return RecBatch
+
+
 def _describe(c):
     return ("seed %d natom %d B %d nmd %d plan %s far %s block_len %d t0 %d constr %s rest %s kick %d baths %s" % (
         c["seed"], c["natom"], c["B"], c["nmd"], c["plan"], c["far"], c["block_len"], c["t0"], c["constr"], c["rest"],
@@ -159,9 +186,11 @@ def test_random_configuration_vs_oracle(seed):
         ob = [O.Bath("e", b.cids, b.kernel, noise[i], dt, nmd, bias=b.bias, exim=b.exim, zeta1=b.zeta1,
                      zeta2=b.zeta2) if b.kind == "ebath" else O.Bath("ph", b.cids, b.kernel, noise[i], dt, nmd)
               for i, b in enumerate(baths)]
-        sim = O.GLEBatch(nph, dt, nmd, ob, dyn, ntr=B,
-                         constr=None if c["constr"] is None else [range(x, x + 1) for x in c["constr"]])
+        Rec = _rec_batch()
+        sim = Rec(nph, dt, nmd, ob, dyn, ntr=B,
+                  constr=None if c["constr"] is None else [range(x, x + 1) for x in c["constr"]])
         sim.p, sim.q, sim.t = p.T.copy(), q.T.copy(), c["t0"]
+        st.record(N.REC_P | N.REC_Q | N.REC_F)
         for i in range(len(baths)):
             sim.set_history(i, hist[i])
         nst, t_start = 0, c["t0"]
@@ -189,8 +218,8 @@ def test_random_configuration_vs_oracle(seed):
                 st.set_state(p, q, k)
                 for i in range(len(baths)):
                     st.set_history(i, hist[i])
-                sim = O.GLEBatch(nph, dt, nmd, ob, dyn, ntr=B,
-                                 constr=None if c["constr"] is None else [range(x, x + 1) for x in c["constr"]])
+                sim = Rec(nph, dt, nmd, ob, dyn, ntr=B,
+                          constr=None if c["constr"] is None else [range(x, x + 1) for x in c["constr"]])
                 sim.p, sim.q, sim.t = p.T.copy(), q.T.copy(), k
                 for i in range(len(baths)):
                     sim.set_history(i, hist[i])
@@ -205,6 +234,7 @@ def test_random_configuration_vs_oracle(seed):
         pg, qg, t = st.get_state()
         cur = st.get_current()
         en = st.get_energy()
+        rec = (st.get_record(N.REC_P), st.get_record(N.REC_Q), [st.get_record(N.REC_F, i) for i in range(len(baths))])
     finally:
         st.close()
     assert t == t_start + nst, desc
@@ -217,3 +247,7 @@ def test_random_configuration_vs_oracle(seed):
     want = np.stack([cc[:, steps] for cc in sim.cur])
     assert rel(cur[:, :, steps], want) < TOL, desc
     assert rel(en[:, steps], sim.etot[:, steps]) < TOL, desc
+    # recordings (gle_record): ps / qs and the bath forces of md.force id0
+    assert rel(rec[0][:, steps], sim.rps[:, steps]) < TOL and rel(rec[1][:, steps], sim.rqs[:, steps]) < TOL, desc
+    for i in range(len(baths)):
+        assert rel(rec[2][i][:, steps], sim.rf[i][:, steps]) < TOL, (desc, "fhis", i)
