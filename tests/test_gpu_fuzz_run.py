@@ -1,0 +1,130 @@
+"""Seeded random md.Run configurations against the oracle's restatement of the reference's run
+(md.py:493-682 as in tests/test_oracle_golden.py::test_oracle_matches_reference_run): the drop-in
+md API with the numpy-compatible noise (np.random.seed, the reference's RandomState draws in the
+reference's order: initialise, then per run each bath's gnoi) against oracle.initial_state +
+oracle.phnoise / enoise + the reference-shaped oracle.GLE stepping and the per-run kappa.  Each case
+draws a chain junction, 1-3 baths (phonon baths with gamma spectra, ml in [1, 40], electron baths
+with random exim / exip, biased or not), constraints, nrun in [1, 3], npie and an even nmd that is
+sometimes not a power of two (the device noise then takes the mixed-radix / Bluestein transforms).
+1e-9 relative on the final p, q and on every run's kappa."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+NCASE = int(os.environ.get("SCLMD_FUZZ_RUNS", "16"))  # a wider sweep: SCLMD_FUZZ_RUNS=120
+
+
+def rel(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
+
+
+def _case(seed):
+    r = np.random.default_rng(5000 + seed)
+    natom = int(r.integers(4, 20))
+    nph = 3 * natom
+    nmd = int(r.choice([64, 100, 128, 2 * 97, 256]))
+    npie = int(r.choice([1, 2, 4]))
+    while nmd % npie:
+        npie //= 2
+    nrun = int(r.integers(1, 4))
+    baths = []
+    for k in range(int(r.integers(1, 4))):
+        nc = int(r.integers(2, min(nph, 24) + 1))
+        a0 = int(r.integers(0, nph - nc + 1))
+        cids = list(range(a0, a0 + nc)) if r.random() < 0.6 else sorted(int(x) for x in r.choice(nph, nc, replace=False))
+        if r.random() < 0.4:
+            n = nc
+            s = 1e-3
+            baths.append(dict(kind="e", cids=cids, T=300.0 * (1 + 0.05 * k),
+                              efric=np.eye(n) * 1e-2 + s * (lambda m: m @ m.T / n)(r.normal(size=(n, n))),
+                              exim=s * r.normal(size=(n, n)), exip=s * r.normal(size=(n, n)),
+                              zeta1=s * r.normal(size=(n, n)), zeta2=s * r.normal(size=(n, n)),
+                              bias=float(r.choice([0.0, 0.5])), wmax=1.0, nw=50))
+        else:
+            ngw = 41
+            gwl = np.linspace(0.0, 0.5, ngw)
+            A = r.normal(size=(nc, nc))
+            A = A @ A.T / nc + np.eye(nc)
+            gam = (0.658 / 100.0) * np.exp(-(gwl / 0.1) ** 2)[:, None, None] * A[None]
+            baths.append(dict(kind="ph", cids=cids, T=300.0 * (1 + 0.05 * k), gam=gam, gwl=gwl, debye=0.2,
+                              nw=int(r.integers(20, 80)), ml=int(r.choice([1, 2, 5, 16, 40]))))
+    constr = None
+    if r.random() < 0.5:
+        c0 = int(r.integers(0, nph - 3))
+        constr = [range(c0, c0 + int(r.integers(1, 4)))]
+    return dict(natom=natom, nph=nph, nmd=nmd, npie=npie, nrun=nrun, baths=baths, constr=constr, seed=seed,
+                np_seed=int(r.integers(0, 2 ** 31)))
+
+
+def _describe(c):
+    return "seed %d natom %d nmd %d npie %d nrun %d constr %s baths %s" % (
+        c["seed"], c["natom"], c["nmd"], c["npie"], c["nrun"], c["constr"],
+        [(b["kind"], len(b["cids"]), b.get("ml", 1), b.get("bias")) for b in c["baths"]])
+
+
+def _oracle_run(c, dyn, dt, T):
+    from oracle import sclmd_oracle as O
+
+    np.random.seed(c["np_seed"])
+    p0, q0, dyn_used = O.initial_state(dyn, T, c["constr"])
+    obs = []
+    for b in c["baths"]:
+        if b["kind"] == "ph":
+            wl = [2.0 * b["debye"] * i / b["nw"] for i in range(b["nw"])]
+            k, _ = O.gmem(b["ml"], dt, wl, b["gwl"], b["gam"])
+            obs.append(O.Bath("ph", b["cids"], k, None, dt, c["nmd"]))
+        else:
+            obs.append(O.Bath("e", b["cids"], np.array([O.symm(b["efric"])]), None, dt, c["nmd"], bias=b["bias"],
+                              exim=O.antisymm(b["exim"]), zeta1=O.symm(b["zeta1"]), zeta2=O.antisymm(b["zeta2"])))
+    sim = O.GLE(c["nph"], dt, c["nmd"], obs, dyn=dyn_used, constr=c["constr"])
+    sim.p, sim.q = p0, q0
+    kappa = []
+    for _ in range(c["nrun"]):
+        for b, ob in zip(c["baths"], obs):
+            if b["kind"] == "ph":
+                ob.noise = np.real(O.phnoise(b["gam"], b["gwl"], b["T"], 2.0 * b["debye"], dt, c["nmd"]))
+            else:
+                ob.noise = np.real(O.enoise(O.symm(b["efric"]), O.antisymm(b["exim"]), O.symm(b["exip"]), b["bias"],
+                                            b["T"], b["wmax"], dt, c["nmd"]))
+        for _ in range(c["nmd"]):
+            sim.step()
+        kappa.append([np.mean(ob.cur) * O.CURCOF for ob in obs])
+    return sim.p, sim.q, np.array(kappa)
+
+
+@pytest.mark.parametrize("seed", range(NCASE))
+def test_random_run_vs_oracle(seed, tmp_path, monkeypatch):
+    from sclmd_amd import md as MD
+    from sclmd_amd import synthetic
+    from sclmd_amd.baths import ebath, phbath
+
+    c = _case(seed)
+    desc = _describe(c)
+    monkeypatch.chdir(tmp_path)
+    dt, T = synthetic.DT, 300.0
+    dyn = synthetic.chain_dyn(c["natom"])
+    m = MD.md(dt, c["nmd"], T, axyz=synthetic.axyz_chain(c["natom"]), dyn=dyn, nstart=0, nstop=c["nrun"],
+              npie=c["npie"], verbose=False)
+    for b in c["baths"]:
+        if b["kind"] == "ph":
+            pb = phbath(b["T"], b["cids"], debye=b["debye"], nw=b["nw"], dt=dt, nmd=c["nmd"], ml=b["ml"],
+                        gamma=b["gam"], gwl=b["gwl"])
+            pb.gmem()
+            m.AddBath(pb)
+        else:
+            m.AddBath(ebath(b["cids"], b["T"], dt, c["nmd"], wmax=b["wmax"], nw=b["nw"], bias=b["bias"], efric=b["efric"],
+                            exim=b["exim"], exip=b["exip"], zeta1=b["zeta1"], zeta2=b["zeta2"]))
+    if c["constr"] is not None:
+        m.AddConstr(c["constr"])
+    np.random.seed(c["np_seed"])
+    m.Run()
+    p, q, kap, t = np.array(m.p), np.array(m.q), np.array(m.kappa_runs), m.t
+    m.close()
+    wp, wq, wk = _oracle_run(c, dyn, dt, T)
+    assert t == c["nrun"] * c["nmd"], desc
+    assert rel(q, wq) < 1e-9 and rel(p, wp) < 1e-9, (desc, rel(q, wq), rel(p, wp))
+    assert rel(kap, wk) < 1e-9, (desc, kap, wk)
