@@ -251,3 +251,57 @@ def test_random_configuration_vs_oracle(seed):
     assert rel(rec[0][:, steps], sim.rps[:, steps]) < TOL and rel(rec[1][:, steps], sim.rqs[:, steps]) < TOL, desc
     for i in range(len(baths)):
         assert rel(rec[2][i][:, steps], sim.rf[i][:, steps]) < TOL, (desc, "fhis", i)
+
+
+def test_interleaved_handles_vs_oracle():
+    """Three live handles of different shapes (plan classes, widths, nmd) on one device, stepped in
+    interleaved calls: no state leaks between handles (launch attributes, streams, audit words)."""
+    from oracle import sclmd_oracle as O
+    from sclmd_amd import _native as N
+
+    cases = [_case(s) for s in (3, 7, 11)]
+    live = []
+    try:
+        for c in cases:
+            B, nph, nmd, dyn, baths = c["B"], c["nph"], c["nmd"], c["dyn"], c["baths"]
+            dt = baths[0].dt
+            r = np.random.default_rng(c["seed"] + 99)
+            st = N.Stepper(nph, B, nmd, dt, 0, c["block_len"], c["far"], 0)
+            for b in baths:
+                if b.kind == "ebath":
+                    st.add_bath(N.GLE_BATH_ELECTRON, b.cids, b.kernel, b.bias, b.exim, b.zeta1, b.zeta2)
+                else:
+                    st.add_bath(N.GLE_BATH_PHONON, b.cids, b.kernel)
+            st.set_dyn(dyn)
+            st.set_plan_class(c["plan"])
+            p = r.normal(size=(B, nph)) * 1e-2
+            q = r.normal(size=(B, nph)) * 1e-2
+            noise = [r.normal(size=(B, nmd, b.nc)) * 1e-3 for b in baths]
+            st.set_state(p, q, 0)
+            for i in range(len(baths)):
+                st.set_noise(i, noise[i])
+            ob = [O.Bath("e", b.cids, b.kernel, noise[i], dt, nmd, bias=b.bias, exim=b.exim, zeta1=b.zeta1,
+                         zeta2=b.zeta2) if b.kind == "ebath" else O.Bath("ph", b.cids, b.kernel, noise[i], dt, nmd)
+                  for i, b in enumerate(baths)]
+            sim = O.GLEBatch(nph, dt, nmd, ob, dyn, ntr=B)
+            sim.p, sim.q = p.T.copy(), q.T.copy()
+            live.append((st, sim, dyn))
+        rr = np.random.default_rng(0)
+        for _ in range(12):
+            for st, sim, dyn in live:
+                k = int(rr.integers(1, 40))
+                if rr.random() < 0.2:
+                    for _ in range(k % 3 + 1):
+                        qt = st.step_begin(-(st.get_state()[1] @ dyn.T))
+                        st.step_end(-(qt @ dyn.T))
+                        sim.step()
+                else:
+                    st.run(k)
+                    for _ in range(k):
+                        sim.step()
+        for st, sim, _ in live:
+            pg, qg, _ = st.get_state()
+            assert rel(qg, sim.q.T) < TOL and rel(pg, sim.p.T) < TOL
+    finally:
+        for st, _, _ in live:
+            st.close()
