@@ -49,7 +49,8 @@ typedef struct gle_handle gle_handle;
 typedef struct gle_config {
     int64_t nph;        /* system degrees of freedom, md.nph (md.py:86)                      */
     int64_t ntraj;      /* independent trajectories batched on this device (ensemble size)   */
-    int64_t nmd;        /* MD steps per run = noise period, md.nmd (md.py:59); even          */
+    int64_t nmd;        /* MD steps per run = noise period, md.nmd (md.py:59); even (any even */
+                        /* length: powers of two <= 8192 in LDS, others in global memory)    */
     double dt;          /* MD time step, md.dt (md.py:59)                                    */
     int32_t device;     /* HIP device ordinal                                                */
     int32_t block_len;  /* P0: first block length of the memory-sum ladder (near field = lags
