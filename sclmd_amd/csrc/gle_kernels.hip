@@ -806,8 +806,7 @@ __global__ void gpower_acc_kernel(const double2* __restrict__ z, double* __restr
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < (int64_t)B * N; g += (int64_t)gridDim.x * blockDim.x) {
     const int64_t b = g / N, f = g - b * N;
     int grp = 0;
-    for (int64_t c = 0; c < S; ++c) {
-      if ((c0 + c) % B != b) continue;
+    for (int64_t c = (b - c0 % B + B) % B; c < S; c += B) {  // the chunk's series of trajectory b
       const int64_t e = (c0 + c) / B;
       while (grp + 1 < ngroup && goff[grp + 1] <= e) ++grp;
       const double2 v = z[c * ld + f];

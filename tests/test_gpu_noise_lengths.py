@@ -136,3 +136,53 @@ def test_md_run_nmd_1000_device_noise(tmp_path, monkeypatch):
     p0, q0, _ = run(4, 0)
     p1, q1, _ = run(2, 4)
     assert rel(np.concatenate([q0, q1]), q) < 1e-9 and rel(np.concatenate([p0, p1]), p) < 1e-9
+
+
+def test_generic_transforms_chunked_equal_unchunked():
+    """Above ~1 GiB of work buffers the generic transforms run in chunks of series: a 64-trajectory
+    ensemble at nmd = 24576 (2 noise chunks) and its power spectrum at nmd = 12288 (2 chunks) equal
+    the same trajectories transformed one at a time (one chunk each)."""
+    from sclmd_amd import _native as N
+    from sclmd_amd import noise as Nz
+    from sclmd_amd import synthetic
+
+    rng = np.random.default_rng(8)
+    nmd, B, nc = 24576, 64, 60
+    gwl, gam = synthetic.gamma_spectrum(nc, rng)
+    fac = Nz.NoiseFactor(Nz.phonon_spectrum(gam, gwl, 300.0, 0.4, synthetic.DT, nmd))
+    x = np.stack([fac.draws(np.random.RandomState(100 + b)) for b in range(B)])
+
+    def gen(xs):
+        st = N.Stepper(nc, len(xs), nmd, synthetic.DT, 0)
+        st.add_bath(N.GLE_BATH_PHONON, np.arange(nc), np.zeros((1, nc, nc)))
+        st.noise_factors(0, fac.evecs)
+        st.noise_generate(0, xs)
+        out = st.get_noise(0)
+        st.close()
+        return out
+
+    whole = gen(x)
+    for b in (0, 31, 63):
+        assert rel(gen(x[b:b + 1])[0], whole[b]) < 1e-13, b
+
+    nmd = 12288
+    dyn, _, baths, meta = synthetic.junction("C3", natom=20, ml=4, nmd=nmd, nw=40, seed=2)
+    nph = meta["nph"]
+    r = np.random.default_rng(3)
+    st = N.Stepper(nph, B, nmd, meta["dt"], 0)
+    for b in baths:
+        st.add_bath(N.GLE_BATH_PHONON, b.cids, b.kernel)
+    st.set_dyn(dyn)
+    st.set_state(r.normal(size=(B, nph)) * 1e-2, r.normal(size=(B, nph)) * 1e-2, 0)
+    for i, b in enumerate(baths):
+        st.set_noise(i, r.normal(size=(B, nmd, b.nc)) * 1e-3)
+    st.record(N.REC_P)
+    st.run(nmd)
+    groups = [list(range(0, nph, 2)), list(range(1, nph, 2))]
+    got = st.power_spectrum(groups)  # 64 x 60 series of 12288: two chunks
+    ps = st.get_record(N.REC_P)
+    st.close()
+    for b in (0, 40):
+        X = np.fft.fft(ps[b], axis=0)
+        want = np.stack([np.sum(np.abs(X[:, g]) ** 2, axis=1) for g in groups])
+        assert rel(got[:, b], want) < 1e-12, b
