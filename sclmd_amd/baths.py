@@ -15,6 +15,11 @@ from . import units as U
 from .functions import antisymmetrize, chkShape, flinterp_many, interp_weights, symmetrize
 
 
+def exlist(a, indices):
+    """The rows of a at the given indices (baths.py:12-14)."""
+    return np.asarray(a)[indices]
+
+
 def gamt(tl, wl, gwl, gam, eta_ad=0):
     """Friction kernel in time, K(t) = (2 wl[-1]/pi) mean_w Gamma(w) cos(w t) (baths.py:19-52),
     evaluated as one matrix product cos(w t) . Gamma(w) over all times and frequencies."""
@@ -241,6 +246,18 @@ class ebath(_BathBase):
                 if chkShape(m) != self.nc:
                     raise ValueError("ebath.CheckEmat: the dimension of %s is wrong" % name)
                 setattr(self, name, op(m))
+
+    def GetSig(self):
+        """Effective retarded self-energy in the wide-band limit on the frequencies wl
+        (baths.py:194-208): sig(w) = -i w (efric + bias zeta2) + bias zeta1 - bias exim."""
+        if self.wl is None:
+            raise ValueError("ebath.GetSig: wl is not set")
+        z = np.zeros((self.nc, self.nc))
+        e = lambda m: z if m is None else np.asarray(m)  # noqa: E731
+        v = float(self.bias)
+        self.sig = np.array([-1j * w * (e(self.efric) + v * e(self.zeta2)) + v * e(self.zeta1) - v * e(self.exim)
+                             for w in self.wl], dtype=complex).reshape(len(self.wl), self.nc, self.nc)
+        return self.sig
 
     def setbias(self, bias=0.0):
         self.bias = bias

@@ -18,6 +18,26 @@ def bose(w, T):
         return 1.0 / (np.exp(w / U.kb / T) - 1.0)
 
 
+def coth(x):
+    """Hyperbolic cotangent (functions.py:59-67); coth(0) raises (the reference exits)."""
+    if x == 0.0:
+        raise ValueError("coth: coth(0) is infinite")
+    return np.cosh(x) / np.sinh(x)
+
+
+def xcoth(x):
+    """x coth(x), 1 at x = 0 (functions.py:70-77)."""
+    return 1.0 if x == 0.0 else x * np.cosh(x) / np.sinh(x)
+
+
+def fermi(ep, mu, T):
+    """Fermi occupation; at T = 0 a step with 1/2 at ep = mu (functions.py:102-114)."""
+    if T == 0.0:
+        return 1.0 if ep < mu else (0.0 if ep > mu else 0.5)
+    with np.errstate(over="ignore"):
+        return 1.0 / (np.exp((ep - mu) / U.kb / T) + 1.0)
+
+
 def nearest(b, bs):
     """Index of the first element of bs closest to b (functions.py:137-143)."""
     return int(np.argmin(np.abs(np.asarray(bs) - b)))
@@ -71,6 +91,22 @@ def antisymmetrize(a):
     return 0.5 * (a - a.T)
 
 
+def dagger(a):
+    """Conjugate transpose of a square matrix (functions.py:189-195)."""
+    a = np.asarray(a)
+    if a.ndim != 2 or a.shape[0] != a.shape[1]:
+        raise ValueError("dagger: not a square matrix")
+    return np.conjugate(a).T
+
+
+def mm(*args):
+    """Left-to-right product of any number of matrices (functions.py:159-163)."""
+    out = np.array(args[0], copy=True)
+    for m in args[1:]:
+        out = np.dot(out, m)
+    return out
+
+
 def hermitianize(a):
     a = np.asarray(a)
     return 0.5 * (a + np.conj(np.swapaxes(a, -1, -2)))
@@ -115,3 +151,15 @@ def powerspecp(ps, dt, nmd):
     spec = (2.0 * np.pi / dw) * np.fft.ifft(ps, axis=0)
     pw = np.real(spec * np.conj(spec)).sum(axis=1) / dt / nmd
     return np.column_stack((dw * np.arange(nmd), pw))
+
+
+def powerspecq(qs, dt, nmd):
+    """Displacement power spectrum summed over DOFs (functions.py:203-218): rows [w_i, w_i^2 P_q(w_i)]
+    with P_q = sum_k |Fourier1D(qs[:, k])|^2 / (dt nmd)."""
+    qs = np.asarray(qs)
+    if qs.shape[0] != nmd:
+        raise ValueError("power: qs shape error")
+    dw = 2.0 * np.pi / dt / nmd
+    spec = (2.0 * np.pi / dw) * np.fft.ifft(qs, axis=0)
+    w = dw * np.arange(nmd)
+    return np.column_stack((w, w ** 2 * np.real(spec * np.conj(spec)).sum(axis=1) / dt / nmd))

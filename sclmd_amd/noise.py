@@ -40,6 +40,73 @@ def equ(w, cut, T, classical=False, zpmotion=True):
     return 0.0
 
 
+def _neq(w, bias, T, classical, sign):
+    """2 (hw + sign bias) (bose(hw + sign bias) - bose(hw)); classically kT / x with x = 0 moved to
+    1e-19 (noise.py:211-246)."""
+    from .functions import bose
+
+    h1, h2 = U.hbar * w + sign * bias, U.hbar * w
+    if classical:
+        h1 = h1 if h1 != 0.0 else 10e-20
+        h2 = h2 if h2 != 0.0 else 10e-20
+        return 2.0 * h1 * (U.kb * T / h1 - U.kb * T / h2)
+    return 2.0 * h1 * (bose(h1, T) - bose(h2, T))
+
+
+def nonequm(w, bias, T, classical=False):
+    """Non-equilibrium electron occupation factor at hw - bias (noise.py:211-227)."""
+    return _neq(w, bias, T, classical, -1.0)
+
+
+def nonequp(w, bias, T, classical=False):
+    """Non-equilibrium electron occupation factor at hw + bias (noise.py:230-246)."""
+    return _neq(w, bias, T, classical, 1.0)
+
+
+def phnoisew(gamma, wl, T, phcut, classical=False, zpmotion=True):
+    """Phonon noise spectrum on the frequencies wl: equ(w_i) gamma[i] (noise.py:28-47)."""
+    gamma = np.asarray(gamma)
+    out = np.zeros(gamma.shape, dtype=np.result_type(gamma, np.float64))
+    for i, w in enumerate(wl):
+        out[i] = equ(w, phcut, T, classical, zpmotion) * gamma[i]
+    return out
+
+
+def _electron_matrix(w, efric, exim, exip, bias, T, ecut, scale, classical, zpmotion):
+    """Hermitian part of the electron-bath spectral matrix at w, times `scale` (noise.py:172-186)."""
+    aw = scale * equ(w, ecut, T, classical, zpmotion)
+    awm = scale * equ(U.hbar * w - bias, ecut, T, classical, zpmotion)
+    awp = scale * equ(U.hbar * w + bias, ecut, T, classical, zpmotion)
+    m = aw * efric
+    m = m + (-0.5 * aw * exip + 0.5 * awm * (exip + 1j * exim))
+    m = m + (-0.5 * aw * exip + 0.5 * awp * (exip - 1j * exim))
+    return hermitianize(m)
+
+
+def enoisew(wl, efric, exim, exip, bias, T, ecut, classical=False, zpmotion=True):
+    """Electron noise spectrum on the frequencies wl (noise.py:105-146: the same matrix as enoise's
+    without the Delta = dt nmd factor).  (The reference's own enoisew raises before computing: its
+    local `np = chkShape(exip)` shadows numpy, noise.py:122-128.)"""
+    efric, exim, exip = (np.asarray(m, dtype=float) for m in (efric, exim, exip))
+    if not (efric.shape == exim.shape == exip.shape and efric.shape[0] == efric.shape[1]):
+        raise ValueError("enoisew: efric / exim / exip shape error")
+    out = np.empty((len(wl),) + efric.shape, dtype=complex)
+    for n, w in enumerate(wl):
+        out[n] = _electron_matrix(w, efric, exim, exip, bias, T, ecut, 1.0, classical, zpmotion)
+    return out
+
+
+def vargau(eval, evec, cof=1.0):
+    """One multivariate Gaussian draw U r, r_k ~ N(0, sqrt(cof lambda_k)) for cof lambda_k > 0 (0
+    otherwise), from the global numpy RNG in eigenvalue order (noise.py:273-305).  The generators
+    draw all frequencies at once with the same sequence (NoiseFactor.draws)."""
+    evec = np.asarray(evec)
+    if evec.ndim != 2 or evec.shape[0] != evec.shape[1] or len(eval) != evec.shape[0]:
+        raise ValueError("vargau: shape error")
+    r = [np.random.normal(0.0, np.sqrt(cof * v)) if cof * v > 0 else 0.0 for v in eval]
+    return np.linalg.multi_dot([evec, r]) if len(r) > 1 else evec @ np.asarray(r)
+
+
 def frequencies(dt, nmd):
     hlen = int(nmd / 2)
     dw = 2.0 * np.pi / dt / nmd
@@ -62,13 +129,7 @@ def electron_spectrum(efric, exim, exip, bias, T, ecut, dt, nmd, classical=False
     efric, exim, exip = (np.asarray(m, dtype=float) for m in (efric, exim, exip))
     out = np.empty((len(ws),) + efric.shape, dtype=complex)
     for n, w in enumerate(ws):
-        aw = delta * equ(w, ecut, T, classical, zpmotion)
-        awm = delta * equ(U.hbar * w - bias, ecut, T, classical, zpmotion)
-        awp = delta * equ(U.hbar * w + bias, ecut, T, classical, zpmotion)
-        m = aw * efric
-        m = m + (-0.5 * aw * exip + 0.5 * awm * (exip + 1j * exim))
-        m = m + (-0.5 * aw * exip + 0.5 * awp * (exip - 1j * exim))
-        out[n] = hermitianize(m)
+        out[n] = _electron_matrix(w, efric, exim, exip, bias, T, ecut, delta, classical, zpmotion)
     return out
 
 

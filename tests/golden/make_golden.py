@@ -23,6 +23,9 @@ Fixtures (each < 1 MB):
                                                                          functions.py:221-236)
   ggamma.npz      phbath built from a self-energy sig: gamma = -Im sig / w, gmem kernel
                                                                         (baths.py:294-340, 375-395, 412-445)
+  helpers.npz     public helpers: coth / xcoth / fermi / dagger / mm / powerspecq, phnoisew /
+                  nonequm / nonequp / vargau, exlist, ebath.GetSig    (functions.py:59-218, noise.py:28-305,
+                                                                         baths.py:12-14, 194-208)
 
     python3 tests/golden/make_golden.py [name ...]     (default: all)
 """
@@ -488,9 +491,78 @@ def make_ggamma():
                         debye=0.2, nw=50, cids=np.array([3, 4, 5, 6]), gamma=gamma, kernel=np.array(b.kernel))
 
 
+def make_helpers():
+    """The reference's small public helpers a user script may import: functions.coth / xcoth /
+    fermi / dagger / mm / powerspecq, noise.phnoisew / nonequm / nonequp / vargau, baths.exlist,
+    ebath.GetSig.  (np.complex, removed in numpy 2, is aliased for GetSig.)"""
+    rng = np.random.default_rng(21)
+    had = hasattr(np, "complex")
+    if not had:
+        np.complex = complex
+    try:
+        out = {}
+        xs = np.array([-3.0, -0.5, 1e-6, 0.25, 2.0, 30.0])
+        out["coth_x"] = xs
+        out["coth"] = np.array([RF.coth(x) for x in xs])
+        xs0 = np.concatenate([[0.0], xs])
+        out["xcoth_x"] = xs0
+        out["xcoth"] = np.array([RF.xcoth(x) for x in xs0])
+        fe = [(e, mu, T) for e in (-0.2, 0.0, 0.1) for mu in (0.0, 0.1) for T in (0.0, 300.0)]
+        out["fermi_args"] = np.array(fe)
+        out["fermi"] = np.array([RF.fermi(e, mu, T) for e, mu, T in fe])
+        a = rng.normal(size=(4, 4)) + 1j * rng.normal(size=(4, 4))
+        out["dagger_in"], out["dagger"] = a, RF.dagger(a)
+        m1, m2, m3 = rng.normal(size=(3, 4)), rng.normal(size=(4, 5)), rng.normal(size=(5, 2))
+        out["mm_1"], out["mm_2"], out["mm_3"], out["mm"] = m1, m2, m3, RF.mm(m1, m2, m3)
+        nmd, dt = 64, 0.25 / 0.658
+        qs = rng.normal(size=(nmd, 6))
+        out["qs"], out["powerspecq"], out["pq_dt"] = qs, RF.powerspecq(qs, dt, nmd), dt
+        nc = 4
+        gwl, gam = gamma_table(nc, rng)
+        wl = np.linspace(0.0, 0.6, 13)
+        gamw = np.array([RF.flinterp(w, gwl, gam) for w in wl])
+        out["phw_wl"], out["phw_gam"] = wl, gamw
+        for tag, T, cut, cl, zp in (("q", 300.0, 0.4, False, True), ("c", 300.0, 0.4, True, True),
+                                    ("nozp", 50.0, 0.3, False, False)):
+            out["phnoisew_" + tag] = RN.phnoisew(gamw, wl, T, cut, cl, zp)
+            out["phw_params_" + tag] = np.array([T, cut, float(cl), float(zp)])
+        efric = spd(nc, rng, 0.658 / 100)
+        exim, exip = anti(nc, rng, 1e-3), sym(nc, rng, 1e-3)
+        out["ew_efric"], out["ew_exim"], out["ew_exip"] = efric, exim, exip
+        # (the reference's enoisew raises: its local `np = chkShape(exip)` shadows numpy before
+        # np.zeros, noise.py:122-128; enoise's own spectral matrix pins the formula instead)
+        neq = [(w, b, T, cl) for w in (0.0, 0.05, 0.3) for b in (0.0, 0.1, -0.2) for T in (0.0, 300.0)
+               for cl in (False, True) if not (cl and T == 0.0)]
+        out["neq_args"] = np.array(neq, dtype=float)
+        with quiet():
+            out["nonequm"] = np.array([RN.nonequm(w, b, T, cl) for w, b, T, cl in neq])
+            out["nonequp"] = np.array([RN.nonequp(w, b, T, cl) for w, b, T, cl in neq])
+        ev = np.array([-1e-3, 0.0, 2.0, 0.5])
+        evec = np.linalg.qr(rng.normal(size=(4, 4)))[0]
+        np.random.seed(5)
+        out["vargau_ev"], out["vargau_evec"] = ev, evec
+        out["vargau"] = np.array([RN.vargau(ev, evec, 1.5) for _ in range(3)])
+        arr = rng.normal(size=(10, 3))
+        idx = np.array([7, 2, 2, 9])
+        out["exlist_in"], out["exlist_idx"], out["exlist"] = arr, idx, RB.exlist(arr, idx)
+        cats = [3, 4, 5]
+        with quiet():
+            eb = RB.ebath(cats, 300.0, 0.5, 64, wmax=1.0, nw=7, bias=0.4, efric=spd(3, rng, 0.01),
+                          exim=anti(3, rng, 1e-3), exip=sym(3, rng, 1e-3), zeta1=sym(3, rng, 1e-3),
+                          zeta2=anti(3, rng, 1e-3))
+            eb.GetSig()
+        out["sig_efric"], out["sig_exim"], out["sig_zeta1"], out["sig_zeta2"] = eb.efric, eb.exim, eb.zeta1, eb.zeta2
+        out["sig_wl"], out["sig"] = np.array(eb.wl), eb.sig
+    finally:
+        if not had:
+            del np.complex
+    np.savez_compressed(os.path.join(HERE, "helpers.npz"), **out)
+
+
 if __name__ == "__main__":
     makers = {"scalars": make_scalars, "gamt": make_gamt, "noise": make_noise, "vv": make_vv_cases,
-              "run_seeded": make_run_seeded, "tools": make_tools, "power": make_power, "ggamma": make_ggamma}
+              "run_seeded": make_run_seeded, "tools": make_tools, "power": make_power, "ggamma": make_ggamma,
+              "helpers": make_helpers}
     for name in (sys.argv[1:] or list(makers)):
         makers[name]()
     for f in sorted(os.listdir(HERE)):
