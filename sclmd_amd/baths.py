@@ -151,6 +151,12 @@ class _BathBase:
     def _noise_key(self):
         raise NotImplementedError
 
+    def bforce(self, t, phis, qhis):
+        """bath.bforce (baths.py:224-255 / 448-458) is evaluated inside the HIP stepper as part of
+        md.force (no host copy of the per-step force exists): raises."""
+        raise NotImplementedError("%s.bforce runs on the device inside md.force / the stepper (gle_run, "
+                                  "gle_step_begin / gle_step_end); there is no host evaluation" % type(self).__name__)
+
     def noise_factor(self, share=None):
         """Eigendecomposition of the noise spectrum, cached until a parameter changes.  share: a
         noise.NodeShare -- the node's ranks each decompose a block of the frequencies and exchange
