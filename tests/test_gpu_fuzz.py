@@ -305,3 +305,76 @@ def test_interleaved_handles_vs_oracle():
     finally:
         for st, _, _ in live:
             st.close()
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_random_large_bath_vs_oracle(seed):
+    """Baths above the small-bath limit (nc > 512: the large-bath plan picked by the automatic rule,
+    first block length 4, the potential-force launch, dyn as ELL), random widths, memory lengths,
+    constraints and host-force segments against the oracle."""
+    from oracle import sclmd_oracle as O
+    from sclmd_amd import _native as N
+    from sclmd_amd import synthetic
+
+    r = np.random.default_rng(7000 + seed)
+    natom = int(r.integers(178, 200))
+    nph = 3 * natom
+    dyn = synthetic.chain_dyn(natom)
+    nmd = 128
+    B = int(r.choice([1, 8, 33]))
+    nc = int(r.integers(513, 560))
+    a0 = int(r.integers(0, nph - nc + 1))
+    baths = [synthetic.make_phbath(300.0, list(range(a0, a0 + nc)), int(r.choice([2, 24])), nmd, r, nw=60)]
+    if r.random() < 0.5:
+        d = sorted(int(x) for x in r.choice(nph, 40, replace=False))
+        baths.append(synthetic.make_biased_ebath(300.0, d, nmd, r))
+    constr = sorted(set(int(x) for x in r.choice(nph, 4, replace=False))) if seed != 1 else None
+    dt = baths[0].dt
+    st = N.Stepper(nph, B, nmd, dt, 0)
+    try:
+        for b in baths:
+            if b.kind == "ebath":
+                st.add_bath(N.GLE_BATH_ELECTRON, b.cids, b.kernel, b.bias, b.exim, b.zeta1, b.zeta2)
+            else:
+                st.add_bath(N.GLE_BATH_PHONON, b.cids, b.kernel)
+        st.set_dyn(dyn)
+        if constr is not None:
+            st.set_constraint(constr)
+        p = r.normal(size=(B, nph)) * 1e-2
+        q = r.normal(size=(B, nph)) * 1e-2
+        if constr is not None:
+            p[:, constr] = 0.0
+            q[:, constr] = 0.0
+        noise = [r.normal(size=(B, nmd, b.nc)) * 1e-3 for b in baths]
+        hist = [r.normal(size=(B, b.kernel.shape[0], b.nc)) * 1e-2 for b in baths]
+        st.set_state(p, q, 11)
+        for i in range(len(baths)):
+            st.set_history(i, hist[i])
+            st.set_noise(i, noise[i])
+        assert st.plan_detail()["plan_class"] == "large"
+        ob = [O.Bath("e", b.cids, b.kernel, noise[i], dt, nmd, bias=b.bias, exim=b.exim, zeta1=b.zeta1,
+                     zeta2=b.zeta2) if b.kind == "ebath" else O.Bath("ph", b.cids, b.kernel, noise[i], dt, nmd)
+              for i, b in enumerate(baths)]
+        sim = O.GLEBatch(nph, dt, nmd, ob, dyn, ntr=B,
+                         constr=None if constr is None else [range(x, x + 1) for x in constr])
+        sim.p, sim.q, sim.t = p.T.copy(), q.T.copy(), 11
+        for i in range(len(baths)):
+            sim.set_history(i, hist[i])
+        for kind, k in (("run", 47), ("host", 2), ("run", 70)):
+            if kind == "run":
+                st.run(k)
+                for _ in range(k):
+                    sim.step()
+            else:
+                for _ in range(k):
+                    qt = st.step_begin(-(st.get_state()[1] @ dyn.T))
+                    st.step_end(-(qt @ dyn.T))
+                    sim.step()
+        pg, qg, _ = st.get_state()
+        cur = st.get_current()
+    finally:
+        st.close()
+    assert rel(qg, sim.q.T) < TOL and rel(pg, sim.p.T) < TOL, (rel(qg, sim.q.T), rel(pg, sim.p.T))
+    steps = (11 + np.arange(119)) % nmd
+    want = np.stack([cc[:, steps] for cc in sim.cur])
+    assert rel(cur[:, :, steps], want) < TOL
