@@ -896,25 +896,33 @@ int fill_tasks(gle_handle* h, ChTile& T, const std::vector<Seg>& segs, int nout,
   const int NW = c.nw;
   double* flops = &c.flops;
   std::vector<int> nsl(nout, 0), first(nout, -1);
+  // wave w takes [bnd[w], bnd[w + 1]): the even split point, cut short at a segment end if it would
+  // need more than CH_TPW runs (the following waves take the rest); when that leaves work past the
+  // last wave (many short segments: small baths, several baths in one tile), each wave instead takes
+  // whole runs up to CH_TPW of them
+  std::vector<int64_t> bnd(NW + 1, g_begin);
+  auto cut = [&](int64_t g0, int64_t g1, bool greedy) {
+    int64_t pos = 0;
+    int runs = 0;
+    for (const Seg& sg : segs) {
+      const int64_t s0 = std::max(g0, pos), s1 = std::min(greedy ? g_end : g1, pos + sg.nks);
+      if (s1 > s0 && ++runs == CH_TPW) return greedy ? pos + sg.nks : std::min(g1, pos + sg.nks);
+      pos += sg.nks;
+    }
+    return greedy ? g_end : g1;
+  };
+  for (int pass = 0; pass < 2; ++pass) {
+    for (int w = 0; w < NW; ++w) {
+      const int64_t g0 = bnd[w];
+      bnd[w + 1] = pass == 0 ? cut(g0, std::max(g0, g_begin + (g_end - g_begin) * (w + 1) / NW), false)
+                             : cut(g0, g_end, true);
+    }
+    if (bnd[NW] >= g_end) break;
+    if (pass == 1) return fail(h, GLE_ERR_UNSUP, "chain plan: too many k-step runs per wave");
+  }
   int64_t g0 = g_begin;
   for (int w = 0; w < NW; ++w) {
-    // wave w: [g0, g1) with g1 the even split point, cut short at a segment end if it would need
-    // more than CH_TPW runs (the following waves take the rest)
-    int64_t g1 = std::max(g0, g_begin + (g_end - g_begin) * (w + 1) / NW);
-    {
-      int64_t pos = 0;
-      int runs = 0;
-      for (const Seg& sg : segs) {
-        const int64_t s0 = std::max(g0, pos), s1 = std::min(g1, pos + sg.nks);
-        if (s1 > s0 && ++runs == CH_TPW) {
-          g1 = std::max(g1, std::min(pos + sg.nks, w == NW - 1 ? g_end : g1));
-          g1 = std::min(g1, pos + sg.nks);
-          break;
-        }
-        pos += sg.nks;
-      }
-    }
-    if (w == NW - 1 && g1 < g_end) return fail(h, GLE_ERR_UNSUP, "chain plan: too many k-step runs per wave");
+    const int64_t g1 = std::min(bnd[w + 1], g_end);
     int64_t pos = 0;
     int cur_o = -1, cnt = 0, cur_slot = -1;
     for (const Seg& sg : segs) {

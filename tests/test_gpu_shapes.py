@@ -186,3 +186,12 @@ def test_device_steps_after_host_force_with_constraints(plan_class, scatter):
     tests/test_gpu_fuzz.py).  Three-launch (overlapping baths), fused and composed plans."""
     for B in (3, 40):
         _run(B, plan_class, constr=[0, 1, 2, 60, 61, 119], scatter=scatter)
+
+
+@pytest.mark.parametrize("plan_class", ["small", "large"])
+def test_three_baths_in_one_tile_vs_oracle(plan_class):
+    """A tiny junction (24 DOFs) whose DOF tiles meet all three baths, each a few k-steps wide: more
+    short product runs per tile than the even wave split holds (it failed to plan, 'too many k-step
+    runs per wave', found by tests/test_gpu_fuzz_ckpt.py); the waves then take whole runs."""
+    for B in (3, 40):
+        _run(B, plan_class, config="C5", natom=8, ml=24)
