@@ -28,7 +28,8 @@ def _case(seed):
     from sclmd_amd import synthetic
 
     r = np.random.default_rng(1000 + seed)
-    natom = int(r.integers(5, 60))
+    tiny = r.random() < 0.3  # a few DOF tiles meeting several small baths (many short product runs)
+    natom = int(r.integers(4, 11)) if tiny else int(r.integers(5, 60))
     nph = 3 * natom
     dyn = synthetic.chain_dyn(natom)
     if r.random() < 0.5:  # long-range couplings: the block-sparse dyn with scattered blocks
@@ -41,11 +42,11 @@ def _case(seed):
         dyn = dyn + add + np.eye(nph) * 2 * np.abs(add).sum(axis=1).max()
     nmd = int(r.choice([64, 128, 256]))
     B = int(r.choice([1, 2, 3, 5, 8, 13, 16, 17, 24, 31, 32, 33, 40, 48, 49, 63, 64, 70]))
-    nb = int(r.integers(1, 4))
+    nb = 3 if tiny else int(r.integers(1, 4))
     baths, used = [], np.zeros(nph, bool)
     for k in range(nb):
         kind = "e" if (k == nb - 1 and r.random() < 0.4) else "ph"
-        nc = int(r.integers(2, max(3, min(nph, 90))))
+        nc = int(r.integers(2, max(3, min(nph, 12 if tiny else 90))))
         mode = r.choice(["range", "scatter", "overlap"])
         if mode == "range":
             a = int(r.integers(0, nph - nc + 1))

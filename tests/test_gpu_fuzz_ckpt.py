@@ -4,12 +4,14 @@ md) started in the same directory, ends where the uninterrupted run ends (1e-10 
 every run's kappa).  Each case draws the junction size, the ensemble width (composed and two-launch
 plans), the baths (memory lengths, a biased electron bath), constraints, npie and the number of
 runs; device noise (trajectory-keyed, so the resumed run regenerates the same realisations)."""
+import os
+
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
-NCASE = 8
+NCASE = int(os.environ.get("SCLMD_FUZZ_CKPT", "8"))  # a wider sweep: SCLMD_FUZZ_CKPT=40
 
 
 def rel(a, b):
