@@ -84,6 +84,19 @@ def test_random_interrupt_and_resume(seed, tmp_path, monkeypatch):
     p2, q2, kap2 = np.array(m.p), np.array(m.q), np.array(m.kappa_runs)
     m.close()
     desc = "case %s stop run %d piece %d" % ({k: v for k, v in c.items() if k != "r"}, stop_run, stop_piece)
+    last = c["nrun"] - 1
+    if stop_run == last and stop_piece == c["npie"] - 1:
+        # every run was finished: the new process only finds the files (md.py:537-544) and steps
+        # nothing; the last file holds the uninterrupted final state
+        from sclmd_amd.checkpoint import ReadNetCDFVar
+
+        fn = "MD%d.nc" % last
+        assert len(kap2) == 0, desc
+        assert rel(ReadNetCDFVar(str(part / fn), "q"), ReadNetCDFVar(str(full / fn), "q")) == 0.0, desc
+        assert rel(ReadNetCDFVar(str(part / fn), "p"), ReadNetCDFVar(str(full / fn), "p")) == 0.0, desc
+        return
     assert rel(q2, q) < 1e-10 and rel(p2, p) < 1e-10, (desc, rel(q2, q), rel(p2, p))
-    # the resumed process reports the runs it computed itself (finished runs are skipped)
-    assert len(kap2) >= 1 and rel(kap2[-1], kap[-1]) < 1e-9, desc
+    # kappa of the resumed run covers only the steps this process ran (the reference keeps no
+    # bath.cur in MD{j}.nc, md.py:506-535, 684-764); runs after it are whole and equal
+    if stop_run < last:
+        assert rel(kap2[-1], kap[-1]) < 1e-9, desc
