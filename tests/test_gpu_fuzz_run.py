@@ -6,7 +6,9 @@ oracle.phnoise / enoise + the reference-shaped oracle.GLE stepping and the per-r
 draws a chain junction, 1-3 baths (phonon baths with gamma spectra, ml in [1, 40], electron baths
 with random exim / exip, biased or not), constraints, nrun in [1, 3], npie and an even nmd that is
 sometimes not a power of two (the device noise then takes the mixed-radix / Bluestein transforms).
-1e-9 relative on the final p, q and on every run's kappa."""
+1e-9 relative on the final p, q, on every run's kappa and on the power spectra (CalPowerSpec, with
+random AddPowerSection groups: the running mean over the runs of functions.powerspecp of the
+recorded velocities)."""
 import os
 
 import numpy as np
@@ -56,8 +58,12 @@ def _case(seed):
     if r.random() < 0.5:
         c0 = int(r.integers(0, nph - 3))
         constr = [range(c0, c0 + int(r.integers(1, 4)))]
+    groups = None
+    if r.random() < 0.5:  # AddPowerSection: DOF groups of the power spectra (md.py:604-653)
+        groups = [sorted(int(x) for x in r.choice(nph, int(r.integers(1, nph + 1)), replace=False))
+                  for _ in range(int(r.integers(1, 4)))]
     return dict(natom=natom, nph=nph, nmd=nmd, npie=npie, nrun=nrun, baths=baths, constr=constr, seed=seed,
-                np_seed=int(r.integers(0, 2 ** 31)))
+                np_seed=int(r.integers(0, 2 ** 31)), groups=groups)
 
 
 def _describe(c):
@@ -80,9 +86,11 @@ def _oracle_run(c, dyn, dt, T):
         else:
             obs.append(O.Bath("e", b["cids"], np.array([O.symm(b["efric"])]), None, dt, c["nmd"], bias=b["bias"],
                               exim=O.antisymm(b["exim"]), zeta1=O.symm(b["zeta1"]), zeta2=O.antisymm(b["zeta2"])))
+    from sclmd_amd.functions import powerspecp  # the host restatement, pinned by tests/golden/power.npz
+
     sim = O.GLE(c["nph"], dt, c["nmd"], obs, dyn=dyn_used, constr=c["constr"])
     sim.p, sim.q = p0, q0
-    kappa = []
+    kappa, powers = [], []
     for _ in range(c["nrun"]):
         for b, ob in zip(c["baths"], obs):
             if b["kind"] == "ph":
@@ -90,10 +98,15 @@ def _oracle_run(c, dyn, dt, T):
             else:
                 ob.noise = np.real(O.enoise(O.symm(b["efric"]), O.antisymm(b["exim"]), O.symm(b["exip"]), b["bias"],
                                             b["T"], b["wmax"], dt, c["nmd"]))
+        ps = np.zeros((c["nmd"], c["nph"]))
         for _ in range(c["nmd"]):
+            ps[int(sim.t) % c["nmd"]] = sim.p  # savep: md.ps[t % nmd] = p_t (md.py:374-375)
             sim.step()
         kappa.append([np.mean(ob.cur) * O.CURCOF for ob in obs])
-    return sim.p, sim.q, np.array(kappa)
+        powers.append([powerspecp(ps, dt, c["nmd"])] + [powerspecp(ps[:, g], dt, c["nmd"]) for g in c["groups"] or []])
+    # md.Run keeps the running mean over its runs (md.py:604-653)
+    power = np.mean(np.array(powers), axis=0)
+    return sim.p, sim.q, np.array(kappa), power
 
 
 @pytest.mark.parametrize("seed", range(NCASE))
@@ -120,11 +133,19 @@ def test_random_run_vs_oracle(seed, tmp_path, monkeypatch):
                             exim=b["exim"], exip=b["exip"], zeta1=b["zeta1"], zeta2=b["zeta2"]))
     if c["constr"] is not None:
         m.AddConstr(c["constr"])
+    m.CalPowerSpec()
+    if c["groups"] is not None:
+        m.AddPowerSection(c["groups"])
     np.random.seed(c["np_seed"])
     m.Run()
     p, q, kap, t = np.array(m.p), np.array(m.q), np.array(m.kappa_runs), m.t
+    power = np.array(m.power)
+    al = None if c["groups"] is None else np.array(m.poweratomlist)
     m.close()
-    wp, wq, wk = _oracle_run(c, dyn, dt, T)
+    wp, wq, wk, wpow = _oracle_run(c, dyn, dt, T)
     assert t == c["nrun"] * c["nmd"], desc
     assert rel(q, wq) < 1e-9 and rel(p, wp) < 1e-9, (desc, rel(q, wq), rel(p, wp))
     assert rel(kap, wk) < 1e-9, (desc, kap, wk)
+    assert rel(power, wpow[0]) < 1e-9, (desc, "power")
+    if al is not None:
+        assert rel(al, wpow[1:]) < 1e-9, (desc, "poweratomlist")
