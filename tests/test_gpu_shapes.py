@@ -195,3 +195,11 @@ def test_three_baths_in_one_tile_vs_oracle(plan_class):
     runs per wave', found by tests/test_gpu_fuzz_ckpt.py); the waves then take whole runs."""
     for B in (3, 40):
         _run(B, plan_class, config="C5", natom=8, ml=24)
+
+
+@pytest.mark.parametrize("plan_class", ["small", "large"])
+def test_memory_longer_than_run_vs_oracle(plan_class):
+    """ml > nmd (a memory kernel longer than the noise period; nothing in the reference forbids it):
+    the history ring is sized by ml, the noise index wraps by nmd."""
+    for B in (3, 40):
+        _run(B, plan_class, ml=200, nmd=64)
