@@ -4,7 +4,7 @@ md API with the numpy-compatible noise (np.random.seed, the reference's RandomSt
 reference's order: initialise, then per run each bath's gnoi) against oracle.initial_state +
 oracle.phnoise / enoise + the reference-shaped oracle.GLE stepping and the per-run kappa.  Each case
 draws a chain junction, 1-3 baths (phonon baths with gamma spectra, ml in [1, 40], electron baths
-with random exim / exip, biased or not), constraints, nrun in [1, 3], npie and an even nmd that is
+with random exim / exip, biased or not; T = 0 sometimes, classical or without zero-point motion), constraints, nrun in [1, 3], npie and an even nmd that is
 sometimes not a power of two (the device noise then takes the mixed-radix / Bluestein transforms).
 1e-9 relative on the final p, q, on every run's kappa and on the power spectra (CalPowerSpec, with
 random AddPowerSection groups: the running mean over the runs of functions.powerspecp of the
@@ -41,7 +41,8 @@ def _case(seed):
         if r.random() < 0.4:
             n = nc
             s = 1e-3
-            baths.append(dict(kind="e", cids=cids, T=300.0 * (1 + 0.05 * k),
+            baths.append(dict(kind="e", cids=cids, T=float(r.choice([0.0, 300.0 * (1 + 0.05 * k)], p=[0.2, 0.8])),
+                              classical=bool(r.random() < 0.2), zpmotion=bool(r.random() < 0.8),
                               efric=np.eye(n) * 1e-2 + s * (lambda m: m @ m.T / n)(r.normal(size=(n, n))),
                               exim=s * r.normal(size=(n, n)), exip=s * r.normal(size=(n, n)),
                               zeta1=s * r.normal(size=(n, n)), zeta2=s * r.normal(size=(n, n)),
@@ -52,7 +53,8 @@ def _case(seed):
             A = r.normal(size=(nc, nc))
             A = A @ A.T / nc + np.eye(nc)
             gam = (0.658 / 100.0) * np.exp(-(gwl / 0.1) ** 2)[:, None, None] * A[None]
-            baths.append(dict(kind="ph", cids=cids, T=300.0 * (1 + 0.05 * k), gam=gam, gwl=gwl, debye=0.2,
+            baths.append(dict(kind="ph", cids=cids, T=float(r.choice([0.0, 300.0 * (1 + 0.05 * k)], p=[0.2, 0.8])),
+                              classical=bool(r.random() < 0.2), zpmotion=bool(r.random() < 0.8), gam=gam, gwl=gwl, debye=0.2,
                               nw=int(r.integers(20, 80)), ml=int(r.choice([1, 2, 5, 16, 40]))))
     constr = None
     if r.random() < 0.5:
@@ -94,10 +96,11 @@ def _oracle_run(c, dyn, dt, T):
     for _ in range(c["nrun"]):
         for b, ob in zip(c["baths"], obs):
             if b["kind"] == "ph":
-                ob.noise = np.real(O.phnoise(b["gam"], b["gwl"], b["T"], 2.0 * b["debye"], dt, c["nmd"]))
+                ob.noise = np.real(O.phnoise(b["gam"], b["gwl"], b["T"], 2.0 * b["debye"], dt, c["nmd"],
+                                             b["classical"], b["zpmotion"]))
             else:
                 ob.noise = np.real(O.enoise(O.symm(b["efric"]), O.antisymm(b["exim"]), O.symm(b["exip"]), b["bias"],
-                                            b["T"], b["wmax"], dt, c["nmd"]))
+                                            b["T"], b["wmax"], dt, c["nmd"], b["classical"], b["zpmotion"]))
         ps = np.zeros((c["nmd"], c["nph"]))
         for _ in range(c["nmd"]):
             ps[int(sim.t) % c["nmd"]] = sim.p  # savep: md.ps[t % nmd] = p_t (md.py:374-375)
@@ -125,12 +128,13 @@ def test_random_run_vs_oracle(seed, tmp_path, monkeypatch):
     for b in c["baths"]:
         if b["kind"] == "ph":
             pb = phbath(b["T"], b["cids"], debye=b["debye"], nw=b["nw"], dt=dt, nmd=c["nmd"], ml=b["ml"],
-                        gamma=b["gam"], gwl=b["gwl"])
+                        gamma=b["gam"], gwl=b["gwl"], classical=b["classical"], zpmotion=b["zpmotion"])
             pb.gmem()
             m.AddBath(pb)
         else:
             m.AddBath(ebath(b["cids"], b["T"], dt, c["nmd"], wmax=b["wmax"], nw=b["nw"], bias=b["bias"], efric=b["efric"],
-                            exim=b["exim"], exip=b["exip"], zeta1=b["zeta1"], zeta2=b["zeta2"]))
+                            exim=b["exim"], exip=b["exip"], zeta1=b["zeta1"], zeta2=b["zeta2"],
+                            classical=b["classical"], zpmotion=b["zpmotion"]))
     if c["constr"] is not None:
         m.AddConstr(c["constr"])
     m.CalPowerSpec()
