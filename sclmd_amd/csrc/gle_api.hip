@@ -3916,11 +3916,9 @@ int gle_set_dyn(gle_handle* h, const double* dyn) {
 int gle_set_constraint(gle_handle* h, const int64_t* dofs, int64_t n) {
   if (!h || (n > 0 && !dofs) || n < 0) return GLE_ERR_ARG;
   if (h->frozen) return fail(h, GLE_ERR_STATE, "constraints must be set before the first state/step call");
-  h->constr.clear();
-  for (int64_t i = 0; i < n; ++i) {
+  for (int64_t i = 0; i < n; ++i)  // a rejected call leaves the previous constraints in place
     if (dofs[i] < 0 || dofs[i] >= h->nph) return fail(h, GLE_ERR_ARG, "constraint DOF out of range");
-    h->constr.push_back(dofs[i]);
-  }
+  h->constr.assign(dofs, dofs + n);
   return GLE_OK;
 }
 
