@@ -153,3 +153,45 @@ def test_random_run_vs_oracle(seed, tmp_path, monkeypatch):
     assert rel(power, wpow[0]) < 1e-9, (desc, "power")
     if al is not None:
         assert rel(al, wpow[1:]) < 1e-9, (desc, "poweratomlist")
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_numpy_noise_ensemble_equals_single_trajectories(seed, tmp_path, monkeypatch):
+    """The numpy-compatible noise with md(seed=s): trajectory b draws from RandomState(s + b) (its
+    initial state and every run's vargau draws), so a 3-trajectory md.Run equals three one-trajectory
+    runs with traj_offset = b -- the reference's per-trajectory sequence, batched."""
+    from sclmd_amd import md as MD
+    from sclmd_amd import synthetic
+    from sclmd_amd.baths import ebath, phbath
+
+    c = _case(seed)
+    dt, T = synthetic.DT, 300.0
+    dyn = synthetic.chain_dyn(c["natom"])
+
+    def run(ntraj, offset):
+        d = tmp_path / ("n%d_o%d" % (ntraj, offset))
+        d.mkdir()
+        monkeypatch.chdir(d)
+        m = MD.md(dt, c["nmd"], T, axyz=synthetic.axyz_chain(c["natom"]), dyn=dyn, nstart=0, nstop=c["nrun"],
+                  npie=c["npie"], ntraj=ntraj, seed=77, traj_offset=offset, noise_mode="numpy", verbose=False)
+        for b in c["baths"]:
+            if b["kind"] == "ph":
+                pb = phbath(b["T"], b["cids"], debye=b["debye"], nw=b["nw"], dt=dt, nmd=c["nmd"], ml=b["ml"],
+                            gamma=b["gam"], gwl=b["gwl"], classical=b["classical"], zpmotion=b["zpmotion"])
+                pb.gmem()
+                m.AddBath(pb)
+            else:
+                m.AddBath(ebath(b["cids"], b["T"], dt, c["nmd"], wmax=b["wmax"], nw=b["nw"], bias=b["bias"],
+                                efric=b["efric"], exim=b["exim"], exip=b["exip"], zeta1=b["zeta1"], zeta2=b["zeta2"],
+                                classical=b["classical"], zpmotion=b["zpmotion"]))
+        if c["constr"] is not None:
+            m.AddConstr(c["constr"])
+        m.Run()
+        p, q = np.array(m.p).reshape(ntraj, -1), np.array(m.q).reshape(ntraj, -1)
+        m.close()
+        return p, q
+
+    p, q = run(3, 0)
+    for b in range(3):
+        pb, qb = run(1, b)
+        assert rel(qb[0], q[b]) < 1e-9 and rel(pb[0], p[b]) < 1e-9, (_describe(c), b)
